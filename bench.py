@@ -1,0 +1,222 @@
+#!/usr/bin/env python3
+"""Benchmark: DQN minibatch updates/sec on MI355X (BASELINE.json metric).
+
+One step = one minibatch update of the deepq network on one GPU:
+  device index draw -> replay gather -> P/Q forward -> Bellman target + loss ->
+  Q backward -> [RCCL sum all-reduce of the gradient] -> rmsprop apply
+  (param-server default rule) -> P <- Q every 10 updates,
+captured once into a hipGraph and replayed.  Workload at N=1: BASELINE.json
+configs[1] -- deepq Snake, batch 32, 4-frame 64x64 history, 30 000-slot HBM
+replay filled with synthetic Snake frames.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+
+Prints ONE JSON line (rank 0).  ``value`` = minibatch updates/s summed over
+all ranks (each rank consumes its own minibatch per step: weak scaling).
+``roofline``: dominant kernel measured with HIP events on the ctx stream
+(ddq_profile_step) vs the f32 MFMA peak.  ``cpu_baseline``: the oracle's C
+restatement of the Caffe CPU step (oracle/libddq_cpu.so) timed on the host
+cores on a bounded sample of the same workload.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "distributed-deep-q_amd")]
+
+METRIC = "DQN minibatch updates/sec (fwd+bwd+sync+apply) @1/2/4/8 GPU; % MFMA/HBM peak"
+F32_MFMA_PEAK = 157.3e12      # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense
+HBM_PEAK = 8.0e12
+
+
+def kernel_flops(B, S):
+    """Algorithmic FLOPs per launch of each MFMA kernel (2 * MACs)."""
+    s2, s3, s4 = S // 2, S // 4, S // 8
+    k4 = 64 * s4 * s4
+    c1 = 2.0 * B * S * S * 32 * 196
+    c2 = 2.0 * B * s2 * s2 * 64 * 800
+    c3 = 2.0 * B * s3 * s3 * 64 * 576
+    fc = 2.0 * B * 512 * k4
+    return {"conv1_fwd": 2 * c1, "conv2_fwd": 2 * c2, "conv3_fwd": 2 * c3, "fc4_fwd": 2 * fc,
+            "fc4_dgrad": fc, "fc4_wgrad": fc, "conv3_wgrad": c3, "conv3_dgrad": c3,
+            "conv2_wgrad": c2, "conv2_dgrad": c2, "conv1_wgrad": c1}
+
+
+def fill_replay(net, N, S, seed):
+    from ddq.expgain import synthetic_transitions
+    pool = min(N, 4096)
+    st, ac, rw, nt = synthetic_transitions(pool, S, seed=seed)
+    reps = (N + pool - 1) // pool
+    net.replay_import(np.tile(st, (reps, 1, 1, 1))[:N], np.tile(ac, reps)[:N],
+                      np.tile(rw, reps)[:N], np.tile(nt, reps)[:N].astype(np.uint8), 0, N)
+
+
+def cpu_baseline(B, S, seed, budget_s=12.0, max_steps=16):
+    """Oracle C restatement (Caffe CPU algorithm) of the same update step."""
+    from oracle import ref_numpy as ref
+    from ddq.expgain import synthetic_transitions
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "libddq_cpu.so"))
+    fp = ctypes.POINTER(ctypes.c_float)
+    lib.ddq_cpu_full_pass.restype = ctypes.c_int
+    lib.ddq_cpu_apply.restype = ctypes.c_int
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count()
+    cores = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores))))
+    N = 1024
+    st, ac, rw, nt = synthetic_transitions(N, S, seed=seed)
+    theta = ref.flatten(ref.init_params(S, seed=42))
+    thetaP = theta.copy()
+    cache = np.zeros_like(theta)
+    grad = np.zeros_like(theta)
+    rng = np.random.default_rng(seed)
+    img = 4 * S * S
+    t0 = time.perf_counter()
+    steps = 0
+    P = lambda a: a.ctypes.data_as(fp)
+    while steps < max_steps and (steps == 0 or time.perf_counter() - t0 < budget_s):
+        idx = ref.draw_indices(rng, N, 0, B)
+        nxt = np.where(idx + 1 == N, 0, idx + 1)
+        s = st[idx].astype(np.float32).reshape(B, img)
+        s2 = st[nxt].astype(np.float32).reshape(B, img)
+        a = np.zeros((B, 4), np.float32)
+        a[np.arange(B), ac[nxt]] = 1
+        r = rw[nxt].astype(np.float32)
+        n = nt[nxt].astype(np.float32)
+        rc = lib.ddq_cpu_full_pass(B, S, P(theta), P(thetaP), P(s), P(a), P(r), P(s2), P(n),
+                                   ctypes.c_float(0.85), P(grad), None, cores)
+        assert rc == 0
+        lib.ddq_cpu_apply(1, ctypes.c_long(theta.size), P(theta), P(grad), P(cache),
+                          int(steps == 0), ctypes.c_float(1e-4), ctypes.c_float(0.9),
+                          ctypes.c_float(1e-8))
+        steps += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(steps / dt, 4), "unit": "updates/s", "cores": cores, "kind": "port",
+            "sample": "%d updates (sample->gather->P/Q fwd->target->Q bwd->rmsprop apply) "
+                      "at B=%d, %dx%d, oracle/ddq_cpu.c im2col+SGEMM fp32, %d OpenMP threads, "
+                      "%.1f s" % (steps, B, S, S, cores, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--frame", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--replay", type=int, default=30000)
+    ap.add_argument("--rule", default="rmsprop")
+    ap.add_argument("--profile-steps", type=int, default=20)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--eager", action="store_true", help="no hipGraph (debug)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(local)
+
+    import ddq
+    B, S = args.batch, args.frame
+    net = ddq.DeepQNet(batch=B, frame=S, device=local)
+    from ddq.params import init_params_flat
+    theta = init_params_flat(S, seed=42)            # identical on every rank
+    net.set_flat(0, theta)
+    net.set_flat(1, theta)
+    net.replay_create(args.replay)
+    fill_replay(net, args.replay, S, seed=1000 + rank)
+    if world > 1:
+        uid = [ddq.DeepQNet.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        net.comm_init(uid[0], world, rank)
+    cfg = net.step_cfg(args.rule, lr=1e-4, target_period=10, allreduce=world > 1,
+                       seed=1234 + rank)
+
+    def run(k):
+        if args.eager:
+            for _ in range(k):
+                net.step(cfg)
+        else:
+            net.step_graph(cfg, k)
+
+    run(args.warmup)
+    net.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(args.steps)
+    net.synchronize()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    loss = float(net.blob("loss"))
+
+    # per-kernel device times (HIP events on the ctx stream), averaged
+    prof = {}
+    for _ in range(args.profile_steps):
+        for name, us in net.profile_step(cfg):
+            prof.setdefault(name, []).append(us)
+    avg = {k: float(np.mean(v)) for k, v in prof.items()}
+    flops = kernel_flops(B, S)
+    dom = max((k for k in avg if k in flops), key=lambda k: avg[k])
+    achieved = flops[dom] / (avg[dom] * 1e-6) / 1e12
+    step_flops = net.step_flops()
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(world * args.steps / dt, 2),
+            "unit": "updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (random-policy Snake frames, Gaussian-init weights seed 42)",
+            "config": {"workload": "deepq Snake DQN step, batch 32/GPU, 4-frame %dx%d, "
+                                   "%d-slot HBM replay, %s apply, target sync every 10"
+                                   % (S, S, args.replay, args.rule),
+                       "global_batch": B * world, "frame": S,
+                       "parallelism": "dp%d" % world, "graph": not args.eager},
+            "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3),
+                         "peak": F32_MFMA_PEAK / 1e12, "unit": "TFLOP/s",
+                         "frac": round(achieved * 1e12 / F32_MFMA_PEAK, 4), "traffic": None,
+                         "kernel_us": round(avg[dom], 3),
+                         "step_tflops": round(step_flops / (dt / args.steps) / 1e12, 3),
+                         "step_frac": round(step_flops / (dt / args.steps) / F32_MFMA_PEAK, 4)},
+            "kernels_us": {k: round(v, 2) for k, v in avg.items()},
+            "final_loss": loss,
+        }
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(B, S, seed=7)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    net.close()
+
+
+if __name__ == "__main__":
+    main()

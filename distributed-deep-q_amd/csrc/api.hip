@@ -1,0 +1,797 @@
+// libddq_hip C-ABI (include/ddq_hip.h): context, device memory, replay ring,
+// step orchestration, hipGraph capture, RCCL gradient exchange.
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/ddq_hip.h"
+#include "kernels.h"
+
+namespace ddq {
+int fc4_splits_for(int S);
+int wgrad_splits_for(int layer, int B, int S, int* np);
+}  // namespace ddq
+
+using namespace ddq;
+
+static thread_local std::string g_last_error;
+
+struct ddq_ctx {
+  int device = 0;
+  ddq_net_desc desc{};
+  hipStream_t stream = nullptr;
+  bool own_stream = true;
+  NetBuffers nb{};
+  std::vector<void*> allocs;
+  std::string err;
+  // replay ring
+  uint8_t* r_state = nullptr;
+  uint8_t* r_action = nullptr;
+  int16_t* r_reward = nullptr;
+  uint8_t* r_nonterm = nullptr;
+  ReplayMeta* r_meta = nullptr;    // device
+  int64_t head = 0, valid = 0, capacity = 0;
+  // acting scratch
+  uint8_t* act_u8 = nullptr;
+  float *act_in = nullptr, *act_p1 = nullptr, *act_p2 = nullptr, *act_p3 = nullptr;
+  float *act_h4 = nullptr, *act_part = nullptr, *act_q = nullptr;
+  int32_t* act_out = nullptr;
+  // comm
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+  // graph
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t gexec = nullptr;
+  ddq_step_cfg gcfg{};
+  bool have_graph = false;
+  int64_t steps = 0;
+  // profiling marks
+  std::vector<std::pair<std::string, hipEvent_t>> marks;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+};
+
+static int fail(ddq_ctx* c, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  g_last_error = buf;
+  return code;
+}
+
+#define HIP_TRY(c, x)                                                                         \
+  do {                                                                                        \
+    hipError_t e_ = (x);                                                                      \
+    if (e_ != hipSuccess)                                                                     \
+      return fail((c), DDQ_EHIP, "%s failed: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, \
+                  __LINE__);                                                                  \
+  } while (0)
+
+#define NCCL_TRY(c, x)                                                                           \
+  do {                                                                                           \
+    ncclResult_t r_ = (x);                                                                       \
+    if (r_ != ncclSuccess) return fail((c), DDQ_ERCCL, "%s failed: %s", #x, ncclGetErrorString(r_)); \
+  } while (0)
+
+template <class T>
+static int dalloc(ddq_ctx* c, T** p, size_t count) {
+  void* q = nullptr;
+  const size_t bytes = std::max<size_t>(count * sizeof(T), 16);
+  hipError_t e = hipMalloc(&q, bytes);
+  if (e != hipSuccess) return fail(c, DDQ_ENOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+  e = hipMemset(q, 0, bytes);
+  if (e != hipSuccess) return fail(c, DDQ_EHIP, "hipMemset failed: %s", hipGetErrorString(e));
+  c->allocs.push_back(q);
+  *p = reinterpret_cast<T*>(q);
+  return DDQ_OK;
+}
+
+#define TRY(x)                \
+  do {                        \
+    int r_ = (x);             \
+    if (r_ != DDQ_OK) return r_; \
+  } while (0)
+
+static int set_dev(ddq_ctx* c) {
+  HIP_TRY(c, hipSetDevice(c->device));
+  return DDQ_OK;
+}
+
+static void invalidate_graph(ddq_ctx* c) {
+  if (c->gexec) hipGraphExecDestroy(c->gexec);
+  if (c->graph) hipGraphDestroy(c->graph);
+  c->gexec = nullptr;
+  c->graph = nullptr;
+  c->have_graph = false;
+}
+
+extern "C" {
+
+int ddq_abi_version(void) { return DDQ_ABI_VERSION; }
+
+const char* ddq_last_error(const ddq_ctx* ctx) {
+  return ctx ? ctx->err.c_str() : g_last_error.c_str();
+}
+
+int ddq_create(ddq_ctx** out, int device, const ddq_net_desc* desc) {
+  if (!out || !desc) return fail(nullptr, DDQ_EINVAL, "null argument");
+  *out = nullptr;
+  if (desc->channels != 4 || desc->actions != 4)
+    return fail(nullptr, DDQ_EINVAL, "channels and actions must be 4 (got %d, %d)",
+                desc->channels, desc->actions);
+  if (desc->frame < 16 || desc->frame % 8 != 0 || desc->frame > 1024)
+    return fail(nullptr, DDQ_EINVAL, "frame side must be a multiple of 8 in [16,1024] (got %d)",
+                desc->frame);
+  if (desc->batch < 1 || desc->batch > 1024)
+    return fail(nullptr, DDQ_EINVAL, "batch must be in [1,1024] (got %d)", desc->batch);
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev == 0)
+    return fail(nullptr, DDQ_EHIP, "no HIP device available (%s)", hipGetErrorString(e));
+  if (device < 0 || device >= ndev)
+    return fail(nullptr, DDQ_EINVAL, "device %d out of range (%d devices)", device, ndev);
+  ddq_ctx* c = new ddq_ctx();
+  c->device = device;
+  c->desc = *desc;
+  int rc = [&]() -> int {
+    TRY(set_dev(c));
+    HIP_TRY(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    NetBuffers& nb = c->nb;
+    const int B = desc->batch, S = desc->frame;
+    nb.B = B; nb.S = S; nb.gamma = desc->gamma;
+    nb.L = make_layout(S);
+    const int64_t P = nb.L.total;
+    const int S2 = S / 2, S3 = S / 4, S4 = S / 8;
+    TRY(dalloc(c, &nb.state, (size_t)B * S * S * 4));
+    TRY(dalloc(c, &nb.next_state, (size_t)B * S * S * 4));
+    TRY(dalloc(c, &nb.action, (size_t)B * 4));
+    TRY(dalloc(c, &nb.reward, (size_t)B));
+    TRY(dalloc(c, &nb.nonterm, (size_t)B));
+    TRY(dalloc(c, &nb.idx, (size_t)B));
+    for (int z = 0; z < 2; ++z) {
+      TRY(dalloc(c, &nb.pool1[z], (size_t)B * S2 * S2 * 32));
+      TRY(dalloc(c, &nb.pool2[z], (size_t)B * S3 * S3 * 64));
+      TRY(dalloc(c, &nb.pool3[z], (size_t)B * S4 * S4 * 64));
+      TRY(dalloc(c, &nb.h4[z], (size_t)B * 512));
+      TRY(dalloc(c, &nb.theta[z], (size_t)P));
+      TRY(dalloc(c, &nb.wk[z], (size_t)nb.L.wk_total));
+    }
+    TRY(dalloc(c, &nb.mask1, (size_t)B * S2 * S2 * 32));
+    TRY(dalloc(c, &nb.mask2, (size_t)B * S3 * S3 * 64));
+    TRY(dalloc(c, &nb.mask3, (size_t)B * S4 * S4 * 64));
+    nb.fc4_splits = fc4_splits_for(S);
+    TRY(dalloc(c, &nb.fc4_part, (size_t)nb.fc4_splits * 2 * B * 512));
+    TRY(dalloc(c, &nb.q_out, (size_t)B * 4));
+    TRY(dalloc(c, &nb.p_out, (size_t)B * 4));
+    TRY(dalloc(c, &nb.q_sa, (size_t)B));
+    TRY(dalloc(c, &nb.p_sa, (size_t)B));
+    TRY(dalloc(c, &nb.target, (size_t)B));
+    TRY(dalloc(c, &nb.loss, 1));
+    TRY(dalloc(c, &nb.dh4, (size_t)B * 512));
+    TRY(dalloc(c, &nb.dconv3, (size_t)B * S3 * S3 * 64));
+    TRY(dalloc(c, &nb.dconv2, (size_t)B * S2 * S2 * 64));
+    TRY(dalloc(c, &nb.dconv1, (size_t)B * S * S * 32));
+    int64_t off = 0;
+    const int cout[3] = {32, 64, 64};
+    for (int l = 0; l < 3; ++l) {
+      nb.wsplits[l] = wgrad_splits_for(l, B, S, &nb.wnp[l]);
+      nb.wpart_off[l] = off;
+      off += (int64_t)nb.wsplits[l] * cout[l] * nb.wnp[l];
+    }
+    TRY(dalloc(c, &nb.wpart, (size_t)off));
+    TRY(dalloc(c, &nb.grad, (size_t)P));
+    TRY(dalloc(c, &nb.opt, (size_t)P));
+    TRY(dalloc(c, &nb.opt_init, 4));
+    TRY(dalloc(c, &nb.iter, 1));
+    // acting scratch (n <= B)
+    TRY(dalloc(c, &c->act_u8, (size_t)B * 4 * S * S));
+    TRY(dalloc(c, &c->act_in, (size_t)B * S * S * 4));
+    TRY(dalloc(c, &c->act_p1, (size_t)B * S2 * S2 * 32));
+    TRY(dalloc(c, &c->act_p2, (size_t)B * S3 * S3 * 64));
+    TRY(dalloc(c, &c->act_p3, (size_t)B * S4 * S4 * 64));
+    TRY(dalloc(c, &c->act_h4, (size_t)B * 512));
+    TRY(dalloc(c, &c->act_part, (size_t)nb.fc4_splits * 2 * B * 512));
+    TRY(dalloc(c, &c->act_q, (size_t)B * 4));
+    TRY(dalloc(c, &c->act_out, (size_t)B));
+    TRY(dalloc(c, &c->r_meta, 1));
+    return DDQ_OK;
+  }();
+  if (rc != DDQ_OK) {
+    g_last_error = c->err;
+    ddq_destroy(c);
+    return rc;
+  }
+  *out = c;
+  return DDQ_OK;
+}
+
+int ddq_destroy(ddq_ctx* c) {
+  if (!c) return DDQ_OK;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  invalidate_graph(c);
+  for (auto& e : c->ev_pool) hipEventDestroy(e);
+  if (c->comm) ncclCommDestroy(c->comm);
+  for (void* p : c->allocs) hipFree(p);
+  if (c->stream && c->own_stream) hipStreamDestroy(c->stream);
+  delete c;
+  return DDQ_OK;
+}
+
+int ddq_set_stream(ddq_ctx* c, void* s) {
+  if (!c) return fail(nullptr, DDQ_EINVAL, "null ctx");
+  TRY(set_dev(c));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (c->own_stream) hipStreamDestroy(c->stream);
+  if (s) {
+    c->stream = reinterpret_cast<hipStream_t>(s);
+    c->own_stream = false;
+  } else {
+    HIP_TRY(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    c->own_stream = true;
+  }
+  invalidate_graph(c);
+  return DDQ_OK;
+}
+
+int ddq_synchronize(ddq_ctx* c) {
+  if (!c) return fail(nullptr, DDQ_EINVAL, "null ctx");
+  TRY(set_dev(c));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return DDQ_OK;
+}
+
+// ---------------- parameters ----------------
+int64_t ddq_num_params(const ddq_ctx* c) { return c ? c->nb.L.total : -1; }
+
+int ddq_param_layout(const ddq_ctx* c, ddq_blob_desc* out, int32_t cap, int32_t* n) {
+  if (!c || !n) return fail(nullptr, DDQ_EINVAL, "null argument");
+  const ParamLayout& L = c->nb.L;
+  const char* names[5] = {"Qconv1", "Qconv2", "Qconv3", "Qfc4", "Q_out"};
+  const int cout[3] = {32, 64, 64}, cin[3] = {4, 32, 64}, ks[3] = {7, 5, 3};
+  *n = 10;
+  if (!out) return DDQ_OK;
+  if (cap < 10) return fail(const_cast<ddq_ctx*>(c), DDQ_EINVAL, "layout needs 10 entries");
+  for (int l = 0; l < 5; ++l) {
+    for (int i = 0; i < 2; ++i) {
+      ddq_blob_desc& d = out[2 * l + i];
+      memset(&d, 0, sizeof(d));
+      snprintf(d.name, sizeof(d.name), "%s", names[l]);
+      d.index = i;
+      if (i == 0) {
+        if (l < 3) { d.shape[0] = cout[l]; d.shape[1] = cin[l]; d.shape[2] = ks[l]; d.shape[3] = ks[l]; }
+        else { d.shape[0] = 1; d.shape[1] = 1; d.shape[2] = l == 3 ? 512 : 4;
+               d.shape[3] = l == 3 ? (int)(64 * L.S4 * L.S4) : 512; }
+        d.offset = L.w[l]; d.count = L.wn[l];
+      } else {
+        d.shape[0] = 1; d.shape[1] = 1; d.shape[2] = 1; d.shape[3] = (int)L.bn[l];
+        d.offset = L.b[l]; d.count = L.bn[l];
+      }
+    }
+  }
+  return DDQ_OK;
+}
+
+static int copy_in(ddq_ctx* c, float* dst, const float* src, int64_t n, int on_dev) {
+  HIP_TRY(c, hipMemcpyAsync(dst, src, n * sizeof(float),
+                            on_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->stream));
+  return DDQ_OK;
+}
+static int copy_out(ddq_ctx* c, float* dst, const float* src, int64_t n, int on_dev) {
+  HIP_TRY(c, hipMemcpyAsync(dst, src, n * sizeof(float),
+                            on_dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return DDQ_OK;
+}
+
+int ddq_set_params(ddq_ctx* c, int32_t which, const float* src, int64_t n, int32_t on_dev) {
+  if (!c || !src) return fail(c, DDQ_EINVAL, "null argument");
+  if (which != 0 && which != 1) return fail(c, DDQ_EINVAL, "which must be 0 (Q) or 1 (P)");
+  if (n != c->nb.L.total)
+    return fail(c, DDQ_EINVAL, "expected %lld params, got %lld", (long long)c->nb.L.total, (long long)n);
+  TRY(set_dev(c));
+  TRY(copy_in(c, c->nb.theta[which], src, n, on_dev));
+  HIP_TRY(c, launch_relayout(c->nb, which, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return DDQ_OK;
+}
+
+int ddq_get_params(ddq_ctx* c, int32_t which, float* dst, int64_t n, int32_t on_dev) {
+  if (!c || !dst) return fail(c, DDQ_EINVAL, "null argument");
+  if (which != 0 && which != 1) return fail(c, DDQ_EINVAL, "which must be 0 (Q) or 1 (P)");
+  if (n != c->nb.L.total) return fail(c, DDQ_EINVAL, "size mismatch");
+  TRY(set_dev(c));
+  return copy_out(c, dst, c->nb.theta[which], n, on_dev);
+}
+
+int ddq_get_grads(ddq_ctx* c, float* dst, int64_t n, int32_t on_dev) {
+  if (!c || !dst) return fail(c, DDQ_EINVAL, "null argument");
+  if (n != c->nb.L.total) return fail(c, DDQ_EINVAL, "size mismatch");
+  TRY(set_dev(c));
+  return copy_out(c, dst, c->nb.grad, n, on_dev);
+}
+
+int ddq_set_grads(ddq_ctx* c, const float* src, int64_t n, int32_t on_dev) {
+  if (!c || !src) return fail(c, DDQ_EINVAL, "null argument");
+  if (n != c->nb.L.total) return fail(c, DDQ_EINVAL, "size mismatch");
+  TRY(set_dev(c));
+  TRY(copy_in(c, c->nb.grad, src, n, on_dev));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return DDQ_OK;
+}
+
+int ddq_sync_target(ddq_ctx* c) {
+  if (!c) return fail(nullptr, DDQ_EINVAL, "null ctx");
+  TRY(set_dev(c));
+  HIP_TRY(c, hipMemcpyAsync(c->nb.theta[1], c->nb.theta[0], c->nb.L.total * 4,
+                            hipMemcpyDeviceToDevice, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(c->nb.wk[1], c->nb.wk[0], c->nb.L.wk_total * 4,
+                            hipMemcpyDeviceToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return DDQ_OK;
+}
+
+// ---------------- replay ----------------
+static int push_meta(ddq_ctx* c) {
+  int64_t hv[2] = {c->head, c->valid};
+  HIP_TRY(c, hipMemcpyAsync(c->r_meta, hv, sizeof(hv), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return DDQ_OK;
+}
+
+int ddq_replay_create(ddq_ctx* c, int64_t capacity) {
+  if (!c) return fail(nullptr, DDQ_EINVAL, "null ctx");
+  if (capacity < 2 || capacity > (int64_t)INT32_MAX)
+    return fail(c, DDQ_EINVAL, "capacity must be in [2, 2^31) (got %lld)", (long long)capacity);
+  if (c->r_state) return fail(c, DDQ_ESTATE, "replay already created");
+  TRY(set_dev(c));
+  const size_t slot = (size_t)4 * c->nb.S * c->nb.S;
+  TRY(dalloc(c, &c->r_state, slot * capacity));
+  TRY(dalloc(c, &c->r_action, (size_t)capacity));
+  TRY(dalloc(c, &c->r_reward, (size_t)capacity));
+  TRY(dalloc(c, &c->r_nonterm, (size_t)capacity));
+  c->capacity = capacity;
+  c->head = c->valid = 0;
+  ReplayMeta m{};
+  m.capacity = capacity;
+  HIP_TRY(c, hipMemcpy(c->r_meta, &m, sizeof(m), hipMemcpyHostToDevice));
+  invalidate_graph(c);
+  return DDQ_OK;
+}
+
+int ddq_replay_add(ddq_ctx* c, int32_t action, int32_t reward, const uint8_t* state) {
+  if (!c) return fail(nullptr, DDQ_EINVAL, "null ctx");
+  if (!c->r_state) return fail(c, DDQ_ESTATE, "no replay buffer (call ddq_replay_create)");
+  if (action < 0 || action > 255) return fail(c, DDQ_EINVAL, "action must fit uint8");
+  if (reward < -32768 || reward > 32767) return fail(c, DDQ_EINVAL, "reward must fit int16");
+  TRY(set_dev(c));
+  const size_t slot = (size_t)4 * c->nb.S * c->nb.S;
+  const int64_t h = c->head;
+  uint8_t a = (uint8_t)action, nt = state ? 1 : 0;
+  int16_t r = (int16_t)reward;
+  HIP_TRY(c, hipMemcpyAsync(c->r_action + h, &a, 1, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(c->r_reward + h, &r, 2, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(c->r_nonterm + h, &nt, 1, hipMemcpyHostToDevice, c->stream));
+  if (state)
+    HIP_TRY(c, hipMemcpyAsync(c->r_state + h * slot, state, slot, hipMemcpyHostToDevice, c->stream));
+  c->head = (c->head + 1) % c->capacity;
+  c->valid = std::min(c->capacity, c->valid + 1);
+  return push_meta(c);
+}
+
+int ddq_replay_info(const ddq_ctx* c, int64_t* head, int64_t* valid, int64_t* capacity) {
+  if (!c) return fail(nullptr, DDQ_EINVAL, "null ctx");
+  if (head) *head = c->head;
+  if (valid) *valid = c->valid;
+  if (capacity) *capacity = c->capacity;
+  return DDQ_OK;
+}
+
+int ddq_replay_import(ddq_ctx* c, const uint8_t* state, const uint8_t* action,
+                      const int16_t* reward, const uint8_t* nonterm, int64_t n, int64_t head,
+                      int64_t valid) {
+  if (!c || !state || !action || !reward || !nonterm) return fail(c, DDQ_EINVAL, "null argument");
+  if (!c->r_state) return fail(c, DDQ_ESTATE, "no replay buffer");
+  if (n != c->capacity) return fail(c, DDQ_EINVAL, "import size %lld != capacity %lld",
+                                    (long long)n, (long long)c->capacity);
+  if (head < 0 || head >= n || valid < 0 || valid > n)
+    return fail(c, DDQ_EINVAL, "head/valid out of range");
+  TRY(set_dev(c));
+  const size_t slot = (size_t)4 * c->nb.S * c->nb.S;
+  HIP_TRY(c, hipMemcpy(c->r_state, state, slot * n, hipMemcpyHostToDevice));
+  HIP_TRY(c, hipMemcpy(c->r_action, action, n, hipMemcpyHostToDevice));
+  HIP_TRY(c, hipMemcpy(c->r_reward, reward, 2 * n, hipMemcpyHostToDevice));
+  HIP_TRY(c, hipMemcpy(c->r_nonterm, nonterm, n, hipMemcpyHostToDevice));
+  c->head = head;
+  c->valid = valid;
+  return push_meta(c);
+}
+
+int ddq_replay_export(ddq_ctx* c, uint8_t* state, uint8_t* action, int16_t* reward,
+                      uint8_t* nonterm, int64_t n) {
+  if (!c) return fail(nullptr, DDQ_EINVAL, "null ctx");
+  if (!c->r_state) return fail(c, DDQ_ESTATE, "no replay buffer");
+  if (n != c->capacity) return fail(c, DDQ_EINVAL, "export size mismatch");
+  TRY(set_dev(c));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  const size_t slot = (size_t)4 * c->nb.S * c->nb.S;
+  if (state) HIP_TRY(c, hipMemcpy(state, c->r_state, slot * n, hipMemcpyDeviceToHost));
+  if (action) HIP_TRY(c, hipMemcpy(action, c->r_action, n, hipMemcpyDeviceToHost));
+  if (reward) HIP_TRY(c, hipMemcpy(reward, c->r_reward, 2 * n, hipMemcpyDeviceToHost));
+  if (nonterm) HIP_TRY(c, hipMemcpy(nonterm, c->r_nonterm, n, hipMemcpyDeviceToHost));
+  return DDQ_OK;
+}
+
+static int check_err_flag(ddq_ctx* c) {
+  ReplayMeta m;
+  HIP_TRY(c, hipMemcpyAsync(&m, c->r_meta, sizeof(m), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (m.err) {
+    int32_t z = 0;
+    HIP_TRY(c, hipMemcpy(reinterpret_cast<char*>(c->r_meta) + offsetof(ReplayMeta, err), &z, 4,
+                         hipMemcpyHostToDevice));
+    return fail(c, DDQ_ERANGE, "stored action index out of range for %d actions", 4);
+  }
+  return DDQ_OK;
+}
+
+int ddq_replay_sample(ddq_ctx* c, const int32_t* idx, int32_t batch) {
+  if (!c || !idx) return fail(c, DDQ_EINVAL, "null argument");
+  if (!c->r_state) return fail(c, DDQ_ESTATE, "no replay buffer");
+  if (batch >= c->valid)
+    return fail(c, DDQ_EINVAL, "Can't draw sample of size %d from replay dataset of size %lld",
+                batch, (long long)c->valid);
+  if (batch != c->nb.B)
+    return fail(c, DDQ_EINVAL, "sample size %d != net batch %d", batch, c->nb.B);
+  for (int i = 0; i < batch; ++i) {
+    if (idx[i] < 0 || idx[i] >= c->valid) return fail(c, DDQ_EINVAL, "index %d out of [0,valid)", idx[i]);
+    if (i && idx[i] <= idx[i - 1]) return fail(c, DDQ_EINVAL, "indices must be sorted and distinct");
+  }
+  TRY(set_dev(c));
+  HIP_TRY(c, hipMemcpyAsync(c->nb.idx, idx, batch * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, launch_gather(c->nb, c->r_state, c->r_action, c->r_reward, c->r_nonterm, c->r_meta,
+                           c->stream));
+  return check_err_flag(c);
+}
+
+int ddq_replay_sample_device_async(ddq_ctx* c, uint64_t seed) {
+  if (!c) return fail(nullptr, DDQ_EINVAL, "null ctx");
+  if (!c->r_state) return fail(c, DDQ_ESTATE, "no replay buffer");
+  if (c->nb.B >= c->valid)
+    return fail(c, DDQ_EINVAL, "Can't draw sample of size %d from replay dataset of size %lld",
+                c->nb.B, (long long)c->valid);
+  TRY(set_dev(c));
+  HIP_TRY(c, launch_sample(c->nb, c->r_meta, seed, c->stream));
+  HIP_TRY(c, launch_gather(c->nb, c->r_state, c->r_action, c->r_reward, c->r_nonterm, c->r_meta,
+                           c->stream));
+  return DDQ_OK;
+}
+
+int ddq_read_indices(ddq_ctx* c, int32_t* idx, int32_t batch) {
+  if (!c || !idx || batch != c->nb.B) return fail(c, DDQ_EINVAL, "bad argument");
+  TRY(set_dev(c));
+  HIP_TRY(c, hipMemcpyAsync(idx, c->nb.idx, batch * 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return DDQ_OK;
+}
+
+int ddq_read_minibatch(ddq_ctx* c, float* state, float* action, float* reward, float* next_state,
+                       float* nonterm) {
+  if (!c) return fail(nullptr, DDQ_EINVAL, "null ctx");
+  TRY(set_dev(c));
+  const int B = c->nb.B, SS = c->nb.S * c->nb.S;
+  std::vector<float> tmp((size_t)B * SS * 4);
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  for (int which = 0; which < 2; ++which) {
+    float* dst = which ? next_state : state;
+    if (!dst) continue;
+    HIP_TRY(c, hipMemcpy(tmp.data(), which ? c->nb.next_state : c->nb.state, tmp.size() * 4,
+                         hipMemcpyDeviceToHost));
+    for (int b = 0; b < B; ++b)
+      for (int ch = 0; ch < 4; ++ch)
+        for (int p = 0; p < SS; ++p)
+          dst[((size_t)b * 4 + ch) * SS + p] = tmp[((size_t)b * SS + p) * 4 + ch];
+  }
+  if (action) HIP_TRY(c, hipMemcpy(action, c->nb.action, B * 16, hipMemcpyDeviceToHost));
+  if (reward) HIP_TRY(c, hipMemcpy(reward, c->nb.reward, B * 4, hipMemcpyDeviceToHost));
+  if (nonterm) HIP_TRY(c, hipMemcpy(nonterm, c->nb.nonterm, B * 4, hipMemcpyDeviceToHost));
+  return DDQ_OK;
+}
+
+int ddq_write_minibatch(ddq_ctx* c, const float* state, const float* action, const float* reward,
+                        const float* next_state, const float* nonterm) {
+  if (!c) return fail(nullptr, DDQ_EINVAL, "null ctx");
+  TRY(set_dev(c));
+  const int B = c->nb.B, SS = c->nb.S * c->nb.S;
+  std::vector<float> tmp((size_t)B * SS * 4);
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  for (int which = 0; which < 2; ++which) {
+    const float* src = which ? next_state : state;
+    if (!src) continue;
+    for (int b = 0; b < B; ++b)
+      for (int ch = 0; ch < 4; ++ch)
+        for (int p = 0; p < SS; ++p)
+          tmp[((size_t)b * SS + p) * 4 + ch] = src[((size_t)b * 4 + ch) * SS + p];
+    HIP_TRY(c, hipMemcpy(which ? c->nb.next_state : c->nb.state, tmp.data(), tmp.size() * 4,
+                         hipMemcpyHostToDevice));
+  }
+  if (action) HIP_TRY(c, hipMemcpy(c->nb.action, action, B * 16, hipMemcpyHostToDevice));
+  if (reward) HIP_TRY(c, hipMemcpy(c->nb.reward, reward, B * 4, hipMemcpyHostToDevice));
+  if (nonterm) HIP_TRY(c, hipMemcpy(c->nb.nonterm, nonterm, B * 4, hipMemcpyHostToDevice));
+  return DDQ_OK;
+}
+
+// ---------------- compute ----------------
+static int enqueue_fwd_bwd(ddq_ctx* c, void (*mark)(void*, const char*), void* marg) {
+  HIP_TRY(c, launch_forward(c->nb, 2, c->stream, mark, marg));
+  if (mark) mark(marg, "head");
+  HIP_TRY(c, launch_head(c->nb, c->stream));
+  HIP_TRY(c, launch_backward(c->nb, c->stream, mark, marg));
+  return DDQ_OK;
+}
+
+int ddq_forward_backward_async(ddq_ctx* c) {
+  if (!c) return fail(nullptr, DDQ_EINVAL, "null ctx");
+  TRY(set_dev(c));
+  return enqueue_fwd_bwd(c, nullptr, nullptr);
+}
+
+int ddq_forward_backward(ddq_ctx* c, float* loss) {
+  TRY(ddq_forward_backward_async(c));
+  if (loss) return copy_out(c, loss, c->nb.loss, 1, 0);
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return DDQ_OK;
+}
+
+int ddq_forward_q(ddq_ctx* c) {
+  if (!c) return fail(nullptr, DDQ_EINVAL, "null ctx");
+  TRY(set_dev(c));
+  HIP_TRY(c, launch_act(c->nb, c->nb.state, c->nb.B, c->act_p1, c->act_p2, c->act_p3, c->act_h4,
+                        c->act_part, c->nb.q_out, nullptr, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return DDQ_OK;
+}
+
+int ddq_read_blob(ddq_ctx* c, const char* name, float* dst, int64_t n) {
+  if (!c || !name || !dst) return fail(c, DDQ_EINVAL, "null argument");
+  const int B = c->nb.B;
+  struct { const char* nm; float* p; int64_t cnt; } t[] = {
+      {"Q_out", c->nb.q_out, 4ll * B}, {"P_out", c->nb.p_out, 4ll * B},
+      {"Q_sa", c->nb.q_sa, B},         {"P_sa", c->nb.p_sa, B},
+      {"target_Q_sa", c->nb.target, B}, {"loss", c->nb.loss, 1}};
+  for (auto& e : t) {
+    if (strcmp(e.nm, name) == 0) {
+      if (n != e.cnt) return fail(c, DDQ_EINVAL, "blob %s has %lld elements", name, (long long)e.cnt);
+      TRY(set_dev(c));
+      return copy_out(c, dst, e.p, n, 0);
+    }
+  }
+  return fail(c, DDQ_EINVAL, "unknown blob '%s'", name);
+}
+
+int ddq_read_pool_mask(ddq_ctx* c, int32_t layer, uint8_t* dst, int64_t n) {
+  if (!c || !dst) return fail(c, DDQ_EINVAL, "null argument");
+  if (layer < 1 || layer > 3) return fail(c, DDQ_EINVAL, "layer must be 1..3");
+  const int B = c->nb.B, C = layer == 1 ? 32 : 64, Hp = c->nb.S >> layer;
+  const int64_t cnt = (int64_t)B * C * Hp * Hp;
+  if (n != cnt) return fail(c, DDQ_EINVAL, "mask %d has %lld elements", layer, (long long)cnt);
+  TRY(set_dev(c));
+  std::vector<uint8_t> tmp(cnt);
+  const uint8_t* src = layer == 1 ? c->nb.mask1 : (layer == 2 ? c->nb.mask2 : c->nb.mask3);
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  HIP_TRY(c, hipMemcpy(tmp.data(), src, cnt, hipMemcpyDeviceToHost));
+  for (int b = 0; b < B; ++b)
+    for (int ch = 0; ch < C; ++ch)
+      for (int p = 0; p < Hp * Hp; ++p)
+        dst[((size_t)b * C + ch) * Hp * Hp + p] = tmp[((size_t)b * Hp * Hp + p) * C + ch];
+  return DDQ_OK;
+}
+
+int ddq_select_action(ddq_ctx* c, const uint8_t* states, int32_t n, int32_t* actions) {
+  if (!c || !states || !actions) return fail(c, DDQ_EINVAL, "null argument");
+  if (n < 1 || n > c->nb.B) return fail(c, DDQ_EINVAL, "n must be in [1,B]");
+  TRY(set_dev(c));
+  const size_t bytes = (size_t)n * 4 * c->nb.S * c->nb.S;
+  HIP_TRY(c, hipMemcpyAsync(c->act_u8, states, bytes, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, launch_u8_to_nhwc(c->act_u8, n, c->nb.S, c->act_in, c->stream));
+  HIP_TRY(c, launch_act(c->nb, c->act_in, n, c->act_p1, c->act_p2, c->act_p3, c->act_h4,
+                        c->act_part, c->act_q, c->act_out, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(actions, c->act_out, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return DDQ_OK;
+}
+
+// ---------------- apply ----------------
+static int check_cfg(ddq_ctx* c, const ddq_update_cfg* u) {
+  if (!u) return fail(c, DDQ_EINVAL, "null update cfg");
+  if (u->rule < 0 || u->rule > 3) return fail(c, DDQ_EINVAL, "unknown update rule %d", u->rule);
+  return DDQ_OK;
+}
+
+int ddq_apply_async(ddq_ctx* c, const ddq_update_cfg* u) {
+  if (!c) return fail(nullptr, DDQ_EINVAL, "null ctx");
+  TRY(check_cfg(c, u));
+  TRY(set_dev(c));
+  HIP_TRY(c, launch_apply(c->nb, u->rule, u->lr, u->decay, u->eps, u->momentum, u->weight_decay,
+                          c->stream));
+  return DDQ_OK;
+}
+
+int ddq_apply(ddq_ctx* c, const ddq_update_cfg* u) {
+  TRY(ddq_apply_async(c, u));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return DDQ_OK;
+}
+
+int ddq_reset_optimizer(ddq_ctx* c) {
+  if (!c) return fail(nullptr, DDQ_EINVAL, "null ctx");
+  TRY(set_dev(c));
+  HIP_TRY(c, hipMemsetAsync(c->nb.opt, 0, c->nb.L.total * 4, c->stream));
+  HIP_TRY(c, hipMemsetAsync(c->nb.opt_init, 0, 4, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return DDQ_OK;
+}
+
+int ddq_get_optimizer_state(ddq_ctx* c, float* dst, int64_t n) {
+  if (!c || !dst) return fail(c, DDQ_EINVAL, "null argument");
+  if (n != c->nb.L.total) return fail(c, DDQ_EINVAL, "size mismatch");
+  TRY(set_dev(c));
+  return copy_out(c, dst, c->nb.opt, n, 0);
+}
+
+// ---------------- comm ----------------
+int ddq_comm_get_unique_id(uint8_t id[128]) {
+  static_assert(sizeof(ncclUniqueId) == 128, "unique id size");
+  ncclUniqueId u;
+  ncclResult_t r = ncclGetUniqueId(&u);
+  if (r != ncclSuccess) return fail(nullptr, DDQ_ERCCL, "ncclGetUniqueId: %s", ncclGetErrorString(r));
+  memcpy(id, &u, 128);
+  return DDQ_OK;
+}
+
+int ddq_comm_init(ddq_ctx* c, const uint8_t id[128], int32_t nranks, int32_t rank) {
+  if (!c || !id) return fail(c, DDQ_EINVAL, "null argument");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(c, DDQ_EINVAL, "bad rank/nranks");
+  TRY(set_dev(c));
+  if (c->comm) ncclCommDestroy(c->comm);
+  ncclUniqueId u;
+  memcpy(&u, id, 128);
+  NCCL_TRY(c, ncclCommInitRank(&c->comm, nranks, u, rank));
+  c->nranks = nranks;
+  c->rank = rank;
+  invalidate_graph(c);
+  return DDQ_OK;
+}
+
+int ddq_allreduce_grads_async(ddq_ctx* c) {
+  if (!c) return fail(nullptr, DDQ_EINVAL, "null ctx");
+  if (!c->comm) return fail(c, DDQ_ESTATE, "no communicator (call ddq_comm_init)");
+  TRY(set_dev(c));
+  NCCL_TRY(c, ncclAllReduce(c->nb.grad, c->nb.grad, (size_t)c->nb.L.total, ncclFloat, ncclSum,
+                            c->comm, c->stream));
+  return DDQ_OK;
+}
+
+int ddq_allreduce_grads(ddq_ctx* c) {
+  TRY(ddq_allreduce_grads_async(c));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return DDQ_OK;
+}
+
+// ---------------- step ----------------
+static int enqueue_step(ddq_ctx* c, const ddq_step_cfg* cfg, void (*mark)(void*, const char*),
+                        void* marg) {
+  if (mark) mark(marg, "target_sync");
+  HIP_TRY(c, launch_target_sync_if(c->nb, cfg->target_period, c->stream));
+  if (mark) mark(marg, "sample");
+  HIP_TRY(c, launch_sample(c->nb, c->r_meta, cfg->seed, c->stream));
+  if (mark) mark(marg, "gather");
+  HIP_TRY(c, launch_gather(c->nb, c->r_state, c->r_action, c->r_reward, c->r_nonterm, c->r_meta,
+                           c->stream));
+  TRY(enqueue_fwd_bwd(c, mark, marg));
+  if (cfg->allreduce && c->nranks > 1) {
+    if (mark) mark(marg, "allreduce");
+    NCCL_TRY(c, ncclAllReduce(c->nb.grad, c->nb.grad, (size_t)c->nb.L.total, ncclFloat, ncclSum,
+                              c->comm, c->stream));
+  }
+  if (mark) mark(marg, "apply");
+  const ddq_update_cfg& u = cfg->update;
+  HIP_TRY(c, launch_apply(c->nb, u.rule, u.lr, u.decay, u.eps, u.momentum, u.weight_decay,
+                          c->stream));
+  return DDQ_OK;
+}
+
+static int check_step(ddq_ctx* c, const ddq_step_cfg* cfg) {
+  if (!c) return fail(nullptr, DDQ_EINVAL, "null ctx");
+  if (!cfg) return fail(c, DDQ_EINVAL, "null step cfg");
+  TRY(check_cfg(c, &cfg->update));
+  if (!c->r_state) return fail(c, DDQ_ESTATE, "no replay buffer");
+  if (c->nb.B >= c->valid)
+    return fail(c, DDQ_EINVAL, "Can't draw sample of size %d from replay dataset of size %lld",
+                c->nb.B, (long long)c->valid);
+  if (cfg->allreduce && c->nranks > 1 && !c->comm) return fail(c, DDQ_ESTATE, "no communicator");
+  return DDQ_OK;
+}
+
+int ddq_step_async(ddq_ctx* c, const ddq_step_cfg* cfg) {
+  TRY(check_step(c, cfg));
+  TRY(set_dev(c));
+  TRY(enqueue_step(c, cfg, nullptr, nullptr));
+  c->steps++;
+  return DDQ_OK;
+}
+
+int ddq_step_graph_async(ddq_ctx* c, const ddq_step_cfg* cfg, int32_t nsteps) {
+  TRY(check_step(c, cfg));
+  TRY(set_dev(c));
+  if (!c->have_graph || memcmp(&c->gcfg, cfg, sizeof(*cfg)) != 0) {
+    invalidate_graph(c);
+    HIP_TRY(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    int rc = enqueue_step(c, cfg, nullptr, nullptr);
+    hipGraph_t g = nullptr;
+    hipError_t e = hipStreamEndCapture(c->stream, &g);
+    if (rc != DDQ_OK) { if (g) hipGraphDestroy(g); return rc; }
+    if (e != hipSuccess) return fail(c, DDQ_EHIP, "hipStreamEndCapture: %s", hipGetErrorString(e));
+    c->graph = g;
+    HIP_TRY(c, hipGraphInstantiate(&c->gexec, c->graph, nullptr, nullptr, 0));
+    c->gcfg = *cfg;
+    c->have_graph = true;
+  }
+  for (int i = 0; i < nsteps; ++i) {
+    HIP_TRY(c, hipGraphLaunch(c->gexec, c->stream));
+    c->steps++;
+  }
+  return DDQ_OK;
+}
+
+int64_t ddq_step_count(const ddq_ctx* c) { return c ? c->steps : -1; }
+
+// ---------------- measurement ----------------
+static void mark_cb(void* arg, const char* name) {
+  ddq_ctx* c = reinterpret_cast<ddq_ctx*>(arg);
+  if (c->ev_used == c->ev_pool.size()) {
+    hipEvent_t e;
+    hipEventCreate(&e);
+    c->ev_pool.push_back(e);
+  }
+  hipEvent_t e = c->ev_pool[c->ev_used++];
+  hipEventRecord(e, c->stream);
+  c->marks.emplace_back(name, e);
+}
+
+int ddq_profile_step(ddq_ctx* c, const ddq_step_cfg* cfg, char* names, float* usec, int32_t cap,
+                     int32_t* n) {
+  TRY(check_step(c, cfg));
+  if (!n) return fail(c, DDQ_EINVAL, "null n");
+  TRY(set_dev(c));
+  c->marks.clear();
+  c->ev_used = 0;
+  TRY(enqueue_step(c, cfg, mark_cb, c));
+  mark_cb(c, "end");
+  c->steps++;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  const int k = (int)c->marks.size() - 1;
+  *n = k;
+  for (int i = 0; i < k && i < cap; ++i) {
+    float ms = 0.f;
+    HIP_TRY(c, hipEventElapsedTime(&ms, c->marks[i].second, c->marks[i + 1].second));
+    if (usec) usec[i] = ms * 1000.f;
+    if (names) {
+      memset(names + 16 * i, 0, 16);
+      strncpy(names + 16 * i, c->marks[i].first.c_str(), 15);
+    }
+  }
+  return DDQ_OK;
+}
+
+double ddq_step_flops(const ddq_ctx* c) { return c ? step_flops(c->nb.B, c->nb.S) : 0.0; }
+
+}  // extern "C"

@@ -1,0 +1,44 @@
+// Shared device helpers for libddq_hip (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+namespace ddq {
+
+constexpr int kWave = 64;          // CDNA wavefront
+constexpr int kActions = 4;        // barista/constants.py:8
+constexpr int kFrames = 4;         // expgain.py:9
+constexpr int kFc4 = 512;          // train_val.prototxt:169
+
+// Division by a runtime constant (multiply-high + shift), exact for
+// 0 <= n < 2^31 (Granlund-Montgomery / Hacker's Delight round-up method).
+struct FastDiv {
+  uint32_t d, mul, shr;
+  FastDiv() = default;
+  __host__ explicit FastDiv(uint32_t divisor) : d(divisor) {
+    if (divisor == 1) { mul = 0; shr = 0; return; }
+    uint32_t l = 0;
+    while ((1ull << l) < divisor) ++l;
+    uint64_t m = ((1ull << 32) * ((1ull << l) - divisor)) / divisor + 1;
+    mul = (uint32_t)m;
+    shr = l - 1;
+  }
+  __device__ __forceinline__ uint32_t div(uint32_t n) const {
+    if (d == 1) return n;
+    uint32_t t = __umulhi(n, mul);
+    return (t + ((n - t) >> 1)) >> shr;
+  }
+  __device__ __forceinline__ void divmod(uint32_t n, uint32_t& q, uint32_t& r) const {
+    q = div(n);
+    r = n - q * d;
+  }
+};
+
+__device__ __forceinline__ float4 f4(float a, float b, float c, float d) {
+  return make_float4(a, b, c, d);
+}
+__device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+
+}  // namespace ddq

@@ -1,0 +1,75 @@
+// Host-side launch wrappers for the deepq step kernels (implemented in
+// kernels.hip).  All launches are asynchronous on the given stream and
+// graph-capture safe (no allocation, no synchronisation).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ddq {
+
+// Flat parameter layout of one tower (pycaffe order), element offsets.
+struct ParamLayout {
+  int S, S2, S3, S4;
+  int64_t w[5], b[5];      // offsets of layer weights / biases
+  int64_t wn[5], bn[5];    // counts
+  int64_t total;
+  int64_t wk_off[3];       // offsets of conv kernel-layout copies in the wk buffer
+  int64_t wk_total;
+};
+ParamLayout make_layout(int S);
+
+// Replay ring bookkeeping kept in device memory so captured graphs see the
+// live head/valid and a fresh RNG counter on every replay.
+struct ReplayMeta {
+  int64_t head, valid, capacity;
+  uint64_t counter;        // device index-stream draws so far
+  int32_t err;             // sticky: stored action >= num_actions seen
+  int32_t pad;
+};
+
+struct NetBuffers {
+  int B, S;
+  // minibatch (NHWC frames; action one-hot (B,4); reward / non_terminal (B))
+  float *state, *next_state, *action, *reward, *nonterm;
+  int32_t* idx;
+  // activations per tower z (0 = Q on state, 1 = P on next_state)
+  float *pool1[2], *pool2[2], *pool3[2], *h4[2];
+  uint8_t *mask1, *mask2, *mask3;   // Q tower only
+  float* fc4_part;                  // [splits][2][B][512]
+  int fc4_splits;
+  // blobs
+  float *q_out, *p_out, *q_sa, *p_sa, *target, *loss;
+  // backward scratch
+  float *dh4, *dconv3, *dconv2, *dconv1;
+  float* wpart;                     // conv wgrad slabs (3 layers, disjoint)
+  int64_t wpart_off[3];
+  int wsplits[3];
+  int wnp[3];
+  // parameters: theta[z] flat Caffe layout; wk[z] conv kernel layout; grad; opt state
+  float *theta[2], *wk[2], *grad, *opt;
+  int32_t* opt_init;                // 0 until the first apply after a reset
+  int64_t* iter;                    // applied updates (param-server iteration)
+  ParamLayout L;
+  float gamma;
+};
+
+hipError_t launch_gather(const NetBuffers& nb, const uint8_t* st, const uint8_t* act,
+                         const int16_t* rew, const uint8_t* nt, ReplayMeta* meta,
+                         hipStream_t s);
+hipError_t launch_sample(const NetBuffers& nb, ReplayMeta* meta, uint64_t seed, hipStream_t s);
+hipError_t launch_target_sync_if(const NetBuffers& nb, int period, hipStream_t s);
+hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s, void (*mark)(void*, const char*), void* mark_arg);
+hipError_t launch_head(const NetBuffers& nb, hipStream_t s);
+hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(void*, const char*), void* mark_arg);
+hipError_t launch_apply(const NetBuffers& nb, int rule, float lr, float decay, float eps,
+                        float momentum, float wd, hipStream_t s);
+hipError_t launch_relayout(const NetBuffers& nb, int z, hipStream_t s);
+// Q-tower forward of n states (NHWC f32 in `in`) into scratch, argmax into out.
+hipError_t launch_act(const NetBuffers& nb, const float* in, int n, float* pool1, float* pool2,
+                      float* pool3, float* h4, float* part, float* qout, int32_t* actions,
+                      hipStream_t s);
+hipError_t launch_u8_to_nhwc(const uint8_t* src, int n, int S, float* dst, hipStream_t s);
+
+double step_flops(int B, int S);
+
+}  // namespace ddq

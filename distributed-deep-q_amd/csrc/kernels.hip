@@ -1,0 +1,709 @@
+// deepq step kernels for MI355X (gfx950).  See DESIGN.md for the data layout
+// and the roofline of each kernel; layers.h for the implicit-GEMM problems.
+#include "kernels.h"
+#include "layers.h"
+
+namespace ddq {
+
+// ---------------------------------------------------------------------------
+// layout
+// ---------------------------------------------------------------------------
+ParamLayout make_layout(int S) {
+  ParamLayout L;
+  L.S = S; L.S2 = S / 2; L.S3 = S / 4; L.S4 = S / 8;
+  const int64_t k4 = 64ll * L.S4 * L.S4;
+  const int64_t wn[5] = {32ll * 4 * 49, 64ll * 32 * 25, 64ll * 64 * 9, 512ll * k4, 4ll * 512};
+  const int64_t bn[5] = {32, 64, 64, 512, 4};
+  int64_t o = 0;
+  for (int i = 0; i < 5; ++i) {
+    L.w[i] = o; L.wn[i] = wn[i]; o += wn[i];
+    L.b[i] = o; L.bn[i] = bn[i]; o += bn[i];
+  }
+  L.total = o;
+  int64_t q = 0;
+  for (int i = 0; i < 3; ++i) { L.wk_off[i] = q; q += wn[i]; }
+  L.wk_total = q;
+  return L;
+}
+
+double step_flops(int B, int S) {
+  // F = B*(6272 S1^2 + 51200 S2^2 + 36864 S3^2 + 32768 S4^2 + 2048)
+  // MACs per tower forward; step = Q fwd + P fwd + Q wgrad + Q dgrad (no conv1 dgrad).
+  const double s1 = S, s2 = S / 2, s3 = S / 4, s4 = S / 8;
+  const double F = (double)B * (6272 * s1 * s1 + 51200 * s2 * s2 + 36864 * s3 * s3 +
+                                32768 * s4 * s4 + 2048);
+  return 2.0 * (4 * F - 6272.0 * B * s1 * s1);
+}
+
+// ---------------------------------------------------------------------------
+// replay: index draw (device RNG) and minibatch gather (replay.py:144-183)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+// One workgroup: B <= 1024 distinct indices, uniform over [0,valid) \ {head-1}
+// (the distribution of replay.py:152-157's whole-list redraw), sorted.
+// Colliding / forbidden draws are redrawn independently each round; the
+// process is symmetric in the population, so the final set is uniform.
+__global__ __launch_bounds__(1024) void sample_kernel(ReplayMeta* meta, int B, uint64_t seed,
+                                                      int32_t* idx_out) {
+  __shared__ int64_t cand[1024];
+  __shared__ int bad_any;
+  const int t = threadIdx.x;
+  const int64_t valid = meta->valid;
+  const int64_t forbid = meta->head - 1;   // -1 when head == 0: nothing forbidden
+  const uint64_t ctr = meta->counter;
+  int P2 = 1;
+  while (P2 < B) P2 <<= 1;
+  auto draw = [&](int round) -> int64_t {
+    uint64_t r = splitmix64(seed ^ splitmix64(ctr * 0x100000001B3ull + (uint64_t)t * 0x9E37ull +
+                                              ((uint64_t)round << 40)));
+    return (int64_t)__umul64hi(r, (uint64_t)valid);
+  };
+  if (t < P2) cand[t] = (t < B) ? draw(0) : INT64_MAX;
+  for (int round = 1; round < 256; ++round) {
+    __syncthreads();
+    // bitonic sort of cand[0..P2)
+    for (int k = 2; k <= P2; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        if (t < P2) {
+          const int p = t ^ j;
+          if (p > t) {
+            const bool up = (t & k) == 0;
+            const int64_t a = cand[t], b = cand[p];
+            if ((a > b) == up) { cand[t] = b; cand[p] = a; }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    if (t == 0) bad_any = 0;
+    __syncthreads();
+    bool bad = false;
+    if (t < B) bad = (cand[t] == forbid) || (t > 0 && cand[t] == cand[t - 1]);
+    if (bad) bad_any = 1;
+    __syncthreads();
+    if (!bad_any) break;
+    if (bad) cand[t] = draw(round);
+  }
+  __syncthreads();
+  if (t < B) idx_out[t] = (int32_t)cand[t];
+  if (t == 0) meta->counter = ctr + 1;
+}
+
+// grid (ceil(S*S/4/256), B, 2): z = 0 -> state from idx, z = 1 -> next_state
+// from next_idx (wrap N-1 -> 0, replay.py:160-166).  u8 (C,H,W) slot -> f32
+// NHWC; the z = 1 blocks with blockIdx.x == 0 also write action one-hot,
+// reward and non_terminal of next_idx (replay.py:172-183).
+__global__ __launch_bounds__(256) void gather_kernel(
+    const uint8_t* __restrict__ st, const uint8_t* __restrict__ act,
+    const int16_t* __restrict__ rew, const uint8_t* __restrict__ nt, ReplayMeta* meta,
+    const int32_t* __restrict__ idx, int S, float* __restrict__ sQ, float* __restrict__ sP,
+    float* __restrict__ action, float* __restrict__ reward, float* __restrict__ nonterm) {
+  const int b = blockIdx.y, z = blockIdx.z;
+  const int64_t N = meta->capacity;
+  const int64_t i = idx[b];
+  const int64_t nxt = (i + 1 == N) ? 0 : i + 1;
+  const int64_t slot = z ? nxt : i;
+  const int SS = S * S;
+  const int p4 = blockIdx.x * 256 + threadIdx.x;     // group of 4 pixels
+  if (p4 * 4 < SS) {
+    const uint8_t* src = st + slot * 4 * SS + p4 * 4;
+    const uchar4 c0 = *reinterpret_cast<const uchar4*>(src);
+    const uchar4 c1 = *reinterpret_cast<const uchar4*>(src + SS);
+    const uchar4 c2 = *reinterpret_cast<const uchar4*>(src + 2 * SS);
+    const uchar4 c3 = *reinterpret_cast<const uchar4*>(src + 3 * SS);
+    float4* dst = reinterpret_cast<float4*>((z ? sP : sQ) + ((size_t)b * SS + p4 * 4) * 4);
+    dst[0] = f4(c0.x, c1.x, c2.x, c3.x);
+    dst[1] = f4(c0.y, c1.y, c2.y, c3.y);
+    dst[2] = f4(c0.z, c1.z, c2.z, c3.z);
+    dst[3] = f4(c0.w, c1.w, c2.w, c3.w);
+  }
+  if (z == 1 && blockIdx.x == 0 && threadIdx.x < 4) {
+    const int a = act[nxt];
+    if (a >= kActions) meta->err = 1;
+    action[b * 4 + threadIdx.x] = (threadIdx.x == a) ? 1.f : 0.f;
+    if (threadIdx.x == 0) {
+      reward[b] = (float)rew[nxt];
+      nonterm[b] = nt[nxt] ? 1.f : 0.f;
+    }
+  }
+}
+
+hipError_t launch_sample(const NetBuffers& nb, ReplayMeta* meta, uint64_t seed, hipStream_t s) {
+  hipLaunchKernelGGL(sample_kernel, dim3(1), dim3(1024), 0, s, meta, nb.B, seed, nb.idx);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather(const NetBuffers& nb, const uint8_t* st, const uint8_t* act,
+                         const int16_t* rew, const uint8_t* nt, ReplayMeta* meta,
+                         hipStream_t s) {
+  const int SS = nb.S * nb.S;
+  dim3 grid((SS / 4 + 255) / 256, nb.B, 2);
+  hipLaunchKernelGGL(gather_kernel, grid, dim3(256), 0, s, st, act, rew, nt, meta, nb.idx, nb.S,
+                     nb.state, nb.next_state, nb.action, nb.reward, nb.nonterm);
+  return hipGetLastError();
+}
+
+// u8 (n,4,S,S) -> f32 NHWC (n,S,S,4)  (acting path, select_action)
+__global__ void u8_to_nhwc_kernel(const uint8_t* src, int n, int S, float* dst) {
+  const int SS = S * S;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * SS) return;
+  const int b = i / SS, p = i % SS;
+  const uint8_t* s = src + (size_t)b * 4 * SS + p;
+  reinterpret_cast<float4*>(dst)[i] = f4(s[0], s[SS], s[2 * SS], s[3 * SS]);
+}
+
+hipError_t launch_u8_to_nhwc(const uint8_t* src, int n, int S, float* dst, hipStream_t s) {
+  const int tot = n * S * S;
+  hipLaunchKernelGGL(u8_to_nhwc_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, src, n, S, dst);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// target sync (server.py:127-137, applied at pull when iteration % period == 0,
+// server.py:188-189): P <- Q for theta and the conv kernel-layout copy.
+// ---------------------------------------------------------------------------
+__global__ void target_sync_kernel(const int64_t* iter, int period, const float* __restrict__ tq,
+                                   float* __restrict__ tp, int64_t n, const float* __restrict__ wq,
+                                   float* __restrict__ wp, int64_t nw) {
+  if (period <= 0 || (*iter % period) != 0) return;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += stride) {
+    if (i + 3 < n) {
+      *reinterpret_cast<float4*>(tp + i) = *reinterpret_cast<const float4*>(tq + i);
+    } else {
+      for (int64_t j = i; j < n; ++j) tp[j] = tq[j];
+    }
+  }
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < nw; i += stride) {
+    if (i + 3 < nw) {
+      *reinterpret_cast<float4*>(wp + i) = *reinterpret_cast<const float4*>(wq + i);
+    } else {
+      for (int64_t j = i; j < nw; ++j) wp[j] = wq[j];
+    }
+  }
+}
+
+hipError_t launch_target_sync_if(const NetBuffers& nb, int period, hipStream_t s) {
+  const int64_t n = nb.L.total;
+  int blocks = (int)std::min<int64_t>(2048, (n / 4 + 255) / 256 + 1);
+  hipLaunchKernelGGL(target_sync_kernel, dim3(blocks), dim3(256), 0, s, nb.iter, period,
+                     nb.theta[0], nb.theta[1], n, nb.wk[0], nb.wk[1], nb.L.wk_total);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Caffe (co,ci,ky,kx) -> kernel layout (co,ky,kx,ci) for the three convs
+// ---------------------------------------------------------------------------
+struct ConvDims { int64_t w_off, wk_off; int cout, cin, ks; };
+
+__device__ __forceinline__ int64_t wk_index(const ConvDims& d, int64_t e) {
+  // e: Caffe-order element of the layer's weight
+  const int kk = d.ks * d.ks;
+  const int64_t co = e / ((int64_t)d.cin * kk);
+  const int64_t rem = e - co * d.cin * kk;
+  const int ci = (int)(rem / kk), tap = (int)(rem % kk);
+  return d.wk_off + (co * kk + tap) * d.cin + ci;
+}
+
+__global__ void relayout_kernel(const float* __restrict__ theta, float* __restrict__ wk,
+                                ConvDims d0, ConvDims d1, ConvDims d2) {
+  const int l = blockIdx.y;
+  const ConvDims d = l == 0 ? d0 : (l == 1 ? d1 : d2);
+  const int64_t n = (int64_t)d.cout * d.cin * d.ks * d.ks;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x)
+    wk[wk_index(d, e)] = theta[d.w_off + e];
+}
+
+static void conv_dims(const ParamLayout& L, ConvDims* d) {
+  const int cout[3] = {32, 64, 64}, cin[3] = {4, 32, 64}, ks[3] = {7, 5, 3};
+  for (int i = 0; i < 3; ++i) d[i] = {L.w[i], L.wk_off[i], cout[i], cin[i], ks[i]};
+}
+
+hipError_t launch_relayout(const NetBuffers& nb, int z, hipStream_t s) {
+  ConvDims d[3];
+  conv_dims(nb.L, d);
+  hipLaunchKernelGGL(relayout_kernel, dim3(64, 3), dim3(256), 0, s, nb.theta[z], nb.wk[z], d[0],
+                     d[1], d[2]);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// fc4 split-K reduce + bias + ReLU (dropout = identity, TEST phase)
+// ---------------------------------------------------------------------------
+__global__ void fc4_reduce_kernel(const float* __restrict__ part, int splits, int nz, int B,
+                                  const float* __restrict__ b0, const float* __restrict__ b1,
+                                  float* __restrict__ h0, float* __restrict__ h1) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;   // over nz*B*512
+  const int per = B * kFc4;
+  if (i >= nz * per) return;
+  const int z = i / per, r = i % per, n = r % kFc4;
+  float acc = 0.f;
+  for (int s = 0; s < splits; ++s) acc += part[((size_t)(s * nz + z) * B) * kFc4 + r];
+  const float v = acc + (z ? b1 : b0)[n];
+  (z ? h1 : h0)[r] = v > 0.f ? v : 0.f;
+}
+
+// ---------------------------------------------------------------------------
+// head: Q_out / P_out, Q(s,a), Bellman target, Euclidean loss and the
+// backward through Q_out (train_val.prototxt:195-215, :385-483):
+//   Q_sa = sum_a Q*act, P_sa = max_a P * nt, target = 0.85 P_sa + r,
+//   loss = sum (Q_sa-target)^2 / 2B, dQ = act (Q_sa-target)/B,
+//   dW5 = dQ^T h4, db5 = sum dQ, dh4 = (dQ W5) * (h4>0), db4 = sum_b dh4.
+// One workgroup (the whole problem is B x 4 x 512).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void head_kernel(
+    int B, float gamma, const float* __restrict__ h4q, const float* __restrict__ h4p,
+    const float* __restrict__ w5q, const float* __restrict__ b5q, const float* __restrict__ w5p,
+    const float* __restrict__ b5p, const float* __restrict__ action,
+    const float* __restrict__ reward, const float* __restrict__ nonterm, float* q_out,
+    float* p_out, float* q_sa_o, float* p_sa_o, float* target_o, float* loss_o,
+    float* __restrict__ gw5, float* __restrict__ gb5, float* __restrict__ gb4,
+    float* __restrict__ dh4) {
+  extern __shared__ float sh[];            // [2][B][4] outputs, [B][4] dQ, red[32]
+  float* outs = sh;
+  float* dq = sh + 2 * B * 4;
+  float* red = dq + B * 4;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, nw = blockDim.x >> 6;
+  // phase 1: 2*B*4 dot products of length 512, one wave each
+  for (int o = w; o < 2 * B * 4; o += nw) {
+    const int z = o / (B * 4), r = o % (B * 4), b = r / 4, a = r % 4;
+    const float* h = (z ? h4p : h4q) + (size_t)b * kFc4;
+    const float* wr = (z ? w5p : w5q) + (size_t)a * kFc4;
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < kFc4 / 64; ++j) acc += h[lane + 64 * j] * wr[lane + 64 * j];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+    if (lane == 0) {
+      const float v = acc + (z ? b5p : b5q)[a];
+      outs[o] = v;
+      (z ? p_out : q_out)[r] = v;
+    }
+  }
+  __syncthreads();
+  // phase 2: per-sample target / loss / dQ
+  float d2 = 0.f;
+  for (int b = t; b < B; b += blockDim.x) {
+    const float* q = outs + b * 4;
+    const float* p = outs + B * 4 + b * 4;
+    const float* ac = action + b * 4;
+    // ELTWISE PROD then SLICE + SUM (in slice order)
+    float qs = q[0] * ac[0];
+    qs += q[1] * ac[1];
+    qs += q[2] * ac[2];
+    qs += q[3] * ac[3];
+    float ps = fmaxf(fmaxf(p[0], p[1]), fmaxf(p[2], p[3]));
+    ps = ps * nonterm[b];
+    const float tg = gamma * ps + 1.0f * reward[b];
+    const float diff = qs - tg;
+    q_sa_o[b] = qs; p_sa_o[b] = ps; target_o[b] = tg;
+    const float g = diff / (float)B;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) dq[b * 4 + a] = ac[a] * g;
+    d2 += diff * diff;
+  }
+  for (int off = 32; off > 0; off >>= 1) d2 += __shfl_xor(d2, off);
+  if (lane == 0) red[w] = d2;
+  __syncthreads();
+  if (t == 0) {
+    float s = 0.f;
+    for (int i = 0; i < nw; ++i) s += red[i];
+    *loss_o = s / (float)B / 2.f;
+  }
+  // phase 3: Q_out backward
+  for (int o = t; o < 4 * kFc4; o += blockDim.x) {       // dW5[a][j]
+    const int a = o / kFc4, j = o % kFc4;
+    float acc = 0.f;
+    for (int b = 0; b < B; ++b) acc += dq[b * 4 + a] * h4q[(size_t)b * kFc4 + j];
+    gw5[o] = acc;
+  }
+  if (t < 4) {
+    float acc = 0.f;
+    for (int b = 0; b < B; ++b) acc += dq[b * 4 + t];
+    gb5[t] = acc;
+  }
+  for (int j = t; j < kFc4; j += blockDim.x) {            // dh4[:, j], db4[j]
+    const float w0 = w5q[j], w1 = w5q[kFc4 + j], w2 = w5q[2 * kFc4 + j], w3 = w5q[3 * kFc4 + j];
+    float db = 0.f;
+    for (int b = 0; b < B; ++b) {
+      const float* d = dq + b * 4;
+      float v = d[0] * w0 + d[1] * w1 + d[2] * w2 + d[3] * w3;
+      v = h4q[(size_t)b * kFc4 + j] > 0.f ? v : 0.f;
+      dh4[(size_t)b * kFc4 + j] = v;
+      db += v;
+    }
+    gb4[j] = db;
+  }
+}
+
+hipError_t launch_head(const NetBuffers& nb, hipStream_t s) {
+  const ParamLayout& L = nb.L;
+  const size_t shm = (size_t)(2 * nb.B * 4 + nb.B * 4 + 32) * sizeof(float);
+  hipLaunchKernelGGL(head_kernel, dim3(1), dim3(1024), shm, s, nb.B, nb.gamma, nb.h4[0],
+                     nb.h4[1], nb.theta[0] + L.w[4], nb.theta[0] + L.b[4], nb.theta[1] + L.w[4],
+                     nb.theta[1] + L.b[4], nb.action, nb.reward, nb.nonterm, nb.q_out, nb.p_out,
+                     nb.q_sa, nb.p_sa, nb.target, nb.loss, nb.grad + L.w[4], nb.grad + L.b[4],
+                     nb.grad + L.b[3], nb.dh4);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// conv wgrad slab reduce -> Caffe (co,ci,ky,kx) weight diff + bias diff
+// ---------------------------------------------------------------------------
+struct WredDims {
+  int64_t w_off, b_off, part_off;
+  int cout, cin, ks, splits, np;
+};
+
+__global__ void wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ grad,
+                                    WredDims d0, WredDims d1, WredDims d2) {
+  const int l = blockIdx.y;
+  const WredDims d = l == 0 ? d0 : (l == 1 ? d1 : d2);
+  const int kk = d.ks * d.ks, kc = kk * d.cin;
+  const int64_t nw = (int64_t)d.cout * kc;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nw + d.cout;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    int co, n;
+    if (e < nw) {
+      co = (int)(e / kc);
+      const int rem = (int)(e - (int64_t)co * kc);
+      const int ci = rem / kk, tap = rem % kk;
+      n = tap * d.cin + ci;
+    } else {
+      co = (int)(e - nw);
+      n = kc;
+    }
+    const float* p = part + d.part_off + (size_t)co * d.np + n;
+    float acc = 0.f;
+    for (int s = 0; s < d.splits; ++s) acc += p[(size_t)s * d.cout * d.np];
+    grad[e < nw ? d.w_off + e : d.b_off + co] = acc;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// apply: server.py update rules on the flat Q tower (+ fused kernel-layout
+// refresh of the conv weights and the param-server iteration counter)
+// ---------------------------------------------------------------------------
+struct ApplyArgs {
+  int64_t n;
+  int rule;
+  float lr, decay, one_minus_decay, eps, momentum, wd;
+  int64_t bias_lo[5], bias_hi[5];   // [lo,hi) element ranges of biases (momentum multipliers)
+  ConvDims conv[3];
+};
+
+__global__ void apply_kernel(float* __restrict__ theta, const float* __restrict__ grad,
+                             float* __restrict__ opt, int32_t* __restrict__ opt_init,
+                             float* __restrict__ wk, int64_t* __restrict__ iter, ApplyArgs a) {
+  const bool first = (*opt_init == 0);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
+    const float g = grad[i];
+    float th = theta[i];
+    switch (a.rule) {
+      case 0:   // sgd: theta - lr*g
+        th = th - a.lr * g;
+        break;
+      case 1: { // rmsprop with one-step-lagged cache
+        const float g2 = g * g;
+        const float c_use = first ? g2 : opt[i];
+        opt[i] = first ? g2 : (a.decay * opt[i] + a.one_minus_decay * g2);
+        th = th - (a.lr * g) / sqrtf(c_use + a.eps);
+        break;
+      }
+      case 2: { // adagrad with current accumulator
+        const float acc = first ? g * g : opt[i] + g * g;
+        opt[i] = acc;
+        th = th - (a.lr * g) / sqrtf(acc + a.eps);
+        break;
+      }
+      default: { // Caffe SGDSolver momentum (blobs_lr {1,2}, weight_decay {1,0})
+        bool is_bias = false;
+#pragma unroll
+        for (int l = 0; l < 5; ++l) is_bias |= (i >= a.bias_lo[l] && i < a.bias_hi[l]);
+        const float lr = a.lr * (is_bias ? 2.f : 1.f);
+        const float wd = is_bias ? 0.f : a.wd;
+        const float v = a.momentum * (first ? 0.f : opt[i]) + lr * (g + wd * th);
+        opt[i] = v;
+        th = th - v;
+        break;
+      }
+    }
+    theta[i] = th;
+#pragma unroll
+    for (int l = 0; l < 3; ++l) {
+      const ConvDims& d = a.conv[l];
+      const int64_t e = i - d.w_off;
+      if (e >= 0 && e < (int64_t)d.cout * d.cin * d.ks * d.ks) wk[wk_index(d, e)] = th;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *iter += 1;
+}
+
+__global__ void set_flag_kernel(int32_t* f) { *f = 1; }
+
+hipError_t launch_apply(const NetBuffers& nb, int rule, float lr, float decay, float eps,
+                        float momentum, float wd, hipStream_t s) {
+  ApplyArgs a;
+  a.n = nb.L.total;
+  a.rule = rule; a.lr = lr; a.decay = decay; a.eps = eps;
+  a.momentum = momentum; a.wd = wd;
+  a.one_minus_decay = (float)(1.0 - (double)decay);   // numpy: (1 - rmsprop_decay) in double
+  for (int l = 0; l < 5; ++l) { a.bias_lo[l] = nb.L.b[l]; a.bias_hi[l] = nb.L.b[l] + nb.L.bn[l]; }
+  conv_dims(nb.L, a.conv);
+  const int blocks = (int)std::min<int64_t>(2048, (a.n + 255) / 256);
+  hipLaunchKernelGGL(apply_kernel, dim3(blocks), dim3(256), 0, s, nb.theta[0], nb.grad, nb.opt,
+                     nb.opt_init, nb.wk[0], nb.iter, a);
+  hipLaunchKernelGGL(set_flag_kernel, dim3(1), dim3(1), 0, s, nb.opt_init);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// GEMM configurations per layer
+// ---------------------------------------------------------------------------
+using CfgConv1F = GemmCfg<128, 32, 28, 4, 1>;
+using CfgConv2F = GemmCfg<128, 64, 32, 2, 2>;
+using CfgConv3F = GemmCfg<64, 64, 32, 2, 2>;
+using CfgFcF = GemmCfg<32, 128, 32, 1, 4>;
+using CfgFcD = GemmCfg<32, 64, 32, 1, 2>;
+using CfgFcW = GemmCfg<64, 64, 32, 2, 2>;
+using CfgW1 = GemmCfg<32, 64, 32, 1, 2>;
+using CfgW23 = GemmCfg<64, 64, 32, 2, 2>;
+using CfgD2 = GemmCfg<128, 32, 32, 4, 1>;
+using CfgD3 = GemmCfg<64, 64, 32, 2, 2>;
+
+// split-K: K per split is a multiple of BK, about `target`
+static inline int split_len(int K, int BK, int target, int* nsplit) {
+  int len = std::max(BK, (target / BK) * BK);
+  if (len >= K) { *nsplit = 1; return ((K + BK - 1) / BK) * BK; }
+  *nsplit = (K + len - 1) / len;
+  return len;
+}
+
+int fc4_splits_for(int S) {
+  const int K = 64 * (S / 8) * (S / 8);
+  int ns;
+  split_len(K, CfgFcF::BK, 256, &ns);
+  return ns;
+}
+
+int wgrad_splits_for(int layer, int B, int S, int* np) {
+  const int H = S >> layer;
+  const int K = B * H * H;
+  const int KC[3] = {196, 800, 576};
+  const int target[3] = {1024, 1024, 512};
+  *np = ((KC[layer] + 1 + 63) / 64) * 64;
+  int ns;
+  split_len(K, 32, target[layer], &ns);
+  return ns;
+}
+
+#define CHECK_LAUNCH(x)                         \
+  do {                                          \
+    hipError_t e_ = (x);                        \
+    if (e_ != hipSuccess) return e_;            \
+  } while (0)
+
+hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
+                          void (*mark)(void*, const char*), void* marg) {
+  const ParamLayout& L = nb.L;
+  const int B = nb.B, S = nb.S;
+  auto M = [&](const char* n) { if (mark) mark(marg, n); };
+  {
+    ConvFwd<4, 32, 7, 3> p;
+    p.M = B * S * S; p.N = 32; p.K = 196; p.ksplit_len = 196;
+    p.H = S; p.W = S; p.fWp = FastDiv(S / 2); p.fHp = FastDiv(S / 2);
+    p.in[0] = nb.state; p.in[1] = nb.next_state;
+    for (int z = 0; z < 2; ++z) {
+      p.wk[z] = nb.wk[z] + L.wk_off[0]; p.bias[z] = nb.theta[z] + L.b[0];
+      p.out[z] = nb.pool1[z];
+    }
+    p.mask[0] = nb.mask1; p.mask[1] = nullptr;
+    M("conv1_fwd");
+    CHECK_LAUNCH(launch_gemm<CfgConv1F>(p, nz, 1, s));
+  }
+  {
+    const int H = S / 2;
+    ConvFwd<32, 64, 5, 2> p;
+    p.M = B * H * H; p.N = 64; p.K = 800; p.ksplit_len = 800;
+    p.H = H; p.W = H; p.fWp = FastDiv(H / 2); p.fHp = FastDiv(H / 2);
+    for (int z = 0; z < 2; ++z) {
+      p.in[z] = nb.pool1[z]; p.wk[z] = nb.wk[z] + L.wk_off[1]; p.bias[z] = nb.theta[z] + L.b[1];
+      p.out[z] = nb.pool2[z];
+    }
+    p.mask[0] = nb.mask2; p.mask[1] = nullptr;
+    M("conv2_fwd");
+    CHECK_LAUNCH(launch_gemm<CfgConv2F>(p, nz, 1, s));
+  }
+  {
+    const int H = S / 4;
+    ConvFwd<64, 64, 3, 1> p;
+    p.M = B * H * H; p.N = 64; p.K = 576; p.ksplit_len = 576;
+    p.H = H; p.W = H; p.fWp = FastDiv(H / 2); p.fHp = FastDiv(H / 2);
+    for (int z = 0; z < 2; ++z) {
+      p.in[z] = nb.pool2[z]; p.wk[z] = nb.wk[z] + L.wk_off[2]; p.bias[z] = nb.theta[z] + L.b[2];
+      p.out[z] = nb.pool3[z];
+    }
+    p.mask[0] = nb.mask3; p.mask[1] = nullptr;
+    M("conv3_fwd");
+    CHECK_LAUNCH(launch_gemm<CfgConv3F>(p, nz, 1, s));
+  }
+  {
+    const int s4 = S / 8;
+    FcFwd p;
+    p.M = B; p.N = kFc4; p.K = 64 * s4 * s4;
+    int ns;
+    p.ksplit_len = split_len(p.K, CfgFcF::BK, 256, &ns);
+    p.s4sq = s4 * s4; p.fS4sq = FastDiv(s4 * s4);
+    for (int z = 0; z < 2; ++z) { p.x[z] = nb.pool3[z]; p.w[z] = nb.theta[z] + L.w[3]; }
+    p.part = nb.fc4_part; p.nz = nz;
+    M("fc4_fwd");
+    CHECK_LAUNCH(launch_gemm<CfgFcF>(p, nz, ns, s));
+    const int tot = nz * B * kFc4;
+    M("fc4_reduce");
+    hipLaunchKernelGGL(fc4_reduce_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, nb.fc4_part,
+                       ns, nz, B, nb.theta[0] + L.b[3], nb.theta[1] + L.b[3], nb.h4[0], nb.h4[1]);
+    CHECK_LAUNCH(hipGetLastError());
+  }
+  return hipSuccess;
+}
+
+hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(void*, const char*),
+                           void* marg) {
+  const ParamLayout& L = nb.L;
+  const int B = nb.B, S = nb.S;
+  const int s4 = S / 8;
+  auto M = [&](const char* n) { if (mark) mark(marg, n); };
+  {  // fc4 dgrad -> dconv3
+    FcDgrad p;
+    p.M = B; p.N = 64 * s4 * s4; p.K = kFc4; p.ksplit_len = kFc4;
+    p.s4 = s4; p.s4sq = s4 * s4; p.fS4sq = FastDiv(s4 * s4); p.fS4 = FastDiv(s4);
+    p.dh4 = nb.dh4; p.w4 = nb.theta[0] + L.w[3]; p.mask3 = nb.mask3; p.dconv3 = nb.dconv3;
+    M("fc4_dgrad");
+    CHECK_LAUNCH(launch_gemm<CfgFcD>(p, 1, 1, s));
+  }
+  {  // fc4 wgrad
+    FcWgrad p;
+    p.M = kFc4; p.N = 64 * s4 * s4; p.K = B; p.ksplit_len = ((B + 31) / 32) * 32;
+    p.s4sq = s4 * s4; p.fS4sq = FastDiv(s4 * s4);
+    p.dh4 = nb.dh4; p.x = nb.pool3[0]; p.gw4 = nb.grad + L.w[3];
+    M("fc4_wgrad");
+    CHECK_LAUNCH(launch_gemm<CfgFcW>(p, 1, 1, s));
+  }
+  {  // conv3 wgrad
+    const int H = S / 4;
+    ConvWgrad<64, 64, 3, 1> p;
+    p.M = 64; p.N = 577; p.K = B * H * H;
+    int ns;
+    p.ksplit_len = split_len(p.K, 32, 512, &ns);
+    p.H = H; p.W = H; p.fW = FastDiv(H); p.fH = FastDiv(H);
+    p.NP = nb.wnp[2]; p.dconv = nb.dconv3; p.in = nb.pool2[0]; p.part = nb.wpart + nb.wpart_off[2];
+    M("conv3_wgrad");
+    CHECK_LAUNCH(launch_gemm<CfgW23>(p, 1, ns, s));
+  }
+  {  // conv3 dgrad -> dconv2
+    const int H = S / 4;
+    ConvDgrad<64, 64, 3, 1> p;
+    p.M = B * H * H; p.N = 64; p.K = 576; p.ksplit_len = 576;
+    p.H = H; p.W = H; p.fW = FastDiv(H); p.fH = FastDiv(H);
+    p.dconv = nb.dconv3; p.wk = nb.wk[0] + L.wk_off[2]; p.pmask = nb.mask2; p.pdconv = nb.dconv2;
+    M("conv3_dgrad");
+    CHECK_LAUNCH(launch_gemm<CfgD3>(p, 1, 1, s));
+  }
+  {  // conv2 wgrad
+    const int H = S / 2;
+    ConvWgrad<32, 64, 5, 2> p;
+    p.M = 64; p.N = 801; p.K = B * H * H;
+    int ns;
+    p.ksplit_len = split_len(p.K, 32, 1024, &ns);
+    p.H = H; p.W = H; p.fW = FastDiv(H); p.fH = FastDiv(H);
+    p.NP = nb.wnp[1]; p.dconv = nb.dconv2; p.in = nb.pool1[0]; p.part = nb.wpart + nb.wpart_off[1];
+    M("conv2_wgrad");
+    CHECK_LAUNCH(launch_gemm<CfgW23>(p, 1, ns, s));
+  }
+  {  // conv2 dgrad -> dconv1
+    const int H = S / 2;
+    ConvDgrad<32, 64, 5, 2> p;
+    p.M = B * H * H; p.N = 32; p.K = 1600; p.ksplit_len = 1600;
+    p.H = H; p.W = H; p.fW = FastDiv(H); p.fH = FastDiv(H);
+    p.dconv = nb.dconv2; p.wk = nb.wk[0] + L.wk_off[1]; p.pmask = nb.mask1; p.pdconv = nb.dconv1;
+    M("conv2_dgrad");
+    CHECK_LAUNCH(launch_gemm<CfgD2>(p, 1, 1, s));
+  }
+  {  // conv1 wgrad
+    ConvWgrad<4, 32, 7, 3> p;
+    p.M = 32; p.N = 197; p.K = B * S * S;
+    int ns;
+    p.ksplit_len = split_len(p.K, 32, 1024, &ns);
+    p.H = S; p.W = S; p.fW = FastDiv(S); p.fH = FastDiv(S);
+    p.NP = nb.wnp[0]; p.dconv = nb.dconv1; p.in = nb.state; p.part = nb.wpart + nb.wpart_off[0];
+    M("conv1_wgrad");
+    CHECK_LAUNCH(launch_gemm<CfgW1>(p, 1, ns, s));
+  }
+  {  // slab reduce -> grads (Caffe layout)
+    WredDims d[3];
+    const int cout[3] = {32, 64, 64}, cin[3] = {4, 32, 64}, ks[3] = {7, 5, 3};
+    for (int l = 0; l < 3; ++l)
+      d[l] = {L.w[l], L.b[l], nb.wpart_off[l], cout[l], cin[l], ks[l], nb.wsplits[l], nb.wnp[l]};
+    M("wgrad_reduce");
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(64, 3), dim3(256), 0, s, nb.wpart, nb.grad, d[0],
+                       d[1], d[2]);
+    CHECK_LAUNCH(hipGetLastError());
+  }
+  return hipSuccess;
+}
+
+// ---------------------------------------------------------------------------
+// acting: Q forward of n states + argmax (select_action, baristanet.py:142-146)
+// ---------------------------------------------------------------------------
+__global__ void act_head_kernel(int n, const float* __restrict__ h4, const float* __restrict__ w5,
+                                const float* __restrict__ b5, float* __restrict__ qout,
+                                int32_t* __restrict__ actions) {
+  const int b = blockIdx.x, lane = threadIdx.x;   // one wave per state
+  if (b >= n) return;
+  float q[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < kFc4 / 64; ++j)
+      acc += h4[(size_t)b * kFc4 + lane + 64 * j] * w5[a * kFc4 + lane + 64 * j];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+    q[a] = acc + b5[a];
+  }
+  if (lane == 0) {
+    int best = 0;
+    for (int a = 1; a < 4; ++a)
+      if (q[a] > q[best]) best = a;   // numpy argmax: first max
+    for (int a = 0; a < 4; ++a) qout[b * 4 + a] = q[a];
+    if (actions) actions[b] = best;
+  }
+}
+
+hipError_t launch_act(const NetBuffers& nb, const float* in, int n, float* pool1, float* pool2,
+                      float* pool3, float* h4, float* part, float* qout, int32_t* actions,
+                      hipStream_t s) {
+  NetBuffers a = nb;
+  a.B = n;
+  a.state = const_cast<float*>(in);
+  a.next_state = const_cast<float*>(in);
+  a.pool1[0] = pool1; a.pool2[0] = pool2; a.pool3[0] = pool3; a.h4[0] = h4;
+  a.pool1[1] = pool1; a.pool2[1] = pool2; a.pool3[1] = pool3; a.h4[1] = h4;
+  a.mask1 = a.mask2 = a.mask3 = nullptr;
+  a.fc4_part = part;
+  CHECK_LAUNCH(launch_forward(a, 1, s, nullptr, nullptr));
+  hipLaunchKernelGGL(act_head_kernel, dim3(n), dim3(64), 0, s, n, h4, nb.theta[0] + nb.L.w[4],
+                     nb.theta[0] + nb.L.b[4], qout, actions);
+  return hipGetLastError();
+}
+
+}  // namespace ddq

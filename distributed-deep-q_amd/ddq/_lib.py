@@ -1,0 +1,147 @@
+"""ctypes binding of libddq_hip.so (include/ddq_hip.h).
+
+There is no fallback: if the HIP library is missing or fails to load, importing
+the product path raises.  Build it with ``make -C distributed-deep-q_amd`` (or
+``python -c "import __graft_entry__ as g; g.build()"``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libddq_hip.so")
+
+DDQ_OK, DDQ_EINVAL, DDQ_ENOMEM, DDQ_EHIP, DDQ_ERCCL, DDQ_ESTATE, DDQ_ERANGE = 0, -1, -2, -3, -4, -5, -6
+RULES = {"sgd": 0, "rmsprop": 1, "adagrad": 2, "momentum": 3}
+
+
+class DDQError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("ddq error %d: %s" % (code, msg))
+        self.code = code
+        self.msg = msg
+
+
+class NetDesc(ctypes.Structure):
+    _fields_ = [("batch", ctypes.c_int32), ("frame", ctypes.c_int32),
+                ("channels", ctypes.c_int32), ("actions", ctypes.c_int32),
+                ("gamma", ctypes.c_float)]
+
+
+class BlobDesc(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * 16), ("index", ctypes.c_int32),
+                ("shape", ctypes.c_int32 * 4), ("offset", ctypes.c_int64),
+                ("count", ctypes.c_int64)]
+
+
+class UpdateCfg(ctypes.Structure):
+    _fields_ = [("rule", ctypes.c_int32), ("lr", ctypes.c_float), ("decay", ctypes.c_float),
+                ("eps", ctypes.c_float), ("momentum", ctypes.c_float),
+                ("weight_decay", ctypes.c_float)]
+
+
+class StepCfg(ctypes.Structure):
+    _fields_ = [("update", UpdateCfg), ("target_period", ctypes.c_int32),
+                ("allreduce", ctypes.c_int32), ("seed", ctypes.c_uint64)]
+
+
+_P = ctypes.c_void_p
+_i32, _i64, _u64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64
+_fp = ctypes.POINTER(ctypes.c_float)
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "ddq_abi_version": (ctypes.c_int, []),
+    "ddq_create": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, ctypes.POINTER(NetDesc)]),
+    "ddq_destroy": (ctypes.c_int, [_P]),
+    "ddq_last_error": (ctypes.c_char_p, [_P]),
+    "ddq_set_stream": (ctypes.c_int, [_P, _P]),
+    "ddq_synchronize": (ctypes.c_int, [_P]),
+    "ddq_num_params": (_i64, [_P]),
+    "ddq_param_layout": (ctypes.c_int, [_P, ctypes.POINTER(BlobDesc), _i32, ctypes.POINTER(_i32)]),
+    "ddq_set_params": (ctypes.c_int, [_P, _i32, _P, _i64, _i32]),
+    "ddq_get_params": (ctypes.c_int, [_P, _i32, _P, _i64, _i32]),
+    "ddq_get_grads": (ctypes.c_int, [_P, _P, _i64, _i32]),
+    "ddq_set_grads": (ctypes.c_int, [_P, _P, _i64, _i32]),
+    "ddq_sync_target": (ctypes.c_int, [_P]),
+    "ddq_replay_create": (ctypes.c_int, [_P, _i64]),
+    "ddq_replay_add": (ctypes.c_int, [_P, _i32, _i32, _P]),
+    "ddq_replay_info": (ctypes.c_int, [_P, ctypes.POINTER(_i64), ctypes.POINTER(_i64),
+                                       ctypes.POINTER(_i64)]),
+    "ddq_replay_import": (ctypes.c_int, [_P, _P, _P, _P, _P, _i64, _i64, _i64]),
+    "ddq_replay_export": (ctypes.c_int, [_P, _P, _P, _P, _P, _i64]),
+    "ddq_replay_sample": (ctypes.c_int, [_P, _P, _i32]),
+    "ddq_replay_sample_device_async": (ctypes.c_int, [_P, _u64]),
+    "ddq_read_minibatch": (ctypes.c_int, [_P, _P, _P, _P, _P, _P]),
+    "ddq_write_minibatch": (ctypes.c_int, [_P, _P, _P, _P, _P, _P]),
+    "ddq_read_indices": (ctypes.c_int, [_P, _P, _i32]),
+    "ddq_forward_backward": (ctypes.c_int, [_P, _fp]),
+    "ddq_forward_backward_async": (ctypes.c_int, [_P]),
+    "ddq_forward_q": (ctypes.c_int, [_P]),
+    "ddq_read_blob": (ctypes.c_int, [_P, ctypes.c_char_p, _P, _i64]),
+    "ddq_read_pool_mask": (ctypes.c_int, [_P, _i32, _P, _i64]),
+    "ddq_select_action": (ctypes.c_int, [_P, _P, _i32, _P]),
+    "ddq_apply": (ctypes.c_int, [_P, ctypes.POINTER(UpdateCfg)]),
+    "ddq_apply_async": (ctypes.c_int, [_P, ctypes.POINTER(UpdateCfg)]),
+    "ddq_reset_optimizer": (ctypes.c_int, [_P]),
+    "ddq_get_optimizer_state": (ctypes.c_int, [_P, _P, _i64]),
+    "ddq_comm_get_unique_id": (ctypes.c_int, [_P]),
+    "ddq_comm_init": (ctypes.c_int, [_P, _P, _i32, _i32]),
+    "ddq_allreduce_grads": (ctypes.c_int, [_P]),
+    "ddq_allreduce_grads_async": (ctypes.c_int, [_P]),
+    "ddq_step_async": (ctypes.c_int, [_P, ctypes.POINTER(StepCfg)]),
+    "ddq_step_graph_async": (ctypes.c_int, [_P, ctypes.POINTER(StepCfg), _i32]),
+    "ddq_step_count": (_i64, [_P]),
+    "ddq_profile_step": (ctypes.c_int, [_P, ctypes.POINTER(StepCfg), _P, _fp, _i32,
+                                        ctypes.POINTER(_i32)]),
+    "ddq_step_flops": (ctypes.c_double, [_P]),
+}
+
+EXPORTED = tuple(_SIGS)
+_lib = None
+
+
+def load(path=LIB_PATH):
+    """Load libddq_hip.so (raises if it is absent -- no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError("libddq_hip.so not found at %s; build it with "
+                          "`make -C distributed-deep-q_amd` (hipcc --offload-arch=gfx950)" % path)
+    try:  # share torch's HIP runtime when torch is present (same SONAME)
+        import torch  # noqa: F401
+    except Exception:  # pragma: no cover - torch is plumbing only
+        pass
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc, ctx=None):
+    if rc != DDQ_OK:
+        lib = load()
+        msg = lib.ddq_last_error(ctx)
+        raise DDQError(rc, msg.decode() if msg else "")
+    return rc
+
+
+def ptr(a):
+    """Host pointer of a C-contiguous numpy array (or None)."""
+    if a is None:
+        return None
+    assert isinstance(a, np.ndarray) and a.flags["C_CONTIGUOUS"], "need C-contiguous ndarray"
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def update_cfg(rule="rmsprop", lr=1e-4, decay=0.9, eps=1e-8, momentum=0.9, weight_decay=0.0005):
+    """Defaults: param-server/server.py:265-271 (rmsprop, lr 1e-4, decay 0.9),
+    eps 1e-8 (server.py:105); momentum/weight_decay: solver.prototxt:9-10."""
+    r = RULES[rule] if isinstance(rule, str) else int(rule)
+    return UpdateCfg(r, lr, decay, eps, momentum, weight_decay)

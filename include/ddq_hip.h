@@ -1,0 +1,212 @@
+/*
+ * ddq_hip.h -- C-ABI of libddq_hip.so, the MI355X (gfx950) implementation of
+ * distributed-deep-q's data-parallel DQN training step.
+ *
+ * The reference's hot path sits behind pycaffe (Boost.Python -> C++ caffe::Net)
+ * plus numpy/h5py/Flask host code.  Every entry point below names the reference
+ * interface it replaces (file:line in defc0n1/distributed-deep-q).  The Python
+ * drop-ins in distributed-deep-q_amd/ddq bind these symbols with ctypes
+ * (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *  - Every function returns int: DDQ_OK (0) or a negative DDQ_E* code; no C++
+ *    exception and no exit() crosses the ABI.  ddq_last_error(ctx) returns the
+ *    message of the last failure on that ctx (ctx == NULL: last global error).
+ *  - The library owns all device memory.  Host pointers are borrowed for the
+ *    duration of the call; a call that takes host buffers copies and
+ *    synchronises before returning unless its name ends in _async.  A
+ *    "*_on_device" flag != 0 means the pointer is a device pointer (e.g. a
+ *    torch tensor's data_ptr()) and the copy is device-to-device.
+ *  - One ddq_ctx per (process, GPU), bound to one HIP stream.  Calls on one
+ *    ctx must be serialised by the caller; different ctxs are independent.
+ *  - Float tensors cross the ABI in the reference's Caffe shapes/orders:
+ *    parameters as one flat fp32 buffer in pycaffe net.params order
+ *    (Qconv1.w, Qconv1.b, ..., Q_out.b), conv W (Cout,Cin,k,k), minibatch
+ *    state/next_state (B,4,S,S), action (B,4,1,1) one-hot, reward and
+ *    non_terminal (B,1,1,1).  Internal device layouts are private.
+ */
+#ifndef DDQ_HIP_H
+#define DDQ_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DDQ_ABI_VERSION 1
+
+enum ddq_status {
+  DDQ_OK = 0,
+  DDQ_EINVAL = -1,   /* bad argument (sizes, names, B >= valid ...)          */
+  DDQ_ENOMEM = -2,   /* device allocation failed                             */
+  DDQ_EHIP = -3,     /* HIP runtime error                                    */
+  DDQ_ERCCL = -4,    /* RCCL error                                           */
+  DDQ_ESTATE = -5,   /* call not valid in the current state (no replay ...)  */
+  DDQ_ERANGE = -6    /* data out of range (e.g. stored action >= num_actions) */
+};
+
+typedef struct ddq_ctx ddq_ctx;
+
+/* Network description.  Replaces train_val.prototxt's MEMORY_DATA dims
+ * (models/deepq/train_val.prototxt:2-37) and the GAMMA coefficient (:473). */
+typedef struct ddq_net_desc {
+  int32_t batch;        /* B, memory_data_param.batch_size (32)               */
+  int32_t frame;        /* S, height == width (16 in deepq16); multiple of 8  */
+  int32_t channels;     /* must be 4 (4-frame history, expgain.py:9)          */
+  int32_t actions;      /* must be 4 (barista/constants.py:8)                 */
+  float gamma;          /* 0.85 (train_val.prototxt:473)                      */
+} ddq_net_desc;
+
+/* One parameter blob of the flat layout (one tower).  Replaces iteration over
+ * pycaffe net.params (messaging.py:57-66, server.py:238-244). */
+typedef struct ddq_blob_desc {
+  char name[16];        /* "Qconv1" ... "Q_out" (P tower: same with 'P')      */
+  int32_t index;        /* 0 = weight, 1 = bias                               */
+  int32_t shape[4];     /* Caffe-2014 4-D blob shape                          */
+  int64_t offset;       /* element offset in the flat tower buffer            */
+  int64_t count;        /* element count                                      */
+} ddq_blob_desc;
+
+/* Update rules of param-server/server.py:81-124 (+ Caffe SGDSolver momentum). */
+enum ddq_rule {
+  DDQ_RULE_SGD = 0,            /* server.py:81-83   theta -= lr*g             */
+  DDQ_RULE_RMSPROP = 1,        /* server.py:86-105  lagged cache (default)    */
+  DDQ_RULE_ADAGRAD = 2,        /* server.py:108-124                           */
+  DDQ_RULE_MOMENTUM_CAFFE = 3  /* solver.prototxt:4-11 semantics (optional)   */
+};
+
+typedef struct ddq_update_cfg {
+  int32_t rule;          /* enum ddq_rule                                     */
+  float lr;              /* server.py:268 default 1e-4 (momentum: base_lr)    */
+  float decay;           /* rmsprop decay, server.py:270 default 0.9          */
+  float eps;             /* 1e-8 inside the sqrt, server.py:105,124           */
+  float momentum;        /* momentum rule only (0.9)                          */
+  float weight_decay;    /* momentum rule only (0.0005)                       */
+} ddq_update_cfg;
+
+/* One fused training step (main.py:61-103 debug_process_connection body,
+ * minus acting): sample B indices (device RNG) -> gather -> P/Q forward ->
+ * Bellman target + loss -> Q backward -> [grad all-reduce] -> apply ->
+ * [P <- Q every target_period steps]. */
+typedef struct ddq_step_cfg {
+  ddq_update_cfg update;
+  int32_t target_period;   /* server.py:274 --special-update (10); 0 = never */
+  int32_t allreduce;       /* 1: sum grads over the RCCL communicator        */
+  uint64_t seed;           /* device index-stream seed (per rank)            */
+} ddq_step_cfg;
+
+/* ---------------- context ---------------------------------------------- */
+/* caffe.Net(prototxt, model) + set_mode_gpu + set_phase_test
+ * (baristanet.py:16, main.py:147-151).  Dropout is identity (TEST phase). */
+int ddq_create(ddq_ctx** out, int device, const ddq_net_desc* desc);
+int ddq_destroy(ddq_ctx* ctx);
+const char* ddq_last_error(const ddq_ctx* ctx);
+int ddq_abi_version(void);
+/* Use an external HIP stream (e.g. torch.cuda.current_stream().cuda_stream). */
+int ddq_set_stream(ddq_ctx* ctx, void* hip_stream);
+int ddq_synchronize(ddq_ctx* ctx);
+
+/* ---------------- parameters ------------------------------------------- */
+/* Number of fp32 parameters of ONE tower (228,132 at S=16,
+ * results/cost-vs-image-size.txt:2). */
+int64_t ddq_num_params(const ddq_ctx* ctx);
+/* net.params names/shapes/offsets (Q tower; P identical with prefix 'P'). */
+int ddq_param_layout(const ddq_ctx* ctx, ddq_blob_desc* out, int32_t cap, int32_t* n);
+/* .data / .diff .flat[:] access (messaging.py:66,111).  which: 0 = Q, 1 = P. */
+int ddq_set_params(ddq_ctx* ctx, int32_t which, const float* src, int64_t n, int32_t src_on_device);
+int ddq_get_params(ddq_ctx* ctx, int32_t which, float* dst, int64_t n, int32_t dst_on_device);
+int ddq_get_grads(ddq_ctx* ctx, float* dst, int64_t n, int32_t dst_on_device);
+int ddq_set_grads(ddq_ctx* ctx, const float* src, int64_t n, int32_t src_on_device);
+/* special_update_transform_model (server.py:127-137): P <- Q. */
+int ddq_sync_target(ddq_ctx* ctx);
+
+/* ---------------- replay (replay.py) ----------------------------------- */
+/* ReplayDataset.__init__ storage (replay.py:48-61), HBM resident, zeroed. */
+int ddq_replay_create(ddq_ctx* ctx, int64_t capacity);
+/* add_experience (replay.py:70-92); state == NULL marks a terminal step and
+ * leaves the slot stale.  state: 4*S*S uint8 (C,H,W). */
+int ddq_replay_add(ddq_ctx* ctx, int32_t action, int32_t reward, const uint8_t* state);
+int ddq_replay_info(const ddq_ctx* ctx, int64_t* head, int64_t* valid, int64_t* capacity);
+/* Bulk load / store of the ring (the HDF5 datasets of replay.py:48-61,
+ * persisted by __del__ :185-192). */
+int ddq_replay_import(ddq_ctx* ctx, const uint8_t* state, const uint8_t* action,
+                      const int16_t* reward, const uint8_t* non_terminal,
+                      int64_t n, int64_t head, int64_t valid);
+int ddq_replay_export(ddq_ctx* ctx, uint8_t* state, uint8_t* action, int16_t* reward,
+                      uint8_t* non_terminal, int64_t n);
+/* sample_direct (replay.py:144-183) given the sorted index list the host
+ * drew (replay.py:152-159): assembles the device minibatch bit-exactly.
+ * Returns DDQ_EINVAL if B >= valid (replay.py:147-150). */
+int ddq_replay_sample(ddq_ctx* ctx, const int32_t* sorted_idx, int32_t batch);
+/* Device-RNG draw of B distinct indices in [0,valid) \ {head-1}, sorted,
+ * then the same gather (perf mode).  Enqueued, no sync. */
+int ddq_replay_sample_device_async(ddq_ctx* ctx, uint64_t seed);
+/* Copy the current device minibatch out in Caffe shapes (baristanet.py:30-34). */
+int ddq_read_minibatch(ddq_ctx* ctx, float* state, float* action, float* reward,
+                       float* next_state, float* non_terminal);
+/* Set the minibatch directly (set_input_arrays binding, baristanet.py:41-43;
+ * dummy_load_minibatch :70-83). */
+int ddq_write_minibatch(ddq_ctx* ctx, const float* state, const float* action,
+                        const float* reward, const float* next_state,
+                        const float* non_terminal);
+/* Last sorted index list used by the gather (device -> host). */
+int ddq_read_indices(ddq_ctx* ctx, int32_t* idx, int32_t batch);
+
+/* ---------------- compute ---------------------------------------------- */
+/* net.forward(); net.backward() (baristanet.py:138-140).  loss may be NULL. */
+int ddq_forward_backward(ddq_ctx* ctx, float* loss);
+int ddq_forward_backward_async(ddq_ctx* ctx);
+/* forward(end='Q_out') over the bound minibatch (baristanet.py:144). */
+int ddq_forward_q(ddq_ctx* ctx);
+/* net.blobs[name].data for name in {"Q_out","P_out","Q_sa","P_sa",
+ * "target_Q_sa","loss"} (B*4, B*4, B, B, B, 1 floats). */
+int ddq_read_blob(ddq_ctx* ctx, const char* name, float* dst, int64_t n);
+/* Argmax/ReLU routing bytes of pool layer 1..3 of the Q tower for the last
+ * forward_backward, in Caffe (B,C,H/2,W/2) order: 0..3 = first-max position
+ * in the 2x2 window (row-major), 4 = window max <= 0 (no gradient). */
+int ddq_read_pool_mask(ddq_ctx* ctx, int32_t layer, uint8_t* dst, int64_t n);
+/* select_action (baristanet.py:142-146) for n states (n <= B, uint8 C,H,W):
+ * argmax_a Q(s,a), first max wins.  Does not touch the bound minibatch. */
+int ddq_select_action(ddq_ctx* ctx, const uint8_t* states, int32_t n, int32_t* actions);
+
+/* ---------------- apply (param server) --------------------------------- */
+/* apply_descent + update_fn (server.py:49-124) on the Q tower with the
+ * current gradient buffer.  Optimizer state lives on device. */
+int ddq_apply(ddq_ctx* ctx, const ddq_update_cfg* cfg);
+int ddq_apply_async(ddq_ctx* ctx, const ddq_update_cfg* cfg);
+/* Forget rmsprop/adagrad/momentum state (server.py:229-231 clear()). */
+int ddq_reset_optimizer(ddq_ctx* ctx);
+int ddq_get_optimizer_state(ddq_ctx* ctx, float* dst, int64_t n);
+
+/* ---------------- communication (RCCL over xGMI) ----------------------- */
+/* Replace the HTTP/Redis gradient round trip (baristanet.py:105-123,
+ * server.py:196-209) with a sum all-reduce of the flat gradient buffer. */
+int ddq_comm_get_unique_id(uint8_t id[128]);
+int ddq_comm_init(ddq_ctx* ctx, const uint8_t id[128], int32_t nranks, int32_t rank);
+int ddq_allreduce_grads(ddq_ctx* ctx);
+int ddq_allreduce_grads_async(ddq_ctx* ctx);
+
+/* ---------------- fused step + graphs ---------------------------------- */
+int ddq_step_async(ddq_ctx* ctx, const ddq_step_cfg* cfg);
+/* Capture one step into a hipGraph (re-captured when cfg changes) and replay
+ * it nsteps times back to back.  Enqueued, no sync. */
+int ddq_step_graph_async(ddq_ctx* ctx, const ddq_step_cfg* cfg, int32_t nsteps);
+/* Steps taken so far (drives the target-sync period). */
+int64_t ddq_step_count(const ddq_ctx* ctx);
+
+/* ---------------- measurement ------------------------------------------ */
+/* Kernel ids for ddq_profile_step. */
+#define DDQ_MAX_KERNELS 32
+/* Run one eager step with HIP events around every kernel on the ctx stream;
+ * fills names (16 chars each, NUL padded) and device-time microseconds. */
+int ddq_profile_step(ddq_ctx* ctx, const ddq_step_cfg* cfg, char* names, float* usec,
+                     int32_t cap, int32_t* n);
+/* Algorithmic FLOPs of one step (SURVEY.md 8(d) model, for the roofline). */
+double ddq_step_flops(const ddq_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DDQ_HIP_H */
