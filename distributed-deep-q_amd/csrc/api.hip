@@ -50,6 +50,7 @@ struct ddq_ctx {
   ddq_step_cfg gcfg{};
   bool have_graph = false;
   int64_t steps = 0;
+  int64_t applied = 0;               // host mirror of the device iteration counter
   // profiling marks
   std::vector<std::pair<std::string, hipEvent_t>> marks;
   std::vector<hipEvent_t> ev_pool;
@@ -87,8 +88,11 @@ static int dalloc(ddq_ctx* c, T** p, size_t count) {
   const size_t bytes = std::max<size_t>(count * sizeof(T), 16);
   hipError_t e = hipMalloc(&q, bytes);
   if (e != hipSuccess) return fail(c, DDQ_ENOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
-  e = hipMemset(q, 0, bytes);
-  if (e != hipSuccess) return fail(c, DDQ_EHIP, "hipMemset failed: %s", hipGetErrorString(e));
+  // stream-ordered zero fill: every device access of the ctx goes through
+  // c->stream (a non-blocking stream does not order against the null stream)
+  e = hipMemsetAsync(q, 0, bytes, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) return fail(c, DDQ_EHIP, "hipMemsetAsync failed: %s", hipGetErrorString(e));
   c->allocs.push_back(q);
   *p = reinterpret_cast<T*>(q);
   return DDQ_OK;
@@ -99,6 +103,13 @@ static int dalloc(ddq_ctx* c, T** p, size_t count) {
     int r_ = (x);             \
     if (r_ != DDQ_OK) return r_; \
   } while (0)
+
+// Blocking copy ordered on the ctx stream.
+static hipError_t scopy(ddq_ctx* c, void* dst, const void* src, size_t bytes, hipMemcpyKind kind) {
+  hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, c->stream);
+  if (e != hipSuccess) return e;
+  return hipStreamSynchronize(c->stream);
+}
 
 static int set_dev(ddq_ctx* c) {
   HIP_TRY(c, hipSetDevice(c->device));
@@ -145,6 +156,8 @@ int ddq_create(ddq_ctx** out, int device, const ddq_net_desc* desc) {
     TRY(set_dev(c));
     HIP_TRY(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     NetBuffers& nb = c->nb;
+    HIP_TRY(c, hipStreamCreateWithFlags(&nb.side, hipStreamNonBlocking));
+    for (auto& e : nb.ev) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     const int B = desc->batch, S = desc->frame;
     nb.B = B; nb.S = S; nb.gamma = desc->gamma;
     nb.L = make_layout(S);
@@ -222,6 +235,9 @@ int ddq_destroy(ddq_ctx* c) {
   if (c->comm) ncclCommDestroy(c->comm);
   for (void* p : c->allocs) hipFree(p);
   if (c->stream && c->own_stream) hipStreamDestroy(c->stream);
+  for (auto& e : c->nb.ev)
+    if (e) hipEventDestroy(e);
+  if (c->nb.side) hipStreamDestroy(c->nb.side);
   delete c;
   return DDQ_OK;
 }
@@ -362,7 +378,7 @@ int ddq_replay_create(ddq_ctx* c, int64_t capacity) {
   c->head = c->valid = 0;
   ReplayMeta m{};
   m.capacity = capacity;
-  HIP_TRY(c, hipMemcpy(c->r_meta, &m, sizeof(m), hipMemcpyHostToDevice));
+  HIP_TRY(c, scopy(c, c->r_meta, &m, sizeof(m), hipMemcpyHostToDevice));
   invalidate_graph(c);
   return DDQ_OK;
 }
@@ -406,10 +422,10 @@ int ddq_replay_import(ddq_ctx* c, const uint8_t* state, const uint8_t* action,
     return fail(c, DDQ_EINVAL, "head/valid out of range");
   TRY(set_dev(c));
   const size_t slot = (size_t)4 * c->nb.S * c->nb.S;
-  HIP_TRY(c, hipMemcpy(c->r_state, state, slot * n, hipMemcpyHostToDevice));
-  HIP_TRY(c, hipMemcpy(c->r_action, action, n, hipMemcpyHostToDevice));
-  HIP_TRY(c, hipMemcpy(c->r_reward, reward, 2 * n, hipMemcpyHostToDevice));
-  HIP_TRY(c, hipMemcpy(c->r_nonterm, nonterm, n, hipMemcpyHostToDevice));
+  HIP_TRY(c, scopy(c, c->r_state, state, slot * n, hipMemcpyHostToDevice));
+  HIP_TRY(c, scopy(c, c->r_action, action, n, hipMemcpyHostToDevice));
+  HIP_TRY(c, scopy(c, c->r_reward, reward, 2 * n, hipMemcpyHostToDevice));
+  HIP_TRY(c, scopy(c, c->r_nonterm, nonterm, n, hipMemcpyHostToDevice));
   c->head = head;
   c->valid = valid;
   return push_meta(c);
@@ -423,10 +439,10 @@ int ddq_replay_export(ddq_ctx* c, uint8_t* state, uint8_t* action, int16_t* rewa
   TRY(set_dev(c));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   const size_t slot = (size_t)4 * c->nb.S * c->nb.S;
-  if (state) HIP_TRY(c, hipMemcpy(state, c->r_state, slot * n, hipMemcpyDeviceToHost));
-  if (action) HIP_TRY(c, hipMemcpy(action, c->r_action, n, hipMemcpyDeviceToHost));
-  if (reward) HIP_TRY(c, hipMemcpy(reward, c->r_reward, 2 * n, hipMemcpyDeviceToHost));
-  if (nonterm) HIP_TRY(c, hipMemcpy(nonterm, c->r_nonterm, n, hipMemcpyDeviceToHost));
+  if (state) HIP_TRY(c, scopy(c, state, c->r_state, slot * n, hipMemcpyDeviceToHost));
+  if (action) HIP_TRY(c, scopy(c, action, c->r_action, n, hipMemcpyDeviceToHost));
+  if (reward) HIP_TRY(c, scopy(c, reward, c->r_reward, 2 * n, hipMemcpyDeviceToHost));
+  if (nonterm) HIP_TRY(c, scopy(c, nonterm, c->r_nonterm, n, hipMemcpyDeviceToHost));
   return DDQ_OK;
 }
 
@@ -436,7 +452,7 @@ static int check_err_flag(ddq_ctx* c) {
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   if (m.err) {
     int32_t z = 0;
-    HIP_TRY(c, hipMemcpy(reinterpret_cast<char*>(c->r_meta) + offsetof(ReplayMeta, err), &z, 4,
+    HIP_TRY(c, scopy(c, reinterpret_cast<char*>(c->r_meta) + offsetof(ReplayMeta, err), &z, 4,
                          hipMemcpyHostToDevice));
     return fail(c, DDQ_ERANGE, "stored action index out of range for %d actions", 4);
   }
@@ -493,16 +509,16 @@ int ddq_read_minibatch(ddq_ctx* c, float* state, float* action, float* reward, f
   for (int which = 0; which < 2; ++which) {
     float* dst = which ? next_state : state;
     if (!dst) continue;
-    HIP_TRY(c, hipMemcpy(tmp.data(), which ? c->nb.next_state : c->nb.state, tmp.size() * 4,
+    HIP_TRY(c, scopy(c, tmp.data(), which ? c->nb.next_state : c->nb.state, tmp.size() * 4,
                          hipMemcpyDeviceToHost));
     for (int b = 0; b < B; ++b)
       for (int ch = 0; ch < 4; ++ch)
         for (int p = 0; p < SS; ++p)
           dst[((size_t)b * 4 + ch) * SS + p] = tmp[((size_t)b * SS + p) * 4 + ch];
   }
-  if (action) HIP_TRY(c, hipMemcpy(action, c->nb.action, B * 16, hipMemcpyDeviceToHost));
-  if (reward) HIP_TRY(c, hipMemcpy(reward, c->nb.reward, B * 4, hipMemcpyDeviceToHost));
-  if (nonterm) HIP_TRY(c, hipMemcpy(nonterm, c->nb.nonterm, B * 4, hipMemcpyDeviceToHost));
+  if (action) HIP_TRY(c, scopy(c, action, c->nb.action, B * 16, hipMemcpyDeviceToHost));
+  if (reward) HIP_TRY(c, scopy(c, reward, c->nb.reward, B * 4, hipMemcpyDeviceToHost));
+  if (nonterm) HIP_TRY(c, scopy(c, nonterm, c->nb.nonterm, B * 4, hipMemcpyDeviceToHost));
   return DDQ_OK;
 }
 
@@ -520,12 +536,12 @@ int ddq_write_minibatch(ddq_ctx* c, const float* state, const float* action, con
       for (int ch = 0; ch < 4; ++ch)
         for (int p = 0; p < SS; ++p)
           tmp[((size_t)b * SS + p) * 4 + ch] = src[((size_t)b * 4 + ch) * SS + p];
-    HIP_TRY(c, hipMemcpy(which ? c->nb.next_state : c->nb.state, tmp.data(), tmp.size() * 4,
+    HIP_TRY(c, scopy(c, which ? c->nb.next_state : c->nb.state, tmp.data(), tmp.size() * 4,
                          hipMemcpyHostToDevice));
   }
-  if (action) HIP_TRY(c, hipMemcpy(c->nb.action, action, B * 16, hipMemcpyHostToDevice));
-  if (reward) HIP_TRY(c, hipMemcpy(c->nb.reward, reward, B * 4, hipMemcpyHostToDevice));
-  if (nonterm) HIP_TRY(c, hipMemcpy(c->nb.nonterm, nonterm, B * 4, hipMemcpyHostToDevice));
+  if (action) HIP_TRY(c, scopy(c, c->nb.action, action, B * 16, hipMemcpyHostToDevice));
+  if (reward) HIP_TRY(c, scopy(c, c->nb.reward, reward, B * 4, hipMemcpyHostToDevice));
+  if (nonterm) HIP_TRY(c, scopy(c, c->nb.nonterm, nonterm, B * 4, hipMemcpyHostToDevice));
   return DDQ_OK;
 }
 
@@ -534,7 +550,8 @@ static int enqueue_fwd_bwd(ddq_ctx* c, void (*mark)(void*, const char*), void* m
   HIP_TRY(c, launch_forward(c->nb, 2, c->stream, mark, marg));
   if (mark) mark(marg, "head");
   HIP_TRY(c, launch_head(c->nb, c->stream));
-  HIP_TRY(c, launch_backward(c->nb, c->stream, mark, marg));
+  // per-kernel event timing needs one stream; otherwise overlap wgrad with dgrad
+  HIP_TRY(c, launch_backward(c->nb, c->stream, mark, marg, mark == nullptr));
   return DDQ_OK;
 }
 
@@ -587,7 +604,7 @@ int ddq_read_pool_mask(ddq_ctx* c, int32_t layer, uint8_t* dst, int64_t n) {
   std::vector<uint8_t> tmp(cnt);
   const uint8_t* src = layer == 1 ? c->nb.mask1 : (layer == 2 ? c->nb.mask2 : c->nb.mask3);
   HIP_TRY(c, hipStreamSynchronize(c->stream));
-  HIP_TRY(c, hipMemcpy(tmp.data(), src, cnt, hipMemcpyDeviceToHost));
+  HIP_TRY(c, scopy(c, tmp.data(), src, cnt, hipMemcpyDeviceToHost));
   for (int b = 0; b < B; ++b)
     for (int ch = 0; ch < C; ++ch)
       for (int p = 0; p < Hp * Hp; ++p)
@@ -621,7 +638,8 @@ int ddq_apply_async(ddq_ctx* c, const ddq_update_cfg* u) {
   TRY(check_cfg(c, u));
   TRY(set_dev(c));
   HIP_TRY(c, launch_apply(c->nb, u->rule, u->lr, u->decay, u->eps, u->momentum, u->weight_decay,
-                          c->stream));
+                          0, c->stream));
+  c->applied++;
   return DDQ_OK;
 }
 
@@ -636,6 +654,9 @@ int ddq_reset_optimizer(ddq_ctx* c) {
   TRY(set_dev(c));
   HIP_TRY(c, hipMemsetAsync(c->nb.opt, 0, c->nb.L.total * 4, c->stream));
   HIP_TRY(c, hipMemsetAsync(c->nb.opt_init, 0, 4, c->stream));
+  HIP_TRY(c, hipMemsetAsync(c->nb.iter, 0, 8, c->stream));
+  c->applied = 0;
+  c->steps = 0;
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return DDQ_OK;
 }
@@ -689,8 +710,6 @@ int ddq_allreduce_grads(ddq_ctx* c) {
 // ---------------- step ----------------
 static int enqueue_step(ddq_ctx* c, const ddq_step_cfg* cfg, void (*mark)(void*, const char*),
                         void* marg) {
-  if (mark) mark(marg, "target_sync");
-  HIP_TRY(c, launch_target_sync_if(c->nb, cfg->target_period, c->stream));
   if (mark) mark(marg, "sample");
   HIP_TRY(c, launch_sample(c->nb, c->r_meta, cfg->seed, c->stream));
   if (mark) mark(marg, "gather");
@@ -705,7 +724,19 @@ static int enqueue_step(ddq_ctx* c, const ddq_step_cfg* cfg, void (*mark)(void*,
   if (mark) mark(marg, "apply");
   const ddq_update_cfg& u = cfg->update;
   HIP_TRY(c, launch_apply(c->nb, u.rule, u.lr, u.decay, u.eps, u.momentum, u.weight_decay,
-                          c->stream));
+                          cfg->target_period, c->stream));
+  return DDQ_OK;
+}
+
+// The pull at iteration 0 copies Q -> P (server.py:188-189, 0 % period == 0);
+// later syncs are fused into the apply kernel of the preceding update.
+static int initial_target_sync(ddq_ctx* c, const ddq_step_cfg* cfg) {
+  if (cfg->target_period > 0 && c->applied % cfg->target_period == 0) {
+    HIP_TRY(c, hipMemcpyAsync(c->nb.theta[1], c->nb.theta[0], c->nb.L.total * 4,
+                              hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->nb.wk[1], c->nb.wk[0], c->nb.L.wk_total * 4,
+                              hipMemcpyDeviceToDevice, c->stream));
+  }
   return DDQ_OK;
 }
 
@@ -724,8 +755,10 @@ static int check_step(ddq_ctx* c, const ddq_step_cfg* cfg) {
 int ddq_step_async(ddq_ctx* c, const ddq_step_cfg* cfg) {
   TRY(check_step(c, cfg));
   TRY(set_dev(c));
+  if (c->steps == 0) TRY(initial_target_sync(c, cfg));
   TRY(enqueue_step(c, cfg, nullptr, nullptr));
   c->steps++;
+  c->applied++;
   return DDQ_OK;
 }
 
@@ -745,9 +778,11 @@ int ddq_step_graph_async(ddq_ctx* c, const ddq_step_cfg* cfg, int32_t nsteps) {
     c->gcfg = *cfg;
     c->have_graph = true;
   }
+  if (c->steps == 0 && nsteps > 0) TRY(initial_target_sync(c, cfg));
   for (int i = 0; i < nsteps; ++i) {
     HIP_TRY(c, hipGraphLaunch(c->gexec, c->stream));
     c->steps++;
+    c->applied++;
   }
   return DDQ_OK;
 }
@@ -774,9 +809,11 @@ int ddq_profile_step(ddq_ctx* c, const ddq_step_cfg* cfg, char* names, float* us
   TRY(set_dev(c));
   c->marks.clear();
   c->ev_used = 0;
+  if (c->steps == 0) TRY(initial_target_sync(c, cfg));
   TRY(enqueue_step(c, cfg, mark_cb, c));
   mark_cb(c, "end");
   c->steps++;
+  c->applied++;
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   const int k = (int)c->marks.size() - 1;
   *n = k;

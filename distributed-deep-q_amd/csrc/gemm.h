@@ -14,40 +14,46 @@
 //   static constexpr bool kAK4, kBK4;   // loader returns 4 consecutive k (true)
 //                                       // or 4 consecutive m / n (false)
 //   struct ACtx; struct BCtx;           // per-thread-slot state fixed over K
-//   ACtx actx(int z, int m) const;      // (m of the slot; K4 mode) or
-//                                       // (m4 of the slot; MN4 mode)
+//   ACtx actx(int z, int m) const;      BCtx bctx(int z, int n) const;
 //   float4 loadA(int z, const ACtx&, int m, int k) const;
-//   BCtx bctx(int z, int n) const;  float4 loadB(int z, const BCtx&, int k, int n) const;
-//   template <class Acc> void epilogue(int z, int split, int m0, int n0,
-//                                      const Acc& acc, int lane) const;
+//   float4 loadB(int z, const BCtx&, int k, int n) const;
+//   void epilogue(int z, int split, int m0, int n0, const f32x16& acc, int lane) const;
 //   int M, N, K, ksplit_len;            // K range per split (multiple of BK)
 //
-// Tiling: workgroup BM x BN, K-step BK, WM x WN waves, each wave owns a
-// (BM/WM) x (BN/WN) sub-tile of 32x32 MFMA blocks.  Operands are staged
-// global -> registers -> LDS with a two-buffer ring (one barrier per K-step;
-// the next tile's global loads are in flight under the current tile's MFMAs).
-// LDS images are [k][m] / [k][n] so one wave-wide ds_read_b32 per operand
-// and k-pair feeds an MFMA conflict-free (lanes 0-31 and 32-63 read two
-// 32-dword rows).
+// Tiling: workgroup BM x BN, K-step BK, WM x WN x WK waves.  Each (wm, wn)
+// wave group owns a (BM/WM) x (BN/WN) sub-tile of 32x32 MFMA blocks; the WK
+// waves of a group split every K-step's depth between them (more waves per
+// workgroup = more latency hiding and more MFMA work per barrier for the
+// skinny / long-K shapes of this network) and are summed through LDS at the
+// end.  Operands are staged global -> registers -> LDS with a two-buffer ring
+// (one barrier per K-step; the next tile's global loads are in flight under
+// the current tile's MFMAs).  LDS images are [k][m] / [k][n] so one wave-wide
+// ds_read_b32 per operand and k-pair feeds an MFMA conflict-free (lanes 0-31
+// and 32-63 read two 32-dword rows).
 #pragma once
 #include "common.h"
 
 namespace ddq {
 
-template <int BM_, int BN_, int BK_, int WM_, int WN_>
+template <int BM_, int BN_, int BK_, int WM_, int WN_, int WK_ = 1>
 struct GemmCfg {
-  static constexpr int BM = BM_, BN = BN_, BK = BK_, WM = WM_, WN = WN_;
-  static constexpr int kThreads = 64 * WM * WN;
+  static constexpr int BM = BM_, BN = BN_, BK = BK_, WM = WM_, WN = WN_, WK = WK_;
+  static constexpr int kThreads = 64 * WM * WN * WK;
   static constexpr int TM = BM / WM / 32;   // 32x32 blocks per wave along m
   static constexpr int TN = BN / WN / 32;
   static constexpr int APAD = 4, BPAD = 4;  // keeps float4 LDS writes aligned
   static constexpr int LDA = BM + APAD, LDB = BN + BPAD;
+  static constexpr int KW = BK / WK;        // k depth per wave per K-step
+  static constexpr int kStage = 2 * BK * (LDA + LDB);
+  static constexpr int kRed = (WK - 1) * BM * BN;
+  static constexpr int kSmem = kStage > kRed ? kStage : kRed;
   static_assert(TM >= 1 && TN >= 1, "wave tile must be >= 32x32");
-  static_assert(BK % 4 == 0, "BK multiple of 4");
+  static_assert(BK % 4 == 0 && KW % 2 == 0 && BK % WK == 0, "bad BK / WK");
+  static_assert(kSmem * 4 <= 160 * 1024, "LDS budget");
 };
 
 // Number of float4 slots each thread stages per K-step.
-template <class C, bool K4, int DIM>
+template <class C, int DIM>
 struct Slots {
   static constexpr int kElems = DIM * C::BK / 4;
   static constexpr int kPer = (kElems + C::kThreads - 1) / C::kThreads;
@@ -58,18 +64,20 @@ __global__ __launch_bounds__(C::kThreads) void gemm_f32_kernel(const P prob) {
   constexpr int BM = C::BM, BN = C::BN, BK = C::BK;
   constexpr int TM = C::TM, TN = C::TN;
   constexpr int LDA = C::LDA, LDB = C::LDB;
-  using SA = Slots<C, P::kAK4, BM>;
-  using SB = Slots<C, P::kBK4, BN>;
+  using SA = Slots<C, BM>;
+  using SB = Slots<C, BN>;
 
-  __shared__ __attribute__((aligned(16))) float smem[2 * BK * (LDA + LDB)];
+  __shared__ __attribute__((aligned(16))) float smem[C::kSmem];
   float* As = smem;                    // [2][BK][LDA]
   float* Bs = smem + 2 * BK * LDA;     // [2][BK][LDB]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
-  const int wm = (wid / C::WN) * (BM / C::WM);
-  const int wn = (wid % C::WN) * (BN / C::WN);
+  const int wk = wid / (C::WM * C::WN);
+  const int w2 = wid % (C::WM * C::WN);
+  const int wm = (w2 / C::WN) * (BM / C::WM);
+  const int wn = (w2 % C::WN) * (BN / C::WN);
 
   const int z = blockIdx.z;
   const int split = blockIdx.y;
@@ -106,12 +114,12 @@ __global__ __launch_bounds__(C::kThreads) void gemm_f32_kernel(const P prob) {
     const int kb = kbeg + kt * BK;
 #pragma unroll
     for (int s = 0; s < SA::kPer; ++s) {
-      bool in = (tid + s * C::kThreads) < SA::kElems;
+      bool in = (SA::kElems % C::kThreads == 0) || (tid + s * C::kThreads) < SA::kElems;
       ra[s] = in ? prob.loadA(z, actx[s], m0 + a_mn[s], kb + a_k[s]) : f4zero();
     }
 #pragma unroll
     for (int s = 0; s < SB::kPer; ++s) {
-      bool in = (tid + s * C::kThreads) < SB::kElems;
+      bool in = (SB::kElems % C::kThreads == 0) || (tid + s * C::kThreads) < SB::kElems;
       rb[s] = in ? prob.loadB(z, bctx[s], kb + b_k[s], n0 + b_mn[s]) : f4zero();
     }
   };
@@ -120,7 +128,7 @@ __global__ __launch_bounds__(C::kThreads) void gemm_f32_kernel(const P prob) {
     float* bs = Bs + buf * BK * LDB;
 #pragma unroll
     for (int s = 0; s < SA::kPer; ++s) {
-      if ((tid + s * C::kThreads) >= SA::kElems) continue;
+      if ((SA::kElems % C::kThreads) && (tid + s * C::kThreads) >= SA::kElems) continue;
       if (P::kAK4) {
         as[(a_k[s] + 0) * LDA + a_mn[s]] = ra[s].x;
         as[(a_k[s] + 1) * LDA + a_mn[s]] = ra[s].y;
@@ -132,7 +140,7 @@ __global__ __launch_bounds__(C::kThreads) void gemm_f32_kernel(const P prob) {
     }
 #pragma unroll
     for (int s = 0; s < SB::kPer; ++s) {
-      if ((tid + s * C::kThreads) >= SB::kElems) continue;
+      if ((SB::kElems % C::kThreads) && (tid + s * C::kThreads) >= SB::kElems) continue;
       if (P::kBK4) {
         bs[(b_k[s] + 0) * LDB + b_mn[s]] = rb[s].x;
         bs[(b_k[s] + 1) * LDB + b_mn[s]] = rb[s].y;
@@ -163,10 +171,10 @@ __global__ __launch_bounds__(C::kThreads) void gemm_f32_kernel(const P prob) {
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) gload(kt + 1);
-    const float* as = As + cur * BK * LDA + kh * LDA + wm + l31;
-    const float* bs = Bs + cur * BK * LDB + kh * LDB + wn + l31;
+    const float* as = As + cur * BK * LDA + (wk * C::KW + kh) * LDA + wm + l31;
+    const float* bs = Bs + cur * BK * LDB + (wk * C::KW + kh) * LDB + wn + l31;
 #pragma unroll
-    for (int kk = 0; kk < BK; kk += 2) {
+    for (int kk = 0; kk < C::KW; kk += 2) {
       float a[TM], b[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) a[i] = as[kk * LDA + 32 * i];
@@ -180,6 +188,33 @@ __global__ __launch_bounds__(C::kThreads) void gemm_f32_kernel(const P prob) {
     }
     if (kt + 1 < nk) lstore(cur ^ 1);
     __syncthreads();
+  }
+
+  if constexpr (C::WK > 1) {
+    // sum the WK partial accumulators of each (wm, wn) group through LDS
+    float* red = smem;   // [(WK-1)][WM*WN][TM][TN][16][64]
+    constexpr int per = TM * TN * 16 * 64;
+    if (wk > 0) {
+      float* dst = red + ((wk - 1) * C::WM * C::WN + w2) * per + lane;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) dst[((i * TN + j) * 16 + r) * 64] = acc[i][j][r];
+    }
+    __syncthreads();
+    if (wk > 0) return;
+#pragma unroll
+    for (int q = 1; q < C::WK; ++q) {
+      const float* src = red + ((q - 1) * C::WM * C::WN + w2) * per + lane;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] += src[((i * TN + j) * 16 + r) * 64];
+    }
   }
 
   // Accumulator (i, j) register r of this lane holds

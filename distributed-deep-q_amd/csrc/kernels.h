@@ -49,6 +49,9 @@ struct NetBuffers {
   float *theta[2], *wk[2], *grad, *opt;
   int32_t* opt_init;                // 0 until the first apply after a reset
   int64_t* iter;                    // applied updates (param-server iteration)
+  // second stream + events for concurrent wgrad / dgrad branches (optional)
+  hipStream_t side;
+  hipEvent_t ev[8];
   ParamLayout L;
   float gamma;
 };
@@ -57,12 +60,14 @@ hipError_t launch_gather(const NetBuffers& nb, const uint8_t* st, const uint8_t*
                          const int16_t* rew, const uint8_t* nt, ReplayMeta* meta,
                          hipStream_t s);
 hipError_t launch_sample(const NetBuffers& nb, ReplayMeta* meta, uint64_t seed, hipStream_t s);
-hipError_t launch_target_sync_if(const NetBuffers& nb, int period, hipStream_t s);
 hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s, void (*mark)(void*, const char*), void* mark_arg);
 hipError_t launch_head(const NetBuffers& nb, hipStream_t s);
-hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(void*, const char*), void* mark_arg);
+// concurrent: run the weight-gradient GEMMs on nb.side beside the data-gradient chain.
+hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(void*, const char*),
+                           void* mark_arg, bool concurrent);
+// period > 0: also copy Q -> P when the next pull sees iteration % period == 0.
 hipError_t launch_apply(const NetBuffers& nb, int rule, float lr, float decay, float eps,
-                        float momentum, float wd, hipStream_t s);
+                        float momentum, float wd, int period, hipStream_t s);
 hipError_t launch_relayout(const NetBuffers& nb, int z, hipStream_t s);
 // Q-tower forward of n states (NHWC f32 in `in`) into scratch, argmax into out.
 hipError_t launch_act(const NetBuffers& nb, const float* in, int n, float* pool1, float* pool2,

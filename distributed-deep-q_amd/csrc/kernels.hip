@@ -135,7 +135,9 @@ __global__ __launch_bounds__(256) void gather_kernel(
 }
 
 hipError_t launch_sample(const NetBuffers& nb, ReplayMeta* meta, uint64_t seed, hipStream_t s) {
-  hipLaunchKernelGGL(sample_kernel, dim3(1), dim3(1024), 0, s, meta, nb.B, seed, nb.idx);
+  int threads = 64;                 // one wave for B <= 64: cheap barriers
+  while (threads < nb.B) threads <<= 1;
+  hipLaunchKernelGGL(sample_kernel, dim3(1), dim3(threads), 0, s, meta, nb.B, seed, nb.idx);
   return hipGetLastError();
 }
 
@@ -162,39 +164,6 @@ __global__ void u8_to_nhwc_kernel(const uint8_t* src, int n, int S, float* dst) 
 hipError_t launch_u8_to_nhwc(const uint8_t* src, int n, int S, float* dst, hipStream_t s) {
   const int tot = n * S * S;
   hipLaunchKernelGGL(u8_to_nhwc_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, src, n, S, dst);
-  return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
-// target sync (server.py:127-137, applied at pull when iteration % period == 0,
-// server.py:188-189): P <- Q for theta and the conv kernel-layout copy.
-// ---------------------------------------------------------------------------
-__global__ void target_sync_kernel(const int64_t* iter, int period, const float* __restrict__ tq,
-                                   float* __restrict__ tp, int64_t n, const float* __restrict__ wq,
-                                   float* __restrict__ wp, int64_t nw) {
-  if (period <= 0 || (*iter % period) != 0) return;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
-  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += stride) {
-    if (i + 3 < n) {
-      *reinterpret_cast<float4*>(tp + i) = *reinterpret_cast<const float4*>(tq + i);
-    } else {
-      for (int64_t j = i; j < n; ++j) tp[j] = tq[j];
-    }
-  }
-  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < nw; i += stride) {
-    if (i + 3 < nw) {
-      *reinterpret_cast<float4*>(wp + i) = *reinterpret_cast<const float4*>(wq + i);
-    } else {
-      for (int64_t j = i; j < nw; ++j) wp[j] = wq[j];
-    }
-  }
-}
-
-hipError_t launch_target_sync_if(const NetBuffers& nb, int period, hipStream_t s) {
-  const int64_t n = nb.L.total;
-  int blocks = (int)std::min<int64_t>(2048, (n / 4 + 255) / 256 + 1);
-  hipLaunchKernelGGL(target_sync_kernel, dim3(blocks), dim3(256), 0, s, nb.iter, period,
-                     nb.theta[0], nb.theta[1], n, nb.wk[0], nb.wk[1], nb.L.wk_total);
   return hipGetLastError();
 }
 
@@ -236,249 +205,315 @@ hipError_t launch_relayout(const NetBuffers& nb, int z, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------
-// fc4 split-K reduce + bias + ReLU (dropout = identity, TEST phase)
+// fc4 split-K reduce + bias + ReLU (dropout = identity, TEST phase) fused with
+// the Q_out / P_out inner product (train_val.prototxt:195-215, :365-383).
+// grid (B, nz), 512 threads: thread n owns h4[z][b][n].
 // ---------------------------------------------------------------------------
-__global__ void fc4_reduce_kernel(const float* __restrict__ part, int splits, int nz, int B,
-                                  const float* __restrict__ b0, const float* __restrict__ b1,
-                                  float* __restrict__ h0, float* __restrict__ h1) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;   // over nz*B*512
-  const int per = B * kFc4;
-  if (i >= nz * per) return;
-  const int z = i / per, r = i % per, n = r % kFc4;
+__global__ __launch_bounds__(512) void fc4_reduce_out_kernel(
+    const float* __restrict__ part, int splits, int nz, int B, const float* __restrict__ b4q,
+    const float* __restrict__ b4p, const float* __restrict__ w5q, const float* __restrict__ b5q,
+    const float* __restrict__ w5p, const float* __restrict__ b5p, float* __restrict__ h4q,
+    float* __restrict__ h4p, float* __restrict__ outq, float* __restrict__ outp) {
+  __shared__ float red[8][4];
+  const int b = blockIdx.x, z = blockIdx.y, n = threadIdx.x;
+  const float* p = part + ((size_t)z * B + b) * kFc4 + n;
+  const size_t stride = (size_t)nz * B * kFc4;
   float acc = 0.f;
-  for (int s = 0; s < splits; ++s) acc += part[((size_t)(s * nz + z) * B) * kFc4 + r];
-  const float v = acc + (z ? b1 : b0)[n];
-  (z ? h1 : h0)[r] = v > 0.f ? v : 0.f;
+  int s = 0;
+  for (; s + 4 <= splits; s += 4) {
+    const float v0 = p[(s + 0) * stride], v1 = p[(s + 1) * stride];
+    const float v2 = p[(s + 2) * stride], v3 = p[(s + 3) * stride];
+    acc += v0; acc += v1; acc += v2; acc += v3;
+  }
+  for (; s < splits; ++s) acc += p[s * stride];
+  const float v = acc + (z ? b4p : b4q)[n];
+  const float h = v > 0.f ? v : 0.f;
+  (z ? h4p : h4q)[(size_t)b * kFc4 + n] = h;
+  const float* w5 = z ? w5p : w5q;
+  float q[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) q[a] = h * w5[a * kFc4 + n];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+    for (int a = 0; a < 4; ++a) q[a] += __shfl_xor(q[a], off);
+  const int w = n >> 6;
+  if ((n & 63) == 0)
+#pragma unroll
+    for (int a = 0; a < 4; ++a) red[w][a] = q[a];
+  __syncthreads();
+  if (n < 4) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t += red[i][n];
+    (z ? outp : outq)[b * 4 + n] = t + (z ? b5p : b5q)[n];
+  }
 }
 
 // ---------------------------------------------------------------------------
-// head: Q_out / P_out, Q(s,a), Bellman target, Euclidean loss and the
-// backward through Q_out (train_val.prototxt:195-215, :385-483):
+// head + Q_out backward (train_val.prototxt:385-483):
 //   Q_sa = sum_a Q*act, P_sa = max_a P * nt, target = 0.85 P_sa + r,
 //   loss = sum (Q_sa-target)^2 / 2B, dQ = act (Q_sa-target)/B,
 //   dW5 = dQ^T h4, db5 = sum dQ, dh4 = (dQ W5) * (h4>0), db4 = sum_b dh4.
-// One workgroup (the whole problem is B x 4 x 512).
+// grid 512/64 workgroups of 256 threads (64 columns x 4 sample groups); every
+// workgroup recomputes the B x 4 head (trivial) so no extra launch is needed.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void head_kernel(
-    int B, float gamma, const float* __restrict__ h4q, const float* __restrict__ h4p,
-    const float* __restrict__ w5q, const float* __restrict__ b5q, const float* __restrict__ w5p,
-    const float* __restrict__ b5p, const float* __restrict__ action,
-    const float* __restrict__ reward, const float* __restrict__ nonterm, float* q_out,
-    float* p_out, float* q_sa_o, float* p_sa_o, float* target_o, float* loss_o,
-    float* __restrict__ gw5, float* __restrict__ gb5, float* __restrict__ gb4,
+__global__ __launch_bounds__(256) void out_bwd_kernel(
+    int B, float gamma, const float* __restrict__ qout, const float* __restrict__ pout,
+    const float* __restrict__ h4q, const float* __restrict__ w5q,
+    const float* __restrict__ action, const float* __restrict__ reward,
+    const float* __restrict__ nonterm, float* q_sa_o, float* p_sa_o, float* target_o,
+    float* loss_o, float* __restrict__ gw5, float* __restrict__ gb5, float* __restrict__ gb4,
     float* __restrict__ dh4) {
-  extern __shared__ float sh[];            // [2][B][4] outputs, [B][4] dQ, red[32]
-  float* outs = sh;
-  float* dq = sh + 2 * B * 4;
-  float* red = dq + B * 4;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, nw = blockDim.x >> 6;
-  // phase 1: 2*B*4 dot products of length 512, one wave each
-  for (int o = w; o < 2 * B * 4; o += nw) {
-    const int z = o / (B * 4), r = o % (B * 4), b = r / 4, a = r % 4;
-    const float* h = (z ? h4p : h4q) + (size_t)b * kFc4;
-    const float* wr = (z ? w5p : w5q) + (size_t)a * kFc4;
-    float acc = 0.f;
-#pragma unroll
-    for (int j = 0; j < kFc4 / 64; ++j) acc += h[lane + 64 * j] * wr[lane + 64 * j];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
-    if (lane == 0) {
-      const float v = acc + (z ? b5p : b5q)[a];
-      outs[o] = v;
-      (z ? p_out : q_out)[r] = v;
-    }
-  }
-  __syncthreads();
-  // phase 2: per-sample target / loss / dQ
+  extern __shared__ float sh[];
+  float* dq = sh;                   // [B][4]
+  float* red = sh + 4 * B;          // [4 groups][64 cols][5]
+  const int t = threadIdx.x, lane = t & 63, g = t >> 6;
   float d2 = 0.f;
-  for (int b = t; b < B; b += blockDim.x) {
-    const float* q = outs + b * 4;
-    const float* p = outs + B * 4 + b * 4;
+  for (int b = t; b < B; b += 256) {
+    const float* q = qout + b * 4;
+    const float* p = pout + b * 4;
     const float* ac = action + b * 4;
-    // ELTWISE PROD then SLICE + SUM (in slice order)
+    // ELTWISE PROD, SLICE, SUM in slice order (train_val.prototxt:386-422)
     float qs = q[0] * ac[0];
     qs += q[1] * ac[1];
     qs += q[2] * ac[2];
     qs += q[3] * ac[3];
-    float ps = fmaxf(fmaxf(p[0], p[1]), fmaxf(p[2], p[3]));
-    ps = ps * nonterm[b];
-    const float tg = gamma * ps + 1.0f * reward[b];
+    float ps = fmaxf(fmaxf(p[0], p[1]), fmaxf(p[2], p[3]));   // SLICE + MAX
+    ps = ps * nonterm[b];                                      // P_sa_or_term
+    const float tg = gamma * ps + 1.0f * reward[b];            // SUM coeff {0.85, 1}
     const float diff = qs - tg;
-    q_sa_o[b] = qs; p_sa_o[b] = ps; target_o[b] = tg;
-    const float g = diff / (float)B;
+    const float gsc = diff / (float)B;                         // EUCLIDEAN_LOSS diff
 #pragma unroll
-    for (int a = 0; a < 4; ++a) dq[b * 4 + a] = ac[a] * g;
+    for (int a = 0; a < 4; ++a) dq[b * 4 + a] = ac[a] * gsc;
+    if (blockIdx.x == 0) { q_sa_o[b] = qs; p_sa_o[b] = ps; target_o[b] = tg; }
     d2 += diff * diff;
   }
-  for (int off = 32; off > 0; off >>= 1) d2 += __shfl_xor(d2, off);
-  if (lane == 0) red[w] = d2;
   __syncthreads();
-  if (t == 0) {
-    float s = 0.f;
-    for (int i = 0; i < nw; ++i) s += red[i];
-    *loss_o = s / (float)B / 2.f;
-  }
-  // phase 3: Q_out backward
-  for (int o = t; o < 4 * kFc4; o += blockDim.x) {       // dW5[a][j]
-    const int a = o / kFc4, j = o % kFc4;
-    float acc = 0.f;
-    for (int b = 0; b < B; ++b) acc += dq[b * 4 + a] * h4q[(size_t)b * kFc4 + j];
-    gw5[o] = acc;
-  }
-  if (t < 4) {
-    float acc = 0.f;
-    for (int b = 0; b < B; ++b) acc += dq[b * 4 + t];
-    gb5[t] = acc;
-  }
-  for (int j = t; j < kFc4; j += blockDim.x) {            // dh4[:, j], db4[j]
-    const float w0 = w5q[j], w1 = w5q[kFc4 + j], w2 = w5q[2 * kFc4 + j], w3 = w5q[3 * kFc4 + j];
-    float db = 0.f;
-    for (int b = 0; b < B; ++b) {
-      const float* d = dq + b * 4;
-      float v = d[0] * w0 + d[1] * w1 + d[2] * w2 + d[3] * w3;
-      v = h4q[(size_t)b * kFc4 + j] > 0.f ? v : 0.f;
-      dh4[(size_t)b * kFc4 + j] = v;
-      db += v;
+  if (blockIdx.x == 0) {
+    for (int off = 32; off > 0; off >>= 1) d2 += __shfl_xor(d2, off);
+    if (lane == 0) red[g] = d2;
+    __syncthreads();
+    if (t == 0) *loss_o = (red[0] + red[1] + red[2] + red[3]) / (float)B / 2.f;
+    if (t < 4) {
+      float acc = 0.f;
+      for (int b = 0; b < B; ++b) acc += dq[b * 4 + t];
+      gb5[t] = acc;
     }
-    gb4[j] = db;
+    __syncthreads();
+  }
+  const int j = blockIdx.x * 64 + lane;
+  const float w0 = w5q[j], w1 = w5q[kFc4 + j], w2 = w5q[2 * kFc4 + j], w3 = w5q[3 * kFc4 + j];
+  float db = 0.f, dw[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int b = g; b < B; b += 4) {
+    const float* d = dq + b * 4;
+    const float h = h4q[(size_t)b * kFc4 + j];
+    float v = d[0] * w0 + d[1] * w1 + d[2] * w2 + d[3] * w3;
+    v = h > 0.f ? v : 0.f;                                     // ReLU backward
+    dh4[(size_t)b * kFc4 + j] = v;
+    db += v;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) dw[a] += d[a] * h;
+  }
+  float* r = red + (g * 64 + lane) * 5;
+  r[0] = db;
+#pragma unroll
+  for (int a = 0; a < 4; ++a) r[1 + a] = dw[a];
+  __syncthreads();
+  if (g == 0) {
+    float s[5];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) s[q] = red[lane * 5 + q];
+#pragma unroll
+    for (int gg = 1; gg < 4; ++gg)
+#pragma unroll
+      for (int q = 0; q < 5; ++q) s[q] += red[(gg * 64 + lane) * 5 + q];
+    gb4[j] = s[0];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) gw5[a * kFc4 + j] = s[1 + a];
   }
 }
 
 hipError_t launch_head(const NetBuffers& nb, hipStream_t s) {
   const ParamLayout& L = nb.L;
-  const size_t shm = (size_t)(2 * nb.B * 4 + nb.B * 4 + 32) * sizeof(float);
-  hipLaunchKernelGGL(head_kernel, dim3(1), dim3(1024), shm, s, nb.B, nb.gamma, nb.h4[0],
-                     nb.h4[1], nb.theta[0] + L.w[4], nb.theta[0] + L.b[4], nb.theta[1] + L.w[4],
-                     nb.theta[1] + L.b[4], nb.action, nb.reward, nb.nonterm, nb.q_out, nb.p_out,
-                     nb.q_sa, nb.p_sa, nb.target, nb.loss, nb.grad + L.w[4], nb.grad + L.b[4],
-                     nb.grad + L.b[3], nb.dh4);
+  const size_t shm = (size_t)(4 * nb.B + 4 * 64 * 5) * sizeof(float);
+  hipLaunchKernelGGL(out_bwd_kernel, dim3(kFc4 / 64), dim3(256), shm, s, nb.B, nb.gamma,
+                     nb.q_out, nb.p_out, nb.h4[0], nb.theta[0] + L.w[4], nb.action, nb.reward,
+                     nb.nonterm, nb.q_sa, nb.p_sa, nb.target, nb.loss, nb.grad + L.w[4],
+                     nb.grad + L.b[4], nb.grad + L.b[3], nb.dh4);
   return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
-// conv wgrad slab reduce -> Caffe (co,ci,ky,kx) weight diff + bias diff
+// conv wgrad slab reduce -> Caffe (co,ci,ky,kx) weight diff + bias diff.
+// One workgroup = 64 consecutive slab columns n of one (layer, co) x 4 split
+// groups; coalesced slab reads, fixed-order (deterministic) sums, scattered
+// writes into the Caffe layout.
 // ---------------------------------------------------------------------------
 struct WredDims {
   int64_t w_off, b_off, part_off;
-  int cout, cin, ks, splits, np;
+  int cout, cin, ks, splits, np, blk0;   // blk0: first workgroup of this layer
 };
 
-__global__ void wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ grad,
-                                    WredDims d0, WredDims d1, WredDims d2) {
-  const int l = blockIdx.y;
-  const WredDims d = l == 0 ? d0 : (l == 1 ? d1 : d2);
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part,
+                                                           float* __restrict__ grad, WredDims d0,
+                                                           WredDims d1, WredDims d2) {
+  __shared__ float red[4][64];
+  const int bid = blockIdx.x;
+  const WredDims d = bid >= d2.blk0 ? d2 : (bid >= d1.blk0 ? d1 : d0);
+  const int lb = bid - d.blk0;
+  const int nblk = d.np / 64;
+  const int co = lb / nblk, n = (lb % nblk) * 64 + (threadIdx.x & 63);
+  const int g = threadIdx.x >> 6;
   const int kk = d.ks * d.ks, kc = kk * d.cin;
-  const int64_t nw = (int64_t)d.cout * kc;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nw + d.cout;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    int co, n;
-    if (e < nw) {
-      co = (int)(e / kc);
-      const int rem = (int)(e - (int64_t)co * kc);
-      const int ci = rem / kk, tap = rem % kk;
-      n = tap * d.cin + ci;
+  const float* p = part + d.part_off + (size_t)co * d.np + n;
+  const size_t stride = (size_t)d.cout * d.np;
+  float acc = 0.f;
+  int s = g;
+  for (; s + 12 < d.splits; s += 16) {
+    const float v0 = p[s * stride], v1 = p[(s + 4) * stride];
+    const float v2 = p[(s + 8) * stride], v3 = p[(s + 12) * stride];
+    acc += v0; acc += v1; acc += v2; acc += v3;
+  }
+  for (; s < d.splits; s += 4) acc += p[s * stride];
+  red[g][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (g == 0 && n <= kc) {
+    const int l = threadIdx.x;
+    const float v = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
+    if (n < kc) {
+      const int tap = n / d.cin, ci = n % d.cin;
+      grad[d.w_off + ((size_t)co * d.cin + ci) * kk + tap] = v;
     } else {
-      co = (int)(e - nw);
-      n = kc;
+      grad[d.b_off + co] = v;
     }
-    const float* p = part + d.part_off + (size_t)co * d.np + n;
-    float acc = 0.f;
-    for (int s = 0; s < d.splits; ++s) acc += p[(size_t)s * d.cout * d.np];
-    grad[e < nw ? d.w_off + e : d.b_off + co] = acc;
   }
 }
 
 // ---------------------------------------------------------------------------
-// apply: server.py update rules on the flat Q tower (+ fused kernel-layout
-// refresh of the conv weights and the param-server iteration counter)
+// apply: server.py update rules on the flat Q tower, float4 per thread, with
+//  - the conv kernel-layout copy refreshed from the new values,
+//  - the target sync P <- Q fused in when the NEXT pull will see
+//    iteration % period == 0 (server.py:188-189),
 // ---------------------------------------------------------------------------
 struct ApplyArgs {
   int64_t n;
-  int rule;
+  int rule, period;
   float lr, decay, one_minus_decay, eps, momentum, wd;
   int64_t bias_lo[5], bias_hi[5];   // [lo,hi) element ranges of biases (momentum multipliers)
   ConvDims conv[3];
 };
 
-__global__ void apply_kernel(float* __restrict__ theta, const float* __restrict__ grad,
-                             float* __restrict__ opt, int32_t* __restrict__ opt_init,
-                             float* __restrict__ wk, int64_t* __restrict__ iter, ApplyArgs a) {
-  const bool first = (*opt_init == 0);
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
-    const float g = grad[i];
-    float th = theta[i];
-    switch (a.rule) {
-      case 0:   // sgd: theta - lr*g
-        th = th - a.lr * g;
-        break;
-      case 1: { // rmsprop with one-step-lagged cache
-        const float g2 = g * g;
-        const float c_use = first ? g2 : opt[i];
-        opt[i] = first ? g2 : (a.decay * opt[i] + a.one_minus_decay * g2);
-        th = th - (a.lr * g) / sqrtf(c_use + a.eps);
-        break;
-      }
-      case 2: { // adagrad with current accumulator
-        const float acc = first ? g * g : opt[i] + g * g;
-        opt[i] = acc;
-        th = th - (a.lr * g) / sqrtf(acc + a.eps);
-        break;
-      }
-      default: { // Caffe SGDSolver momentum (blobs_lr {1,2}, weight_decay {1,0})
-        bool is_bias = false;
-#pragma unroll
-        for (int l = 0; l < 5; ++l) is_bias |= (i >= a.bias_lo[l] && i < a.bias_hi[l]);
-        const float lr = a.lr * (is_bias ? 2.f : 1.f);
-        const float wd = is_bias ? 0.f : a.wd;
-        const float v = a.momentum * (first ? 0.f : opt[i]) + lr * (g + wd * th);
-        opt[i] = v;
-        th = th - v;
-        break;
-      }
+__device__ __forceinline__ float apply_one(const ApplyArgs& a, bool first, int64_t i, float th,
+                                           float g, float& st) {
+  switch (a.rule) {
+    case 0:   // sgd: theta - lr*g  (server.py:81-83, apply_descent :66-68)
+      return th - a.lr * g;
+    case 1: { // rmsprop with the one-step-lagged cache (server.py:86-105)
+      const float g2 = g * g;
+      const float c_use = first ? g2 : st;
+      st = first ? g2 : (a.decay * st + a.one_minus_decay * g2);
+      return th - (a.lr * g) / sqrtf(c_use + a.eps);
     }
-    theta[i] = th;
+    case 2: { // adagrad with the current accumulator (server.py:108-124)
+      const float acc = first ? g * g : st + g * g;
+      st = acc;
+      return th - (a.lr * g) / sqrtf(acc + a.eps);
+    }
+    default: { // Caffe SGDSolver momentum (blobs_lr {1,2}, weight_decay {1,0})
+      bool is_bias = false;
+#pragma unroll
+      for (int l = 0; l < 5; ++l) is_bias |= (i >= a.bias_lo[l] && i < a.bias_hi[l]);
+      const float lr = a.lr * (is_bias ? 2.f : 1.f);
+      const float wd = is_bias ? 0.f : a.wd;
+      const float v = a.momentum * (first ? 0.f : st) + lr * (g + wd * th);
+      st = v;
+      return th - v;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void apply_kernel(
+    float* __restrict__ theta, const float* __restrict__ grad, float* __restrict__ opt,
+    int32_t* __restrict__ opt_init, float* __restrict__ wk, float* __restrict__ thetaP,
+    float* __restrict__ wkP, const int64_t* __restrict__ iter, ApplyArgs a) {
+  const bool first = (*opt_init == 0);
+  const int64_t it = *iter;
+  const bool sync = a.period > 0 && ((it + 1) % a.period) == 0;
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i < a.n) {
+    const float4 g4 = *reinterpret_cast<const float4*>(grad + i);
+    const float4 t4 = *reinterpret_cast<const float4*>(theta + i);
+    float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.rule != 0 && !first) s4 = *reinterpret_cast<const float4*>(opt + i);
+    float th[4] = {t4.x, t4.y, t4.z, t4.w};
+    const float g[4] = {g4.x, g4.y, g4.z, g4.w};
+    float st[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) th[e] = apply_one(a, first, i + e, th[e], g[e], st[e]);
+    const float4 o4 = make_float4(th[0], th[1], th[2], th[3]);
+    *reinterpret_cast<float4*>(theta + i) = o4;
+    if (a.rule != 0) *reinterpret_cast<float4*>(opt + i) = make_float4(st[0], st[1], st[2], st[3]);
+    if (sync) *reinterpret_cast<float4*>(thetaP + i) = o4;
 #pragma unroll
     for (int l = 0; l < 3; ++l) {
       const ConvDims& d = a.conv[l];
-      const int64_t e = i - d.w_off;
-      if (e >= 0 && e < (int64_t)d.cout * d.cin * d.ks * d.ks) wk[wk_index(d, e)] = th;
+      const int64_t e0 = i - d.w_off;
+      if (e0 >= 0 && e0 < (int64_t)d.cout * d.cin * d.ks * d.ks) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int64_t idx = wk_index(d, e0 + e);
+          wk[idx] = th[e];
+          if (sync) wkP[idx] = th[e];
+        }
+      }
     }
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) *iter += 1;
 }
 
-__global__ void set_flag_kernel(int32_t* f) { *f = 1; }
+// param-server iteration / first-call bookkeeping after every apply (a separate
+// one-thread kernel: every apply workgroup has read the old values by then)
+__global__ void apply_book_kernel(int64_t* iter, int32_t* opt_init) {
+  *iter += 1;
+  *opt_init = 1;
+}
 
 hipError_t launch_apply(const NetBuffers& nb, int rule, float lr, float decay, float eps,
-                        float momentum, float wd, hipStream_t s) {
+                        float momentum, float wd, int period, hipStream_t s) {
   ApplyArgs a;
   a.n = nb.L.total;
-  a.rule = rule; a.lr = lr; a.decay = decay; a.eps = eps;
-  a.momentum = momentum; a.wd = wd;
+  a.rule = rule; a.period = period;
+  a.lr = lr; a.decay = decay; a.eps = eps; a.momentum = momentum; a.wd = wd;
   a.one_minus_decay = (float)(1.0 - (double)decay);   // numpy: (1 - rmsprop_decay) in double
   for (int l = 0; l < 5; ++l) { a.bias_lo[l] = nb.L.b[l]; a.bias_hi[l] = nb.L.b[l] + nb.L.bn[l]; }
   conv_dims(nb.L, a.conv);
-  const int blocks = (int)std::min<int64_t>(2048, (a.n + 255) / 256);
+  const int blocks = (int)((a.n / 4 + 255) / 256);
   hipLaunchKernelGGL(apply_kernel, dim3(blocks), dim3(256), 0, s, nb.theta[0], nb.grad, nb.opt,
-                     nb.opt_init, nb.wk[0], nb.iter, a);
-  hipLaunchKernelGGL(set_flag_kernel, dim3(1), dim3(1), 0, s, nb.opt_init);
+                     nb.opt_init, nb.wk[0], nb.theta[1], nb.wk[1], nb.iter, a);
+  hipLaunchKernelGGL(apply_book_kernel, dim3(1), dim3(1), 0, s, nb.iter, nb.opt_init);
   return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
-// GEMM configurations per layer
+// GEMM configurations per layer (tuned at B = 32, S = 64)
 // ---------------------------------------------------------------------------
-using CfgConv1F = GemmCfg<128, 32, 28, 4, 1>;
-using CfgConv2F = GemmCfg<128, 64, 32, 2, 2>;
-using CfgConv3F = GemmCfg<64, 64, 32, 2, 2>;
-using CfgFcF = GemmCfg<32, 128, 32, 1, 4>;
-using CfgFcD = GemmCfg<32, 64, 32, 1, 2>;
-using CfgFcW = GemmCfg<64, 64, 32, 2, 2>;
-using CfgW1 = GemmCfg<32, 64, 32, 1, 2>;
-using CfgW23 = GemmCfg<64, 64, 32, 2, 2>;
-using CfgD2 = GemmCfg<128, 32, 32, 4, 1>;
-using CfgD3 = GemmCfg<64, 64, 32, 2, 2>;
+using CfgConv1F = GemmCfg<128, 32, 28, 4, 1, 1>;
+using CfgConv2F = GemmCfg<128, 64, 32, 2, 2, 2>;
+using CfgConv3F = GemmCfg<64, 64, 32, 2, 2, 2>;
+using CfgFcF = GemmCfg<32, 64, 64, 1, 2, 2>;
+using CfgFcD = GemmCfg<32, 64, 64, 1, 2, 4>;
+using CfgFcW = GemmCfg<64, 64, 32, 2, 2, 1>;
+using CfgW1 = GemmCfg<32, 256, 32, 1, 4, 2>;
+using CfgW2 = GemmCfg<64, 128, 32, 2, 2, 2>;
+using CfgW3 = GemmCfg<64, 128, 32, 2, 2, 2>;
+using CfgD2 = GemmCfg<128, 32, 32, 4, 1, 2>;
+using CfgD3 = GemmCfg<64, 64, 32, 2, 2, 2>;
+
+constexpr int kFc4SplitLen = 256;
+constexpr int kWgradSplitLen[3] = {512, 1024, 256};
+constexpr int kWgradBN[3] = {CfgW1::BN, CfgW2::BN, CfgW3::BN};
+constexpr int kWgradBK = 32;
+static_assert(CfgW1::BK == kWgradBK && CfgW2::BK == kWgradBK && CfgW3::BK == kWgradBK, "BK");
 
 // split-K: K per split is a multiple of BK, about `target`
 static inline int split_len(int K, int BK, int target, int* nsplit) {
@@ -491,7 +526,7 @@ static inline int split_len(int K, int BK, int target, int* nsplit) {
 int fc4_splits_for(int S) {
   const int K = 64 * (S / 8) * (S / 8);
   int ns;
-  split_len(K, CfgFcF::BK, 256, &ns);
+  split_len(K, CfgFcF::BK, kFc4SplitLen, &ns);
   return ns;
 }
 
@@ -499,10 +534,9 @@ int wgrad_splits_for(int layer, int B, int S, int* np) {
   const int H = S >> layer;
   const int K = B * H * H;
   const int KC[3] = {196, 800, 576};
-  const int target[3] = {1024, 1024, 512};
-  *np = ((KC[layer] + 1 + 63) / 64) * 64;
+  *np = ((KC[layer] + 1 + kWgradBN[layer] - 1) / kWgradBN[layer]) * kWgradBN[layer];
   int ns;
-  split_len(K, 32, target[layer], &ns);
+  split_len(K, kWgradBK, kWgradSplitLen[layer], &ns);
   return ns;
 }
 
@@ -561,32 +595,45 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     FcFwd p;
     p.M = B; p.N = kFc4; p.K = 64 * s4 * s4;
     int ns;
-    p.ksplit_len = split_len(p.K, CfgFcF::BK, 256, &ns);
+    p.ksplit_len = split_len(p.K, CfgFcF::BK, kFc4SplitLen, &ns);
     p.s4sq = s4 * s4; p.fS4sq = FastDiv(s4 * s4);
     for (int z = 0; z < 2; ++z) { p.x[z] = nb.pool3[z]; p.w[z] = nb.theta[z] + L.w[3]; }
     p.part = nb.fc4_part; p.nz = nz;
     M("fc4_fwd");
     CHECK_LAUNCH(launch_gemm<CfgFcF>(p, nz, ns, s));
-    const int tot = nz * B * kFc4;
-    M("fc4_reduce");
-    hipLaunchKernelGGL(fc4_reduce_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, nb.fc4_part,
-                       ns, nz, B, nb.theta[0] + L.b[3], nb.theta[1] + L.b[3], nb.h4[0], nb.h4[1]);
+    M("fc4_reduce_out");
+    hipLaunchKernelGGL(fc4_reduce_out_kernel, dim3(B, nz), dim3(kFc4), 0, s, nb.fc4_part, ns, nz,
+                       B, nb.theta[0] + L.b[3], nb.theta[1] + L.b[3], nb.theta[0] + L.w[4],
+                       nb.theta[0] + L.b[4], nb.theta[1] + L.w[4], nb.theta[1] + L.b[4],
+                       nb.h4[0], nb.h4[1], nb.q_out, nb.p_out);
     CHECK_LAUNCH(hipGetLastError());
   }
   return hipSuccess;
 }
 
 hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(void*, const char*),
-                           void* marg) {
+                           void* marg, bool concurrent) {
   const ParamLayout& L = nb.L;
   const int B = nb.B, S = nb.S;
   const int s4 = S / 8;
   auto M = [&](const char* n) { if (mark) mark(marg, n); };
+  // weight-gradient GEMMs depend only on the data-gradient chain's outputs:
+  // fork them onto the side stream so they overlap the chain.
+  const hipStream_t sw = concurrent ? nb.side : s;
+  int nev = 0;
+  auto fork = [&]() -> hipError_t {
+    if (!concurrent) return hipSuccess;
+    hipError_t e = hipEventRecord(nb.ev[nev], s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(nb.side, nb.ev[nev], 0);
+    ++nev;
+    return e;
+  };
   {  // fc4 dgrad -> dconv3
     FcDgrad p;
     p.M = B; p.N = 64 * s4 * s4; p.K = kFc4; p.ksplit_len = kFc4;
     p.s4 = s4; p.s4sq = s4 * s4; p.fS4sq = FastDiv(s4 * s4); p.fS4 = FastDiv(s4);
     p.dh4 = nb.dh4; p.w4 = nb.theta[0] + L.w[3]; p.mask3 = nb.mask3; p.dconv3 = nb.dconv3;
+    CHECK_LAUNCH(fork());   // side: fc4 wgrad needs only dh4 (head) -> fork before dgrad
     M("fc4_dgrad");
     CHECK_LAUNCH(launch_gemm<CfgFcD>(p, 1, 1, s));
   }
@@ -596,18 +643,19 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     p.s4sq = s4 * s4; p.fS4sq = FastDiv(s4 * s4);
     p.dh4 = nb.dh4; p.x = nb.pool3[0]; p.gw4 = nb.grad + L.w[3];
     M("fc4_wgrad");
-    CHECK_LAUNCH(launch_gemm<CfgFcW>(p, 1, 1, s));
+    CHECK_LAUNCH(launch_gemm<CfgFcW>(p, 1, 1, sw));
+    CHECK_LAUNCH(fork());   // side waits for fc4 dgrad (dconv3)
   }
   {  // conv3 wgrad
     const int H = S / 4;
     ConvWgrad<64, 64, 3, 1> p;
     p.M = 64; p.N = 577; p.K = B * H * H;
     int ns;
-    p.ksplit_len = split_len(p.K, 32, 512, &ns);
+    p.ksplit_len = split_len(p.K, kWgradBK, kWgradSplitLen[2], &ns);
     p.H = H; p.W = H; p.fW = FastDiv(H); p.fH = FastDiv(H);
     p.NP = nb.wnp[2]; p.dconv = nb.dconv3; p.in = nb.pool2[0]; p.part = nb.wpart + nb.wpart_off[2];
     M("conv3_wgrad");
-    CHECK_LAUNCH(launch_gemm<CfgW23>(p, 1, ns, s));
+    CHECK_LAUNCH(launch_gemm<CfgW3>(p, 1, ns, sw));
   }
   {  // conv3 dgrad -> dconv2
     const int H = S / 4;
@@ -617,17 +665,18 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     p.dconv = nb.dconv3; p.wk = nb.wk[0] + L.wk_off[2]; p.pmask = nb.mask2; p.pdconv = nb.dconv2;
     M("conv3_dgrad");
     CHECK_LAUNCH(launch_gemm<CfgD3>(p, 1, 1, s));
+    CHECK_LAUNCH(fork());   // side waits for conv3 dgrad (dconv2)
   }
   {  // conv2 wgrad
     const int H = S / 2;
     ConvWgrad<32, 64, 5, 2> p;
     p.M = 64; p.N = 801; p.K = B * H * H;
     int ns;
-    p.ksplit_len = split_len(p.K, 32, 1024, &ns);
+    p.ksplit_len = split_len(p.K, kWgradBK, kWgradSplitLen[1], &ns);
     p.H = H; p.W = H; p.fW = FastDiv(H); p.fH = FastDiv(H);
     p.NP = nb.wnp[1]; p.dconv = nb.dconv2; p.in = nb.pool1[0]; p.part = nb.wpart + nb.wpart_off[1];
     M("conv2_wgrad");
-    CHECK_LAUNCH(launch_gemm<CfgW23>(p, 1, ns, s));
+    CHECK_LAUNCH(launch_gemm<CfgW2>(p, 1, ns, sw));
   }
   {  // conv2 dgrad -> dconv1
     const int H = S / 2;
@@ -642,7 +691,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     ConvWgrad<4, 32, 7, 3> p;
     p.M = 32; p.N = 197; p.K = B * S * S;
     int ns;
-    p.ksplit_len = split_len(p.K, 32, 1024, &ns);
+    p.ksplit_len = split_len(p.K, kWgradBK, kWgradSplitLen[0], &ns);
     p.H = S; p.W = S; p.fW = FastDiv(S); p.fH = FastDiv(S);
     p.NP = nb.wnp[0]; p.dconv = nb.dconv1; p.in = nb.state; p.part = nb.wpart + nb.wpart_off[0];
     M("conv1_wgrad");
@@ -651,10 +700,19 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
   {  // slab reduce -> grads (Caffe layout)
     WredDims d[3];
     const int cout[3] = {32, 64, 64}, cin[3] = {4, 32, 64}, ks[3] = {7, 5, 3};
-    for (int l = 0; l < 3; ++l)
-      d[l] = {L.w[l], L.b[l], nb.wpart_off[l], cout[l], cin[l], ks[l], nb.wsplits[l], nb.wnp[l]};
+    int blk = 0;
+    for (int l = 0; l < 3; ++l) {
+      d[l] = {L.w[l], L.b[l], nb.wpart_off[l], cout[l], cin[l], ks[l], nb.wsplits[l], nb.wnp[l],
+              blk};
+      blk += cout[l] * (nb.wnp[l] / 64);
+    }
+    if (concurrent) {       // join the side stream
+      CHECK_LAUNCH(hipEventRecord(nb.ev[nev], nb.side));
+      CHECK_LAUNCH(hipStreamWaitEvent(s, nb.ev[nev], 0));
+      ++nev;
+    }
     M("wgrad_reduce");
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(64, 3), dim3(256), 0, s, nb.wpart, nb.grad, d[0],
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blk), dim3(256), 0, s, nb.wpart, nb.grad, d[0],
                        d[1], d[2]);
     CHECK_LAUNCH(hipGetLastError());
   }
@@ -664,29 +722,14 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
 // ---------------------------------------------------------------------------
 // acting: Q forward of n states + argmax (select_action, baristanet.py:142-146)
 // ---------------------------------------------------------------------------
-__global__ void act_head_kernel(int n, const float* __restrict__ h4, const float* __restrict__ w5,
-                                const float* __restrict__ b5, float* __restrict__ qout,
-                                int32_t* __restrict__ actions) {
-  const int b = blockIdx.x, lane = threadIdx.x;   // one wave per state
+__global__ void argmax_kernel(int n, const float* __restrict__ qout, int32_t* __restrict__ actions) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= n) return;
-  float q[4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a) {
-    float acc = 0.f;
-#pragma unroll
-    for (int j = 0; j < kFc4 / 64; ++j)
-      acc += h4[(size_t)b * kFc4 + lane + 64 * j] * w5[a * kFc4 + lane + 64 * j];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
-    q[a] = acc + b5[a];
-  }
-  if (lane == 0) {
-    int best = 0;
-    for (int a = 1; a < 4; ++a)
-      if (q[a] > q[best]) best = a;   // numpy argmax: first max
-    for (int a = 0; a < 4; ++a) qout[b * 4 + a] = q[a];
-    if (actions) actions[b] = best;
-  }
+  const float* q = qout + b * 4;
+  int best = 0;
+  for (int a = 1; a < 4; ++a)
+    if (q[a] > q[best]) best = a;   // numpy argmax: first max
+  actions[b] = best;
 }
 
 hipError_t launch_act(const NetBuffers& nb, const float* in, int n, float* pool1, float* pool2,
@@ -700,10 +743,13 @@ hipError_t launch_act(const NetBuffers& nb, const float* in, int n, float* pool1
   a.pool1[1] = pool1; a.pool2[1] = pool2; a.pool3[1] = pool3; a.h4[1] = h4;
   a.mask1 = a.mask2 = a.mask3 = nullptr;
   a.fc4_part = part;
+  a.q_out = qout; a.p_out = qout;
   CHECK_LAUNCH(launch_forward(a, 1, s, nullptr, nullptr));
-  hipLaunchKernelGGL(act_head_kernel, dim3(n), dim3(64), 0, s, n, h4, nb.theta[0] + nb.L.w[4],
-                     nb.theta[0] + nb.L.b[4], qout, actions);
-  return hipGetLastError();
+  if (actions) {
+    hipLaunchKernelGGL(argmax_kernel, dim3((n + 63) / 64), dim3(64), 0, s, n, qout, actions);
+    CHECK_LAUNCH(hipGetLastError());
+  }
+  return hipSuccess;
 }
 
 }  // namespace ddq
