@@ -119,14 +119,10 @@ def main():
     ap.add_argument("--eager", action="store_true", help="no hipGraph (debug)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from ddq import dist as ddist
+    rank, world, local = ddist.env_ranks()
     import torch
-    import torch.distributed as dist
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist = ddist.init_process_group(rank, world, "gloo")   # bootstrap only; data path is RCCL
     torch.cuda.set_device(local)
 
     import ddq
@@ -139,11 +135,9 @@ def main():
     net.replay_create(args.replay)
     fill_replay(net, args.replay, S, seed=1000 + rank)
     if world > 1:
-        uid = [ddq.DeepQNet.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        net.comm_init(uid[0], world, rank)
+        ddist.setup_comm(net, rank, world)
     cfg = net.step_cfg(args.rule, lr=1e-4, target_period=10, allreduce=world > 1,
-                       seed=1234 + rank)
+                       seed=ddist.index_seed(1234, rank))
 
     def run(k):
         if args.eager:
@@ -163,11 +157,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt = ddist.max_over_ranks(time.perf_counter() - t0)
     loss = float(net.blob("loss"))
 
     # per-kernel device times (HIP events on the ctx stream), averaged

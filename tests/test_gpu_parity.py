@@ -262,3 +262,30 @@ def test_graph_step_runs_and_matches_eager(ddq, ref):
     assert np.all(np.isfinite(th))
     close(th, e.get_flat(0), rtol=1e-6, what="theta after 5 graph steps")
     np.testing.assert_array_equal(nets[0].read_indices(), e.read_indices())
+
+
+def test_rccl_world1_allreduce_and_step(ddq, ref):
+    """RCCL plumbing on one GPU: a 1-rank communicator all-reduce is the
+    identity, and the fused step with allreduce=1 equals the step without."""
+    S, B, N = 16, 8, 64
+    rng = np.random.default_rng(2)
+    nets = [ddq.DeepQNet(batch=B, frame=S) for _ in range(2)]
+    theta = ref.flatten(ref.init_params(S, seed=9))
+    st = rng.integers(0, 256, (N, 4, S, S)).astype(np.uint8)
+    for n in nets:
+        n.set_flat(0, theta)
+        n.set_flat(1, theta)
+        n.replay_create(N)
+        n.replay_import(st, rng.integers(0, 4, N).astype(np.uint8) * 0,
+                        np.zeros(N, np.int16), np.ones(N, np.uint8), 0, N)
+    uid = ddq.DeepQNet.comm_unique_id()
+    nets[0].comm_init(uid, 1, 0)
+    g = rng.normal(0, 1, theta.size).astype(np.float32)
+    nets[0].set_grads_flat(g)
+    nets[0].allreduce_grads()
+    np.testing.assert_array_equal(nets[0].get_grads_flat(), g)
+    for i, n in enumerate(nets):
+        cfg = n.step_cfg("sgd", lr=1e-3, target_period=10, allreduce=(i == 0), seed=5)
+        n.step_graph(cfg, 3)
+        n.synchronize()
+    np.testing.assert_array_equal(nets[0].get_flat(0), nets[1].get_flat(0))
