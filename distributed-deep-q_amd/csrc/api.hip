@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -160,6 +161,10 @@ int ddq_create(ddq_ctx** out, int device, const ddq_net_desc* desc) {
     for (auto& e : nb.ev) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     const int B = desc->batch, S = desc->frame;
     nb.B = B; nb.S = S; nb.gamma = desc->gamma;
+    {
+      const char* impl = getenv("DDQ_CONV_IMPL");
+      nb.conv_impl = (impl && strcmp(impl, "gemm") == 0) ? 0 : 1;
+    }
     nb.L = make_layout(S);
     const int64_t P = nb.L.total;
     const int S2 = S / 2, S3 = S / 4, S4 = S / 8;

@@ -1,0 +1,272 @@
+// Direct (patch-in-LDS) convolution kernels for the deepq conv layers (gfx950).
+//
+// One workgroup = one image b x one TY x TX tile of output pixels x all N
+// output channels.  The input halo patch (TY+KS-1) x (TX+KS-1) x CP is staged
+// in LDS ONCE (the implicit-GEMM path re-reads it KS^2 times through L1/L2),
+// the weights tap by tap (two-slot ring, one barrier per tap) or all at once
+// (WALL, conv1: 25 KB).  The MFMA operands are read straight from those
+// images: for v_mfma_f32_32x32x2_f32 lane l = (row l&31, k-half h = l>>5)
+// needs A[row][k] and B[k][col]; here each lane reads V = 4 (ds_read_b128) or
+// V = 2 (ds_read_b64) consecutive channels per image and feeds V consecutive
+// MFMA k-steps from them (half h owns channels [g*2V + h*V, +V) of group g),
+// so there is no im2col, no per-element address arithmetic in the K loop and
+// one LDS read per 4 MFMAs per operand block.
+//
+// Modes (template DGRAD):
+//  fwd   : patch = layer input (CP channels), N = Cout, weights Wk[co][tap][ci];
+//          epilogue = bias + ReLU + 2x2 max-pool + routing byte (rows are
+//          window-major: a lane's 4 consecutive accumulator rows are one window).
+//  dgrad : patch = this layer's dconv (CP = Cout channels), N = Cin, weights
+//          transposed and tap-flipped while staged (conv with the flipped kernel,
+//          pad KS-1-PAD); epilogue = un-pool + ReLU routing into the previous
+//          layer's pre-pool gradient.
+#pragma once
+#include "common.h"
+
+namespace ddq {
+
+template <int CP, int N, int KS, int TY, int TX, int WM, int WN, bool DGRAD, bool WALL>
+struct DirectCfg {
+  static constexpr int V = CP >= 8 ? 4 : CP / 2;     // floats per lane per LDS read
+  static constexpr int G = 2 * V;                     // channels per read group
+  static constexpr int CS = CP >= 8 ? CP + 4 : CP;    // patch pixel stride (floats)
+  static constexpr int PH = TY + KS - 1, PW = TX + KS - 1;
+  static constexpr int RS = PW * CS + (CP >= 8 ? 0 : 2);   // patch row stride
+  static constexpr int CW = CP >= 8 ? CP + 4 : CP;    // weight row stride (one row per n)
+  static constexpr int T = KS * KS;
+  static constexpr int WSLOTS = WALL ? T : 2;
+  static constexpr int kThreads = 64 * WM * WN;
+  static constexpr int TM = TY * TX / WM / 32;        // 32-pixel blocks per wave
+  static constexpr int TN = N / WN / 32;              // 32-channel blocks per wave
+  static constexpr int kPatch = PH * RS;
+  static constexpr int kW = WSLOTS * N * CW;
+  static constexpr int kSmem = kPatch + kW;
+  static_assert(TM >= 1 && TN >= 1, "wave tile");
+  static_assert(TY % 2 == 0 && TX % 2 == 0 && CP % 4 == 0 && CP % G == 0, "shape");
+  static_assert(kSmem * 4 <= 160 * 1024, "LDS budget");
+};
+
+struct DirectArgs {
+  int B, H, W;               // conv grid (stride 1, same padding)
+  int tiles_x;
+  int pad;                   // spatial padding of the patch
+  const float* in[2];        // patch source, NHWC (B,H,W,CP)
+  const float* wk[2];        // Wk[co][tap][ci] of the layer
+  const float* bias[2];      // fwd only
+  float* out[2];             // fwd: pooled NHWC (B,H/2,W/2,N)
+  uint8_t* mask[2];          // fwd: routing bytes (nullable)
+  const uint8_t* pmask;      // dgrad: previous pool's routing bytes (B,H,W,N)
+  float* pdconv;             // dgrad: previous layer's pre-pool gradient (B,2H,2W,N)
+};
+
+template <int V>
+struct VecT;
+template <>
+struct VecT<4> { using T = float4; };
+template <>
+struct VecT<2> { using T = float2; };
+
+__device__ __forceinline__ float vget(const float4& v, int i) {
+  return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
+}
+__device__ __forceinline__ float vget(const float2& v, int i) { return i == 0 ? v.x : v.y; }
+
+// Weight staging for one tap, split into a global->register load (issued
+// before the previous tap's MFMAs) and a register->LDS store (after them).
+template <class C, int CP, int N>
+struct WStage {
+  static constexpr int kF4 = N * CP / 4;                       // float4 per tap
+  static constexpr int kPer = (kF4 + C::kThreads - 1) / C::kThreads;
+  float4 r[kPer];
+
+  template <bool DGRAD>
+  __device__ __forceinline__ void load(const float* __restrict__ wk, int t, int tid) {
+#pragma unroll
+    for (int s = 0; s < kPer; ++s) {
+      const int f = tid + s * C::kThreads;
+      if (kF4 % C::kThreads != 0 && f >= kF4) continue;
+      if (!DGRAD) {          // wb[n][k] = Wk[n][t][k], float4 along k
+        const int n = f / (CP / 4), c4 = f % (CP / 4);
+        r[s] = *reinterpret_cast<const float4*>(wk + ((size_t)n * C::T + t) * CP + 4 * c4);
+      } else {               // wb[n=ci][k=co] = Wk[co][T-1-t][ci], float4 along ci
+        const int co = f / (N / 4), n4 = f % (N / 4);
+        r[s] = *reinterpret_cast<const float4*>(wk + ((size_t)co * C::T + (C::T - 1 - t)) * N +
+                                                4 * n4);
+      }
+    }
+  }
+  template <bool DGRAD>
+  __device__ __forceinline__ void store(float* wb, int tid) const {
+#pragma unroll
+    for (int s = 0; s < kPer; ++s) {
+      const int f = tid + s * C::kThreads;
+      if (kF4 % C::kThreads != 0 && f >= kF4) continue;
+      if (!DGRAD) {
+        const int n = f / (CP / 4), c4 = f % (CP / 4);
+        *reinterpret_cast<float4*>(wb + n * C::CW + 4 * c4) = r[s];
+      } else {
+        const int co = f / (N / 4), n4 = f % (N / 4);
+        wb[(4 * n4 + 0) * C::CW + co] = r[s].x;
+        wb[(4 * n4 + 1) * C::CW + co] = r[s].y;
+        wb[(4 * n4 + 2) * C::CW + co] = r[s].z;
+        wb[(4 * n4 + 3) * C::CW + co] = r[s].w;
+      }
+    }
+  }
+};
+
+template <int CP, int N, int KS, int TY, int TX, int WM, int WN, bool DGRAD, bool WALL>
+__global__ __launch_bounds__(64 * WM * WN) void direct_conv_kernel(const DirectArgs a) {
+  using C = DirectCfg<CP, N, KS, TY, TX, WM, WN, DGRAD, WALL>;
+  using VT = typename VecT<C::V>::T;
+  constexpr int TM = C::TM, TN = C::TN, V = C::V;
+  __shared__ __attribute__((aligned(16))) float smem[C::kSmem];
+  float* patch = smem;
+  float* wbuf = smem + C::kPatch;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int z = blockIdx.z, b = blockIdx.y;
+  const int ty = blockIdx.x / a.tiles_x, tx = blockIdx.x % a.tiles_x;
+  const int y0 = ty * TY, x0 = tx * TX;
+  const float* __restrict__ in = a.in[z];
+  const float* __restrict__ wk = a.wk[z];
+
+  // ---- stage the halo patch (zero outside the image) ----
+  for (int f = tid; f < C::PH * C::PW * (CP / 4); f += C::kThreads) {
+    const int pix = f / (CP / 4), c4 = f % (CP / 4);
+    const int py = pix / C::PW, px = pix % C::PW;
+    const int gy = y0 - a.pad + py, gx = x0 - a.pad + px;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if ((unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W)
+      v = *reinterpret_cast<const float4*>(in + (((size_t)b * a.H + gy) * a.W + gx) * CP + 4 * c4);
+    float* dst = patch + py * C::RS + px * C::CS + 4 * c4;
+    if (CP >= 8) {
+      *reinterpret_cast<float4*>(dst) = v;
+    } else {
+      reinterpret_cast<float2*>(dst)[0] = make_float2(v.x, v.y);
+      reinterpret_cast<float2*>(dst)[1] = make_float2(v.z, v.w);
+    }
+  }
+  WStage<C, CP, N> ws;
+  if (WALL) {
+    for (int t = 0; t < C::T; ++t) {
+      ws.template load<DGRAD>(wk, t, tid);
+      ws.template store<DGRAD>(wbuf + t * N * C::CW, tid);
+    }
+  } else {
+    ws.template load<DGRAD>(wk, 0, tid);
+    ws.template store<DGRAD>(wbuf, tid);
+  }
+  __syncthreads();
+
+  // ---- per-lane operand bases ----
+  const int l31 = lane & 31, h = lane >> 5;
+  const int wmi = wid / WN, wni = wid % WN;
+  int abase[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = wmi * TM * 32 + 32 * i + l31;
+    const int win = m >> 2, dy = (m >> 1) & 1, dx = m & 1;
+    const int wy = win / (TX / 2), wx = win % (TX / 2);
+    abase[i] = (2 * wy + dy) * C::RS + (2 * wx + dx) * C::CS + h * V;
+  }
+  int bbase[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) bbase[j] = (wni * TN * 32 + 32 * j + l31) * C::CW + h * V;
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  for (int t = 0; t < C::T; ++t) {
+    const float* wb = wbuf + (WALL ? t : (t & 1)) * N * C::CW;
+    if (!WALL && t + 1 < C::T) ws.template load<DGRAD>(wk, t + 1, tid);   // in flight under MFMAs
+    const int ky = t / KS, kx = t % KS;
+    const float* pa = patch + ky * C::RS + kx * C::CS;
+#pragma unroll
+    for (int g = 0; g < CP / C::G; ++g) {
+      VT av[TM], bv[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) av[i] = *reinterpret_cast<const VT*>(pa + abase[i] + g * C::G);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bv[j] = *reinterpret_cast<const VT*>(wb + bbase[j] + g * C::G);
+#pragma unroll
+      for (int v = 0; v < V; ++v)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(vget(av[i], v), vget(bv[j], v),
+                                                             acc[i][j], 0, 0, 0);
+    }
+    if (!WALL && t + 1 < C::T) {
+      // the other slot was last read in iteration t-1, fenced by its barrier
+      ws.template store<DGRAD>(wbuf + ((t + 1) & 1) * N * C::CW, tid);
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue ----
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int mb = wmi * TM * 32 + 32 * i;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = wni * TN * 32 + 32 * j + l31;
+      if (!DGRAD) {
+        const int Hp = a.H >> 1, Wp = a.W >> 1;
+        const float bv = a.bias[z][n];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int win = (mb + 8 * g + 4 * h) >> 2;
+          const int pyy = y0 / 2 + win / (TX / 2), pxx = x0 / 2 + win % (TX / 2);
+          if (pyy >= Hp || pxx >= Wp) continue;
+          float v0 = acc[i][j][4 * g + 0] + bv, v1 = acc[i][j][4 * g + 1] + bv;
+          float v2 = acc[i][j][4 * g + 2] + bv, v3 = acc[i][j][4 * g + 3] + bv;
+          float mx = v0; int arg = 0;
+          if (v1 > mx) { mx = v1; arg = 1; }
+          if (v2 > mx) { mx = v2; arg = 2; }
+          if (v3 > mx) { mx = v3; arg = 3; }
+          const bool pos = mx > 0.f;
+          const size_t q = ((size_t)b * Hp + pyy) * Wp + pxx;
+          a.out[z][q * N + n] = pos ? mx : 0.f;
+          if (a.mask[z]) a.mask[z][q * N + n] = (uint8_t)(pos ? arg : 4);
+        }
+      } else {
+        const int W2 = 2 * a.W;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = mb + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const int win = m >> 2;
+          const int y = y0 + 2 * (win / (TX / 2)) + ((m >> 1) & 1);
+          const int x = x0 + 2 * (win % (TX / 2)) + (m & 1);
+          if (y >= a.H || x >= a.W) continue;
+          const size_t pix = ((size_t)b * a.H + y) * a.W + x;
+          const int mk = a.pmask[pix * N + n];
+          const float v = acc[i][j][r];
+          float* base = a.pdconv + (((size_t)b * 2 * a.H + 2 * y) * W2 + 2 * x) * N + n;
+          base[0] = (mk == 0) ? v : 0.f;
+          base[N] = (mk == 1) ? v : 0.f;
+          base[(size_t)W2 * N] = (mk == 2) ? v : 0.f;
+          base[(size_t)W2 * N + N] = (mk == 3) ? v : 0.f;
+        }
+      }
+    }
+  }
+}
+
+template <int CP, int N, int KS, int TY, int TX, int WM, int WN, bool DGRAD, bool WALL>
+inline hipError_t launch_direct(DirectArgs a, int nz, hipStream_t st) {
+  a.tiles_x = (a.W + TX - 1) / TX;
+  const int tiles_y = (a.H + TY - 1) / TY;
+  dim3 grid(tiles_y * a.tiles_x, a.B, nz);
+  hipLaunchKernelGGL((direct_conv_kernel<CP, N, KS, TY, TX, WM, WN, DGRAD, WALL>), grid,
+                     dim3(64 * WM * WN), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace ddq

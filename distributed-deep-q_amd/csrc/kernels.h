@@ -54,6 +54,7 @@ struct NetBuffers {
   hipEvent_t ev[8];
   ParamLayout L;
   float gamma;
+  int conv_impl;                    // 0 = implicit-GEMM engine, 1 = direct (patch-in-LDS)
 };
 
 hipError_t launch_gather(const NetBuffers& nb, const uint8_t* st, const uint8_t* act,

@@ -2,6 +2,7 @@
 // and the roofline of each kernel; layers.h for the implicit-GEMM problems.
 #include "kernels.h"
 #include "layers.h"
+#include "direct.h"
 
 namespace ddq {
 
@@ -546,6 +547,28 @@ int wgrad_splits_for(int layer, int B, int S, int* np) {
     if (e_ != hipSuccess) return e_;            \
   } while (0)
 
+static DirectArgs direct_fwd_args(const float* const in[2], const float* const wk[2],
+                                  const float* const bias[2], float* const out[2],
+                                  uint8_t* const mask[2], int B, int H, int pad) {
+  DirectArgs d{};
+  d.B = B; d.H = H; d.W = H; d.pad = pad;
+  for (int z = 0; z < 2; ++z) {
+    d.in[z] = in[z]; d.wk[z] = wk[z]; d.bias[z] = bias[z]; d.out[z] = out[z]; d.mask[z] = mask[z];
+  }
+  return d;
+}
+
+// dgrad = forward conv of the layer's dconv with the transposed, flipped
+// kernel and padding KS-1-PAD (== PAD for the odd kernels of this net).
+static DirectArgs direct_dgrad_args(const float* dconv, const float* wk, const uint8_t* pmask,
+                                    float* pdconv, int B, int H, int pad) {
+  DirectArgs d{};
+  d.B = B; d.H = H; d.W = H; d.pad = pad;
+  d.in[0] = d.in[1] = dconv; d.wk[0] = d.wk[1] = wk;
+  d.pmask = pmask; d.pdconv = pdconv;
+  return d;
+}
+
 hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
                           void (*mark)(void*, const char*), void* marg) {
   const ParamLayout& L = nb.L;
@@ -562,7 +585,12 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     }
     p.mask[0] = nb.mask1; p.mask[1] = nullptr;
     M("conv1_fwd");
-    CHECK_LAUNCH(launch_gemm<CfgConv1F>(p, nz, 1, s));
+    if (nb.conv_impl == 1) {
+      DirectArgs d = direct_fwd_args(p.in, p.wk, p.bias, p.out, p.mask, B, S, 3);
+      CHECK_LAUNCH((launch_direct<4, 32, 7, 16, 16, 4, 1, false, true>(d, nz, s)));
+    } else {
+      CHECK_LAUNCH(launch_gemm<CfgConv1F>(p, nz, 1, s));
+    }
   }
   {
     const int H = S / 2;
@@ -575,7 +603,12 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     }
     p.mask[0] = nb.mask2; p.mask[1] = nullptr;
     M("conv2_fwd");
-    CHECK_LAUNCH(launch_gemm<CfgConv2F>(p, nz, 1, s));
+    if (nb.conv_impl == 1) {
+      DirectArgs d = direct_fwd_args(p.in, p.wk, p.bias, p.out, p.mask, B, H, 2);
+      CHECK_LAUNCH((launch_direct<32, 64, 5, 8, 16, 4, 1, false, false>(d, nz, s)));
+    } else {
+      CHECK_LAUNCH(launch_gemm<CfgConv2F>(p, nz, 1, s));
+    }
   }
   {
     const int H = S / 4;
@@ -588,7 +621,12 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     }
     p.mask[0] = nb.mask3; p.mask[1] = nullptr;
     M("conv3_fwd");
-    CHECK_LAUNCH(launch_gemm<CfgConv3F>(p, nz, 1, s));
+    if (nb.conv_impl == 1) {
+      DirectArgs d = direct_fwd_args(p.in, p.wk, p.bias, p.out, p.mask, B, H, 1);
+      CHECK_LAUNCH((launch_direct<64, 64, 3, 8, 8, 2, 2, false, false>(d, nz, s)));
+    } else {
+      CHECK_LAUNCH(launch_gemm<CfgConv3F>(p, nz, 1, s));
+    }
   }
   {
     const int s4 = S / 8;
@@ -664,7 +702,12 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     p.H = H; p.W = H; p.fW = FastDiv(H); p.fH = FastDiv(H);
     p.dconv = nb.dconv3; p.wk = nb.wk[0] + L.wk_off[2]; p.pmask = nb.mask2; p.pdconv = nb.dconv2;
     M("conv3_dgrad");
-    CHECK_LAUNCH(launch_gemm<CfgD3>(p, 1, 1, s));
+    if (nb.conv_impl == 1) {
+      CHECK_LAUNCH((launch_direct<64, 64, 3, 8, 8, 2, 2, true, false>(
+          direct_dgrad_args(nb.dconv3, p.wk, nb.mask2, nb.dconv2, B, H, 1), 1, s)));
+    } else {
+      CHECK_LAUNCH(launch_gemm<CfgD3>(p, 1, 1, s));
+    }
     CHECK_LAUNCH(fork());   // side waits for conv3 dgrad (dconv2)
   }
   {  // conv2 wgrad
@@ -685,7 +728,12 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     p.H = H; p.W = H; p.fW = FastDiv(H); p.fH = FastDiv(H);
     p.dconv = nb.dconv2; p.wk = nb.wk[0] + L.wk_off[1]; p.pmask = nb.mask1; p.pdconv = nb.dconv1;
     M("conv2_dgrad");
-    CHECK_LAUNCH(launch_gemm<CfgD2>(p, 1, 1, s));
+    if (nb.conv_impl == 1) {
+      CHECK_LAUNCH((launch_direct<64, 32, 5, 8, 16, 4, 1, true, false>(
+          direct_dgrad_args(nb.dconv2, p.wk, nb.mask1, nb.dconv1, B, H, 2), 1, s)));
+    } else {
+      CHECK_LAUNCH(launch_gemm<CfgD2>(p, 1, 1, s));
+    }
   }
   {  // conv1 wgrad
     ConvWgrad<4, 32, 7, 3> p;

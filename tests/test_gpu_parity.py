@@ -128,9 +128,12 @@ def make_inputs(rng, B, S, frames="uniform"):
     return st, act, rw, ns, nt
 
 
+@pytest.mark.parametrize("impl", ["direct", "gemm"])
 @pytest.mark.parametrize("S,B,frames", [(16, 32, "uniform"), (16, 32, "snake"),
-                                        (24, 8, "uniform"), (64, 32, "uniform")])
-def test_full_pass_parity(ddq, ref, S, B, frames):
+                                        (24, 8, "uniform"), (40, 4, "snake"),
+                                        (64, 32, "uniform")])
+def test_full_pass_parity(ddq, ref, S, B, frames, impl, monkeypatch):
+    monkeypatch.setenv("DDQ_CONV_IMPL", impl)
     rng = np.random.default_rng(100 + S + B)
     pQ = ref.init_params(S, seed=7, prefix="Q")
     pP = ref.init_params(S, seed=8, prefix="P")
