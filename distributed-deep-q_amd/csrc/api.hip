@@ -15,7 +15,7 @@
 
 namespace ddq {
 int fc4_splits_for(int S);
-int wgrad_splits_for(int layer, int B, int S, int* np);
+int wgrad_splits_for(int layer, int B, int S, int* np, int impl);
 }  // namespace ddq
 
 using namespace ddq;
@@ -200,7 +200,7 @@ int ddq_create(ddq_ctx** out, int device, const ddq_net_desc* desc) {
     int64_t off = 0;
     const int cout[3] = {32, 64, 64};
     for (int l = 0; l < 3; ++l) {
-      nb.wsplits[l] = wgrad_splits_for(l, B, S, &nb.wnp[l]);
+      nb.wsplits[l] = wgrad_splits_for(l, B, S, &nb.wnp[l], nb.conv_impl);
       nb.wpart_off[l] = off;
       off += (int64_t)nb.wsplits[l] * cout[l] * nb.wnp[l];
     }
@@ -610,6 +610,10 @@ int ddq_read_pool_mask(ddq_ctx* c, int32_t layer, uint8_t* dst, int64_t n) {
   const uint8_t* src = layer == 1 ? c->nb.mask1 : (layer == 2 ? c->nb.mask2 : c->nb.mask3);
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   HIP_TRY(c, scopy(c, tmp.data(), src, cnt, hipMemcpyDeviceToHost));
+  if (layer == 3) {            // pool3 routing is stored in Caffe order already
+    memcpy(dst, tmp.data(), cnt);
+    return DDQ_OK;
+  }
   for (int b = 0; b < B; ++b)
     for (int ch = 0; ch < C; ++ch)
       for (int p = 0; p < Hp * Hp; ++p)

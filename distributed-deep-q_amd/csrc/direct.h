@@ -53,7 +53,8 @@ struct DirectArgs {
   const float* in[2];        // patch source, NHWC (B,H,W,CP)
   const float* wk[2];        // Wk[co][tap][ci] of the layer
   const float* bias[2];      // fwd only
-  float* out[2];             // fwd: pooled NHWC (B,H/2,W/2,N)
+  float* out[2];             // fwd: pooled NHWC (B,H/2,W/2,N), or NCHW if nchw
+  int nchw;                  // fwd: 1 = pooled output / mask in Caffe (B,N,H/2,W/2) order
   uint8_t* mask[2];          // fwd: routing bytes (nullable)
   const uint8_t* pmask;      // dgrad: previous pool's routing bytes (B,H,W,N)
   float* pdconv;             // dgrad: previous layer's pre-pool gradient (B,2H,2W,N)
@@ -232,9 +233,10 @@ __global__ __launch_bounds__(64 * WM * WN) void direct_conv_kernel(const DirectA
           if (v2 > mx) { mx = v2; arg = 2; }
           if (v3 > mx) { mx = v3; arg = 3; }
           const bool pos = mx > 0.f;
-          const size_t q = ((size_t)b * Hp + pyy) * Wp + pxx;
-          a.out[z][q * N + n] = pos ? mx : 0.f;
-          if (a.mask[z]) a.mask[z][q * N + n] = (uint8_t)(pos ? arg : 4);
+          const size_t o = a.nchw ? (((size_t)b * N + n) * Hp + pyy) * Wp + pxx
+                                  : (((size_t)b * Hp + pyy) * Wp + pxx) * N + n;
+          a.out[z][o] = pos ? mx : 0.f;
+          if (a.mask[z]) a.mask[z][o] = (uint8_t)(pos ? arg : 4);
         }
       } else {
         const int W2 = 2 * a.W;

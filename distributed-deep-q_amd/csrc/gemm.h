@@ -15,8 +15,9 @@
 //                                       // or 4 consecutive m / n (false)
 //   struct ACtx; struct BCtx;           // per-thread-slot state fixed over K
 //   ACtx actx(int z, int m) const;      BCtx bctx(int z, int n) const;
-//   float4 loadA(int z, const ACtx&, int m, int k) const;
-//   float4 loadB(int z, const BCtx&, int k, int n) const;
+//   struct KCtx; KCtx ktile(int z, int kb) const;   // per K-tile uniform state
+//   float4 loadA(int z, const ACtx&, const KCtx&, int m, int k) const;
+//   float4 loadB(int z, const BCtx&, const KCtx&, int k, int n) const;
 //   void epilogue(int z, int split, int m0, int n0, const f32x16& acc, int lane) const;
 //   int M, N, K, ksplit_len;            // K range per split (multiple of BK)
 //
@@ -112,15 +113,16 @@ __global__ __launch_bounds__(C::kThreads) void gemm_f32_kernel(const P prob) {
   float4 ra[SA::kPer], rb[SB::kPer];
   auto gload = [&](int kt) {
     const int kb = kbeg + kt * BK;
+    const typename P::KCtx kc = prob.ktile(z, kb);   // K-tile-uniform decode (scalar)
 #pragma unroll
     for (int s = 0; s < SA::kPer; ++s) {
       bool in = (SA::kElems % C::kThreads == 0) || (tid + s * C::kThreads) < SA::kElems;
-      ra[s] = in ? prob.loadA(z, actx[s], m0 + a_mn[s], kb + a_k[s]) : f4zero();
+      ra[s] = in ? prob.loadA(z, actx[s], kc, m0 + a_mn[s], kb + a_k[s]) : f4zero();
     }
 #pragma unroll
     for (int s = 0; s < SB::kPer; ++s) {
       bool in = (SB::kElems % C::kThreads == 0) || (tid + s * C::kThreads) < SB::kElems;
-      rb[s] = in ? prob.loadB(z, bctx[s], kb + b_k[s], n0 + b_mn[s]) : f4zero();
+      rb[s] = in ? prob.loadB(z, bctx[s], kc, kb + b_k[s], n0 + b_mn[s]) : f4zero();
     }
   };
   auto lstore = [&](int buf) {

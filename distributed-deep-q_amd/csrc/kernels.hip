@@ -3,6 +3,7 @@
 #include "kernels.h"
 #include "layers.h"
 #include "direct.h"
+#include "wgrad1.h"
 
 namespace ddq {
 
@@ -502,7 +503,7 @@ using CfgConv1F = GemmCfg<128, 32, 28, 4, 1, 1>;
 using CfgConv2F = GemmCfg<128, 64, 32, 2, 2, 2>;
 using CfgConv3F = GemmCfg<64, 64, 32, 2, 2, 2>;
 using CfgFcF = GemmCfg<32, 64, 64, 1, 2, 2>;
-using CfgFcD = GemmCfg<32, 64, 64, 1, 2, 4>;
+using CfgFcD = GemmCfg<32, 32, 64, 1, 1, 4>;
 using CfgFcW = GemmCfg<64, 64, 32, 2, 2, 1>;
 using CfgW1 = GemmCfg<32, 256, 32, 1, 4, 2>;
 using CfgW2 = GemmCfg<64, 128, 32, 2, 2, 2>;
@@ -510,11 +511,10 @@ using CfgW3 = GemmCfg<64, 128, 32, 2, 2, 2>;
 using CfgD2 = GemmCfg<128, 32, 32, 4, 1, 2>;
 using CfgD3 = GemmCfg<64, 64, 32, 2, 2, 2>;
 
-constexpr int kFc4SplitLen = 256;
+constexpr int kFc4SplitLen = 128;
 constexpr int kWgradSplitLen[3] = {512, 1024, 256};
 constexpr int kWgradBN[3] = {CfgW1::BN, CfgW2::BN, CfgW3::BN};
-constexpr int kWgradBK = 32;
-static_assert(CfgW1::BK == kWgradBK && CfgW2::BK == kWgradBK && CfgW3::BK == kWgradBK, "BK");
+constexpr int kWgradBK[3] = {CfgW1::BK, CfgW2::BK, CfgW3::BK};
 
 // split-K: K per split is a multiple of BK, about `target`
 static inline int split_len(int K, int BK, int target, int* nsplit) {
@@ -531,13 +531,14 @@ int fc4_splits_for(int S) {
   return ns;
 }
 
-int wgrad_splits_for(int layer, int B, int S, int* np) {
+int wgrad_splits_for(int layer, int B, int S, int* np, int impl) {
   const int H = S >> layer;
   const int K = B * H * H;
   const int KC[3] = {196, 800, 576};
   *np = ((KC[layer] + 1 + kWgradBN[layer] - 1) / kWgradBN[layer]) * kWgradBN[layer];
+  if (layer == 0 && impl == 1) return B * (S / wgrad1_band(S, S));   // direct: one slab per band
   int ns;
-  split_len(K, kWgradBK, kWgradSplitLen[layer], &ns);
+  split_len(K, kWgradBK[layer], kWgradSplitLen[layer], &ns);
   return ns;
 }
 
@@ -576,6 +577,7 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
   auto M = [&](const char* n) { if (mark) mark(marg, n); };
   {
     ConvFwd<4, 32, 7, 3> p;
+    p.nchw = 0;
     p.M = B * S * S; p.N = 32; p.K = 196; p.ksplit_len = 196;
     p.H = S; p.W = S; p.fWp = FastDiv(S / 2); p.fHp = FastDiv(S / 2);
     p.in[0] = nb.state; p.in[1] = nb.next_state;
@@ -595,6 +597,7 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
   {
     const int H = S / 2;
     ConvFwd<32, 64, 5, 2> p;
+    p.nchw = 0;
     p.M = B * H * H; p.N = 64; p.K = 800; p.ksplit_len = 800;
     p.H = H; p.W = H; p.fWp = FastDiv(H / 2); p.fHp = FastDiv(H / 2);
     for (int z = 0; z < 2; ++z) {
@@ -620,9 +623,11 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
       p.out[z] = nb.pool3[z];
     }
     p.mask[0] = nb.mask3; p.mask[1] = nullptr;
+    p.nchw = 1; p.fHWp = FastDiv((H / 2) * (H / 2));   // pool3 = fc4 input in Caffe order
     M("conv3_fwd");
     if (nb.conv_impl == 1) {
       DirectArgs d = direct_fwd_args(p.in, p.wk, p.bias, p.out, p.mask, B, H, 1);
+      d.nchw = 1;
       CHECK_LAUNCH((launch_direct<64, 64, 3, 8, 8, 2, 2, false, false>(d, nz, s)));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgConv3F>(p, nz, 1, s));
@@ -634,7 +639,6 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     p.M = B; p.N = kFc4; p.K = 64 * s4 * s4;
     int ns;
     p.ksplit_len = split_len(p.K, CfgFcF::BK, kFc4SplitLen, &ns);
-    p.s4sq = s4 * s4; p.fS4sq = FastDiv(s4 * s4);
     for (int z = 0; z < 2; ++z) { p.x[z] = nb.pool3[z]; p.w[z] = nb.theta[z] + L.w[3]; }
     p.part = nb.fc4_part; p.nz = nz;
     M("fc4_fwd");
@@ -678,7 +682,6 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
   {  // fc4 wgrad
     FcWgrad p;
     p.M = kFc4; p.N = 64 * s4 * s4; p.K = B; p.ksplit_len = ((B + 31) / 32) * 32;
-    p.s4sq = s4 * s4; p.fS4sq = FastDiv(s4 * s4);
     p.dh4 = nb.dh4; p.x = nb.pool3[0]; p.gw4 = nb.grad + L.w[3];
     M("fc4_wgrad");
     CHECK_LAUNCH(launch_gemm<CfgFcW>(p, 1, 1, sw));
@@ -689,7 +692,8 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     ConvWgrad<64, 64, 3, 1> p;
     p.M = 64; p.N = 577; p.K = B * H * H;
     int ns;
-    p.ksplit_len = split_len(p.K, kWgradBK, kWgradSplitLen[2], &ns);
+    p.ksplit_len = split_len(p.K, kWgradBK[2], kWgradSplitLen[2], &ns);
+    p.rowtile = (H % kWgradBK[2]) == 0;
     p.H = H; p.W = H; p.fW = FastDiv(H); p.fH = FastDiv(H);
     p.NP = nb.wnp[2]; p.dconv = nb.dconv3; p.in = nb.pool2[0]; p.part = nb.wpart + nb.wpart_off[2];
     M("conv3_wgrad");
@@ -715,7 +719,8 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     ConvWgrad<32, 64, 5, 2> p;
     p.M = 64; p.N = 801; p.K = B * H * H;
     int ns;
-    p.ksplit_len = split_len(p.K, kWgradBK, kWgradSplitLen[1], &ns);
+    p.ksplit_len = split_len(p.K, kWgradBK[1], kWgradSplitLen[1], &ns);
+    p.rowtile = (H % kWgradBK[1]) == 0;
     p.H = H; p.W = H; p.fW = FastDiv(H); p.fH = FastDiv(H);
     p.NP = nb.wnp[1]; p.dconv = nb.dconv2; p.in = nb.pool1[0]; p.part = nb.wpart + nb.wpart_off[1];
     M("conv2_wgrad");
@@ -739,11 +744,19 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     ConvWgrad<4, 32, 7, 3> p;
     p.M = 32; p.N = 197; p.K = B * S * S;
     int ns;
-    p.ksplit_len = split_len(p.K, kWgradBK, kWgradSplitLen[0], &ns);
+    p.ksplit_len = split_len(p.K, kWgradBK[0], kWgradSplitLen[0], &ns);
+    p.rowtile = (S % kWgradBK[0]) == 0;
     p.H = S; p.W = S; p.fW = FastDiv(S); p.fH = FastDiv(S);
     p.NP = nb.wnp[0]; p.dconv = nb.dconv1; p.in = nb.state; p.part = nb.wpart + nb.wpart_off[0];
     M("conv1_wgrad");
-    CHECK_LAUNCH(launch_gemm<CfgW1>(p, 1, ns, s));
+    if (nb.conv_impl == 1) {
+      Wgrad1Args w;
+      w.B = B; w.H = S; w.W = S; w.R = wgrad1_band(S, S); w.NP = nb.wnp[0];
+      w.dconv = nb.dconv1; w.in = nb.state; w.part = p.part;
+      CHECK_LAUNCH(launch_wgrad1(w, s));
+    } else {
+      CHECK_LAUNCH(launch_gemm<CfgW1>(p, 1, ns, s));
+    }
   }
   {  // slab reduce -> grads (Caffe layout)
     WredDims d[3];

@@ -26,6 +26,8 @@ namespace ddq {
 template <int CIN, int COUT, int KS, int PAD>
 struct ConvFwd {
   static constexpr bool kAK4 = true, kBK4 = true;
+  struct KCtx {};
+  __device__ KCtx ktile(int, int) const { return {}; }
   static constexpr int KC = KS * KS * CIN;
   int M, N, K, ksplit_len;
   int H, W;
@@ -33,8 +35,10 @@ struct ConvFwd {
   const float* in[2];               // NHWC (B,H,W,CIN)
   const float* wk[2];               // [COUT][KS][KS][CIN]
   const float* bias[2];             // [COUT]
-  float* out[2];                    // pooled NHWC (B,H/2,W/2,COUT)
-  uint8_t* mask[2];                 // pooled NHWC argmax bytes (nullable)
+  float* out[2];                    // pooled NHWC (B,H/2,W/2,COUT), or NCHW if nchw
+  uint8_t* mask[2];                 // pooled argmax bytes (nullable), same layout
+  int nchw;                         // 1: pooled output in Caffe (B,C,H/2,W/2) order
+  FastDiv fHWp;                     // (H/2)*(W/2)
 
   struct ACtx { int b, y, x; bool ok; };
   __device__ ACtx actx(int, int m) const {
@@ -48,7 +52,7 @@ struct ConvFwd {
     c.x = 2 * (int)px + (int)(w & 1);
     return c;
   }
-  __device__ float4 loadA(int z, const ACtx& c, int, int k) const {
+  __device__ float4 loadA(int z, const ACtx& c, const KCtx&, int, int k) const {
     if (!c.ok || k >= K) return f4zero();
     const int tap = k / CIN, ci = k % CIN;
     const int ky = tap / KS, kx = tap % KS;
@@ -58,7 +62,7 @@ struct ConvFwd {
   }
   struct BCtx { int n; };
   __device__ BCtx bctx(int, int n) const { return {n}; }
-  __device__ float4 loadB(int z, const BCtx&, int k, int n) const {
+  __device__ float4 loadB(int z, const BCtx&, const KCtx&, int k, int n) const {
     if (n >= N || k >= K) return f4zero();
     return *reinterpret_cast<const float4*>(wk[z] + (size_t)n * KC + k);
   }
@@ -79,8 +83,14 @@ struct ConvFwd {
       if (v2 > mx) { mx = v2; arg = 2; }
       if (v3 > mx) { mx = v3; arg = 3; }
       const bool pos = mx > 0.f;
-      out[z][q * COUT + co] = pos ? mx : 0.f;
-      if (mask[z]) mask[z][q * COUT + co] = (uint8_t)(pos ? arg : 4);
+      size_t o = q * COUT + co;
+      if (nchw) {
+        uint32_t bb, pp;
+        fHWp.divmod((uint32_t)q, bb, pp);
+        o = ((size_t)bb * COUT + co) * fHWp.d + pp;
+      }
+      out[z][o] = pos ? mx : 0.f;
+      if (mask[z]) mask[z][o] = (uint8_t)(pos ? arg : 4);
     }
   }
 };
@@ -99,6 +109,19 @@ struct ConvWgrad {
   int M, N, K, ksplit_len;
   int H, W;
   FastDiv fW, fH;
+  int rowtile;                      // 1: W % BK == 0 (host-checked): every K-tile lies in one image row
+  // K-tile-uniform pixel decode (row tiles): the tile's image b, row y, first x
+  struct KCtx { int b, y, x0, kb; };
+  __device__ KCtx ktile(int, int kb) const {
+    KCtx c{0, 0, 0, kb};
+    if (rowtile) {
+      uint32_t r, x0, b, y;
+      fW.divmod((uint32_t)kb, r, x0);
+      fH.divmod(r, b, y);
+      c.b = (int)b; c.y = (int)y; c.x0 = (int)x0;
+    }
+    return c;
+  }
   int NP;                           // slab row pitch
   const float* dconv;               // NHWC (B,H,W,COUT)
   const float* in;                  // NHWC (B,H,W,CIN)
@@ -106,7 +129,7 @@ struct ConvWgrad {
 
   struct ACtx { int m; };
   __device__ ACtx actx(int, int m) const { return {m}; }
-  __device__ float4 loadA(int, const ACtx&, int m, int k) const {
+  __device__ float4 loadA(int, const ACtx&, const KCtx&, int m, int k) const {
     if (k >= K || m >= M) return f4zero();
     return *reinterpret_cast<const float4*>(dconv + (size_t)k * COUT + m);
   }
@@ -122,12 +145,18 @@ struct ConvWgrad {
     }
     return c;
   }
-  __device__ float4 loadB(int, const BCtx& c, int k, int) const {
+  __device__ float4 loadB(int, const BCtx& c, const KCtx& kc, int k, int) const {
     if (k >= K || c.kind == 2) return f4zero();
     if (c.kind == 1) return f4(1.f, 0.f, 0.f, 0.f);
-    uint32_t t, x, b, y;
-    fW.divmod((uint32_t)k, t, x);
-    fH.divmod(t, b, y);
+    uint32_t x, b, y;
+    if (rowtile) {
+      b = (uint32_t)kc.b; y = (uint32_t)kc.y;
+      x = (uint32_t)(kc.x0 + (k - kc.kb));
+    } else {
+      uint32_t t;
+      fW.divmod((uint32_t)k, t, x);
+      fH.divmod(t, b, y);
+    }
     const int yy = (int)y + c.ky - PAD, xx = (int)x + c.kx - PAD;
     if ((unsigned)yy >= (unsigned)H || (unsigned)xx >= (unsigned)W) return f4zero();
     return *reinterpret_cast<const float4*>(in + (((size_t)b * H + yy) * W + xx) * CIN + c.ci);
@@ -153,6 +182,8 @@ struct ConvWgrad {
 template <int CIN, int COUT, int KS, int PAD>
 struct ConvDgrad {
   static constexpr bool kAK4 = true, kBK4 = false;
+  struct KCtx {};
+  __device__ KCtx ktile(int, int) const { return {}; }
   int M, N, K, ksplit_len;
   int H, W;
   FastDiv fW, fH;
@@ -171,7 +202,7 @@ struct ConvDgrad {
     c.b = (int)b; c.y = (int)y; c.x = (int)x;
     return c;
   }
-  __device__ float4 loadA(int, const ACtx& c, int, int k) const {
+  __device__ float4 loadA(int, const ACtx& c, const KCtx&, int, int k) const {
     if (!c.ok || k >= K) return f4zero();
     const int tap = k / COUT, co = k % COUT;
     const int ky = tap / KS, kx = tap % KS;
@@ -181,7 +212,7 @@ struct ConvDgrad {
   }
   struct BCtx { int n; };
   __device__ BCtx bctx(int, int n) const { return {n}; }
-  __device__ float4 loadB(int, const BCtx&, int k, int n) const {
+  __device__ float4 loadB(int, const BCtx&, const KCtx&, int k, int n) const {
     if (k >= K || n >= N) return f4zero();
     const int tap = k / COUT, co = k % COUT;
     return *reinterpret_cast<const float4*>(wk + ((size_t)co * KS * KS + tap) * CIN + n);
@@ -210,39 +241,28 @@ struct ConvDgrad {
 
 // ---------------------------------------------------------------------------
 // fc4 forward, split-K: part[split][z][b][n] = sum_k x4[b][k] * W4[n][k]
-// x4 is pool3 flattened in Caffe NCHW order k = c*S4^2 + p, gathered from the
-// NHWC pool3 (B,S4^2,64).  M = B, N = 512, K = 64*S4^2.
+// x4 = pool3 stored by conv3's epilogue in Caffe NCHW order (k = c*S4^2 + p),
+// so both operands are contiguous.  M = B, N = 512, K = 64*S4^2.
 // ---------------------------------------------------------------------------
 struct FcFwd {
   static constexpr bool kAK4 = true, kBK4 = true;
+  struct KCtx {};
+  __device__ KCtx ktile(int, int) const { return {}; }
   int M, N, K, ksplit_len;
-  int s4sq;
-  FastDiv fS4sq;
-  const float* x[2];                // NHWC pool3
+  const float* x[2];                // pool3 in Caffe NCHW order = the fc4 input row
   const float* w[2];                // (512, K) Caffe
   float* part;                      // [split][2][M][N]
   int nz;
 
   struct ACtx { int b; bool ok; };
   __device__ ACtx actx(int, int m) const { return {m, m < M}; }
-  __device__ float4 loadA(int z, const ACtx& c, int, int k) const {
-    float v[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int kk = k + j;
-      if (c.ok && kk < K) {
-        uint32_t ch, p;
-        fS4sq.divmod((uint32_t)kk, ch, p);
-        v[j] = x[z][((size_t)c.b * s4sq + p) * 64 + ch];
-      } else {
-        v[j] = 0.f;
-      }
-    }
-    return f4(v[0], v[1], v[2], v[3]);
+  __device__ float4 loadA(int z, const ACtx& c, const KCtx&, int, int k) const {
+    if (!c.ok || k >= K) return f4zero();
+    return *reinterpret_cast<const float4*>(x[z] + (size_t)c.b * K + k);
   }
   struct BCtx { int n; };
   __device__ BCtx bctx(int, int n) const { return {n}; }
-  __device__ float4 loadB(int z, const BCtx&, int k, int n) const {
+  __device__ float4 loadB(int z, const BCtx&, const KCtx&, int k, int n) const {
     if (n >= N || k >= K) return f4zero();
     return *reinterpret_cast<const float4*>(w[z] + (size_t)n * K + k);
   }
@@ -265,23 +285,25 @@ struct FcFwd {
 // ---------------------------------------------------------------------------
 struct FcDgrad {
   static constexpr bool kAK4 = true, kBK4 = false;
+  struct KCtx {};
+  __device__ KCtx ktile(int, int) const { return {}; }
   int M, N, K, ksplit_len;
   int s4, s4sq;
   FastDiv fS4sq, fS4;
   const float* dh4;                 // (B,512)
   const float* w4;                  // (512, N)
-  const uint8_t* mask3;             // NHWC (B,S4,S4,64)
+  const uint8_t* mask3;             // NCHW (B,64,S4,S4)
   float* dconv3;                    // NHWC (B,2S4,2S4,64)
 
   struct ACtx { int b; bool ok; };
   __device__ ACtx actx(int, int m) const { return {m, m < M}; }
-  __device__ float4 loadA(int, const ACtx& c, int, int k) const {
+  __device__ float4 loadA(int, const ACtx& c, const KCtx&, int, int k) const {
     if (!c.ok || k >= K) return f4zero();
     return *reinterpret_cast<const float4*>(dh4 + (size_t)c.b * K + k);
   }
   struct BCtx { int n; };
   __device__ BCtx bctx(int, int n) const { return {n}; }
-  __device__ float4 loadB(int, const BCtx&, int k, int n) const {
+  __device__ float4 loadB(int, const BCtx&, const KCtx&, int k, int n) const {
     if (k >= K || n >= N) return f4zero();
     return *reinterpret_cast<const float4*>(w4 + (size_t)k * N + n);
   }
@@ -296,7 +318,7 @@ struct FcDgrad {
     for (int r = 0; r < 16; ++r) {
       const int b = mb + acc_row(r, lane);
       if (b >= M) continue;
-      const int mk = mask3[((size_t)b * s4sq + p) * 64 + ch];
+      const int mk = mask3[(size_t)b * N + kc];          // NCHW: kc = ch*S4^2 + p
       const float v = acc[r];
       float* base = dconv3 + (((size_t)b * H3 + 2 * py) * H3 + 2 * px) * 64 + ch;
       base[0] = (mk == 0) ? v : 0.f;
@@ -313,35 +335,24 @@ struct FcDgrad {
 // ---------------------------------------------------------------------------
 struct FcWgrad {
   static constexpr bool kAK4 = false, kBK4 = false;
+  struct KCtx {};
+  __device__ KCtx ktile(int, int) const { return {}; }
   int M, N, K, ksplit_len;
-  int s4sq;
-  FastDiv fS4sq;
   const float* dh4;                 // (B,512)
-  const float* x;                   // NHWC pool3 of the Q tower
+  const float* x;                   // pool3 of the Q tower, Caffe NCHW (B, K4)
   float* gw4;                       // (512, N)
 
   struct ACtx { int m; };
   __device__ ACtx actx(int, int m) const { return {m}; }
-  __device__ float4 loadA(int, const ACtx&, int m, int k) const {
+  __device__ float4 loadA(int, const ACtx&, const KCtx&, int m, int k) const {
     if (k >= K || m >= M) return f4zero();
     return *reinterpret_cast<const float4*>(dh4 + (size_t)k * M + m);
   }
   struct BCtx { int n; };
   __device__ BCtx bctx(int, int n) const { return {n}; }
-  __device__ float4 loadB(int, const BCtx&, int k, int n) const {
-    float v[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int kc = n + j;
-      if (k < K && kc < N) {
-        uint32_t ch, p;
-        fS4sq.divmod((uint32_t)kc, ch, p);
-        v[j] = x[((size_t)k * s4sq + p) * 64 + ch];
-      } else {
-        v[j] = 0.f;
-      }
-    }
-    return f4(v[0], v[1], v[2], v[3]);
+  __device__ float4 loadB(int, const BCtx&, const KCtx&, int k, int n) const {
+    if (k >= K || n >= N) return f4zero();
+    return *reinterpret_cast<const float4*>(x + (size_t)k * N + n);
   }
   __device__ void epilogue(int, int, int mb, int nb, const f32x16& acc, int lane) const {
     const int n = nb + (lane & 31);
