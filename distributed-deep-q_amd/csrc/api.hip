@@ -50,6 +50,13 @@ struct ddq_ctx {
   hipGraphExec_t gexec = nullptr;
   ddq_step_cfg gcfg{};
   bool have_graph = false;
+  // pipelined stepping: a second minibatch set and graphs [parity][prefetch]
+  float *mb2_state = nullptr, *mb2_next = nullptr, *mb2_action = nullptr;
+  float *mb2_reward = nullptr, *mb2_nonterm = nullptr;
+  int32_t* mb2_idx = nullptr;
+  hipGraphExec_t pexec[2][2] = {};
+  ddq_step_cfg pcfg{};
+  bool have_pipe = false;
   int64_t steps = 0;
   int64_t applied = 0;               // host mirror of the device iteration counter
   // profiling marks
@@ -123,6 +130,12 @@ static void invalidate_graph(ddq_ctx* c) {
   c->gexec = nullptr;
   c->graph = nullptr;
   c->have_graph = false;
+  for (auto& row : c->pexec)
+    for (auto& g : row) {
+      if (g) hipGraphExecDestroy(g);
+      g = nullptr;
+    }
+  c->have_pipe = false;
 }
 
 extern "C" {
@@ -164,6 +177,8 @@ int ddq_create(ddq_ctx** out, int device, const ddq_net_desc* desc) {
     {
       const char* impl = getenv("DDQ_CONV_IMPL");
       nb.conv_impl = (impl && strcmp(impl, "gemm") == 0) ? 0 : 1;
+      const char* var = getenv("DDQ_VARIANT");
+      nb.variant = var ? atoi(var) : 0;
     }
     nb.L = make_layout(S);
     const int64_t P = nb.L.total;
@@ -551,13 +566,17 @@ int ddq_write_minibatch(ddq_ctx* c, const float* state, const float* action, con
 }
 
 // ---------------- compute ----------------
-static int enqueue_fwd_bwd(ddq_ctx* c, void (*mark)(void*, const char*), void* marg) {
-  HIP_TRY(c, launch_forward(c->nb, 2, c->stream, mark, marg));
+static int enqueue_fwd_bwd(ddq_ctx* c, const NetBuffers& nb, void (*mark)(void*, const char*),
+                           void* marg) {
+  HIP_TRY(c, launch_forward(nb, 2, c->stream, mark, marg));
   if (mark) mark(marg, "head");
-  HIP_TRY(c, launch_head(c->nb, c->stream));
+  HIP_TRY(c, launch_head(nb, c->stream));
   // per-kernel event timing needs one stream; otherwise overlap wgrad with dgrad
-  HIP_TRY(c, launch_backward(c->nb, c->stream, mark, marg, mark == nullptr));
+  HIP_TRY(c, launch_backward(nb, c->stream, mark, marg, mark == nullptr));
   return DDQ_OK;
+}
+static int enqueue_fwd_bwd(ddq_ctx* c, void (*mark)(void*, const char*), void* marg) {
+  return enqueue_fwd_bwd(c, c->nb, mark, marg);
 }
 
 int ddq_forward_backward_async(ddq_ctx* c) {
@@ -717,6 +736,35 @@ int ddq_allreduce_grads(ddq_ctx* c) {
 }
 
 // ---------------- step ----------------
+// fwd/bwd -> [all-reduce] -> apply on the minibatch held by `nb`; when
+// `pre` is given, the NEXT step's sample + gather into `pre`'s minibatch
+// set run on the side stream under this step's forward (the replay ring is
+// not written inside a step, and the device RNG counter advances in the
+// same order, so the index stream equals the sequential one).
+static int enqueue_train(ddq_ctx* c, const ddq_step_cfg* cfg, const NetBuffers& nb,
+                         const NetBuffers* pre, void (*mark)(void*, const char*), void* marg) {
+  if (pre) {
+    HIP_TRY(c, hipEventRecord(nb.ev[6], c->stream));
+    HIP_TRY(c, hipStreamWaitEvent(nb.side, nb.ev[6], 0));
+    HIP_TRY(c, launch_sample(*pre, c->r_meta, cfg->seed, nb.side));
+    HIP_TRY(c, launch_gather(*pre, c->r_state, c->r_action, c->r_reward, c->r_nonterm, c->r_meta,
+                             nb.side));
+    HIP_TRY(c, hipEventRecord(nb.ev[7], nb.side));
+  }
+  TRY(enqueue_fwd_bwd(c, nb, mark, marg));
+  if (cfg->allreduce && c->nranks > 1) {
+    if (mark) mark(marg, "allreduce");
+    NCCL_TRY(c, ncclAllReduce(nb.grad, nb.grad, (size_t)nb.L.total, ncclFloat, ncclSum, c->comm,
+                              c->stream));
+  }
+  if (mark) mark(marg, "apply");
+  const ddq_update_cfg& u = cfg->update;
+  HIP_TRY(c, launch_apply(nb, u.rule, u.lr, u.decay, u.eps, u.momentum, u.weight_decay,
+                          cfg->target_period, c->stream));
+  if (pre) HIP_TRY(c, hipStreamWaitEvent(c->stream, nb.ev[7], 0));
+  return DDQ_OK;
+}
+
 static int enqueue_step(ddq_ctx* c, const ddq_step_cfg* cfg, void (*mark)(void*, const char*),
                         void* marg) {
   if (mark) mark(marg, "sample");
@@ -724,17 +772,17 @@ static int enqueue_step(ddq_ctx* c, const ddq_step_cfg* cfg, void (*mark)(void*,
   if (mark) mark(marg, "gather");
   HIP_TRY(c, launch_gather(c->nb, c->r_state, c->r_action, c->r_reward, c->r_nonterm, c->r_meta,
                            c->stream));
-  TRY(enqueue_fwd_bwd(c, mark, marg));
-  if (cfg->allreduce && c->nranks > 1) {
-    if (mark) mark(marg, "allreduce");
-    NCCL_TRY(c, ncclAllReduce(c->nb.grad, c->nb.grad, (size_t)c->nb.L.total, ncclFloat, ncclSum,
-                              c->comm, c->stream));
+  return enqueue_train(c, cfg, c->nb, nullptr, mark, marg);
+}
+
+// minibatch set p: 0 = the ctx's own buffers, 1 = the pipelining twin
+static NetBuffers mb_view(const ddq_ctx* c, int p) {
+  NetBuffers v = c->nb;
+  if (p == 1) {
+    v.state = c->mb2_state; v.next_state = c->mb2_next; v.action = c->mb2_action;
+    v.reward = c->mb2_reward; v.nonterm = c->mb2_nonterm; v.idx = c->mb2_idx;
   }
-  if (mark) mark(marg, "apply");
-  const ddq_update_cfg& u = cfg->update;
-  HIP_TRY(c, launch_apply(c->nb, u.rule, u.lr, u.decay, u.eps, u.momentum, u.weight_decay,
-                          cfg->target_period, c->stream));
-  return DDQ_OK;
+  return v;
 }
 
 // The pull at iteration 0 copies Q -> P (server.py:188-189, 0 % period == 0);
@@ -792,6 +840,57 @@ int ddq_step_graph_async(ddq_ctx* c, const ddq_step_cfg* cfg, int32_t nsteps) {
     HIP_TRY(c, hipGraphLaunch(c->gexec, c->stream));
     c->steps++;
     c->applied++;
+  }
+  return DDQ_OK;
+}
+
+// nsteps training steps as a chain of graph replays in which step t+1's
+// sample + gather overlap step t.  Graph [p][f] trains on minibatch set p
+// and (f = 1) prefetches into set 1-p; the chain starts on the parity that
+// makes the LAST step train on set 0, so afterwards the ctx's minibatch,
+// indices and counters are exactly those of nsteps sequential steps.
+int ddq_step_pipelined_async(ddq_ctx* c, const ddq_step_cfg* cfg, int32_t nsteps) {
+  TRY(check_step(c, cfg));
+  TRY(set_dev(c));
+  if (nsteps <= 0) return DDQ_OK;
+  if (!c->mb2_state) {
+    const int B = c->nb.B, S = c->nb.S;
+    TRY(dalloc(c, &c->mb2_state, (size_t)B * S * S * 4));
+    TRY(dalloc(c, &c->mb2_next, (size_t)B * S * S * 4));
+    TRY(dalloc(c, &c->mb2_action, (size_t)B * 4));
+    TRY(dalloc(c, &c->mb2_reward, (size_t)B));
+    TRY(dalloc(c, &c->mb2_nonterm, (size_t)B));
+    TRY(dalloc(c, &c->mb2_idx, (size_t)B));
+  }
+  if (!c->have_pipe || memcmp(&c->pcfg, cfg, sizeof(*cfg)) != 0) {
+    invalidate_graph(c);
+    for (int p = 0; p < 2; ++p)
+      for (int f = 0; f < 2; ++f) {
+        const NetBuffers cur = mb_view(c, p), nxt = mb_view(c, 1 - p);
+        HIP_TRY(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+        int rc = enqueue_train(c, cfg, cur, f ? &nxt : nullptr, nullptr, nullptr);
+        hipGraph_t g = nullptr;
+        hipError_t e = hipStreamEndCapture(c->stream, &g);
+        if (rc != DDQ_OK) { if (g) hipGraphDestroy(g); return rc; }
+        if (e != hipSuccess) return fail(c, DDQ_EHIP, "hipStreamEndCapture: %s", hipGetErrorString(e));
+        e = hipGraphInstantiate(&c->pexec[p][f], g, nullptr, nullptr, 0);
+        hipGraphDestroy(g);
+        if (e != hipSuccess) return fail(c, DDQ_EHIP, "hipGraphInstantiate: %s", hipGetErrorString(e));
+      }
+    c->pcfg = *cfg;
+    c->have_pipe = true;
+  }
+  if (c->steps == 0) TRY(initial_target_sync(c, cfg));
+  int p = (nsteps - 1) & 1;
+  const NetBuffers first = mb_view(c, p);
+  HIP_TRY(c, launch_sample(first, c->r_meta, cfg->seed, c->stream));
+  HIP_TRY(c, launch_gather(first, c->r_state, c->r_action, c->r_reward, c->r_nonterm, c->r_meta,
+                           c->stream));
+  for (int i = 0; i < nsteps; ++i) {
+    HIP_TRY(c, hipGraphLaunch(c->pexec[p][i + 1 < nsteps ? 1 : 0], c->stream));
+    c->steps++;
+    c->applied++;
+    p ^= 1;
   }
   return DDQ_OK;
 }

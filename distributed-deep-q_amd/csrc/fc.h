@@ -1,0 +1,187 @@
+// fc4 forward / data-gradient kernels, register-direct MFMA (gfx950).
+//
+// fc4 is skinny (M = batch <= 32 per tile, N = 512, K = 64*(S/8)^2 = 4096 at
+// 64x64): its cost is streaming W4 (8.4 MB per tower), not arithmetic.  The
+// LDS-staged GEMM engine pays a global->LDS->MFMA round trip per K-step for
+// operands that are used once, so these kernels feed v_mfma_f32_32x32x2_f32
+// straight from registers: for a 32-deep k block, lane (l31, h) loads 16
+// consecutive k of its row (four float4) and MFMA step j pairs k = 16h + j of
+// both operands, so every wave issues all its loads up front (full memory-
+// level parallelism) and there is no LDS traffic in the K loop.
+#pragma once
+#include "common.h"
+
+namespace ddq {
+
+__device__ __forceinline__ int fc_acc_row(int r, int lane) {
+  return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+}
+__device__ __forceinline__ float f4get(const float4& v, int i) {
+  return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
+}
+
+// ---------------------------------------------------------------------------
+// forward, split-K: part[split][z][b][n] = sum_{k in split} x[z][b][k] W4[z][n][k]
+// grid (512/128, splits, nz), 4 waves; wave w owns n0 = 128*bx + 32*w, all b.
+// x = pool3 in Caffe NCHW order (B, K); W4 Caffe (512, K).  K % 32 == 0.
+// ---------------------------------------------------------------------------
+constexpr int kFc4KLen = 128;     // k per split
+
+struct Fc4FwdArgs {
+  int B, K, nz;
+  const float* x[2];
+  const float* w[2];
+  float* part;                     // [split][nz][B][512]
+};
+
+template <int BT>
+__global__ __launch_bounds__(256) void fc4_fwd_direct_kernel(const Fc4FwdArgs a) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int l31 = lane & 31, h = lane >> 5;
+  const int z = blockIdx.z, split = blockIdx.y;
+  const int n0 = blockIdx.x * 128 + w * 32;
+  const int K = a.K;
+  const int k0 = split * kFc4KLen;
+  const float* wr = a.w[z] + (size_t)(n0 + l31) * K + h * 16;
+  const float* xz = a.x[z] + h * 16;
+
+  f32x16 acc[BT];
+#pragma unroll
+  for (int t = 0; t < BT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+  float4 wv[kFc4KLen / 32][4];
+  float4 xv[kFc4KLen / 32][BT][4];
+#pragma unroll
+  for (int kb = 0; kb < kFc4KLen / 32; ++kb) {
+    const int k = k0 + kb * 32;
+    const bool kin = k < K;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      wv[kb][i] = kin ? *reinterpret_cast<const float4*>(wr + k + 4 * i) : f4zero();
+#pragma unroll
+    for (int t = 0; t < BT; ++t) {
+      const int b = t * 32 + l31;
+      const bool ok = kin && b < a.B;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        xv[kb][t][i] = ok ? *reinterpret_cast<const float4*>(xz + (size_t)b * K + k + 4 * i)
+                          : f4zero();
+    }
+  }
+#pragma unroll
+  for (int kb = 0; kb < kFc4KLen / 32; ++kb)
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+#pragma unroll
+      for (int t = 0; t < BT; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(xv[kb][t][j >> 2], j & 3),
+                                                      f4get(wv[kb][j >> 2], j & 3), acc[t], 0,
+                                                      0, 0);
+  // rows = b, columns = n: lanes store consecutive n
+  float* dst = a.part + ((size_t)(split * a.nz + z) * a.B) * 512 + n0 + l31;
+#pragma unroll
+  for (int t = 0; t < BT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int b = t * 32 + fc_acc_row(r, lane);
+      if (b < a.B) dst[(size_t)b * 512] = acc[t][r];
+    }
+}
+
+inline int fc4_fwd_splits(int K) { return (K + kFc4KLen - 1) / kFc4KLen; }
+
+inline hipError_t launch_fc4_fwd_direct(const Fc4FwdArgs& a, hipStream_t st) {
+  dim3 grid(512 / 128, fc4_fwd_splits(a.K), a.nz);
+  if (a.B <= 32)
+    hipLaunchKernelGGL(fc4_fwd_direct_kernel<1>, grid, dim3(256), 0, st, a);
+  else if (a.B <= 64)
+    hipLaunchKernelGGL(fc4_fwd_direct_kernel<2>, grid, dim3(256), 0, st, a);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// data gradient fused with the pool3 un-pool:
+// dx[b][kc] = sum_n dh4[b][n] W4[n][kc]  (kc Caffe order ch*S4^2 + p), then
+// dconv3[b][2py+dy][2px+dx][ch] = (mask3[b][kc] == 2dy+dx) ? dx : 0.
+// grid (K/32, ceil(B/32)); 8 waves split n (64 each) and are summed through
+// LDS in fixed order.  A = dh4 rows (float4 along n), B = W4 columns (one
+// dword per n, lanes along kc: coalesced 128-byte rows).
+// ---------------------------------------------------------------------------
+struct Fc4DgradArgs {
+  int B, K, s4;
+  FastDiv fS4sq, fS4;
+  const float* dh4;                // (B, 512)
+  const float* w4;                 // (512, K)
+  const uint8_t* mask3;            // NCHW (B, 64, S4, S4)
+  float* dconv3;                   // NHWC (B, 2S4, 2S4, 64)
+};
+
+__global__ __launch_bounds__(512) void fc4_dgrad_direct_kernel(const Fc4DgradArgs a) {
+  __shared__ float red[8][1024];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int l31 = lane & 31, h = lane >> 5;
+  const int kc0 = blockIdx.x * 32, b0 = blockIdx.y * 32;
+  const int K = a.K;
+  const int nbase = w * 64 + h * 16;
+  const int b = b0 + l31;
+  const bool bok = b < a.B;
+  const float* ar = a.dh4 + (size_t)(bok ? b : 0) * 512 + nbase;
+  const float* br = a.w4 + (size_t)nbase * K + kc0 + l31;
+
+  float4 av[2][4];
+  float bv[2][16];
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      av[blk][i] = bok ? *reinterpret_cast<const float4*>(ar + blk * 32 + 4 * i) : f4zero();
+#pragma unroll
+    for (int j = 0; j < 16; ++j) bv[blk][j] = br[(size_t)(blk * 32 + j) * K];
+  }
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(av[blk][j >> 2], j & 3), bv[blk][j], acc,
+                                                 0, 0, 0);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) red[w][r * 64 + lane] = acc[r];
+  __syncthreads();
+  // 512 threads x 2 elements of the 32 x 32 tile; fixed-order wave sum
+  const int H3 = 2 * a.s4;
+#pragma unroll
+  for (int e2 = 0; e2 < 2; ++e2) {
+    const int e = threadIdx.x + 512 * e2;
+    float v = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 8; ++ww) v += red[ww][e];
+    const int r = e >> 6, ln = e & 63;
+    const int bb = b0 + fc_acc_row(r, ln);
+    const int kc = kc0 + (ln & 31);
+    if (bb >= a.B) continue;
+    uint32_t ch, p, py, px;
+    a.fS4sq.divmod((uint32_t)kc, ch, p);
+    a.fS4.divmod(p, py, px);
+    const int mk = a.mask3[(size_t)bb * K + kc];
+    float* base = a.dconv3 + (((size_t)bb * H3 + 2 * py) * H3 + 2 * px) * 64 + ch;
+    base[0] = (mk == 0) ? v : 0.f;
+    base[64] = (mk == 1) ? v : 0.f;
+    base[(size_t)H3 * 64] = (mk == 2) ? v : 0.f;
+    base[(size_t)H3 * 64 + 64] = (mk == 3) ? v : 0.f;
+  }
+}
+
+inline hipError_t launch_fc4_dgrad_direct(const Fc4DgradArgs& a, hipStream_t st) {
+  dim3 grid(a.K / 32, (a.B + 31) / 32);
+  hipLaunchKernelGGL(fc4_dgrad_direct_kernel, grid, dim3(512), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace ddq

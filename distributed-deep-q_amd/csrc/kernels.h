@@ -55,6 +55,7 @@ struct NetBuffers {
   ParamLayout L;
   float gamma;
   int conv_impl;                    // 0 = implicit-GEMM engine, 1 = direct (patch-in-LDS)
+  int variant;                      // tuning experiments (DDQ_VARIANT bits), 0 = default
 };
 
 hipError_t launch_gather(const NetBuffers& nb, const uint8_t* st, const uint8_t* act,

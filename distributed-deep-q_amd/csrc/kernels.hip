@@ -4,6 +4,8 @@
 #include "layers.h"
 #include "direct.h"
 #include "wgrad1.h"
+#include "wgradd.h"
+#include "fc.h"
 
 namespace ddq {
 
@@ -537,6 +539,12 @@ int wgrad_splits_for(int layer, int B, int S, int* np, int impl) {
   const int KC[3] = {196, 800, 576};
   *np = ((KC[layer] + 1 + kWgradBN[layer] - 1) / kWgradBN[layer]) * kWgradBN[layer];
   if (layer == 0 && impl == 1) return B * (S / wgrad1_band(S, S));   // direct: one slab per band
+  if (impl == 1) {                                                    // direct: one slab per row group
+    const int nts[3] = {0, 2 * 5, 2 * 3};
+    int G, RPG;
+    wgradd_groups(B * H, nts[layer], &G, &RPG);
+    return G;
+  }
   int ns;
   split_len(K, kWgradBK[layer], kWgradSplitLen[layer], &ns);
   return ns;
@@ -568,6 +576,15 @@ static DirectArgs direct_dgrad_args(const float* dconv, const float* wk, const u
   d.in[0] = d.in[1] = dconv; d.wk[0] = d.wk[1] = wk;
   d.pmask = pmask; d.pdconv = pdconv;
   return d;
+}
+
+template <class P>
+static WgradDArgs wgradd_args(const P& p, int B, int G) {
+  WgradDArgs a;
+  a.B = B; a.H = p.H; a.W = p.W; a.G = G;
+  a.RPG = (B * p.H + G - 1) / G;
+  a.NP = p.NP; a.dconv = p.dconv; a.in = p.in; a.part = p.part;
+  return a;
 }
 
 hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
@@ -628,7 +645,10 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     if (nb.conv_impl == 1) {
       DirectArgs d = direct_fwd_args(p.in, p.wk, p.bias, p.out, p.mask, B, H, 1);
       d.nchw = 1;
-      CHECK_LAUNCH((launch_direct<64, 64, 3, 8, 8, 2, 2, false, false>(d, nz, s)));
+      if (nb.variant & 2)
+        CHECK_LAUNCH((launch_direct<64, 64, 3, 4, 8, 1, 2, false, false>(d, nz, s)));
+      else
+        CHECK_LAUNCH((launch_direct<64, 64, 3, 8, 8, 2, 2, false, false>(d, nz, s)));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgConv3F>(p, nz, 1, s));
     }
@@ -642,7 +662,14 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     for (int z = 0; z < 2; ++z) { p.x[z] = nb.pool3[z]; p.w[z] = nb.theta[z] + L.w[3]; }
     p.part = nb.fc4_part; p.nz = nz;
     M("fc4_fwd");
-    CHECK_LAUNCH(launch_gemm<CfgFcF>(p, nz, ns, s));
+    if (!(nb.variant & 4)) {   // register-direct (bit 4: LDS GEMM engine, A/B)
+      Fc4FwdArgs f;
+      f.B = B; f.K = p.K; f.nz = nz; f.part = nb.fc4_part;
+      for (int z = 0; z < 2; ++z) { f.x[z] = p.x[z]; f.w[z] = p.w[z]; }
+      CHECK_LAUNCH(launch_fc4_fwd_direct(f, s));
+    } else {
+      CHECK_LAUNCH(launch_gemm<CfgFcF>(p, nz, ns, s));
+    }
     M("fc4_reduce_out");
     hipLaunchKernelGGL(fc4_reduce_out_kernel, dim3(B, nz), dim3(kFc4), 0, s, nb.fc4_part, ns, nz,
                        B, nb.theta[0] + L.b[3], nb.theta[1] + L.b[3], nb.theta[0] + L.w[4],
@@ -677,7 +704,14 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     p.dh4 = nb.dh4; p.w4 = nb.theta[0] + L.w[3]; p.mask3 = nb.mask3; p.dconv3 = nb.dconv3;
     CHECK_LAUNCH(fork());   // side: fc4 wgrad needs only dh4 (head) -> fork before dgrad
     M("fc4_dgrad");
-    CHECK_LAUNCH(launch_gemm<CfgFcD>(p, 1, 1, s));
+    if (!(nb.variant & 8)) {   // register-direct (bit 8: LDS GEMM engine, A/B)
+      Fc4DgradArgs f;
+      f.B = B; f.K = p.N; f.s4 = s4; f.fS4sq = p.fS4sq; f.fS4 = p.fS4;
+      f.dh4 = nb.dh4; f.w4 = p.w4; f.mask3 = nb.mask3; f.dconv3 = nb.dconv3;
+      CHECK_LAUNCH(launch_fc4_dgrad_direct(f, s));
+    } else {
+      CHECK_LAUNCH(launch_gemm<CfgFcD>(p, 1, 1, s));
+    }
   }
   {  // fc4 wgrad
     FcWgrad p;
@@ -697,7 +731,11 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     p.H = H; p.W = H; p.fW = FastDiv(H); p.fH = FastDiv(H);
     p.NP = nb.wnp[2]; p.dconv = nb.dconv3; p.in = nb.pool2[0]; p.part = nb.wpart + nb.wpart_off[2];
     M("conv3_wgrad");
-    CHECK_LAUNCH(launch_gemm<CfgW3>(p, 1, ns, sw));
+    if (nb.conv_impl == 1) {
+      CHECK_LAUNCH((launch_wgradd<64, 64, 3, 1>(wgradd_args(p, B, nb.wsplits[2]), sw)));
+    } else {
+      CHECK_LAUNCH(launch_gemm<CfgW3>(p, 1, ns, sw));
+    }
   }
   {  // conv3 dgrad -> dconv2
     const int H = S / 4;
@@ -707,8 +745,11 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     p.dconv = nb.dconv3; p.wk = nb.wk[0] + L.wk_off[2]; p.pmask = nb.mask2; p.pdconv = nb.dconv2;
     M("conv3_dgrad");
     if (nb.conv_impl == 1) {
-      CHECK_LAUNCH((launch_direct<64, 64, 3, 8, 8, 2, 2, true, false>(
-          direct_dgrad_args(nb.dconv3, p.wk, nb.mask2, nb.dconv2, B, H, 1), 1, s)));
+      const DirectArgs d = direct_dgrad_args(nb.dconv3, p.wk, nb.mask2, nb.dconv2, B, H, 1);
+      if (nb.variant & 1)
+        CHECK_LAUNCH((launch_direct<64, 64, 3, 4, 8, 1, 2, true, false>(d, 1, s)));
+      else
+        CHECK_LAUNCH((launch_direct<64, 64, 3, 8, 8, 2, 2, true, false>(d, 1, s)));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgD3>(p, 1, 1, s));
     }
@@ -724,7 +765,11 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     p.H = H; p.W = H; p.fW = FastDiv(H); p.fH = FastDiv(H);
     p.NP = nb.wnp[1]; p.dconv = nb.dconv2; p.in = nb.pool1[0]; p.part = nb.wpart + nb.wpart_off[1];
     M("conv2_wgrad");
-    CHECK_LAUNCH(launch_gemm<CfgW2>(p, 1, ns, sw));
+    if (nb.conv_impl == 1) {
+      CHECK_LAUNCH((launch_wgradd<32, 64, 5, 2>(wgradd_args(p, B, nb.wsplits[1]), sw)));
+    } else {
+      CHECK_LAUNCH(launch_gemm<CfgW2>(p, 1, ns, sw));
+    }
   }
   {  // conv2 dgrad -> dconv1
     const int H = S / 2;

@@ -1,0 +1,214 @@
+// conv2 / conv3 weight gradient, direct form (gfx950).
+//
+// dW[co][ky][kx][ci] = sum_{b,y,x} dconv[b][y][x][co] * in[b][y+ky-P][x+kx-P][ci]
+// db[co]             = sum_{b,y,x} dconv[b][y][x][co]
+//
+// The implicit-GEMM form re-derives (b, y, x, ky, kx, ci) for every staged
+// operand (8-15 VALU per MFMA measured).  Here a workgroup owns one
+// (co block cb, tap row ky) pair -- KS x CIN/32 output tiles of 32 x 32
+// (tile (kx, cib) = columns n = (ky*KS + kx)*CIN + cib*32 + 0..31) -- over a
+// contiguous group of image rows.  Each wave streams its own rows through a
+// private LDS region: the input row y+ky-P (with a zero halo of P pixels) and
+// the cb block of the dconv row.  One MFMA k-step covers the pixel pair
+// (2s, 2s+1): the dconv operand is read once and feeds every tile of the
+// wave (KS*CIN/32 MFMAs per ds_read of A, one ds_read of B each), so the
+// inner loop is pure LDS->MFMA with no index math.  The bias column is
+// summed on the VALU from the staged dconv rows by the ky == 0 workgroups.
+// At the end the four waves' accumulators are summed through LDS (fixed
+// order, deterministic) and stored as the group's fp32 slab in the wgrad
+// reducer's layout ([group][co][n], bias at n = KC).
+#pragma once
+#include "common.h"
+
+namespace ddq {
+
+struct WgradDArgs {
+  int B, H, W;              // layer grid (input and dconv share H x W)
+  int G, RPG;               // row groups (= slabs) and rows per group
+  int NP;                   // slab pitch
+  const float* dconv;       // NHWC (B,H,W,COUT)
+  const float* in;          // NHWC (B,H,W,CIN)
+  float* part;              // [G][COUT][NP]
+};
+
+template <int CIN, int PAD>
+struct WgradDGeom {
+  // floats of one wave's LDS region for width W
+  static __host__ __device__ int in_floats(int W) { return (((W + 2 * PAD + 1) * CIN) + 3) & ~3; }
+  static __host__ __device__ int region(int W) { return in_floats(W) + ((W + 1) >> 1) * 64; }
+};
+
+template <int CIN, int COUT, int KS, int PAD>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void wgradd_kernel(
+    const WgradDArgs a) {
+  constexpr int NCB = CIN / 32;
+  constexpr int T = KS * NCB;
+  constexpr int KC = KS * KS * CIN;
+  using Geo = WgradDGeom<CIN, PAD>;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int W = a.W, H = a.H;
+  const int W2 = (W + 1) >> 1;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int l31 = lane & 31, h = lane >> 5;
+  const int inf = Geo::in_floats(W);
+  float* rin = sm + w * Geo::region(W);     // input row, pixel 0 <-> x = -PAD
+  float* rd = rin + inf;                    // dconv row, [x][32] of block cb
+  const int cb = blockIdx.y / KS, ky = blockIdx.y % KS;
+  const int r0 = blockIdx.x * a.RPG;
+  const int r1 = min(a.B * H, r0 + a.RPG);
+
+  // zero halo columns (never overwritten) and the odd-width tail pixel
+  for (int i = lane; i < PAD * CIN; i += 64) rin[i] = 0.f;
+  for (int i = lane; i < (PAD + 1) * CIN; i += 64) rin[(PAD + W) * CIN + i] = 0.f;
+  if (W & 1)
+    for (int i = lane; i < 32; i += 64) rd[W * 32 + i] = 0.f;
+
+  f32x16 acc[T];
+  float4 bsum = f4zero();                   // bias: lane sums channels 4*(lane&7).. of block cb
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+  // Row staging: a wave moves W*CIN/4 + W*8 float4 per row through bounds-
+  // checked buffer loads (out-of-range rows / halo rows read as 0 with no
+  // branch).  When both fit one 64-lane x 4 batch (S <= 64) the next row's
+  // loads are issued before the current row's MFMAs from a second register
+  // set (rows unrolled by two so no copies force an early vmcnt wait);
+  // otherwise rows are staged synchronously in 4-deep batches.
+  const int nin = W * CIN / 4, nd = W * 8;
+  const int rows_total = a.B * H;
+  const __amdgpu_buffer_rsrc_t rs_in =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.in, (short)0, rows_total * W * CIN * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_d = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.dconv, (short)0, rows_total * W * COUT * 4, 0x00020000);
+  constexpr int kOOB = 0x7ff00000;   // beyond any tensor here: reads 0
+  struct Regs { float4 i[4], d[4]; };
+  auto load = [&](Regs& g, int row, int base) {
+    const int b = row / H, yi = row - b * H + ky - PAD;
+    const bool vin = (unsigned)yi < (unsigned)H && row < rows_total;
+    const int ib = vin ? (b * H + yi) * W * CIN * 4 : kOOB;
+    const int db = row < rows_total ? (row * W * COUT + cb * 32) * 4 : kOOB;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = base + lane + 64 * j;
+      const int oi = i < nin ? ib + i * 16 : kOOB;
+      const int od = i < nd ? db + ((i >> 3) * COUT + (i & 7) * 4) * 4 : kOOB;
+      auto vi = __builtin_amdgcn_raw_buffer_load_b128(rs_in, oi, 0, 0);
+      auto vd = __builtin_amdgcn_raw_buffer_load_b128(rs_d, od, 0, 0);
+      g.i[j] = *reinterpret_cast<float4*>(&vi);
+      g.d[j] = *reinterpret_cast<float4*>(&vd);
+    }
+  };
+  auto store = [&](const Regs& g, int base) {
+    float4* dst = reinterpret_cast<float4*>(rin + PAD * CIN);
+    float4* dd = reinterpret_cast<float4*>(rd);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = base + lane + 64 * j;
+      if (i < nin) dst[i] = g.i[j];
+      if (i < nd) {
+        dd[i] = g.d[j];
+        bsum.x += g.d[j].x; bsum.y += g.d[j].y; bsum.z += g.d[j].z; bsum.w += g.d[j].w;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  // ---- MFMA: k-step s = pixels (2s, 2s+1); lane half h takes pixel 2s+h ----
+  auto compute = [&]() {
+    const float* pa = rd + h * 32 + l31;
+    const float* pb = rin + h * CIN + l31;
+    for (int s = 0; s < W2; ++s) {
+      const float av = pa[s * 64];
+#pragma unroll
+      for (int kx = 0; kx < KS; ++kx)
+#pragma unroll
+        for (int c = 0; c < NCB; ++c)
+          acc[kx * NCB + c] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+              av, pb[(2 * s + kx) * CIN + c * 32], acc[kx * NCB + c], 0, 0, 0);
+    }
+    __builtin_amdgcn_wave_barrier();
+  };
+
+  if (nin <= 256 && nd <= 256) {
+    Regs ga, gb;
+    int row = r0 + w;
+    if (row < r1) load(ga, row, 0);
+    for (; row < r1; row += 8) {
+      store(ga, 0);
+      load(gb, row + 4, 0);          // rows past r1 only read (bounded), never staged
+      compute();
+      if (row + 4 >= r1) break;
+      store(gb, 0);
+      load(ga, row + 8, 0);
+      compute();
+    }
+  } else {
+    Regs g;
+    const int nmax = nin > nd ? nin : nd;
+    for (int row = r0 + w; row < r1; row += 4) {
+      for (int base = 0; base < nmax; base += 256) { load(g, row, base); store(g, base); }
+      compute();
+    }
+  }
+
+  // ---- sum the four waves' tiles in fixed order, store the group slab ----
+  float* red = sm;                                   // [4 waves][16 r][64 lanes]
+  float* slab = a.part + (size_t)blockIdx.x * COUT * a.NP + (size_t)cb * 32 * a.NP;
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[(w * 16 + r) * 64 + lane] = acc[t][r];
+    __syncthreads();
+    const int nbase = (ky * KS + t / NCB) * CIN + (t % NCB) * 32;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = w + 4 * j;                       // element (r, lane) of the tile
+      const int e = r * 64 + lane;
+      const float v = (red[e] + red[1024 + e]) + (red[2048 + e] + red[3072 + e]);
+      const int co = (r & 3) + 8 * (r >> 2) + 4 * h;
+      slab[(size_t)co * a.NP + nbase + l31] = v;
+    }
+  }
+  if (ky == 0) {   // bias column n = KC: lanes l, l+8, ... of every wave share channels
+    __syncthreads();
+    reinterpret_cast<float4*>(red)[w * 64 + lane] = bsum;
+    __syncthreads();
+    if (threadIdx.x < 32) {
+      const int co = threadIdx.x, q = co >> 2, c = co & 3;
+      float v = 0.f;
+      for (int ww = 0; ww < 4; ++ww)
+        for (int l = q; l < 64; l += 8) v += red[(ww * 64 + l) * 4 + c];
+      slab[(size_t)co * a.NP + KC] = v;
+    }
+  }
+}
+
+template <int CIN, int PAD>
+inline size_t wgradd_smem_bytes(int W) {
+  const int f = 4 * WgradDGeom<CIN, PAD>::region(W);
+  return (size_t)(f > 4096 ? f : 4096) * 4;
+}
+
+// Row groups: about two 4-wave workgroups per CU over all (cb, ky) pairs.
+inline void wgradd_groups(int rows, int nts, int* G, int* RPG) {
+  int g = 512 / nts;
+  if (g < 1) g = 1;
+  if (g > rows) g = rows;
+  const int rpg = (rows + g - 1) / g;
+  *RPG = rpg;
+  *G = (rows + rpg - 1) / rpg;
+}
+
+template <int CIN, int COUT, int KS, int PAD>
+inline hipError_t launch_wgradd(const WgradDArgs& a, hipStream_t st) {
+  const size_t shm = wgradd_smem_bytes<CIN, PAD>(a.W);
+  hipLaunchKernelGGL((wgradd_kernel<CIN, COUT, KS, PAD>), dim3(a.G, (COUT / 32) * KS), dim3(256),
+                     shm, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace ddq

@@ -93,6 +93,7 @@ _SIGS = {
     "ddq_allreduce_grads_async": (ctypes.c_int, [_P]),
     "ddq_step_async": (ctypes.c_int, [_P, ctypes.POINTER(StepCfg)]),
     "ddq_step_graph_async": (ctypes.c_int, [_P, ctypes.POINTER(StepCfg), _i32]),
+    "ddq_step_pipelined_async": (ctypes.c_int, [_P, ctypes.POINTER(StepCfg), _i32]),
     "ddq_step_count": (_i64, [_P]),
     "ddq_profile_step": (ctypes.c_int, [_P, ctypes.POINTER(StepCfg), _P, _fp, _i32,
                                         ctypes.POINTER(_i32)]),

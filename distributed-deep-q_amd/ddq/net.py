@@ -269,6 +269,10 @@ class DeepQNet:
     def step_graph(self, cfg, nsteps):
         self._check(self.lib.ddq_step_graph_async(self.ctx, ctypes.byref(cfg), int(nsteps)))
 
+    def step_pipelined(self, cfg, nsteps):
+        """nsteps graph steps with step t+1's sample + gather overlapped with step t."""
+        self._check(self.lib.ddq_step_pipelined_async(self.ctx, ctypes.byref(cfg), int(nsteps)))
+
     def profile_step(self, cfg, cap=32):
         names = ctypes.create_string_buffer(16 * cap)
         us = (ctypes.c_float * cap)()

@@ -193,6 +193,10 @@ int ddq_step_async(ddq_ctx* ctx, const ddq_step_cfg* cfg);
 /* Capture one step into a hipGraph (re-captured when cfg changes) and replay
  * it nsteps times back to back.  Enqueued, no sync. */
 int ddq_step_graph_async(ddq_ctx* ctx, const ddq_step_cfg* cfg, int32_t nsteps);
+/* nsteps steps as graph replays with step t+1's replay sample + gather
+ * overlapped with step t (double-buffered minibatch).  Same results, indices
+ * and counters as nsteps sequential ddq_step_async calls.  Enqueued, no sync. */
+int ddq_step_pipelined_async(ddq_ctx* ctx, const ddq_step_cfg* cfg, int32_t nsteps);
 /* Steps taken so far (drives the target-sync period). */
 int64_t ddq_step_count(const ddq_ctx* ctx);
 

@@ -267,6 +267,37 @@ def test_graph_step_runs_and_matches_eager(ddq, ref):
     np.testing.assert_array_equal(nets[0].read_indices(), e.read_indices())
 
 
+def test_pipelined_step_matches_graph(ddq, ref):
+    """Double-buffered pipelined stepping (next sample + gather under the
+    current step) gives the same parameters, indices and minibatch as the
+    plain graph step sequence, across several calls of different lengths."""
+    S, B, N = 16, 16, 300
+    rng = np.random.default_rng(21)
+    nets = [ddq.DeepQNet(batch=B, frame=S) for _ in range(2)]
+    theta = ref.flatten(ref.init_params(S, seed=6))
+    st = rng.integers(0, 256, (N, 4, S, S)).astype(np.uint8)
+    acts = rng.integers(0, 4, N).astype(np.uint8)
+    rws = rng.integers(-1, 2, N).astype(np.int16)
+    nts = (rng.random(N) > 0.1).astype(np.uint8)
+    for n in nets:
+        n.set_flat(0, theta)
+        n.set_flat(1, theta)
+        n.replay_create(N)
+        n.replay_import(st, acts, rws, nts, 0, N)
+    cfg = nets[0].step_cfg("sgd", lr=1e-4, target_period=3, seed=5)
+    for k in (1, 4, 3):
+        nets[0].step_pipelined(cfg, k)
+        nets[1].step_graph(cfg, k)
+    for n in nets:
+        n.synchronize()
+    a, b = nets
+    np.testing.assert_array_equal(a.read_indices(), b.read_indices())
+    for x, y in zip(a.read_minibatch(), b.read_minibatch()):
+        np.testing.assert_array_equal(x, y)
+    np.testing.assert_array_equal(a.get_flat(0), b.get_flat(0))
+    np.testing.assert_array_equal(a.get_flat(1), b.get_flat(1))
+
+
 def test_rccl_world1_allreduce_and_step(ddq, ref):
     """RCCL plumbing on one GPU: a 1-rank communicator all-reduce is the
     identity, and the fused step with allreduce=1 equals the step without."""
