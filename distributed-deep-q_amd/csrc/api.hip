@@ -566,13 +566,19 @@ int ddq_write_minibatch(ddq_ctx* c, const float* state, const float* action, con
 }
 
 // ---------------- compute ----------------
+// book >= 0: this backward feeds a step's apply; its slab reduce also does
+// the apply bookkeeping with target period `book` (saves a launch).
 static int enqueue_fwd_bwd(ddq_ctx* c, const NetBuffers& nb, void (*mark)(void*, const char*),
-                           void* marg) {
+                           void* marg, int book = -1) {
   HIP_TRY(c, launch_forward(nb, 2, c->stream, mark, marg));
   if (mark) mark(marg, "head");
   HIP_TRY(c, launch_head(nb, c->stream));
-  // per-kernel event timing needs one stream; otherwise overlap wgrad with dgrad
-  HIP_TRY(c, launch_backward(nb, c->stream, mark, marg, mark == nullptr));
+  // Serial by default: forking the weight-gradient kernels onto a side stream
+  // costs more in cross-stream graph edges (6-14 us idle each, measured) than
+  // the overlap returns, as every kernel here fills the GPU on its own
+  // (DDQ_VARIANT bit 16 re-enables the concurrent branch for A/B runs).
+  HIP_TRY(c, launch_backward(nb, c->stream, mark, marg, mark == nullptr && (nb.variant & 16),
+                             book >= 0, book));
   return DDQ_OK;
 }
 static int enqueue_fwd_bwd(ddq_ctx* c, void (*mark)(void*, const char*), void* marg) {
@@ -666,7 +672,7 @@ int ddq_apply_async(ddq_ctx* c, const ddq_update_cfg* u) {
   TRY(check_cfg(c, u));
   TRY(set_dev(c));
   HIP_TRY(c, launch_apply(c->nb, u->rule, u->lr, u->decay, u->eps, u->momentum, u->weight_decay,
-                          0, c->stream));
+                          0, false, c->stream));
   c->applied++;
   return DDQ_OK;
 }
@@ -751,7 +757,7 @@ static int enqueue_train(ddq_ctx* c, const ddq_step_cfg* cfg, const NetBuffers& 
                              nb.side));
     HIP_TRY(c, hipEventRecord(nb.ev[7], nb.side));
   }
-  TRY(enqueue_fwd_bwd(c, nb, mark, marg));
+  TRY(enqueue_fwd_bwd(c, nb, mark, marg, cfg->target_period > 0 ? cfg->target_period : 0));
   if (cfg->allreduce && c->nranks > 1) {
     if (mark) mark(marg, "allreduce");
     NCCL_TRY(c, ncclAllReduce(nb.grad, nb.grad, (size_t)nb.L.total, ncclFloat, ncclSum, c->comm,
@@ -760,7 +766,7 @@ static int enqueue_train(ddq_ctx* c, const ddq_step_cfg* cfg, const NetBuffers& 
   if (mark) mark(marg, "apply");
   const ddq_update_cfg& u = cfg->update;
   HIP_TRY(c, launch_apply(nb, u.rule, u.lr, u.decay, u.eps, u.momentum, u.weight_decay,
-                          cfg->target_period, c->stream));
+                          cfg->target_period, true, c->stream));
   if (pre) HIP_TRY(c, hipStreamWaitEvent(c->stream, nb.ev[7], 0));
   return DDQ_OK;
 }

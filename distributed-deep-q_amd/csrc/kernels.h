@@ -66,10 +66,10 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s, void (*ma
 hipError_t launch_head(const NetBuffers& nb, hipStream_t s);
 // concurrent: run the weight-gradient GEMMs on nb.side beside the data-gradient chain.
 hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(void*, const char*),
-                           void* mark_arg, bool concurrent);
+                           void* mark_arg, bool concurrent, bool book = false, int book_period = 0);
 // period > 0: also copy Q -> P when the next pull sees iteration % period == 0.
 hipError_t launch_apply(const NetBuffers& nb, int rule, float lr, float decay, float eps,
-                        float momentum, float wd, int period, hipStream_t s);
+                        float momentum, float wd, int period, bool booked, hipStream_t s);
 hipError_t launch_relayout(const NetBuffers& nb, int z, hipStream_t s);
 // Q-tower forward of n states (NHWC f32 in `in`) into scratch, argmax into out.
 hipError_t launch_act(const NetBuffers& nb, const float* in, int n, float* pool1, float* pool2,

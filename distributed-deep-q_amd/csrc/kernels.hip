@@ -359,11 +359,22 @@ struct WredDims {
   int cout, cin, ks, splits, np, blk0;   // blk0: first workgroup of this layer
 };
 
+__device__ __forceinline__ void apply_book(int64_t* iter, int32_t* opt_init, int period) {
+  const int64_t it = *iter;
+  opt_init[2] = (opt_init[0] == 0);
+  opt_init[3] = period > 0 && ((it + 1) % period) == 0;
+  *iter = it + 1;
+  opt_init[0] = 1;
+}
+
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part,
                                                            float* __restrict__ grad, WredDims d0,
-                                                           WredDims d1, WredDims d2) {
+                                                           WredDims d1, WredDims d2,
+                                                           int64_t* iter, int32_t* opt_init,
+                                                           int book_period) {
   __shared__ float red[4][64];
   const int bid = blockIdx.x;
+  if (opt_init && bid == 0 && threadIdx.x == 0) apply_book(iter, opt_init, book_period);
   const WredDims d = bid >= d2.blk0 ? d2 : (bid >= d1.blk0 ? d1 : d0);
   const int lb = bid - d.blk0;
   const int nblk = d.np / 64;
@@ -439,11 +450,10 @@ __device__ __forceinline__ float apply_one(const ApplyArgs& a, bool first, int64
 
 __global__ __launch_bounds__(256) void apply_kernel(
     float* __restrict__ theta, const float* __restrict__ grad, float* __restrict__ opt,
-    int32_t* __restrict__ opt_init, float* __restrict__ wk, float* __restrict__ thetaP,
-    float* __restrict__ wkP, const int64_t* __restrict__ iter, ApplyArgs a) {
-  const bool first = (*opt_init == 0);
-  const int64_t it = *iter;
-  const bool sync = a.period > 0 && ((it + 1) % a.period) == 0;
+    const int32_t* __restrict__ opt_init, float* __restrict__ wk, float* __restrict__ thetaP,
+    float* __restrict__ wkP, ApplyArgs a) {
+  const bool first = opt_init[2] != 0;      // latched by apply_book
+  const bool sync = opt_init[3] != 0;
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i < a.n) {
     const float4 g4 = *reinterpret_cast<const float4*>(grad + i);
@@ -475,15 +485,16 @@ __global__ __launch_bounds__(256) void apply_kernel(
   }
 }
 
-// param-server iteration / first-call bookkeeping after every apply (a separate
-// one-thread kernel: every apply workgroup has read the old values by then)
-__global__ void apply_book_kernel(int64_t* iter, int32_t* opt_init) {
-  *iter += 1;
-  *opt_init = 1;
+// param-server iteration / first-call bookkeeping of one apply: latch the
+// apply's flags (opt_init[2] = first call, opt_init[3] = P<-Q sync due) from
+// the old counters, then advance them.  Runs before the apply, either folded
+// into the step's wgrad slab reduce or as this one-thread kernel.
+__global__ void apply_book_kernel(int64_t* iter, int32_t* opt_init, int period) {
+  apply_book(iter, opt_init, period);
 }
 
 hipError_t launch_apply(const NetBuffers& nb, int rule, float lr, float decay, float eps,
-                        float momentum, float wd, int period, hipStream_t s) {
+                        float momentum, float wd, int period, bool booked, hipStream_t s) {
   ApplyArgs a;
   a.n = nb.L.total;
   a.rule = rule; a.period = period;
@@ -492,9 +503,9 @@ hipError_t launch_apply(const NetBuffers& nb, int rule, float lr, float decay, f
   for (int l = 0; l < 5; ++l) { a.bias_lo[l] = nb.L.b[l]; a.bias_hi[l] = nb.L.b[l] + nb.L.bn[l]; }
   conv_dims(nb.L, a.conv);
   const int blocks = (int)((a.n / 4 + 255) / 256);
+  if (!booked) hipLaunchKernelGGL(apply_book_kernel, dim3(1), dim3(1), 0, s, nb.iter, nb.opt_init, period);
   hipLaunchKernelGGL(apply_kernel, dim3(blocks), dim3(256), 0, s, nb.theta[0], nb.grad, nb.opt,
-                     nb.opt_init, nb.wk[0], nb.theta[1], nb.wk[1], nb.iter, a);
-  hipLaunchKernelGGL(apply_book_kernel, dim3(1), dim3(1), 0, s, nb.iter, nb.opt_init);
+                     nb.opt_init, nb.wk[0], nb.theta[1], nb.wk[1], a);
   return hipGetLastError();
 }
 
@@ -681,7 +692,7 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
 }
 
 hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(void*, const char*),
-                           void* marg, bool concurrent) {
+                           void* marg, bool concurrent, bool book, int book_period) {
   const ParamLayout& L = nb.L;
   const int B = nb.B, S = nb.S;
   const int s4 = S / 8;
@@ -819,7 +830,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     }
     M("wgrad_reduce");
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blk), dim3(256), 0, s, nb.wpart, nb.grad, d[0],
-                       d[1], d[2]);
+                       d[1], d[2], nb.iter, book ? nb.opt_init : nullptr, book_period);
     CHECK_LAUNCH(hipGetLastError());
   }
   return hipSuccess;
