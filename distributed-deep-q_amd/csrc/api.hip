@@ -209,6 +209,8 @@ int ddq_create(ddq_ctx** out, int device, const ddq_net_desc* desc) {
     TRY(dalloc(c, &nb.target, (size_t)B));
     TRY(dalloc(c, &nb.loss, 1));
     TRY(dalloc(c, &nb.dh4, (size_t)B * 512));
+    TRY(dalloc(c, &nb.dqbuf, (size_t)B * 4));
+    TRY(dalloc(c, &nb.lpart, (size_t)B));
     TRY(dalloc(c, &nb.dconv3, (size_t)B * S3 * S3 * 64));
     TRY(dalloc(c, &nb.dconv2, (size_t)B * S2 * S2 * 64));
     TRY(dalloc(c, &nb.dconv1, (size_t)B * S * S * 32));
@@ -569,8 +571,8 @@ int ddq_write_minibatch(ddq_ctx* c, const float* state, const float* action, con
 // book >= 0: this backward feeds a step's apply; its slab reduce also does
 // the apply bookkeeping with target period `book` (saves a launch).
 static int enqueue_fwd_bwd(ddq_ctx* c, const NetBuffers& nb, void (*mark)(void*, const char*),
-                           void* marg, int book = -1) {
-  HIP_TRY(c, launch_forward(nb, 2, c->stream, mark, marg));
+                           void* marg, int book = -1, ReplayMeta* bump = nullptr) {
+  HIP_TRY(c, launch_forward(nb, 2, c->stream, mark, marg, false));
   if (mark) mark(marg, "head");
   HIP_TRY(c, launch_head(nb, c->stream));
   // Serial by default: forking the weight-gradient kernels onto a side stream
@@ -578,7 +580,7 @@ static int enqueue_fwd_bwd(ddq_ctx* c, const NetBuffers& nb, void (*mark)(void*,
   // the overlap returns, as every kernel here fills the GPU on its own
   // (DDQ_VARIANT bit 16 re-enables the concurrent branch for A/B runs).
   HIP_TRY(c, launch_backward(nb, c->stream, mark, marg, mark == nullptr && (nb.variant & 16),
-                             book >= 0, book));
+                             book >= 0, book, bump));
   return DDQ_OK;
 }
 static int enqueue_fwd_bwd(ddq_ctx* c, void (*mark)(void*, const char*), void* marg) {
@@ -748,7 +750,8 @@ int ddq_allreduce_grads(ddq_ctx* c) {
 // not written inside a step, and the device RNG counter advances in the
 // same order, so the index stream equals the sequential one).
 static int enqueue_train(ddq_ctx* c, const ddq_step_cfg* cfg, const NetBuffers& nb,
-                         const NetBuffers* pre, void (*mark)(void*, const char*), void* marg) {
+                         const NetBuffers* pre, void (*mark)(void*, const char*), void* marg,
+                         ReplayMeta* bump = nullptr) {
   if (pre) {
     HIP_TRY(c, hipEventRecord(nb.ev[6], c->stream));
     HIP_TRY(c, hipStreamWaitEvent(nb.side, nb.ev[6], 0));
@@ -757,7 +760,7 @@ static int enqueue_train(ddq_ctx* c, const ddq_step_cfg* cfg, const NetBuffers& 
                              nb.side));
     HIP_TRY(c, hipEventRecord(nb.ev[7], nb.side));
   }
-  TRY(enqueue_fwd_bwd(c, nb, mark, marg, cfg->target_period > 0 ? cfg->target_period : 0));
+  TRY(enqueue_fwd_bwd(c, nb, mark, marg, cfg->target_period > 0 ? cfg->target_period : 0, bump));
   if (cfg->allreduce && c->nranks > 1) {
     if (mark) mark(marg, "allreduce");
     NCCL_TRY(c, ncclAllReduce(nb.grad, nb.grad, (size_t)nb.L.total, ncclFloat, ncclSum, c->comm,
@@ -773,6 +776,12 @@ static int enqueue_train(ddq_ctx* c, const ddq_step_cfg* cfg, const NetBuffers& 
 
 static int enqueue_step(ddq_ctx* c, const ddq_step_cfg* cfg, void (*mark)(void*, const char*),
                         void* marg) {
+  if (c->nb.B <= 256) {   // one kernel: every gather workgroup draws the same index set
+    if (mark) mark(marg, "sample_gather");
+    HIP_TRY(c, launch_sample_gather(c->nb, c->r_state, c->r_action, c->r_reward, c->r_nonterm,
+                                    c->r_meta, cfg->seed, c->stream));
+    return enqueue_train(c, cfg, c->nb, nullptr, mark, marg, c->r_meta);
+  }
   if (mark) mark(marg, "sample");
   HIP_TRY(c, launch_sample(c->nb, c->r_meta, cfg->seed, c->stream));
   if (mark) mark(marg, "gather");

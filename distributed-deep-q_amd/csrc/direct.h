@@ -12,6 +12,12 @@
 // so there is no im2col, no per-element address arithmetic in the K loop and
 // one LDS read per 4 MFMAs per operand block.
 //
+// WK > 1 splits the taps over WK wave groups (group g takes taps g, g+WK, ...,
+// each with its own two-slot weight ring) and sums the groups' accumulators
+// through LDS in fixed order before the epilogue: for layers whose output has
+// too few 32x32 blocks to give every SIMD two waves (conv3: 512 per tower,
+// conv2 dgrad: 1024) this multiplies the waves in flight by WK.
+//
 // Modes (template DGRAD):
 //  fwd   : patch = layer input (CP channels), N = Cout, weights Wk[co][tap][ci];
 //          epilogue = bias + ReLU + 2x2 max-pool + routing byte (rows are
@@ -25,7 +31,7 @@
 
 namespace ddq {
 
-template <int CP, int N, int KS, int TY, int TX, int WM, int WN, bool DGRAD, bool WALL>
+template <int CP, int N, int KS, int TY, int TX, int WM, int WN, bool DGRAD, bool WALL, int WK = 1>
 struct DirectCfg {
   static constexpr int V = CP >= 8 ? 4 : CP / 2;     // floats per lane per LDS read
   static constexpr int G = 2 * V;                     // channels per read group
@@ -34,13 +40,15 @@ struct DirectCfg {
   static constexpr int RS = PW * CS + (CP >= 8 ? 0 : 2);   // patch row stride
   static constexpr int CW = CP >= 8 ? CP + 4 : CP;    // weight row stride (one row per n)
   static constexpr int T = KS * KS;
-  static constexpr int WSLOTS = WALL ? T : 2;
-  static constexpr int kThreads = 64 * WM * WN;
+  static constexpr int WSLOTS = WALL ? T : 2 * WK;
+  static constexpr int kGroup = 64 * WM * WN;         // threads of one tap group
+  static constexpr int kThreads = kGroup * WK;
   static constexpr int TM = TY * TX / WM / 32;        // 32-pixel blocks per wave
   static constexpr int TN = N / WN / 32;              // 32-channel blocks per wave
   static constexpr int kPatch = PH * RS;
   static constexpr int kW = WSLOTS * N * CW;
-  static constexpr int kSmem = kPatch + kW;
+  static constexpr int kRed = (WK - 1) * WM * WN * TM * TN * 1024;   // tap-group sums
+  static constexpr int kSmem = kPatch + kW > kRed ? kPatch + kW : kRed;
   static_assert(TM >= 1 && TN >= 1, "wave tile");
   static_assert(TY % 2 == 0 && TX % 2 == 0 && CP % 4 == 0 && CP % G == 0, "shape");
   static_assert(kSmem * 4 <= 160 * 1024, "LDS budget");
@@ -77,15 +85,15 @@ __device__ __forceinline__ float vget(const float2& v, int i) { return i == 0 ? 
 template <class C, int CP, int N>
 struct WStage {
   static constexpr int kF4 = N * CP / 4;                       // float4 per tap
-  static constexpr int kPer = (kF4 + C::kThreads - 1) / C::kThreads;
+  static constexpr int kPer = (kF4 + C::kGroup - 1) / C::kGroup;   // one tap group stages a tap
   float4 r[kPer];
 
   template <bool DGRAD>
   __device__ __forceinline__ void load(const float* __restrict__ wk, int t, int tid) {
 #pragma unroll
     for (int s = 0; s < kPer; ++s) {
-      const int f = tid + s * C::kThreads;
-      if (kF4 % C::kThreads != 0 && f >= kF4) continue;
+      const int f = tid + s * C::kGroup;
+      if (kF4 % C::kGroup != 0 && f >= kF4) continue;
       if (!DGRAD) {          // wb[n][k] = Wk[n][t][k], float4 along k
         const int n = f / (CP / 4), c4 = f % (CP / 4);
         r[s] = *reinterpret_cast<const float4*>(wk + ((size_t)n * C::T + t) * CP + 4 * c4);
@@ -100,8 +108,8 @@ struct WStage {
   __device__ __forceinline__ void store(float* wb, int tid) const {
 #pragma unroll
     for (int s = 0; s < kPer; ++s) {
-      const int f = tid + s * C::kThreads;
-      if (kF4 % C::kThreads != 0 && f >= kF4) continue;
+      const int f = tid + s * C::kGroup;
+      if (kF4 % C::kGroup != 0 && f >= kF4) continue;
       if (!DGRAD) {
         const int n = f / (CP / 4), c4 = f % (CP / 4);
         *reinterpret_cast<float4*>(wb + n * C::CW + 4 * c4) = r[s];
@@ -116,9 +124,9 @@ struct WStage {
   }
 };
 
-template <int CP, int N, int KS, int TY, int TX, int WM, int WN, bool DGRAD, bool WALL>
-__global__ __launch_bounds__(64 * WM * WN) void direct_conv_kernel(const DirectArgs a) {
-  using C = DirectCfg<CP, N, KS, TY, TX, WM, WN, DGRAD, WALL>;
+template <int CP, int N, int KS, int TY, int TX, int WM, int WN, bool DGRAD, bool WALL, int WK>
+__global__ __launch_bounds__(64 * WM * WN * WK) void direct_conv_kernel(const DirectArgs a) {
+  using C = DirectCfg<CP, N, KS, TY, TX, WM, WN, DGRAD, WALL, WK>;
   using VT = typename VecT<C::V>::T;
   constexpr int TM = C::TM, TN = C::TN, V = C::V;
   __shared__ __attribute__((aligned(16))) float smem[C::kSmem];
@@ -126,6 +134,8 @@ __global__ __launch_bounds__(64 * WM * WN) void direct_conv_kernel(const DirectA
   float* wbuf = smem + C::kPatch;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wkg = wid / (WM * WN);                 // tap group: taps t = s*WK + wkg
+  const int gtid = tid - wkg * C::kGroup;
   const int z = blockIdx.z, b = blockIdx.y;
   const int ty = blockIdx.x / a.tiles_x, tx = blockIdx.x % a.tiles_x;
   const int y0 = ty * TY, x0 = tx * TX;
@@ -150,19 +160,20 @@ __global__ __launch_bounds__(64 * WM * WN) void direct_conv_kernel(const DirectA
   }
   WStage<C, CP, N> ws;
   if (WALL) {
-    for (int t = 0; t < C::T; ++t) {
-      ws.template load<DGRAD>(wk, t, tid);
-      ws.template store<DGRAD>(wbuf + t * N * C::CW, tid);
+    for (int t = wkg; t < C::T; t += WK) {
+      ws.template load<DGRAD>(wk, t, gtid);
+      ws.template store<DGRAD>(wbuf + t * N * C::CW, gtid);
     }
-  } else {
-    ws.template load<DGRAD>(wk, 0, tid);
-    ws.template store<DGRAD>(wbuf, tid);
+  } else if (wkg < C::T) {
+    ws.template load<DGRAD>(wk, wkg, gtid);
+    ws.template store<DGRAD>(wbuf + wkg * N * C::CW, gtid);
   }
   __syncthreads();
 
   // ---- per-lane operand bases ----
   const int l31 = lane & 31, h = lane >> 5;
-  const int wmi = wid / WN, wni = wid % WN;
+  const int w2 = wid % (WM * WN);
+  const int wmi = w2 / WN, wni = w2 % WN;
   int abase[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -183,32 +194,66 @@ __global__ __launch_bounds__(64 * WM * WN) void direct_conv_kernel(const DirectA
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  for (int t = 0; t < C::T; ++t) {
-    const float* wb = wbuf + (WALL ? t : (t & 1)) * N * C::CW;
-    if (!WALL && t + 1 < C::T) ws.template load<DGRAD>(wk, t + 1, tid);   // in flight under MFMAs
-    const int ky = t / KS, kx = t % KS;
-    const float* pa = patch + ky * C::RS + kx * C::CS;
+  // Tap steps: group wkg takes tap s*WK + wkg; non-WALL weights live in a
+  // two-slot ring per group (slot (s&1)*WK + wkg), one barrier per step.
+  constexpr int NSTEP = (C::T + WK - 1) / WK;
+  for (int s = 0; s < NSTEP; ++s) {
+    const int t = s * WK + wkg;
+    const int tn = t + WK;
+    const float* wb = wbuf + (WALL ? t : ((s & 1) * WK + wkg)) * N * C::CW;
+    if (!WALL && s + 1 < NSTEP && tn < C::T) ws.template load<DGRAD>(wk, tn, gtid);   // in flight
+    if (t < C::T) {
+      const int ky = t / KS, kx = t % KS;
+      const float* pa = patch + ky * C::RS + kx * C::CS;
 #pragma unroll
-    for (int g = 0; g < CP / C::G; ++g) {
-      VT av[TM], bv[TN];
+      for (int g = 0; g < CP / C::G; ++g) {
+        VT av[TM], bv[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) av[i] = *reinterpret_cast<const VT*>(pa + abase[i] + g * C::G);
+        for (int i = 0; i < TM; ++i) av[i] = *reinterpret_cast<const VT*>(pa + abase[i] + g * C::G);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bv[j] = *reinterpret_cast<const VT*>(wb + bbase[j] + g * C::G);
+        for (int j = 0; j < TN; ++j) bv[j] = *reinterpret_cast<const VT*>(wb + bbase[j] + g * C::G);
 #pragma unroll
-      for (int v = 0; v < V; ++v)
+        for (int v = 0; v < V; ++v)
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+          for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(vget(av[i], v), vget(bv[j], v),
-                                                             acc[i][j], 0, 0, 0);
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(vget(av[i], v), vget(bv[j], v),
+                                                               acc[i][j], 0, 0, 0);
+      }
     }
-    if (!WALL && t + 1 < C::T) {
-      // the other slot was last read in iteration t-1, fenced by its barrier
-      ws.template store<DGRAD>(wbuf + ((t + 1) & 1) * N * C::CW, tid);
+    if (!WALL && s + 1 < NSTEP) {
+      // the other slot was last read in step s-1, fenced by its barrier
+      if (tn < C::T) ws.template store<DGRAD>(wbuf + (((s + 1) & 1) * WK + wkg) * N * C::CW, gtid);
       __syncthreads();
     }
+  }
+
+  // ---- tap groups 1..WK-1 hand their partial sums to group 0 (fixed order) ----
+  if (WK > 1) {
+    __syncthreads();
+    float* red = smem;
+    if (wkg > 0) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            red[((((wkg - 1) * WM * WN + w2) * TM + i) * TN + j) * 1024 + r * 64 + lane] =
+                acc[i][j][r];
+    }
+    __syncthreads();
+    if (wkg > 0) return;
+#pragma unroll
+    for (int k = 1; k < WK; ++k)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            acc[i][j][r] += red[((((k - 1) * WM * WN + w2) * TM + i) * TN + j) * 1024 + r * 64 + lane];
   }
 
   // ---- epilogue ----
@@ -261,13 +306,13 @@ __global__ __launch_bounds__(64 * WM * WN) void direct_conv_kernel(const DirectA
   }
 }
 
-template <int CP, int N, int KS, int TY, int TX, int WM, int WN, bool DGRAD, bool WALL>
+template <int CP, int N, int KS, int TY, int TX, int WM, int WN, bool DGRAD, bool WALL, int WK = 1>
 inline hipError_t launch_direct(DirectArgs a, int nz, hipStream_t st) {
   a.tiles_x = (a.W + TX - 1) / TX;
   const int tiles_y = (a.H + TY - 1) / TY;
   dim3 grid(tiles_y * a.tiles_x, a.B, nz);
-  hipLaunchKernelGGL((direct_conv_kernel<CP, N, KS, TY, TX, WM, WN, DGRAD, WALL>), grid,
-                     dim3(64 * WM * WN), 0, st, a);
+  hipLaunchKernelGGL((direct_conv_kernel<CP, N, KS, TY, TX, WM, WN, DGRAD, WALL, WK>), grid,
+                     dim3(64 * WM * WN * WK), 0, st, a);
   return hipGetLastError();
 }
 

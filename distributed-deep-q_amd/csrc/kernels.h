@@ -47,6 +47,7 @@ struct NetBuffers {
   int wnp[3];
   // parameters: theta[z] flat Caffe layout; wk[z] conv kernel layout; grad; opt state
   float *theta[2], *wk[2], *grad, *opt;
+  float *dqbuf, *lpart;             // head: per-sample dQ (B,4) and squared error (B)
   int32_t* opt_init;                // 0 until the first apply after a reset
   int64_t* iter;                    // applied updates (param-server iteration)
   // second stream + events for concurrent wgrad / dgrad branches (optional)
@@ -58,15 +59,22 @@ struct NetBuffers {
   int variant;                      // tuning experiments (DDQ_VARIANT bits), 0 = default
 };
 
+// fused device draw + gather for the step (B <= 256); counter advanced by the
+// step's apply bookkeeping (launch_backward's bump)
+hipError_t launch_sample_gather(const NetBuffers& nb, const uint8_t* st, const uint8_t* act,
+                                const int16_t* rew, const uint8_t* nt, ReplayMeta* meta,
+                                uint64_t seed, hipStream_t s);
 hipError_t launch_gather(const NetBuffers& nb, const uint8_t* st, const uint8_t* act,
                          const int16_t* rew, const uint8_t* nt, ReplayMeta* meta,
                          hipStream_t s);
 hipError_t launch_sample(const NetBuffers& nb, ReplayMeta* meta, uint64_t seed, hipStream_t s);
-hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s, void (*mark)(void*, const char*), void* mark_arg);
+hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s, void (*mark)(void*, const char*), void* mark_arg,
+                          bool out = true);
 hipError_t launch_head(const NetBuffers& nb, hipStream_t s);
 // concurrent: run the weight-gradient GEMMs on nb.side beside the data-gradient chain.
 hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(void*, const char*),
-                           void* mark_arg, bool concurrent, bool book = false, int book_period = 0);
+                           void* mark_arg, bool concurrent, bool book = false, int book_period = 0,
+                           ReplayMeta* bump = nullptr);
 // period > 0: also copy Q -> P when the next pull sees iteration % period == 0.
 hipError_t launch_apply(const NetBuffers& nb, int rule, float lr, float decay, float eps,
                         float momentum, float wd, int period, bool booked, hipStream_t s);

@@ -49,25 +49,47 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   return x ^ (x >> 31);
 }
 
-// One workgroup: B <= 1024 distinct indices, uniform over [0,valid) \ {head-1}
-// (the distribution of replay.py:152-157's whole-list redraw), sorted.
-// Colliding / forbidden draws are redrawn independently each round; the
-// process is symmetric in the population, so the final set is uniform.
-__global__ __launch_bounds__(1024) void sample_kernel(ReplayMeta* meta, int B, uint64_t seed,
-                                                      int32_t* idx_out) {
-  __shared__ int64_t cand[1024];
-  __shared__ int bad_any;
+// One workgroup: B <= blockDim distinct indices, uniform over [0,valid) \ {head-1}
+// (the distribution of replay.py:152-157's whole-list redraw), sorted into
+// cand[0..B).  Colliding / forbidden draws are redrawn independently each
+// round; the process is symmetric in the population, so the final set is
+// uniform.  Deterministic in (seed, ctr): every workgroup that runs it gets
+// the same set, which lets the gather workgroups draw for themselves.
+__device__ void draw_sorted(const ReplayMeta* meta, int B, uint64_t seed, uint64_t ctr,
+                            int64_t* cand, int* bad_any) {
   const int t = threadIdx.x;
   const int64_t valid = meta->valid;
   const int64_t forbid = meta->head - 1;   // -1 when head == 0: nothing forbidden
-  const uint64_t ctr = meta->counter;
-  int P2 = 1;
-  while (P2 < B) P2 <<= 1;
   auto draw = [&](int round) -> int64_t {
     uint64_t r = splitmix64(seed ^ splitmix64(ctr * 0x100000001B3ull + (uint64_t)t * 0x9E37ull +
                                               ((uint64_t)round << 40)));
     return (int64_t)__umul64hi(r, (uint64_t)valid);
   };
+  if (B <= 64) {
+    // one wave, registers + cross-lane shuffles: no workgroup barriers.  The
+    // sorted set equals the general path's (padding sorts to the end and the
+    // redraw of sorted position t uses the same hash input t).
+    if (t < 64) {
+      int64_t v = (t < B) ? draw(0) : INT64_MAX;
+      for (int round = 1; round < 256; ++round) {
+        for (int k = 2; k <= 64; k <<= 1)
+          for (int j = k >> 1; j > 0; j >>= 1) {
+            const int64_t o = __shfl_xor(v, j);
+            const bool up = (t & k) == 0, lo = (t & j) == 0;
+            v = (lo == up) ? (v < o ? v : o) : (v < o ? o : v);
+          }
+        const int64_t prev = __shfl_up(v, 1);
+        const bool bad = t < B && (v == forbid || (t > 0 && v == prev));
+        if (__ballot(bad) == 0) break;
+        if (bad) v = draw(round);
+      }
+      cand[t] = v;
+    }
+    __syncthreads();
+    return;
+  }
+  int P2 = 1;
+  while (P2 < B) P2 <<= 1;
   if (t < P2) cand[t] = (t < B) ? draw(0) : INT64_MAX;
   for (int round = 1; round < 256; ++round) {
     __syncthreads();
@@ -85,32 +107,40 @@ __global__ __launch_bounds__(1024) void sample_kernel(ReplayMeta* meta, int B, u
         __syncthreads();
       }
     }
-    if (t == 0) bad_any = 0;
+    if (t == 0) *bad_any = 0;
     __syncthreads();
     bool bad = false;
     if (t < B) bad = (cand[t] == forbid) || (t > 0 && cand[t] == cand[t - 1]);
-    if (bad) bad_any = 1;
+    if (bad) *bad_any = 1;
     __syncthreads();
-    if (!bad_any) break;
+    if (!*bad_any) break;
     if (bad) cand[t] = draw(round);
   }
   __syncthreads();
+}
+
+__global__ __launch_bounds__(1024) void sample_kernel(ReplayMeta* meta, int B, uint64_t seed,
+                                                      int32_t* idx_out) {
+  __shared__ int64_t cand[1024];
+  __shared__ int bad_any;
+  const uint64_t ctr = meta->counter;
+  draw_sorted(meta, B, seed, ctr, cand, &bad_any);
+  const int t = threadIdx.x;
   if (t < B) idx_out[t] = (int32_t)cand[t];
   if (t == 0) meta->counter = ctr + 1;
 }
 
-// grid (ceil(S*S/4/256), B, 2): z = 0 -> state from idx, z = 1 -> next_state
-// from next_idx (wrap N-1 -> 0, replay.py:160-166).  u8 (C,H,W) slot -> f32
-// NHWC; the z = 1 blocks with blockIdx.x == 0 also write action one-hot,
-// reward and non_terminal of next_idx (replay.py:172-183).
-__global__ __launch_bounds__(256) void gather_kernel(
+// u8 (C,H,W) slot -> f32 NHWC, 4 pixels per thread; z = 0 -> state from
+// idx, z = 1 -> next_state from next_idx (wrap N-1 -> 0, replay.py:160-166);
+// the z = 1 blocks with blockIdx.x == 0 also write action one-hot, reward and
+// non_terminal of next_idx (replay.py:172-183).
+__device__ __forceinline__ void gather_body(
     const uint8_t* __restrict__ st, const uint8_t* __restrict__ act,
-    const int16_t* __restrict__ rew, const uint8_t* __restrict__ nt, ReplayMeta* meta,
-    const int32_t* __restrict__ idx, int S, float* __restrict__ sQ, float* __restrict__ sP,
-    float* __restrict__ action, float* __restrict__ reward, float* __restrict__ nonterm) {
+    const int16_t* __restrict__ rew, const uint8_t* __restrict__ nt, ReplayMeta* meta, int64_t i,
+    int S, float* __restrict__ sQ, float* __restrict__ sP, float* __restrict__ action,
+    float* __restrict__ reward, float* __restrict__ nonterm) {
   const int b = blockIdx.y, z = blockIdx.z;
   const int64_t N = meta->capacity;
-  const int64_t i = idx[b];
   const int64_t nxt = (i + 1 == N) ? 0 : i + 1;
   const int64_t slot = z ? nxt : i;
   const int SS = S * S;
@@ -138,10 +168,48 @@ __global__ __launch_bounds__(256) void gather_kernel(
   }
 }
 
+// grid (ceil(S*S/4/256), B, 2), indices from idx (host draw or sample_kernel)
+__global__ __launch_bounds__(256) void gather_kernel(
+    const uint8_t* __restrict__ st, const uint8_t* __restrict__ act,
+    const int16_t* __restrict__ rew, const uint8_t* __restrict__ nt, ReplayMeta* meta,
+    const int32_t* __restrict__ idx, int S, float* __restrict__ sQ, float* __restrict__ sP,
+    float* __restrict__ action, float* __restrict__ reward, float* __restrict__ nonterm) {
+  gather_body(st, act, rew, nt, meta, idx[blockIdx.y], S, sQ, sP, action, reward, nonterm);
+}
+
+// Fused draw + gather for the training step (B <= 256): every workgroup
+// draws the same sorted index set (draw_sorted) and gathers its own sample.
+// The device counter is NOT advanced here (every workgroup must read the
+// same value); the step's apply bookkeeping advances it.
+__global__ __launch_bounds__(256) void sample_gather_kernel(
+    const uint8_t* __restrict__ st, const uint8_t* __restrict__ act,
+    const int16_t* __restrict__ rew, const uint8_t* __restrict__ nt, ReplayMeta* meta, int B,
+    uint64_t seed, int32_t* __restrict__ idx_out, int S, float* __restrict__ sQ,
+    float* __restrict__ sP, float* __restrict__ action, float* __restrict__ reward,
+    float* __restrict__ nonterm) {
+  __shared__ int64_t cand[256];
+  __shared__ int bad_any;
+  draw_sorted(meta, B, seed, meta->counter, cand, &bad_any);
+  if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x < B)
+    idx_out[threadIdx.x] = (int32_t)cand[threadIdx.x];
+  gather_body(st, act, rew, nt, meta, cand[blockIdx.y], S, sQ, sP, action, reward, nonterm);
+}
+
 hipError_t launch_sample(const NetBuffers& nb, ReplayMeta* meta, uint64_t seed, hipStream_t s) {
   int threads = 64;                 // one wave for B <= 64: cheap barriers
   while (threads < nb.B) threads <<= 1;
   hipLaunchKernelGGL(sample_kernel, dim3(1), dim3(threads), 0, s, meta, nb.B, seed, nb.idx);
+  return hipGetLastError();
+}
+
+hipError_t launch_sample_gather(const NetBuffers& nb, const uint8_t* st, const uint8_t* act,
+                                const int16_t* rew, const uint8_t* nt, ReplayMeta* meta,
+                                uint64_t seed, hipStream_t s) {
+  const int SS = nb.S * nb.S;
+  dim3 grid((SS / 4 + 255) / 256, nb.B, 2);
+  hipLaunchKernelGGL(sample_gather_kernel, grid, dim3(256), 0, s, st, act, rew, nt, meta, nb.B,
+                     seed, nb.idx, nb.S, nb.state, nb.next_state, nb.action, nb.reward,
+                     nb.nonterm);
   return hipGetLastError();
 }
 
@@ -255,69 +323,118 @@ __global__ __launch_bounds__(512) void fc4_reduce_out_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// head + Q_out backward (train_val.prototxt:385-483):
+// fc4 split-K reduce + bias + ReLU + Q_out (both towers) fused with the head
+// and the Q_out backward (train_val.prototxt:169-483), one workgroup per
+// sample b (512 threads = the 512 fc4 units):
+//   h4 = ReLU(sum_s part + b4), Q/P = W5 h4 + b5,
 //   Q_sa = sum_a Q*act, P_sa = max_a P * nt, target = 0.85 P_sa + r,
-//   loss = sum (Q_sa-target)^2 / 2B, dQ = act (Q_sa-target)/B,
-//   dW5 = dQ^T h4, db5 = sum dQ, dh4 = (dQ W5) * (h4>0), db4 = sum_b dh4.
-// grid 512/64 workgroups of 256 threads (64 columns x 4 sample groups); every
-// workgroup recomputes the B x 4 head (trivial) so no extra launch is needed.
+//   dQ = act (Q_sa-target)/B, dh4 = (dQ W5) * (h4>0).
+// The cross-sample sums (loss, dW5, db5, db4) are finished by the head blocks
+// of the wgrad slab reduce (per-sample dQ and squared error kept in dqbuf /
+// lpart), so the head costs no launch of its own.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void out_bwd_kernel(
-    int B, float gamma, const float* __restrict__ qout, const float* __restrict__ pout,
-    const float* __restrict__ h4q, const float* __restrict__ w5q,
-    const float* __restrict__ action, const float* __restrict__ reward,
-    const float* __restrict__ nonterm, float* q_sa_o, float* p_sa_o, float* target_o,
-    float* loss_o, float* __restrict__ gw5, float* __restrict__ gb5, float* __restrict__ gb4,
+__global__ __launch_bounds__(512) void fc4_head_kernel(
+    const float* __restrict__ part, int splits, int B, float gamma,
+    const float* __restrict__ thq, const float* __restrict__ thp, int64_t b4_off, int64_t w5_off,
+    int64_t b5_off, const float* __restrict__ action, const float* __restrict__ reward,
+    const float* __restrict__ nonterm, float* __restrict__ h4q, float* __restrict__ h4p,
+    float* __restrict__ outq, float* __restrict__ outp, float* q_sa_o, float* p_sa_o,
+    float* target_o, float* __restrict__ dqbuf, float* __restrict__ lpart,
     float* __restrict__ dh4) {
-  extern __shared__ float sh[];
-  float* dq = sh;                   // [B][4]
-  float* red = sh + 4 * B;          // [4 groups][64 cols][5]
-  const int t = threadIdx.x, lane = t & 63, g = t >> 6;
-  float d2 = 0.f;
-  for (int b = t; b < B; b += 256) {
-    const float* q = qout + b * 4;
-    const float* p = pout + b * 4;
-    const float* ac = action + b * 4;
-    // ELTWISE PROD, SLICE, SUM in slice order (train_val.prototxt:386-422)
-    float qs = q[0] * ac[0];
-    qs += q[1] * ac[1];
-    qs += q[2] * ac[2];
-    qs += q[3] * ac[3];
-    float ps = fmaxf(fmaxf(p[0], p[1]), fmaxf(p[2], p[3]));   // SLICE + MAX
-    ps = ps * nonterm[b];                                      // P_sa_or_term
-    const float tg = gamma * ps + 1.0f * reward[b];            // SUM coeff {0.85, 1}
-    const float diff = qs - tg;
-    const float gsc = diff / (float)B;                         // EUCLIDEAN_LOSS diff
+  __shared__ float red[8][8];
+  __shared__ float qp[8];
+  const int b = blockIdx.x, n = threadIdx.x, w = n >> 6;
+  const size_t stride = (size_t)2 * B * kFc4;
+  float h[2];
+  float q[8];
 #pragma unroll
-    for (int a = 0; a < 4; ++a) dq[b * 4 + a] = ac[a] * gsc;
-    if (blockIdx.x == 0) { q_sa_o[b] = qs; p_sa_o[b] = ps; target_o[b] = tg; }
-    d2 += diff * diff;
+  for (int z = 0; z < 2; ++z) {
+    const float* p = part + ((size_t)z * B + b) * kFc4 + n;
+    float acc = 0.f;
+    int s = 0;
+    for (; s + 4 <= splits; s += 4) {
+      const float v0 = p[(s + 0) * stride], v1 = p[(s + 1) * stride];
+      const float v2 = p[(s + 2) * stride], v3 = p[(s + 3) * stride];
+      acc += v0; acc += v1; acc += v2; acc += v3;
+    }
+    for (; s < splits; ++s) acc += p[s * stride];
+    const float* th = z ? thp : thq;
+    const float v = acc + th[b4_off + n];
+    h[z] = v > 0.f ? v : 0.f;
+    (z ? h4p : h4q)[(size_t)b * kFc4 + n] = h[z];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) q[z * 4 + a] = h[z] * th[w5_off + a * kFc4 + n];
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) q[i] += __shfl_xor(q[i], off);
+  if ((n & 63) == 0)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) red[w][i] = q[i];
+  __syncthreads();
+  if (n < 8) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t += red[i][n];
+    const float* th = n < 4 ? thq : thp;
+    t += th[b5_off + (n & 3)];
+    qp[n] = t;
+    (n < 4 ? outq : outp)[b * 4 + (n & 3)] = t;
   }
   __syncthreads();
-  if (blockIdx.x == 0) {
-    for (int off = 32; off > 0; off >>= 1) d2 += __shfl_xor(d2, off);
-    if (lane == 0) red[g] = d2;
-    __syncthreads();
-    if (t == 0) *loss_o = (red[0] + red[1] + red[2] + red[3]) / (float)B / 2.f;
-    if (t < 4) {
-      float acc = 0.f;
-      for (int b = 0; b < B; ++b) acc += dq[b * 4 + t];
-      gb5[t] = acc;
-    }
-    __syncthreads();
+  const float* ac = action + b * 4;
+  // ELTWISE PROD, SLICE, SUM in slice order (train_val.prototxt:386-422)
+  float qs = qp[0] * ac[0];
+  qs += qp[1] * ac[1];
+  qs += qp[2] * ac[2];
+  qs += qp[3] * ac[3];
+  float ps = fmaxf(fmaxf(qp[4], qp[5]), fmaxf(qp[6], qp[7]));   // SLICE + MAX
+  ps = ps * nonterm[b];                                          // P_sa_or_term
+  const float tg = gamma * ps + 1.0f * reward[b];                // SUM coeff {0.85, 1}
+  const float diff = qs - tg;
+  const float gsc = diff / (float)B;                             // EUCLIDEAN_LOSS diff
+  float dq[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) dq[a] = ac[a] * gsc;
+  if (n == 0) {
+    q_sa_o[b] = qs; p_sa_o[b] = ps; target_o[b] = tg;
+    lpart[b] = diff * diff;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) dqbuf[b * 4 + a] = dq[a];
   }
-  const int j = blockIdx.x * 64 + lane;
-  const float w0 = w5q[j], w1 = w5q[kFc4 + j], w2 = w5q[2 * kFc4 + j], w3 = w5q[3 * kFc4 + j];
+  const float* w5 = thq + w5_off;
+  const float v = dq[0] * w5[n] + dq[1] * w5[kFc4 + n] + dq[2] * w5[2 * kFc4 + n] +
+                  dq[3] * w5[3 * kFc4 + n];
+  dh4[(size_t)b * kFc4 + n] = h[0] > 0.f ? v : 0.f;              // ReLU backward
+}
+
+// Cross-sample head sums, run by the 8 trailing blocks of the wgrad slab
+// reduce: block hb owns fc4 units j = 64 hb + lane, 4 sample groups.
+__device__ void head_sums(int hb, int B, const float* __restrict__ dqbuf,
+                          const float* __restrict__ lpart, const float* __restrict__ h4q,
+                          const float* __restrict__ dh4, float* loss_o, float* __restrict__ gw5,
+                          float* __restrict__ gb5, float* __restrict__ gb4) {
+  __shared__ float red[4 * 64 * 5];
+  const int t = threadIdx.x, lane = t & 63, g = t >> 6;
+  if (hb == 0 && t < 5) {
+    float acc = 0.f;
+    if (t < 4) {
+      for (int b = 0; b < B; ++b) acc += dqbuf[b * 4 + t];
+      gb5[t] = acc;
+    } else {
+      for (int b = 0; b < B; ++b) acc += lpart[b];
+      *loss_o = acc / (float)B / 2.f;
+    }
+  }
+  const int j = hb * 64 + lane;
   float db = 0.f, dw[4] = {0.f, 0.f, 0.f, 0.f};
   for (int b = g; b < B; b += 4) {
-    const float* d = dq + b * 4;
-    const float h = h4q[(size_t)b * kFc4 + j];
-    float v = d[0] * w0 + d[1] * w1 + d[2] * w2 + d[3] * w3;
-    v = h > 0.f ? v : 0.f;                                     // ReLU backward
-    dh4[(size_t)b * kFc4 + j] = v;
-    db += v;
+    const float* d = dqbuf + b * 4;
+    const float hv = h4q[(size_t)b * kFc4 + j];
+    db += dh4[(size_t)b * kFc4 + j];
 #pragma unroll
-    for (int a = 0; a < 4; ++a) dw[a] += d[a] * h;
+    for (int a = 0; a < 4; ++a) dw[a] += d[a] * hv;
   }
   float* r = red + (g * 64 + lane) * 5;
   r[0] = db;
@@ -340,11 +457,10 @@ __global__ __launch_bounds__(256) void out_bwd_kernel(
 
 hipError_t launch_head(const NetBuffers& nb, hipStream_t s) {
   const ParamLayout& L = nb.L;
-  const size_t shm = (size_t)(4 * nb.B + 4 * 64 * 5) * sizeof(float);
-  hipLaunchKernelGGL(out_bwd_kernel, dim3(kFc4 / 64), dim3(256), shm, s, nb.B, nb.gamma,
-                     nb.q_out, nb.p_out, nb.h4[0], nb.theta[0] + L.w[4], nb.action, nb.reward,
-                     nb.nonterm, nb.q_sa, nb.p_sa, nb.target, nb.loss, nb.grad + L.w[4],
-                     nb.grad + L.b[4], nb.grad + L.b[3], nb.dh4);
+  hipLaunchKernelGGL(fc4_head_kernel, dim3(nb.B), dim3(kFc4), 0, s, nb.fc4_part, nb.fc4_splits,
+                     nb.B, nb.gamma, nb.theta[0], nb.theta[1], L.b[3], L.w[4], L.b[4], nb.action,
+                     nb.reward, nb.nonterm, nb.h4[0], nb.h4[1], nb.q_out, nb.p_out, nb.q_sa,
+                     nb.p_sa, nb.target, nb.dqbuf, nb.lpart, nb.dh4);
   return hipGetLastError();
 }
 
@@ -359,7 +475,15 @@ struct WredDims {
   int cout, cin, ks, splits, np, blk0;   // blk0: first workgroup of this layer
 };
 
-__device__ __forceinline__ void apply_book(int64_t* iter, int32_t* opt_init, int period) {
+struct HeadSums {
+  int blk0, B;
+  const float *dqbuf, *lpart, *h4q, *dh4;
+  float *loss, *gw5, *gb5, *gb4;
+};
+
+__device__ __forceinline__ void apply_book(int64_t* iter, int32_t* opt_init, int period,
+                                           ReplayMeta* bump = nullptr) {
+  if (bump) bump->counter += 1;     // the step's fused draw (sample_gather_kernel)
   const int64_t it = *iter;
   opt_init[2] = (opt_init[0] == 0);
   opt_init[3] = period > 0 && ((it + 1) % period) == 0;
@@ -371,10 +495,16 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
                                                            float* __restrict__ grad, WredDims d0,
                                                            WredDims d1, WredDims d2,
                                                            int64_t* iter, int32_t* opt_init,
-                                                           int book_period) {
+                                                           int book_period, ReplayMeta* bump,
+                                                           HeadSums hs) {
   __shared__ float red[4][64];
   const int bid = blockIdx.x;
-  if (opt_init && bid == 0 && threadIdx.x == 0) apply_book(iter, opt_init, book_period);
+  if (opt_init && bid == 0 && threadIdx.x == 0) apply_book(iter, opt_init, book_period, bump);
+  if (bid >= hs.blk0) {
+    head_sums(bid - hs.blk0, hs.B, hs.dqbuf, hs.lpart, hs.h4q, hs.dh4, hs.loss, hs.gw5, hs.gb5,
+              hs.gb4);
+    return;
+  }
   const WredDims d = bid >= d2.blk0 ? d2 : (bid >= d1.blk0 ? d1 : d0);
   const int lb = bid - d.blk0;
   const int nblk = d.np / 64;
@@ -599,7 +729,7 @@ static WgradDArgs wgradd_args(const P& p, int B, int G) {
 }
 
 hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
-                          void (*mark)(void*, const char*), void* marg) {
+                          void (*mark)(void*, const char*), void* marg, bool out) {
   const ParamLayout& L = nb.L;
   const int B = nb.B, S = nb.S;
   auto M = [&](const char* n) { if (mark) mark(marg, n); };
@@ -656,10 +786,8 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     if (nb.conv_impl == 1) {
       DirectArgs d = direct_fwd_args(p.in, p.wk, p.bias, p.out, p.mask, B, H, 1);
       d.nchw = 1;
-      if (nb.variant & 2)
-        CHECK_LAUNCH((launch_direct<64, 64, 3, 4, 8, 1, 2, false, false>(d, nz, s)));
-      else
-        CHECK_LAUNCH((launch_direct<64, 64, 3, 8, 8, 2, 2, false, false>(d, nz, s)));
+      // 3 tap groups: 512 output blocks per tower would leave one wave per SIMD
+      CHECK_LAUNCH((launch_direct<64, 64, 3, 8, 8, 2, 2, false, false, 3>(d, nz, s)));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgConv3F>(p, nz, 1, s));
     }
@@ -681,6 +809,7 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     } else {
       CHECK_LAUNCH(launch_gemm<CfgFcF>(p, nz, ns, s));
     }
+    if (!out) return hipSuccess;   // training: reduce + Q_out fused into the head kernel
     M("fc4_reduce_out");
     hipLaunchKernelGGL(fc4_reduce_out_kernel, dim3(B, nz), dim3(kFc4), 0, s, nb.fc4_part, ns, nz,
                        B, nb.theta[0] + L.b[3], nb.theta[1] + L.b[3], nb.theta[0] + L.w[4],
@@ -692,7 +821,8 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
 }
 
 hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(void*, const char*),
-                           void* marg, bool concurrent, bool book, int book_period) {
+                           void* marg, bool concurrent, bool book, int book_period,
+                           ReplayMeta* bump) {
   const ParamLayout& L = nb.L;
   const int B = nb.B, S = nb.S;
   const int s4 = S / 8;
@@ -757,10 +887,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     M("conv3_dgrad");
     if (nb.conv_impl == 1) {
       const DirectArgs d = direct_dgrad_args(nb.dconv3, p.wk, nb.mask2, nb.dconv2, B, H, 1);
-      if (nb.variant & 1)
-        CHECK_LAUNCH((launch_direct<64, 64, 3, 4, 8, 1, 2, true, false>(d, 1, s)));
-      else
-        CHECK_LAUNCH((launch_direct<64, 64, 3, 8, 8, 2, 2, true, false>(d, 1, s)));
+      CHECK_LAUNCH((launch_direct<64, 64, 3, 8, 8, 2, 2, true, false, 3>(d, 1, s)));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgD3>(p, 1, 1, s));
     }
@@ -790,8 +917,9 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     p.dconv = nb.dconv2; p.wk = nb.wk[0] + L.wk_off[1]; p.pmask = nb.mask1; p.pdconv = nb.dconv1;
     M("conv2_dgrad");
     if (nb.conv_impl == 1) {
-      CHECK_LAUNCH((launch_direct<64, 32, 5, 8, 16, 4, 1, true, false>(
-          direct_dgrad_args(nb.dconv2, p.wk, nb.mask1, nb.dconv1, B, H, 2), 1, s)));
+      const DirectArgs d = direct_dgrad_args(nb.dconv2, p.wk, nb.mask1, nb.dconv1, B, H, 2);
+      // 2 tap groups: two waves per SIMD over the 1024 output blocks
+      CHECK_LAUNCH((launch_direct<64, 32, 5, 8, 16, 4, 1, true, false, 2>(d, 1, s)));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgD2>(p, 1, 1, s));
     }
@@ -829,8 +957,11 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
       ++nev;
     }
     M("wgrad_reduce");
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blk), dim3(256), 0, s, nb.wpart, nb.grad, d[0],
-                       d[1], d[2], nb.iter, book ? nb.opt_init : nullptr, book_period);
+    HeadSums hs{blk, B, nb.dqbuf, nb.lpart, nb.h4[0], nb.dh4, nb.loss, nb.grad + L.w[4],
+                nb.grad + L.b[4], nb.grad + L.b[3]};
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blk + kFc4 / 64), dim3(256), 0, s, nb.wpart,
+                       nb.grad, d[0], d[1], d[2], nb.iter, book ? nb.opt_init : nullptr,
+                       book_period, book ? bump : nullptr, hs);
     CHECK_LAUNCH(hipGetLastError());
   }
   return hipSuccess;

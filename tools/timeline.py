@@ -1,6 +1,6 @@
 """Per-step kernel timeline from a rocprofv3 kernel_trace.csv.
 
-Usage: python tools/timeline.py <kernel_trace.csv> [--step-kernel apply_book_kernel] [--nsteps 3]
+Usage: python tools/timeline.py <kernel_trace.csv> [--step-kernel apply_kernel] [--nsteps 3]
 Prints, for a few consecutive steps in the middle of the trace, every kernel's
 start offset from the step start, its duration and the idle gap before it on
 the device (all streams merged), plus per-step totals.
@@ -18,7 +18,7 @@ def short(name):
 
 def main():
     path = sys.argv[1]
-    marker = "apply_book_kernel"
+    marker = "apply_kernel"
     nsteps = 3
     if "--step-kernel" in sys.argv:
         marker = sys.argv[sys.argv.index("--step-kernel") + 1]
