@@ -19,6 +19,20 @@ __device__ __forceinline__ int fc_acc_row(int r, int lane) {
 __device__ __forceinline__ float f4get(const float4& v, int i) {
   return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
 }
+// Bounds-checked buffer loads: an offset past `bytes` reads 0 with no branch
+// or select, so every load of a wave can be issued before the first wait.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t fc_rsrc(const float* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float4 fc_ld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+  return *reinterpret_cast<float4*>(&v);
+}
+__device__ __forceinline__ float fc_ld1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
+  return __builtin_bit_cast(float, v);
+}
+constexpr uint32_t kFcOOB = 0x80000000u;
 
 // ---------------------------------------------------------------------------
 // forward, split-K: part[split][z][b][n] = sum_{k in split} x[z][b][k] W4[z][n][k]
@@ -42,8 +56,9 @@ __global__ __launch_bounds__(256) void fc4_fwd_direct_kernel(const Fc4FwdArgs a)
   const int n0 = blockIdx.x * 128 + w * 32;
   const int K = a.K;
   const int k0 = split * kFc4KLen;
-  const float* wr = a.w[z] + (size_t)(n0 + l31) * K + h * 16;
-  const float* xz = a.x[z] + h * 16;
+  const __amdgpu_buffer_rsrc_t rw = fc_rsrc(a.w[z], (uint32_t)(512 * K * 4));
+  const __amdgpu_buffer_rsrc_t rx = fc_rsrc(a.x[z], (uint32_t)(a.B * K * 4));
+  const uint32_t wrow = (uint32_t)((n0 + l31) * K + h * 16) * 4;
 
   f32x16 acc[BT];
 #pragma unroll
@@ -58,18 +73,17 @@ __global__ __launch_bounds__(256) void fc4_fwd_direct_kernel(const Fc4FwdArgs a)
     const int k = k0 + kb * 32;
     const bool kin = k < K;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      wv[kb][i] = kin ? *reinterpret_cast<const float4*>(wr + k + 4 * i) : f4zero();
+    for (int i = 0; i < 4; ++i) wv[kb][i] = fc_ld4(rw, kin ? wrow + (k + 4 * i) * 4 : kFcOOB);
 #pragma unroll
     for (int t = 0; t < BT; ++t) {
-      const int b = t * 32 + l31;
-      const bool ok = kin && b < a.B;
+      const int b = t * 32 + l31;     // rows b >= B fall past the x buffer: 0
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        xv[kb][t][i] = ok ? *reinterpret_cast<const float4*>(xz + (size_t)b * K + k + 4 * i)
-                          : f4zero();
+        xv[kb][t][i] =
+            fc_ld4(rx, kin ? (uint32_t)(b * K + h * 16 + k + 4 * i) * 4 : kFcOOB);
     }
   }
+  __builtin_amdgcn_sched_barrier(0);   // keep every load ahead of the first MFMA
 #pragma unroll
   for (int kb = 0; kb < kFc4KLen / 32; ++kb)
 #pragma unroll
@@ -127,21 +141,21 @@ __global__ __launch_bounds__(512) void fc4_dgrad_direct_kernel(const Fc4DgradArg
   const int kc0 = blockIdx.x * 32, b0 = blockIdx.y * 32;
   const int K = a.K;
   const int nbase = w * 64 + h * 16;
-  const int b = b0 + l31;
-  const bool bok = b < a.B;
-  const float* ar = a.dh4 + (size_t)(bok ? b : 0) * 512 + nbase;
-  const float* br = a.w4 + (size_t)nbase * K + kc0 + l31;
+  const __amdgpu_buffer_rsrc_t ra = fc_rsrc(a.dh4, (uint32_t)(a.B * 512 * 4));
+  const __amdgpu_buffer_rsrc_t rb = fc_rsrc(a.w4, (uint32_t)(512 * K * 4));
+  const uint32_t aoff = (uint32_t)((b0 + l31) * 512 + nbase) * 4;   // rows b >= B read 0
+  const uint32_t boff = (uint32_t)(nbase * K + kc0 + l31) * 4;
 
   float4 av[2][4];
   float bv[2][16];
 #pragma unroll
   for (int blk = 0; blk < 2; ++blk) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      av[blk][i] = bok ? *reinterpret_cast<const float4*>(ar + blk * 32 + 4 * i) : f4zero();
+    for (int i = 0; i < 4; ++i) av[blk][i] = fc_ld4(ra, aoff + (blk * 32 + 4 * i) * 4);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) bv[blk][j] = br[(size_t)(blk * 32 + j) * K];
+    for (int j = 0; j < 16; ++j) bv[blk][j] = fc_ld1(rb, boff + (uint32_t)((blk * 32 + j) * K) * 4);
   }
+  __builtin_amdgcn_sched_barrier(0);   // keep every load ahead of the first MFMA
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;

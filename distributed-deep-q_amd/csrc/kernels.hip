@@ -244,23 +244,23 @@ hipError_t launch_u8_to_nhwc(const uint8_t* src, int n, int S, float* dst, hipSt
 // ---------------------------------------------------------------------------
 struct ConvDims { int64_t w_off, wk_off; int cout, cin, ks; };
 
-__device__ __forceinline__ int64_t wk_index(const ConvDims& d, int64_t e) {
-  // e: Caffe-order element of the layer's weight
-  const int kk = d.ks * d.ks;
-  const int64_t co = e / ((int64_t)d.cin * kk);
-  const int64_t rem = e - co * d.cin * kk;
-  const int ci = (int)(rem / kk), tap = (int)(rem % kk);
-  return d.wk_off + (co * kk + tap) * d.cin + ci;
+// e: Caffe-order element (co, ci, ky, kx) of the layer's weight (< 2^31);
+// returns its offset in the kernel layout Wk[co][tap][ci].
+__device__ __forceinline__ int wk_local(const ConvDims& d, int e) {
+  const int kk = d.ks * d.ks, per = d.cin * kk;
+  const int co = e / per, rem = e - co * per;
+  const int ci = rem / kk, tap = rem - ci * kk;
+  return (co * kk + tap) * d.cin + ci;
 }
 
 __global__ void relayout_kernel(const float* __restrict__ theta, float* __restrict__ wk,
                                 ConvDims d0, ConvDims d1, ConvDims d2) {
   const int l = blockIdx.y;
   const ConvDims d = l == 0 ? d0 : (l == 1 ? d1 : d2);
-  const int64_t n = (int64_t)d.cout * d.cin * d.ks * d.ks;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
-       e += (int64_t)gridDim.x * blockDim.x)
-    wk[wk_index(d, e)] = theta[d.w_off + e];
+  const int n = d.cout * d.cin * d.ks * d.ks;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    wk[d.wk_off + wk_local(d, e)] = theta[d.w_off + e];
+  }
 }
 
 static void conv_dims(const ParamLayout& L, ConvDims* d) {
@@ -606,9 +606,9 @@ __global__ __launch_bounds__(256) void apply_kernel(
       if (e0 >= 0 && e0 < (int64_t)d.cout * d.cin * d.ks * d.ks) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int64_t idx = wk_index(d, e0 + e);
-          wk[idx] = th[e];
-          if (sync) wkP[idx] = th[e];
+          const int k = wk_local(d, (int)e0 + e);
+          wk[d.wk_off + k] = th[e];
+          if (sync) wkP[d.wk_off + k] = th[e];
         }
       }
     }
@@ -917,8 +917,8 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     p.dconv = nb.dconv2; p.wk = nb.wk[0] + L.wk_off[1]; p.pmask = nb.mask1; p.pdconv = nb.dconv1;
     M("conv2_dgrad");
     if (nb.conv_impl == 1) {
-      const DirectArgs d = direct_dgrad_args(nb.dconv2, p.wk, nb.mask1, nb.dconv1, B, H, 2);
       // 2 tap groups: two waves per SIMD over the 1024 output blocks
+      const DirectArgs d = direct_dgrad_args(nb.dconv2, p.wk, nb.mask1, nb.dconv1, B, H, 2);
       CHECK_LAUNCH((launch_direct<64, 32, 5, 8, 16, 4, 1, true, false, 2>(d, 1, s)));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgD2>(p, 1, 1, s));

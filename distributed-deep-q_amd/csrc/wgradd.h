@@ -53,8 +53,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
   const int inf = Geo::in_floats(W);
   float* rin = sm + w * Geo::region(W);     // input row, pixel 0 <-> x = -PAD
   float* rd = rin + inf;                    // dconv row, [x][32] of block cb
-  const int cb = blockIdx.y / KS, ky = blockIdx.y % KS;
-  const int r0 = blockIdx.x * a.RPG;
+  // XCD-aware decode of the 1-D grid: workgroups are dealt to the 8 XCDs
+  // round-robin, so give every (cb, ky) workgroup of row group g the same
+  // L % 8 and the group's rows stay in one XCD's L2.
+  constexpr int NTS = (COUT / 32) * KS;
+  const int L = blockIdx.x, xcd = L & 7, q = L >> 3;
+  const int ts = q % NTS, g = xcd + 8 * (q / NTS);
+  if (g >= a.G) return;
+  const int cb = ts / KS, ky = ts % KS;
+  const int r0 = g * a.RPG;
   const int r1 = min(a.B * H, r0 + a.RPG);
 
   // zero halo columns (never overwritten) and the odd-width tail pixel
@@ -156,7 +163,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
 
   // ---- sum the four waves' tiles in fixed order, store the group slab ----
   float* red = sm;                                   // [4 waves][16 r][64 lanes]
-  float* slab = a.part + (size_t)blockIdx.x * COUT * a.NP + (size_t)cb * 32 * a.NP;
+  float* slab = a.part + (size_t)g * COUT * a.NP + (size_t)cb * 32 * a.NP;
 #pragma unroll
   for (int t = 0; t < T; ++t) {
     __syncthreads();
@@ -196,6 +203,7 @@ inline size_t wgradd_smem_bytes(int W) {
 // Row groups: about two 4-wave workgroups per CU over all (cb, ky) pairs.
 inline void wgradd_groups(int rows, int nts, int* G, int* RPG) {
   int g = 512 / nts;
+  if (g >= 16) g &= ~7;            // whole XCD rounds (see the kernel's decode)
   if (g < 1) g = 1;
   if (g > rows) g = rows;
   const int rpg = (rows + g - 1) / g;
@@ -206,7 +214,8 @@ inline void wgradd_groups(int rows, int nts, int* G, int* RPG) {
 template <int CIN, int COUT, int KS, int PAD>
 inline hipError_t launch_wgradd(const WgradDArgs& a, hipStream_t st) {
   const size_t shm = wgradd_smem_bytes<CIN, PAD>(a.W);
-  hipLaunchKernelGGL((wgradd_kernel<CIN, COUT, KS, PAD>), dim3(a.G, (COUT / 32) * KS), dim3(256),
+  const int g8 = (a.G + 7) / 8 * 8;
+  hipLaunchKernelGGL((wgradd_kernel<CIN, COUT, KS, PAD>), dim3(g8 * (COUT / 32) * KS), dim3(256),
                      shm, st, a);
   return hipGetLastError();
 }
