@@ -142,8 +142,13 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void direct_conv_kernel(const Di
   const int z = blockIdx.z, b = blockIdx.y;
   const int ty = blockIdx.x / a.tiles_x, tx = blockIdx.x % a.tiles_x;
   const int y0 = ty * TY, x0 = tx * TX;
-  const float* __restrict__ in = a.in[z];
-  const float* __restrict__ wk = a.wk[z];
+  // select, never index, the per-tower kernel arguments: a runtime index into
+  // a kernarg array makes the compiler copy the struct to scratch memory
+  const float* __restrict__ in = z ? a.in[1] : a.in[0];
+  const float* __restrict__ wk = z ? a.wk[1] : a.wk[0];
+  const float* __restrict__ biasz = z ? a.bias[1] : a.bias[0];
+  float* __restrict__ outz = z ? a.out[1] : a.out[0];
+  uint8_t* __restrict__ maskz = z ? a.mask[1] : a.mask[0];
 
   // ---- stage the halo patch (zero outside the image) ----
   for (int f = tid; f < C::PH * C::PW * (CP / 4); f += C::kThreads) {
@@ -204,7 +209,9 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void direct_conv_kernel(const Di
     const int t = s * WK + wkg;
     const int tn = t + WK;
     const float* wb = wbuf + (WALL ? t : ((s & 1) * WK + wkg)) * N * C::CW;
-    if (!WALL && s + 1 < NSTEP && tn < C::T) ws.template load<DGRAD>(wk, tn, gtid);   // in flight
+    // next tap's weights in flight under this tap's MFMAs (clamped index: the
+    // load is unconditional so the staging registers never go through scratch)
+    if (!WALL && s + 1 < NSTEP) ws.template load<DGRAD>(wk, tn < C::T ? tn : C::T - 1, gtid);
     if (t < C::T) {
       const int ky = t / KS, kx = t % KS;
       const float* pa = patch + ky * C::RS + kx * C::CS;
@@ -268,7 +275,7 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void direct_conv_kernel(const Di
       const int n = wni * TN * 32 + 32 * j + l31;
       if (!DGRAD) {
         const int Hp = a.H >> 1, Wp = a.W >> 1;
-        const float bv = a.bias[z][n];
+        const float bv = biasz[n];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int win = (mb + 8 * g + 4 * h) >> 2;
@@ -283,8 +290,8 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void direct_conv_kernel(const Di
           const bool pos = mx > 0.f;
           const size_t o = a.nchw ? (((size_t)b * N + n) * Hp + pyy) * Wp + pxx
                                   : (((size_t)b * Hp + pyy) * Wp + pxx) * N + n;
-          a.out[z][o] = pos ? mx : 0.f;
-          if (a.mask[z]) a.mask[z][o] = (uint8_t)(pos ? arg : 4);
+          outz[o] = pos ? mx : 0.f;
+          if (maskz) maskz[o] = (uint8_t)(pos ? arg : 4);
         }
       } else {
         const int W2 = 2 * a.W;

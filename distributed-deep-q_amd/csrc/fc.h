@@ -56,8 +56,8 @@ __global__ __launch_bounds__(256) void fc4_fwd_direct_kernel(const Fc4FwdArgs a)
   const int n0 = blockIdx.x * 128 + w * 32;
   const int K = a.K;
   const int k0 = split * kFc4KLen;
-  const __amdgpu_buffer_rsrc_t rw = fc_rsrc(a.w[z], (uint32_t)(512 * K * 4));
-  const __amdgpu_buffer_rsrc_t rx = fc_rsrc(a.x[z], (uint32_t)(a.B * K * 4));
+  const __amdgpu_buffer_rsrc_t rw = fc_rsrc(z ? a.w[1] : a.w[0], (uint32_t)(512 * K * 4));
+  const __amdgpu_buffer_rsrc_t rx = fc_rsrc(z ? a.x[1] : a.x[0], (uint32_t)(a.B * K * 4));
   const uint32_t wrow = (uint32_t)((n0 + l31) * K + h * 16) * 4;
 
   f32x16 acc[BT];

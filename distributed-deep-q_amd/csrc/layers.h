@@ -58,18 +58,18 @@ struct ConvFwd {
     const int ky = tap / KS, kx = tap % KS;
     const int yy = c.y + ky - PAD, xx = c.x + kx - PAD;
     if ((unsigned)yy >= (unsigned)H || (unsigned)xx >= (unsigned)W) return f4zero();
-    return *reinterpret_cast<const float4*>(in[z] + (((size_t)c.b * H + yy) * W + xx) * CIN + ci);
+    return *reinterpret_cast<const float4*>((z ? in[1] : in[0]) + (((size_t)c.b * H + yy) * W + xx) * CIN + ci);
   }
   struct BCtx { int n; };
   __device__ BCtx bctx(int, int n) const { return {n}; }
   __device__ float4 loadB(int z, const BCtx&, const KCtx&, int k, int n) const {
     if (n >= N || k >= K) return f4zero();
-    return *reinterpret_cast<const float4*>(wk[z] + (size_t)n * KC + k);
+    return *reinterpret_cast<const float4*>((z ? wk[1] : wk[0]) + (size_t)n * KC + k);
   }
   __device__ void epilogue(int z, int, int mb, int nb, const f32x16& acc, int lane) const {
     const int co = nb + (lane & 31);
     if (co >= N) return;
-    const float bv = bias[z][co];
+    const float bv = (z ? bias[1] : bias[0])[co];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int m = mb + 8 * g + 4 * (lane >> 5);
@@ -89,8 +89,9 @@ struct ConvFwd {
         fHWp.divmod((uint32_t)q, bb, pp);
         o = ((size_t)bb * COUT + co) * fHWp.d + pp;
       }
-      out[z][o] = pos ? mx : 0.f;
-      if (mask[z]) mask[z][o] = (uint8_t)(pos ? arg : 4);
+      (z ? out[1] : out[0])[o] = pos ? mx : 0.f;
+      uint8_t* mz = z ? mask[1] : mask[0];
+      if (mz) mz[o] = (uint8_t)(pos ? arg : 4);
     }
   }
 };
@@ -258,13 +259,13 @@ struct FcFwd {
   __device__ ACtx actx(int, int m) const { return {m, m < M}; }
   __device__ float4 loadA(int z, const ACtx& c, const KCtx&, int, int k) const {
     if (!c.ok || k >= K) return f4zero();
-    return *reinterpret_cast<const float4*>(x[z] + (size_t)c.b * K + k);
+    return *reinterpret_cast<const float4*>((z ? x[1] : x[0]) + (size_t)c.b * K + k);
   }
   struct BCtx { int n; };
   __device__ BCtx bctx(int, int n) const { return {n}; }
   __device__ float4 loadB(int z, const BCtx&, const KCtx&, int k, int n) const {
     if (n >= N || k >= K) return f4zero();
-    return *reinterpret_cast<const float4*>(w[z] + (size_t)n * K + k);
+    return *reinterpret_cast<const float4*>((z ? w[1] : w[0]) + (size_t)n * K + k);
   }
   __device__ void epilogue(int z, int split, int mb, int nb, const f32x16& acc, int lane) const {
     const int n = nb + (lane & 31);
