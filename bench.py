@@ -49,6 +49,40 @@ def kernel_flops(B, S):
             "conv2_wgrad": c2, "conv2_dgrad": c2, "conv1_wgrad": c1}
 
 
+# rocprof kernel symbol (prefix) of each profiled step kernel
+KERNEL_SYMBOL = {
+    "sample_gather": "ddq::sample_gather_kernel",
+    "conv1_fwd": "void ddq::direct_conv_kernel<4, 32, 7,",
+    "conv2_fwd": "void ddq::direct_conv_kernel<32, 64, 5,",
+    "conv3_fwd": "void ddq::direct_conv_kernel<64, 64, 3, 8, 8, 2, 2, false",
+    "fc4_fwd": "void ddq::fc4_fwd_direct_kernel",
+    "head": "ddq::fc4_head_kernel",
+    "fc4_dgrad": "ddq::fc4_dgrad_direct_kernel",
+    "fc4_wgrad": "void ddq::gemm_f32_kernel<ddq::GemmCfg<64, 64, 32, 2, 2, 1>, ddq::FcWgrad>",
+    "conv3_wgrad": "void ddq::wgradd_kernel<64, 64, 3, 1>",
+    "conv3_dgrad": "void ddq::direct_conv_kernel<64, 64, 3, 8, 8, 2, 2, true",
+    "conv2_wgrad": "void ddq::wgradd_kernel<32, 64, 5, 2>",
+    "conv2_dgrad": "void ddq::direct_conv_kernel<64, 32, 5,",
+    "conv1_wgrad": "ddq::wgrad1_kernel",
+    "wgrad_reduce": "ddq::wgrad_reduce_kernel",
+    "apply": "ddq::apply_kernel",
+}
+
+
+def pmc_traffic(label, B, S):
+    """HBM bytes per launch of `label` from the committed PMC summary
+    (profiles/r01_pmc.json, tools/run_measure.sh: FETCH_SIZE x2 + WRITE_SIZE,
+    MI355X_MICROARCH.md gfx950 correction), valid for the bench default shape."""
+    path = os.path.join(ROOT, "profiles", "r01_pmc.json")
+    if (B, S) != (32, 64) or not os.path.exists(path):
+        return None
+    sym = KERNEL_SYMBOL.get(label)
+    for name, e in json.load(open(path))["kernels"].items():
+        if sym and name.startswith(sym) and "hbm_bytes" in e:
+            return round(e["hbm_bytes"])
+    return None
+
+
 def fill_replay(net, N, S, seed):
     from ddq.expgain import synthetic_transitions
     pool = min(N, 4096)
@@ -170,7 +204,7 @@ def main():
     for _ in range(args.profile_steps):
         for name, us in net.profile_step(cfg):
             prof.setdefault(name, []).append(us)
-    avg = {k: float(np.mean(v)) for k, v in prof.items()}
+    avg = {k: float(np.median(v)) for k, v in prof.items()}
     flops = kernel_flops(B, S)
     dom = max((k for k in avg if k in flops), key=lambda k: avg[k])
     achieved = flops[dom] / (avg[dom] * 1e-6) / 1e12
@@ -198,7 +232,8 @@ def main():
                        "pipelined": bool(args.pipeline and not args.eager)},
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3),
                          "peak": F32_MFMA_PEAK / 1e12, "unit": "TFLOP/s",
-                         "frac": round(achieved * 1e12 / F32_MFMA_PEAK, 4), "traffic": None,
+                         "frac": round(achieved * 1e12 / F32_MFMA_PEAK, 4),
+                         "traffic": pmc_traffic(dom, B, S), "traffic_unit": "bytes/launch",
                          "kernel_us": round(avg[dom], 3),
                          "step_tflops": round(step_flops / (dt / args.steps) / 1e12, 3),
                          "step_frac": round(step_flops / (dt / args.steps) / F32_MFMA_PEAK, 4)},

@@ -47,7 +47,8 @@ struct ddq_ctx {
   int nranks = 1, rank = 0;
   // graph
   hipGraph_t graph = nullptr;
-  hipGraphExec_t gexec = nullptr;
+  hipGraphExec_t gexec = nullptr;     // one step
+  hipGraphExec_t gexec_k = nullptr;   // kGraphSteps steps
   ddq_step_cfg gcfg{};
   bool have_graph = false;
   // pipelined stepping: a second minibatch set and graphs [parity][prefetch]
@@ -126,6 +127,8 @@ static int set_dev(ddq_ctx* c) {
 
 static void invalidate_graph(ddq_ctx* c) {
   if (c->gexec) hipGraphExecDestroy(c->gexec);
+  if (c->gexec_k) hipGraphExecDestroy(c->gexec_k);
+  c->gexec_k = nullptr;
   if (c->graph) hipGraphDestroy(c->graph);
   c->gexec = nullptr;
   c->graph = nullptr;
@@ -834,28 +837,43 @@ int ddq_step_async(ddq_ctx* c, const ddq_step_cfg* cfg) {
   return DDQ_OK;
 }
 
+static int capture_steps(ddq_ctx* c, const ddq_step_cfg* cfg, int k, hipGraphExec_t* out) {
+  HIP_TRY(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+  int rc = DDQ_OK;
+  for (int i = 0; i < k && rc == DDQ_OK; ++i) rc = enqueue_step(c, cfg, nullptr, nullptr);
+  hipGraph_t g = nullptr;
+  hipError_t e = hipStreamEndCapture(c->stream, &g);
+  if (rc != DDQ_OK) { if (g) hipGraphDestroy(g); return rc; }
+  if (e != hipSuccess) return fail(c, DDQ_EHIP, "hipStreamEndCapture: %s", hipGetErrorString(e));
+  e = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
+  hipGraphDestroy(g);
+  if (e != hipSuccess) return fail(c, DDQ_EHIP, "hipGraphInstantiate: %s", hipGetErrorString(e));
+  return DDQ_OK;
+}
+
+// One graph holds kGraphSteps steps back to back (the launch of a graph
+// costs ~9 us of device idle, measured, so it is paid once per kGraphSteps
+// steps), plus a one-step graph for the remainder.  The device-side counters
+// make every captured step read its own iteration / RNG state.
+static constexpr int kGraphSteps = 8;
+
 int ddq_step_graph_async(ddq_ctx* c, const ddq_step_cfg* cfg, int32_t nsteps) {
   TRY(check_step(c, cfg));
   TRY(set_dev(c));
   if (!c->have_graph || memcmp(&c->gcfg, cfg, sizeof(*cfg)) != 0) {
     invalidate_graph(c);
-    HIP_TRY(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    int rc = enqueue_step(c, cfg, nullptr, nullptr);
-    hipGraph_t g = nullptr;
-    hipError_t e = hipStreamEndCapture(c->stream, &g);
-    if (rc != DDQ_OK) { if (g) hipGraphDestroy(g); return rc; }
-    if (e != hipSuccess) return fail(c, DDQ_EHIP, "hipStreamEndCapture: %s", hipGetErrorString(e));
-    c->graph = g;
-    HIP_TRY(c, hipGraphInstantiate(&c->gexec, c->graph, nullptr, nullptr, 0));
+    TRY(capture_steps(c, cfg, 1, &c->gexec));
+    TRY(capture_steps(c, cfg, kGraphSteps, &c->gexec_k));
     c->gcfg = *cfg;
     c->have_graph = true;
   }
   if (c->steps == 0 && nsteps > 0) TRY(initial_target_sync(c, cfg));
-  for (int i = 0; i < nsteps; ++i) {
-    HIP_TRY(c, hipGraphLaunch(c->gexec, c->stream));
-    c->steps++;
-    c->applied++;
-  }
+  int i = 0;
+  for (; i + kGraphSteps <= nsteps; i += kGraphSteps)
+    HIP_TRY(c, hipGraphLaunch(c->gexec_k, c->stream));
+  for (; i < nsteps; ++i) HIP_TRY(c, hipGraphLaunch(c->gexec, c->stream));
+  c->steps += nsteps;
+  c->applied += nsteps;
   return DDQ_OK;
 }
 
