@@ -139,6 +139,99 @@ def cpu_baseline(B, S, seed, budget_s=12.0, max_steps=16):
                       "%.1f s" % (steps, B, S, S, cores, dt)}
 
 
+def dev_timer(net):
+    """HIP-event timer on the ctx stream (torch events on an ExternalStream)."""
+    import torch
+    st = torch.cuda.ExternalStream(net.stream(), device=torch.device("cuda", net.device))
+
+    def run(fn, iters):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(iters):
+            fn()
+        e1.record(st)
+        e1.synchronize()
+        return e0.elapsed_time(e1) * 1e3 / iters       # us per call
+    return run
+
+
+def gather_stress(S=64, N=1_000_000, sizes=(256, 4096, 32768), seed=3):
+    """SURVEY 8(d) C5 gather stress: 1M-transition HBM ring (16.4 GB at 64x64),
+    device draw + Caffe-layout gather of n transitions per launch.  Bytes per
+    launch (algorithmic) = 2*n*4*S*S u8 read + 2*n*4*S*S*4 f32 write
+    + n*(1+2+1) scalars read + n*(4+1+1)*4 written."""
+    import ddq
+    from ddq.expgain import synthetic_transitions
+    net = ddq.DeepQNet(batch=32, frame=S)
+    net.replay_create(N)
+    st, ac, rw, nt = synthetic_transitions(4096, S, seed=seed)
+    net.replay_fill_tiled(st, ac, rw, nt.astype(np.uint8), 12345, N)
+    timer = dev_timer(net)
+    out = []
+    for n in sizes:
+        bufs = net.batch_buffers(n)
+        iters = max(5, min(200, (1 << 22) // n))
+        net.replay_sample_batch(bufs, seed=seed)           # warm (allocates the bitmap)
+        net.synchronize()
+        us_all = timer(lambda: net.replay_sample_batch(bufs, seed=seed, check=False), iters)
+        # gather alone over 16 pre-drawn index sets in rotation, so the slots
+        # read are not still in the 256 MB Infinity Cache from the last call
+        sets = []
+        for _ in range(16):
+            net.replay_sample_batch(bufs, seed=seed)          # synchronises
+            sets.append(bufs["idx"].clone())
+        net.synchronize()
+        rot = [0]
+
+        def gather_next():
+            bufs["idx"] = sets[rot[0] % len(sets)]
+            rot[0] += 1
+            net.replay_gather_batch(bufs, check=False)
+        us_g = timer(gather_next, iters)
+        net._check(net.lib.ddq_replay_status(net.ctx))
+        slot = 4 * S * S
+        algo = 2 * n * slot * 5 + n * 4 + n * 24
+        out.append({"n": n, "sample_gather_us": round(us_all, 2), "gather_us": round(us_g, 2),
+                    "gather_GBps": round(algo / (us_g * 1e-6) / 1e9, 1),
+                    "frac": round(algo / (us_g * 1e-6) / HBM_PEAK, 4),
+                    "sample_gather_GBps": round(algo / (us_all * 1e-6) / 1e9, 1),
+                    "algo_bytes": algo})
+        del bufs
+    net.close()
+    return {"replay_slots": N, "frame": S, "bound": "hbm", "peak_GBps": HBM_PEAK / 1e9,
+            "launches": out}
+
+
+def frame_sweep(B=256, frames=range(16, 129, 8), steps=60, warmup=10, rule="rmsprop"):
+    """batch 256, frame side 16..128 (results/cost-vs-image-size)."""
+    import ddq
+    from ddq.params import init_params_flat
+    from ddq.expgain import synthetic_transitions
+    res = []
+    for S in frames:
+        net = ddq.DeepQNet(batch=B, frame=S)
+        theta = init_params_flat(S, seed=42)
+        net.set_flat(0, theta)
+        net.set_flat(1, theta)
+        N = 30000
+        net.replay_create(N)
+        st, ac, rw, nt = synthetic_transitions(1024, S, seed=1)
+        net.replay_fill_tiled(st, ac, rw, nt.astype(np.uint8), 0, N)
+        cfg = net.step_cfg(rule, lr=1e-4, target_period=10, seed=1234)
+        net.step_graph(cfg, warmup)
+        net.synchronize()
+        t0 = time.perf_counter()
+        net.step_graph(cfg, steps)
+        net.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        fl = net.step_flops()
+        res.append({"frame": S, "updates_per_s": round(1 / dt, 2), "ms_per_step": round(dt * 1e3, 4),
+                    "step_tflops": round(fl / dt / 1e12, 2),
+                    "frac": round(fl / dt / F32_MFMA_PEAK, 4)})
+        net.close()
+    return {"batch": B, "bound": "mfma", "peak_TFLOPs": F32_MFMA_PEAK / 1e12, "frames": res}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -150,6 +243,10 @@ def main():
     ap.add_argument("--rule", default="rmsprop")
     ap.add_argument("--profile-steps", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gather-stress", action="store_true",
+                    help="skip the C5 1M-slot gather stress (rank 0, N=1 only)")
+    ap.add_argument("--sweep", action="store_true",
+                    help="C3: also run the batch-256 frame-size sweep 16..128 (slow)")
     ap.add_argument("--eager", action="store_true", help="no hipGraph (debug)")
     ap.add_argument("--pipeline", action="store_true",
                     help="prefetch the next minibatch on a side stream (slower on MI355X: "
@@ -240,6 +337,10 @@ def main():
             "kernels_us": {k: round(v, 2) for k, v in avg.items()},
             "final_loss": loss,
         }
+        if not args.no_gather_stress and world == 1:
+            out["gather_stress"] = gather_stress()
+        if args.sweep and world == 1:
+            out["frame_sweep"] = frame_sweep()
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(B, S, seed=7)
         print(json.dumps(out), flush=True)

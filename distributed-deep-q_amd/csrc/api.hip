@@ -36,6 +36,9 @@ struct ddq_ctx {
   int16_t* r_reward = nullptr;
   uint8_t* r_nonterm = nullptr;
   ReplayMeta* r_meta = nullptr;    // device
+  uint32_t* r_bitmap = nullptr;    // large-batch sampler scratch (lazy)
+  int32_t* r_blk = nullptr;
+  uint64_t batch_ctr = 0;          // large-batch draws so far (RNG stream position)
   int64_t head = 0, valid = 0, capacity = 0;
   // acting scratch
   uint8_t* act_u8 = nullptr;
@@ -79,10 +82,12 @@ static int fail(ddq_ctx* c, int code, const char* fmt, ...) {
 
 #define HIP_TRY(c, x)                                                                         \
   do {                                                                                        \
+    g_launch_where = "";                                                                      \
+    (void)hipGetLastError();  /* launches report via hipGetLastError: drop stale errors */    \
     hipError_t e_ = (x);                                                                      \
     if (e_ != hipSuccess)                                                                     \
-      return fail((c), DDQ_EHIP, "%s failed: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, \
-                  __LINE__);                                                                  \
+      return fail((c), DDQ_EHIP, "%s failed: %s (%s:%d%s%s)", #x, hipGetErrorString(e_),      \
+                  __FILE__, __LINE__, *g_launch_where ? ", at " : "", g_launch_where);        \
   } while (0)
 
 #define NCCL_TRY(c, x)                                                                           \
@@ -283,6 +288,12 @@ int ddq_set_stream(ddq_ctx* c, void* s) {
   return DDQ_OK;
 }
 
+int ddq_get_stream(const ddq_ctx* c, void** s) {
+  if (!c || !s) return fail(nullptr, DDQ_EINVAL, "null argument");
+  *s = reinterpret_cast<void*>(c->stream);
+  return DDQ_OK;
+}
+
 int ddq_synchronize(ddq_ctx* c) {
   if (!c) return fail(nullptr, DDQ_EINVAL, "null ctx");
   TRY(set_dev(c));
@@ -479,6 +490,7 @@ static int check_err_flag(ddq_ctx* c) {
     int32_t z = 0;
     HIP_TRY(c, scopy(c, reinterpret_cast<char*>(c->r_meta) + offsetof(ReplayMeta, err), &z, 4,
                          hipMemcpyHostToDevice));
+    if (m.err == 2) return fail(c, DDQ_ERANGE, "batch sampler could not find distinct indices");
     return fail(c, DDQ_ERANGE, "stored action index out of range for %d actions", 4);
   }
   return DDQ_OK;
@@ -514,6 +526,89 @@ int ddq_replay_sample_device_async(ddq_ctx* c, uint64_t seed) {
   HIP_TRY(c, launch_gather(c->nb, c->r_state, c->r_action, c->r_reward, c->r_nonterm, c->r_meta,
                            c->stream));
   return DDQ_OK;
+}
+
+int ddq_replay_fill_tiled(ddq_ctx* c, const uint8_t* state, const uint8_t* action,
+                          const int16_t* reward, const uint8_t* nonterm, int64_t pool,
+                          int64_t head, int64_t valid) {
+  if (!c || !state || !action || !reward || !nonterm) return fail(c, DDQ_EINVAL, "null argument");
+  if (!c->r_state) return fail(c, DDQ_ESTATE, "no replay buffer");
+  const int64_t n = c->capacity;
+  if (pool < 1 || pool > n) return fail(c, DDQ_EINVAL, "pool must be in [1, capacity]");
+  if (head < 0 || head >= n || valid < 0 || valid > n)
+    return fail(c, DDQ_EINVAL, "head/valid out of range");
+  TRY(set_dev(c));
+  const size_t slot = (size_t)4 * c->nb.S * c->nb.S;
+  HIP_TRY(c, scopy(c, c->r_state, state, slot * pool, hipMemcpyHostToDevice));
+  if (pool < n)
+    HIP_TRY(c, launch_tile(c->r_state + slot * pool, c->r_state, slot * pool,
+                           slot * (n - pool), c->stream));
+  std::vector<uint8_t> a(n), t(n);
+  std::vector<int16_t> r(n);
+  for (int64_t i = 0; i < n; ++i) {
+    a[i] = action[i % pool]; r[i] = reward[i % pool]; t[i] = nonterm[i % pool];
+  }
+  HIP_TRY(c, scopy(c, c->r_action, a.data(), n, hipMemcpyHostToDevice));
+  HIP_TRY(c, scopy(c, c->r_reward, r.data(), 2 * n, hipMemcpyHostToDevice));
+  HIP_TRY(c, scopy(c, c->r_nonterm, t.data(), n, hipMemcpyHostToDevice));
+  c->head = head;
+  c->valid = valid;
+  return push_meta(c);
+}
+
+static int check_batch_out(ddq_ctx* c, int32_t n, float* s0, float* a, float* r, float* s1,
+                           float* nt) {
+  if (!c) return fail(nullptr, DDQ_EINVAL, "null ctx");
+  if (!s0 || !a || !r || !s1 || !nt) return fail(c, DDQ_EINVAL, "null output buffer");
+  if (!c->r_state) return fail(c, DDQ_ESTATE, "no replay buffer");
+  if (n < 1) return fail(c, DDQ_EINVAL, "n must be >= 1");
+  if ((int64_t)n * c->nb.S * c->nb.S >= (int64_t)1 << 31)
+    return fail(c, DDQ_EINVAL, "n * S^2 must be < 2^31 (n=%d)", n);
+  if (n >= c->valid)
+    return fail(c, DDQ_EINVAL, "Can't draw sample of size %d from replay dataset of size %lld",
+                n, (long long)c->valid);
+  return DDQ_OK;
+}
+
+int ddq_replay_sample_batch_async(ddq_ctx* c, int32_t n, uint64_t seed, int32_t* idx,
+                                  float* state, float* action, float* reward, float* next_state,
+                                  float* nonterm) {
+  TRY(check_batch_out(c, n, state, action, reward, next_state, nonterm));
+  if (!idx) return fail(c, DDQ_EINVAL, "null idx");
+  if (2 * (int64_t)n > c->valid)
+    return fail(c, DDQ_EINVAL, "batch sampler needs n <= valid/2 (n=%d, valid=%lld)", n,
+                (long long)c->valid);
+  TRY(set_dev(c));
+  if (!c->r_bitmap) {   // sized for the full ring: valid never exceeds capacity
+    const int64_t nblk = ((c->capacity + 31) / 32 + 1023) / 1024;
+    TRY(dalloc(c, &c->r_bitmap, (size_t)nblk * 1024));
+    TRY(dalloc(c, &c->r_blk, (size_t)nblk));
+  }
+  HIP_TRY(c, launch_sample_batch(c->r_meta, c->valid, n, seed, c->batch_ctr++, c->r_bitmap,
+                                 c->r_blk, idx, c->stream));
+  HIP_TRY(c, launch_gather_nchw(c->r_state, c->r_action, c->r_reward, c->r_nonterm, c->r_meta,
+                                idx, n, c->nb.S, state, next_state, action, reward, nonterm,
+                                c->stream));
+  return DDQ_OK;
+}
+
+int ddq_replay_gather_batch_async(ddq_ctx* c, const int32_t* idx, int32_t n, float* state,
+                                  float* action, float* reward, float* next_state,
+                                  float* nonterm) {
+  TRY(check_batch_out(c, n, state, action, reward, next_state, nonterm));
+  if (!idx) return fail(c, DDQ_EINVAL, "null idx");
+  TRY(set_dev(c));
+  HIP_TRY(c, launch_gather_nchw(c->r_state, c->r_action, c->r_reward, c->r_nonterm, c->r_meta,
+                                idx, n, c->nb.S, state, next_state, action, reward, nonterm,
+                                c->stream));
+  return DDQ_OK;
+}
+
+int ddq_replay_status(ddq_ctx* c) {
+  if (!c) return fail(nullptr, DDQ_EINVAL, "null ctx");
+  if (!c->r_state) return fail(c, DDQ_ESTATE, "no replay buffer");
+  TRY(set_dev(c));
+  return check_err_flag(c);
 }
 
 int ddq_read_indices(ddq_ctx* c, int32_t* idx, int32_t batch) {

@@ -52,7 +52,9 @@ template <int BT>
 __global__ __launch_bounds__(256) void fc4_fwd_direct_kernel(const Fc4FwdArgs a) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int l31 = lane & 31, h = lane >> 5;
-  const int z = blockIdx.z, split = blockIdx.y;
+  // blockIdx.z = batch tile * nz + tower (B > 64: BT*32-row batch tiles)
+  const int z = blockIdx.z % a.nz, split = blockIdx.y;
+  const int bt0 = (blockIdx.z / a.nz) * (BT * 32);
   const int n0 = blockIdx.x * 128 + w * 32;
   const int K = a.K;
   const int k0 = split * kFc4KLen;
@@ -76,7 +78,7 @@ __global__ __launch_bounds__(256) void fc4_fwd_direct_kernel(const Fc4FwdArgs a)
     for (int i = 0; i < 4; ++i) wv[kb][i] = fc_ld4(rw, kin ? wrow + (k + 4 * i) * 4 : kFcOOB);
 #pragma unroll
     for (int t = 0; t < BT; ++t) {
-      const int b = t * 32 + l31;     // rows b >= B fall past the x buffer: 0
+      const int b = bt0 + t * 32 + l31;     // rows b >= B fall past the x buffer: 0
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         xv[kb][t][i] =
@@ -99,7 +101,7 @@ __global__ __launch_bounds__(256) void fc4_fwd_direct_kernel(const Fc4FwdArgs a)
   for (int t = 0; t < BT; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int b = t * 32 + fc_acc_row(r, lane);
+      const int b = bt0 + t * 32 + fc_acc_row(r, lane);
       if (b < a.B) dst[(size_t)b * 512] = acc[t][r];
     }
 }
@@ -107,13 +109,14 @@ __global__ __launch_bounds__(256) void fc4_fwd_direct_kernel(const Fc4FwdArgs a)
 inline int fc4_fwd_splits(int K) { return (K + kFc4KLen - 1) / kFc4KLen; }
 
 inline hipError_t launch_fc4_fwd_direct(const Fc4FwdArgs& a, hipStream_t st) {
-  dim3 grid(512 / 128, fc4_fwd_splits(a.K), a.nz);
-  if (a.B <= 32)
-    hipLaunchKernelGGL(fc4_fwd_direct_kernel<1>, grid, dim3(256), 0, st, a);
-  else if (a.B <= 64)
-    hipLaunchKernelGGL(fc4_fwd_direct_kernel<2>, grid, dim3(256), 0, st, a);
-  else
-    return hipErrorInvalidValue;
+  if (a.B <= 32) {
+    hipLaunchKernelGGL(fc4_fwd_direct_kernel<1>, dim3(512 / 128, fc4_fwd_splits(a.K), a.nz),
+                       dim3(256), 0, st, a);
+  } else {
+    const int nbt = (a.B + 63) / 64;
+    hipLaunchKernelGGL(fc4_fwd_direct_kernel<2>,
+                       dim3(512 / 128, fc4_fwd_splits(a.K), a.nz * nbt), dim3(256), 0, st, a);
+  }
   return hipGetLastError();
 }
 

@@ -83,8 +83,21 @@ hipError_t launch_relayout(const NetBuffers& nb, int z, hipStream_t s);
 hipError_t launch_act(const NetBuffers& nb, const float* in, int n, float* pool1, float* pool2,
                       float* pool3, float* h4, float* part, float* qout, int32_t* actions,
                       hipStream_t s);
+// large-batch device draw (bitmap claim + ordered compaction) into idx[0..n)
+// and the Caffe-layout (n,4,S,S) f32 gather of replay.py:167-183
+hipError_t launch_sample_batch(ReplayMeta* meta, int64_t valid, int n, uint64_t seed,
+                               uint64_t ctr, uint32_t* bm, int32_t* blk, int32_t* idx,
+                               hipStream_t s);
+hipError_t launch_gather_nchw(const uint8_t* st, const uint8_t* act, const int16_t* rew,
+                              const uint8_t* nt, ReplayMeta* meta, const int32_t* idx, int n,
+                              int S, float* s0, float* s1, float* action, float* reward,
+                              float* nonterm, hipStream_t s);
+hipError_t launch_tile(uint8_t* dst, const uint8_t* src, uint64_t pool_bytes, uint64_t total,
+                       hipStream_t s);
 hipError_t launch_u8_to_nhwc(const uint8_t* src, int n, int S, float* dst, hipStream_t s);
 
 double step_flops(int B, int S);
+
+extern thread_local const char* g_launch_where;
 
 }  // namespace ddq

@@ -9,6 +9,20 @@
 
 namespace ddq {
 
+// first failing launch site of the last failed launch sequence (api.hip
+// appends it to the error message)
+thread_local const char* g_launch_where = "";
+#define DDQ_STR2(x) #x
+#define DDQ_STR(x) DDQ_STR2(x)
+#define CHECK_LAUNCH(x)                                             \
+  do {                                                              \
+    hipError_t e_ = (x);                                            \
+    if (e_ != hipSuccess) {                                         \
+      if (!*g_launch_where) g_launch_where = "kernels.hip:" DDQ_STR(__LINE__); \
+      return e_;                                                    \
+    }                                                               \
+  } while (0)
+
 // ---------------------------------------------------------------------------
 // layout
 // ---------------------------------------------------------------------------
@@ -220,6 +234,209 @@ hipError_t launch_gather(const NetBuffers& nb, const uint8_t* st, const uint8_t*
   dim3 grid((SS / 4 + 255) / 256, nb.B, 2);
   hipLaunchKernelGGL(gather_kernel, grid, dim3(256), 0, s, st, act, rew, nt, meta, nb.idx, nb.S,
                      nb.state, nb.next_state, nb.action, nb.reward, nb.nonterm);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// large-batch sampling + Caffe-layout gather (SURVEY 8(d) C5 gather stress;
+// same selection semantics as replay.py:144-183 for any n <= valid/2)
+// ---------------------------------------------------------------------------
+// Claim: thread t draws uniform x in [0,valid) until it sets a fresh bit of
+// the bitmap (head-1 never accepted).  Every draw sequence is i.i.d. and the
+// process is symmetric in the population, so the claimed set is a uniform
+// n-subset of [0,valid) \ {head-1} -- the distribution of the reference's
+// whole-list redraw.  The bitmap is then compacted in index order, which is
+// the sort of replay.py:159 for free.
+__global__ __launch_bounds__(256) void claim_kernel(ReplayMeta* meta, int n, uint64_t seed,
+                                                   uint64_t ctr, uint32_t* __restrict__ bm) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= n) return;
+  const int64_t valid = meta->valid, forbid = meta->head - 1;
+  for (int round = 0; round < 4096; ++round) {
+    const uint64_t r = splitmix64(seed ^ splitmix64(ctr * 0x100000001B3ull +
+                                                    (uint64_t)t * 0x9E3779B1ull +
+                                                    ((uint64_t)round << 44)));
+    const int64_t x = (int64_t)__umul64hi(r, (uint64_t)valid);
+    if (x == forbid) continue;
+    const uint32_t bit = 1u << (x & 31);
+    if (!(atomicOr(&bm[x >> 5], bit) & bit)) return;
+  }
+  meta->err = 2;   // n too close to valid (cannot happen for n <= valid/2 in practice)
+}
+
+// inclusive scan of v over the 256-thread workgroup; returns the exclusive
+// prefix and writes the workgroup total to *tot
+__device__ __forceinline__ int block_scan_256(int v, int* tot) {
+  __shared__ int wsum[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  int base = 0;
+  for (int i = 0; i < w; ++i) base += wsum[i];
+  *tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  __syncthreads();
+  return base + x - v;
+}
+
+// 4 bitmap words per thread, 1024 per workgroup
+__device__ __forceinline__ uint4 bm_words(const uint32_t* bm, int64_t nwords, int64_t w0) {
+  uint4 q = make_uint4(0, 0, 0, 0);
+  if (w0 + 3 < nwords) {
+    q = *reinterpret_cast<const uint4*>(bm + w0);
+  } else {
+    if (w0 < nwords) q.x = bm[w0];
+    if (w0 + 1 < nwords) q.y = bm[w0 + 1];
+    if (w0 + 2 < nwords) q.z = bm[w0 + 2];
+  }
+  return q;
+}
+
+__global__ __launch_bounds__(256) void bm_count_kernel(const uint32_t* __restrict__ bm,
+                                                       int64_t nwords, int32_t* __restrict__ tot) {
+  const int64_t w0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  const uint4 q = bm_words(bm, nwords, w0);
+  const int c = __popc(q.x) + __popc(q.y) + __popc(q.z) + __popc(q.w);
+  int t;
+  block_scan_256(c, &t);
+  if (threadIdx.x == 0) tot[blockIdx.x] = t;
+}
+
+// exclusive scan of the per-workgroup counts (one workgroup, any length)
+__global__ __launch_bounds__(256) void bm_scan_kernel(int32_t* __restrict__ tot, int nblk) {
+  int carry = 0;
+  for (int b0 = 0; b0 < nblk; b0 += 256) {
+    const int i = b0 + threadIdx.x;
+    const int v = i < nblk ? tot[i] : 0;
+    int t;
+    const int ex = block_scan_256(v, &t);
+    if (i < nblk) tot[i] = carry + ex;
+    carry += t;
+  }
+}
+
+__global__ __launch_bounds__(256) void bm_emit_kernel(const uint32_t* __restrict__ bm,
+                                                      int64_t nwords,
+                                                      const int32_t* __restrict__ off,
+                                                      int32_t* __restrict__ idx, int n) {
+  const int64_t w0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  const uint4 q = bm_words(bm, nwords, w0);
+  const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+  int t;
+  int pos = off[blockIdx.x] +
+            block_scan_256(__popc(w[0]) + __popc(w[1]) + __popc(w[2]) + __popc(w[3]), &t);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t v = w[k];
+    while (v) {
+      const int b = __ffs(v) - 1;
+      if (pos < n) idx[pos] = (int32_t)((w0 + k) * 32 + b);
+      ++pos;
+      v &= v - 1;
+    }
+  }
+}
+
+// u8 (C,H,W) slots -> f32 Caffe (n,4,S,S).  A workgroup converts 1024
+// consecutive 4-byte words of the output's u8 image: 4 independent dword
+// loads per thread at stride 256 (each wave instruction reads 256 contiguous
+// bytes) and 4 float4 non-temporal stores (each wave instruction writes 1 KiB
+// contiguous).  blockIdx.y = 0: state from idx, 1: next_state from idx+1
+// (N-1 wraps to 0; only the last sorted index can, replay.py:160-166) plus
+// one-hot action, reward, non_terminal of idx+1.
+__global__ __launch_bounds__(256) void gather_nchw_kernel(
+    const uint8_t* __restrict__ st, const uint8_t* __restrict__ act,
+    const int16_t* __restrict__ rew, const uint8_t* __restrict__ nt, ReplayMeta* meta,
+    const int32_t* __restrict__ idx, int n, FastDiv wps, float* __restrict__ s0,
+    float* __restrict__ s1, float* __restrict__ action, float* __restrict__ reward,
+    float* __restrict__ nonterm) {
+  typedef float fv4 __attribute__((ext_vector_type(4)));
+  const int z = blockIdx.y;
+  const int64_t N = meta->capacity;
+  const uint64_t total = (uint64_t)n * wps.d;
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(st);
+  fv4* dst = reinterpret_cast<fv4*>(z ? s1 : s0);
+  uint32_t v[4];
+  uint64_t g[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    g[k] = (uint64_t)blockIdx.x * 1024 + k * 256 + threadIdx.x;
+    v[k] = 0;
+    if (g[k] < total) {
+      uint32_t b, q;
+      wps.divmod((uint32_t)g[k], b, q);
+      const int64_t i = idx[b];
+      const int64_t slot = z ? ((i + 1 == N) ? 0 : i + 1) : i;
+      v[k] = src[(uint64_t)slot * wps.d + q];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (g[k] < total) {
+      const fv4 f = {(float)(v[k] & 255), (float)((v[k] >> 8) & 255),
+                     (float)((v[k] >> 16) & 255), (float)(v[k] >> 24)};
+      __builtin_nontemporal_store(f, dst + g[k]);
+    }
+  }
+  if (z == 1) {
+    const uint32_t b = blockIdx.x * 256 + threadIdx.x;   // first blocks: per-row scalars
+    if ((int)b < n) {
+      const int64_t i = idx[b];
+      const int64_t nxt = (i + 1 == N) ? 0 : i + 1;
+      const int a = act[nxt];
+      if (a >= kActions) meta->err = 1;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) action[(size_t)b * 4 + k] = (k == a) ? 1.f : 0.f;
+      reward[b] = (float)rew[nxt];
+      nonterm[b] = nt[nxt] ? 1.f : 0.f;
+    }
+  }
+}
+
+hipError_t launch_sample_batch(ReplayMeta* meta, int64_t valid, int n, uint64_t seed,
+                               uint64_t ctr, uint32_t* bm, int32_t* blk, int32_t* idx,
+                               hipStream_t s) {
+  const int64_t nwords = (valid + 31) / 32;
+  const int nblk = (int)((nwords + 1023) / 1024);
+  CHECK_LAUNCH(hipMemsetAsync(bm, 0, (size_t)nblk * 1024 * 4, s));
+  hipLaunchKernelGGL(claim_kernel, dim3((n + 255) / 256), dim3(256), 0, s, meta, n, seed, ctr, bm);
+  hipLaunchKernelGGL(bm_count_kernel, dim3(nblk), dim3(256), 0, s, bm, nwords, blk);
+  hipLaunchKernelGGL(bm_scan_kernel, dim3(1), dim3(256), 0, s, blk, nblk);
+  hipLaunchKernelGGL(bm_emit_kernel, dim3(nblk), dim3(256), 0, s, bm, nwords, blk, idx, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_nchw(const uint8_t* st, const uint8_t* act, const int16_t* rew,
+                              const uint8_t* nt, ReplayMeta* meta, const int32_t* idx, int n,
+                              int S, float* s0, float* s1, float* action, float* reward,
+                              float* nonterm, hipStream_t s) {
+  const uint32_t wps = (uint32_t)(S * S);          // 4-byte words per slot
+  const uint64_t tot = (uint64_t)n * wps;           // < 2^31 (n <= 2^31 / S^2 checked)
+  const uint64_t blocks = std::max<uint64_t>((tot + 1023) / 1024, (uint64_t)(n + 255) / 256);
+  hipLaunchKernelGGL(gather_nchw_kernel, dim3((uint32_t)blocks, 2), dim3(256), 0, s, st, act,
+                     rew, nt, meta, idx, n, FastDiv(wps), s0, s1, action, reward, nonterm);
+  return hipGetLastError();
+}
+
+// on-device tiling of a transition pool over the ring (1M-slot C5 fills)
+__global__ __launch_bounds__(256) void tile_kernel(uint8_t* __restrict__ dst,
+                                                   const uint8_t* __restrict__ src,
+                                                   uint64_t pool_bytes, uint64_t total) {
+  for (uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 16; i < total;
+       i += (uint64_t)gridDim.x * 256 * 16) {
+    const uint64_t j = i % pool_bytes;
+    *reinterpret_cast<uint4*>(dst + i) = *reinterpret_cast<const uint4*>(src + j);
+  }
+}
+
+hipError_t launch_tile(uint8_t* dst, const uint8_t* src, uint64_t pool_bytes, uint64_t total,
+                       hipStream_t s) {
+  hipLaunchKernelGGL(tile_kernel, dim3(4096), dim3(256), 0, s, dst, src, pool_bytes, total);
   return hipGetLastError();
 }
 
@@ -691,11 +908,6 @@ int wgrad_splits_for(int layer, int B, int S, int* np, int impl) {
   return ns;
 }
 
-#define CHECK_LAUNCH(x)                         \
-  do {                                          \
-    hipError_t e_ = (x);                        \
-    if (e_ != hipSuccess) return e_;            \
-  } while (0)
 
 static DirectArgs direct_fwd_args(const float* const in[2], const float* const wk[2],
                                   const float* const bias[2], float* const out[2],

@@ -59,6 +59,7 @@ _SIGS = {
     "ddq_last_error": (ctypes.c_char_p, [_P]),
     "ddq_set_stream": (ctypes.c_int, [_P, _P]),
     "ddq_synchronize": (ctypes.c_int, [_P]),
+    "ddq_get_stream": (ctypes.c_int, [_P, ctypes.POINTER(_P)]),
     "ddq_num_params": (_i64, [_P]),
     "ddq_param_layout": (ctypes.c_int, [_P, ctypes.POINTER(BlobDesc), _i32, ctypes.POINTER(_i32)]),
     "ddq_set_params": (ctypes.c_int, [_P, _i32, _P, _i64, _i32]),
@@ -77,6 +78,10 @@ _SIGS = {
     "ddq_read_minibatch": (ctypes.c_int, [_P, _P, _P, _P, _P, _P]),
     "ddq_write_minibatch": (ctypes.c_int, [_P, _P, _P, _P, _P, _P]),
     "ddq_read_indices": (ctypes.c_int, [_P, _P, _i32]),
+    "ddq_replay_fill_tiled": (ctypes.c_int, [_P, _P, _P, _P, _P, _i64, _i64, _i64]),
+    "ddq_replay_sample_batch_async": (ctypes.c_int, [_P, _i32, _u64, _P, _P, _P, _P, _P, _P]),
+    "ddq_replay_gather_batch_async": (ctypes.c_int, [_P, _P, _i32, _P, _P, _P, _P, _P]),
+    "ddq_replay_status": (ctypes.c_int, [_P]),
     "ddq_forward_backward": (ctypes.c_int, [_P, _fp]),
     "ddq_forward_backward_async": (ctypes.c_int, [_P]),
     "ddq_forward_q": (ctypes.c_int, [_P]),

@@ -66,6 +66,12 @@ class DeepQNet:
         self._check(self.lib.ddq_synchronize(self.ctx))
 
     # ------------------------------------------------------------- parameters
+    def stream(self):
+        """The ctx's HIP stream handle (int), e.g. for torch.cuda.ExternalStream."""
+        h = ctypes.c_void_p()
+        self._check(self.lib.ddq_get_stream(self.ctx, ctypes.byref(h)))
+        return int(h.value or 0)
+
     def set_flat(self, which, flat):
         flat = np.ascontiguousarray(flat, np.float32).ravel()
         self._check(self.lib.ddq_set_params(self.ctx, which, ptr(flat), flat.size, 0))
@@ -251,6 +257,47 @@ class DeepQNet:
 
     def replay_sample_device(self, seed):
         self._check(self.lib.ddq_replay_sample_device_async(self.ctx, int(seed)))
+
+    def replay_fill_tiled(self, state, action, reward, non_terminal, head, valid):
+        """Tile a pool of transitions over the whole ring on the device."""
+        st = np.ascontiguousarray(state, np.uint8)
+        ac = np.ascontiguousarray(action, np.uint8)
+        rw = np.ascontiguousarray(reward, np.int16)
+        nt = np.ascontiguousarray(non_terminal, np.uint8)
+        self._check(self.lib.ddq_replay_fill_tiled(self.ctx, ptr(st), ptr(ac), ptr(rw), ptr(nt),
+                                                   ac.size, int(head), int(valid)))
+
+    def batch_buffers(self, n):
+        """Device (torch) output buffers for replay_sample_batch (Caffe shapes)."""
+        import torch
+        dev = torch.device("cuda", self.device)
+        S = self.frame
+        f = dict(dtype=torch.float32, device=dev)
+        return {"idx": torch.empty(n, dtype=torch.int32, device=dev),
+                "state": torch.empty((n, NFRAME, S, S), **f),
+                "action": torch.empty((n, NUM_ACTIONS, 1, 1), **f),
+                "reward": torch.empty((n, 1, 1, 1), **f),
+                "next_state": torch.empty((n, NFRAME, S, S), **f),
+                "non_terminal": torch.empty((n, 1, 1, 1), **f)}
+
+    def replay_sample_batch(self, bufs, seed, check=True):
+        """Large-batch device draw + gather into ``bufs`` (batch_buffers)."""
+        n = bufs["idx"].numel()
+        p = [bufs[k].data_ptr() for k in ("idx", "state", "action", "reward", "next_state",
+                                         "non_terminal")]
+        self._check(self.lib.ddq_replay_sample_batch_async(self.ctx, n, int(seed), *p))
+        if check:
+            self._check(self.lib.ddq_replay_status(self.ctx))
+
+    def replay_gather_batch(self, bufs, check=True):
+        """Caffe-layout gather of the sorted indices already in bufs['idx']."""
+        n = bufs["idx"].numel()
+        p = [bufs[k].data_ptr() for k in ("state", "action", "reward", "next_state",
+                                         "non_terminal")]
+        self._check(self.lib.ddq_replay_gather_batch_async(self.ctx, bufs["idx"].data_ptr(), n,
+                                                           *p))
+        if check:
+            self._check(self.lib.ddq_replay_status(self.ctx))
 
     def read_indices(self):
         out = np.empty(self.batch, np.int32)

@@ -106,6 +106,8 @@ const char* ddq_last_error(const ddq_ctx* ctx);
 int ddq_abi_version(void);
 /* Use an external HIP stream (e.g. torch.cuda.current_stream().cuda_stream). */
 int ddq_set_stream(ddq_ctx* ctx, void* hip_stream);
+/* The ctx's HIP stream (e.g. for torch.cuda.ExternalStream events). */
+int ddq_get_stream(const ddq_ctx* ctx, void** hip_stream);
 int ddq_synchronize(ddq_ctx* ctx);
 
 /* ---------------- parameters ------------------------------------------- */
@@ -151,6 +153,29 @@ int ddq_read_minibatch(ddq_ctx* ctx, float* state, float* action, float* reward,
 int ddq_write_minibatch(ddq_ctx* ctx, const float* state, const float* action,
                         const float* reward, const float* next_state,
                         const float* non_terminal);
+/* Fill the whole ring by tiling `pool` transitions (slot i <- pool entry
+ * i % pool) on the device, then set head/valid: the 1M-slot HBM replay of
+ * SURVEY 8(d) C5 without a 16 GB host image.  Host arrays of `pool` entries. */
+int ddq_replay_fill_tiled(ddq_ctx* ctx, const uint8_t* state, const uint8_t* action,
+                          const int16_t* reward, const uint8_t* non_terminal, int64_t pool,
+                          int64_t head, int64_t valid);
+/* Large-batch sample_direct (replay.py:144-183) for n <= valid/2 (any n, not
+ * tied to the net batch): device draw of n distinct indices uniform over
+ * [0,valid) \ {head-1}, sorted, written to idx; then s <- S[idx],
+ * s' <- S[idx+1] (N-1 wraps to 0) as f32 (n,4,S,S), one-hot action (n,4),
+ * reward (n), non_terminal (n) of idx+1.  ALL pointers are device pointers
+ * (e.g. torch tensors).  The first call allocates the sampler's bitmap
+ * (capacity/8 bytes).  Enqueued, no sync; ddq_replay_status reports a
+ * stored action >= 4 or a failed draw. */
+int ddq_replay_sample_batch_async(ddq_ctx* ctx, int32_t n, uint64_t seed, int32_t* idx,
+                                  float* state, float* action, float* reward,
+                                  float* next_state, float* non_terminal);
+/* The same Caffe-layout gather for a caller-given sorted index list (device). */
+int ddq_replay_gather_batch_async(ddq_ctx* ctx, const int32_t* idx, int32_t n, float* state,
+                                  float* action, float* reward, float* next_state,
+                                  float* non_terminal);
+/* Synchronise and report (then clear) the replay's sticky device error flag. */
+int ddq_replay_status(ddq_ctx* ctx);
 /* Last sorted index list used by the gather (device -> host). */
 int ddq_read_indices(ddq_ctx* ctx, int32_t* idx, int32_t batch);
 

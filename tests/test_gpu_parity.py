@@ -131,7 +131,8 @@ def make_inputs(rng, B, S, frames="uniform"):
 @pytest.mark.parametrize("impl", ["direct", "gemm"])
 @pytest.mark.parametrize("S,B,frames", [(16, 32, "uniform"), (16, 32, "snake"),
                                         (24, 8, "uniform"), (40, 4, "snake"),
-                                        (64, 32, "uniform")])
+                                        (64, 32, "uniform"), (16, 256, "snake"),
+                                        (128, 2, "uniform")])
 def test_full_pass_parity(ddq, ref, S, B, frames, impl, monkeypatch):
     monkeypatch.setenv("DDQ_CONV_IMPL", impl)
     rng = np.random.default_rng(100 + S + B)
