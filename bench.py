@@ -248,6 +248,10 @@ def main():
     ap.add_argument("--sweep", action="store_true",
                     help="C3: also run the batch-256 frame-size sweep 16..128 (slow)")
     ap.add_argument("--eager", action="store_true", help="no hipGraph (debug)")
+    ap.add_argument("--exchange", default="allreduce", choices=["allreduce", "sharded", "server"],
+                    help="N>1 gradient exchange (include/ddq_hip.h enum ddq_exchange)")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="allreduce: do not reduce the fc4 bucket under the conv backward")
     ap.add_argument("--pipeline", action="store_true",
                     help="prefetch the next minibatch on a side stream (slower on MI355X: "
                          "the cross-stream graph edges cost more than the overlap)")
@@ -270,8 +274,9 @@ def main():
     fill_replay(net, args.replay, S, seed=1000 + rank)
     if world > 1:
         ddist.setup_comm(net, rank, world)
-    cfg = net.step_cfg(args.rule, lr=1e-4, target_period=10, allreduce=world > 1,
-                       seed=ddist.index_seed(1234, rank))
+    cfg = net.step_cfg(args.rule, lr=1e-4, target_period=10,
+                       exchange=args.exchange if world > 1 else "none",
+                       overlap=not args.no_overlap, seed=ddist.index_seed(1234, rank))
 
     def run(k):
         if args.eager:
@@ -326,6 +331,9 @@ def main():
                                    % (S, S, args.replay, args.rule),
                        "global_batch": B * world, "frame": S,
                        "parallelism": "dp%d" % world, "graph": not args.eager,
+                       "exchange": (args.exchange + ("" if args.no_overlap or
+                                                     args.exchange != "allreduce"
+                                                     else "+overlap")) if world > 1 else "none",
                        "pipelined": bool(args.pipeline and not args.eager)},
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3),
                          "peak": F32_MFMA_PEAK / 1e12, "unit": "TFLOP/s",

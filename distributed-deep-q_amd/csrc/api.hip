@@ -22,6 +22,9 @@ using namespace ddq;
 
 static thread_local std::string g_last_error;
 
+static constexpr int kMaxRanks = 64;
+static constexpr int64_t kShardPad = 64 * kMaxRanks;
+
 struct ddq_ctx {
   int device = 0;
   ddq_net_desc desc{};
@@ -45,9 +48,16 @@ struct ddq_ctx {
   float *act_in = nullptr, *act_p1 = nullptr, *act_p2 = nullptr, *act_p3 = nullptr;
   float *act_h4 = nullptr, *act_part = nullptr, *act_q = nullptr;
   int32_t* act_out = nullptr;
-  // comm
+  // comm (RCCL ranks, or an in-process group of ctxs exchanging by device copies)
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
+  bool local = false;              // member of an in-process group (ddq_group_init)
+  hipStream_t cs = nullptr;        // comm stream of the overlapped all-reduce
+  hipEvent_t cev[2] = {};
+  int64_t shard_len = 0;           // parameters owned per rank (multiple of 64)
+  float* gsl = nullptr;            // [W][shard_len] received gradient slices
+  float* gstage = nullptr;         // [W][P] in-process all-reduce staging
+  std::string comm_err;
   // graph
   hipGraph_t graph = nullptr;
   hipGraphExec_t gexec = nullptr;     // one step
@@ -202,7 +212,7 @@ int ddq_create(ddq_ctx** out, int device, const ddq_net_desc* desc) {
       TRY(dalloc(c, &nb.pool2[z], (size_t)B * S3 * S3 * 64));
       TRY(dalloc(c, &nb.pool3[z], (size_t)B * S4 * S4 * 64));
       TRY(dalloc(c, &nb.h4[z], (size_t)B * 512));
-      TRY(dalloc(c, &nb.theta[z], (size_t)P));
+      TRY(dalloc(c, &nb.theta[z], (size_t)P + kShardPad));
       TRY(dalloc(c, &nb.wk[z], (size_t)nb.L.wk_total));
     }
     TRY(dalloc(c, &nb.mask1, (size_t)B * S2 * S2 * 32));
@@ -230,8 +240,11 @@ int ddq_create(ddq_ctx** out, int device, const ddq_net_desc* desc) {
       off += (int64_t)nb.wsplits[l] * cout[l] * nb.wnp[l];
     }
     TRY(dalloc(c, &nb.wpart, (size_t)off));
-    TRY(dalloc(c, &nb.grad, (size_t)P));
-    TRY(dalloc(c, &nb.opt, (size_t)P));
+    // zero tails of kShardPad floats: W equal shards of a multiple of 64
+    // floats cover P for every W <= kMaxRanks
+    TRY(dalloc(c, &nb.grad, (size_t)P + kShardPad));
+    TRY(dalloc(c, &nb.opt, (size_t)P + kShardPad));
+    nb.book_inc = 1;
     TRY(dalloc(c, &nb.opt_init, 4));
     TRY(dalloc(c, &nb.iter, 1));
     // acting scratch (n <= B)
@@ -268,6 +281,9 @@ int ddq_destroy(ddq_ctx* c) {
   for (auto& e : c->nb.ev)
     if (e) hipEventDestroy(e);
   if (c->nb.side) hipStreamDestroy(c->nb.side);
+  if (c->cs) hipStreamDestroy(c->cs);
+  for (auto& e : c->cev)
+    if (e) hipEventDestroy(e);
   delete c;
   return DDQ_OK;
 }
@@ -812,16 +828,34 @@ int ddq_comm_get_unique_id(uint8_t id[128]) {
   return DDQ_OK;
 }
 
+// Shard geometry and exchange buffers for W ranks (RCCL or in-process).
+static int setup_shards(ddq_ctx* c, int W) {
+  const int64_t P = c->nb.L.total;
+  c->shard_len = ((P + (int64_t)W * 64 - 1) / ((int64_t)W * 64)) * 64;
+  if (!c->cs) {
+    HIP_TRY(c, hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking));
+    for (auto& e : c->cev) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  // exchange buffers are allocated once for the largest W (kMaxRanks slices
+  // of at most P/W + 64 floats fit in P + kShardPad ... per slice set)
+  if (!c->gsl) TRY(dalloc(c, &c->gsl, (size_t)P + kShardPad));
+  return DDQ_OK;
+}
+
 int ddq_comm_init(ddq_ctx* c, const uint8_t id[128], int32_t nranks, int32_t rank) {
   if (!c || !id) return fail(c, DDQ_EINVAL, "null argument");
-  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(c, DDQ_EINVAL, "bad rank/nranks");
+  if (nranks < 1 || nranks > kMaxRanks || rank < 0 || rank >= nranks)
+    return fail(c, DDQ_EINVAL, "bad rank/nranks (nranks <= %d)", kMaxRanks);
+  if (c->local) return fail(c, DDQ_ESTATE, "ctx belongs to an in-process group");
   TRY(set_dev(c));
   if (c->comm) ncclCommDestroy(c->comm);
+  c->comm = nullptr;
   ncclUniqueId u;
   memcpy(&u, id, 128);
   NCCL_TRY(c, ncclCommInitRank(&c->comm, nranks, u, rank));
   c->nranks = nranks;
   c->rank = rank;
+  TRY(setup_shards(c, nranks));
   invalidate_graph(c);
   return DDQ_OK;
 }
@@ -842,14 +876,115 @@ int ddq_allreduce_grads(ddq_ctx* c) {
 }
 
 // ---------------- step ----------------
-// fwd/bwd -> [all-reduce] -> apply on the minibatch held by `nb`; when
-// `pre` is given, the NEXT step's sample + gather into `pre`'s minibatch
-// set run on the side stream under this step's forward (the replay ring is
-// not written inside a step, and the device RNG counter advances in the
-// same order, so the index stream equals the sequential one).
-static int enqueue_train(ddq_ctx* c, const ddq_step_cfg* cfg, const NetBuffers& nb,
+static bool has_exchange(const ddq_ctx* c, const ddq_step_cfg* cfg) {
+  return cfg->exchange != DDQ_EXCHANGE_NONE && (c->comm != nullptr || c->local);
+}
+// param-server iterations one step consumes (server.py:200 INCR per gradient)
+static int step_inc(const ddq_ctx* c, const ddq_step_cfg* cfg) {
+  return (has_exchange(c, cfg) && cfg->exchange == DDQ_EXCHANGE_SERVER) ? c->nranks : 1;
+}
+
+// Overlapped all-reduce, part 1 (called by launch_backward right after the
+// fc4 weight-gradient kernel): the comm stream sums the fc4 weight bucket
+// (2.1 M of the 2.2 M parameters at 64x64) while the conv backward runs.
+static hipError_t fc4_bucket_start(void* arg) {
+  ddq_ctx* c = reinterpret_cast<ddq_ctx*>(arg);
+  const ParamLayout& L = c->nb.L;
+  hipError_t e = hipEventRecord(c->cev[0], c->stream);
+  if (e == hipSuccess) e = hipStreamWaitEvent(c->cs, c->cev[0], 0);
+  if (e != hipSuccess) return e;
+  ncclResult_t r = ncclAllReduce(c->nb.grad + L.w[3], c->nb.grad + L.w[3], (size_t)L.wn[3],
+                                 ncclFloat, ncclSum, c->comm, c->cs);
+  if (r != ncclSuccess) {
+    c->comm_err = ncclGetErrorString(r);
+    return hipErrorUnknown;
+  }
+  return hipSuccess;
+}
+
+static int enqueue_fwd_bwd_x(ddq_ctx* c, const NetBuffers& nb, void (*mark)(void*, const char*),
+                             void* marg, int book, ReplayMeta* bump, bool overlap) {
+  HIP_TRY(c, launch_forward(nb, 2, c->stream, mark, marg, false));
+  if (mark) mark(marg, "head");
+  HIP_TRY(c, launch_head(nb, c->stream));
+  hipError_t e = launch_backward(nb, c->stream, mark, marg, mark == nullptr && (nb.variant & 16),
+                                 book >= 0, book, bump, overlap ? fc4_bucket_start : nullptr, c);
+  if (e != hipSuccess && !c->comm_err.empty()) {
+    std::string m = c->comm_err;
+    c->comm_err.clear();
+    return fail(c, DDQ_ERCCL, "overlapped all-reduce: %s", m.c_str());
+  }
+  HIP_TRY(c, e);
+  return DDQ_OK;
+}
+
+// Gradient exchange + apply of one step over RCCL (graph-capturable):
+//  ALLREDUCE  sum all-reduce, replicated apply (overlap: fc4 bucket on the
+//             comm stream under the conv backward, the rest -- conv layers,
+//             fc4 bias, Q_out -- as one grouped call after the slab reduce);
+//  SHARDED    reduce-scatter(sum) -> owner apply of its 1/W shard ->
+//             in-place all-gather of theta -> conv layouts / P <- Q refresh;
+//  SERVER     all-to-all of gradient slices -> owner applies the W gradients
+//             one by one in rank order (server.py:196-209 on arrival) ->
+//             all-gather -> refresh.
+static int enqueue_exchange_apply(ddq_ctx* c, const ddq_step_cfg* cfg, const NetBuffers& nb,
+                                  void (*mark)(void*, const char*), void* marg, bool overlap) {
+  const ddq_update_cfg& u = cfg->update;
+  const ParamLayout& L = nb.L;
+  const int ex = has_exchange(c, cfg) ? cfg->exchange : DDQ_EXCHANGE_NONE;
+  if (ex == DDQ_EXCHANGE_NONE || ex == DDQ_EXCHANGE_ALLREDUCE) {
+    if (ex == DDQ_EXCHANGE_ALLREDUCE) {
+      if (mark) mark(marg, "allreduce");
+      if (overlap) {
+        HIP_TRY(c, hipEventRecord(c->cev[0], c->stream));
+        HIP_TRY(c, hipStreamWaitEvent(c->cs, c->cev[0], 0));
+        NCCL_TRY(c, ncclGroupStart());
+        NCCL_TRY(c, ncclAllReduce(nb.grad, nb.grad, (size_t)L.w[3], ncclFloat, ncclSum, c->comm,
+                                  c->cs));
+        NCCL_TRY(c, ncclAllReduce(nb.grad + L.b[3], nb.grad + L.b[3], (size_t)(L.total - L.b[3]),
+                                  ncclFloat, ncclSum, c->comm, c->cs));
+        NCCL_TRY(c, ncclGroupEnd());
+        HIP_TRY(c, hipEventRecord(c->cev[1], c->cs));
+        HIP_TRY(c, hipStreamWaitEvent(c->stream, c->cev[1], 0));
+      } else {
+        NCCL_TRY(c, ncclAllReduce(nb.grad, nb.grad, (size_t)L.total, ncclFloat, ncclSum, c->comm,
+                                  c->stream));
+      }
+    }
+    if (mark) mark(marg, "apply");
+    HIP_TRY(c, launch_apply(nb, u.rule, u.lr, u.decay, u.eps, u.momentum, u.weight_decay,
+                            cfg->target_period, true, c->stream));
+    return DDQ_OK;
+  }
+  const int W = c->nranks;
+  const size_t len = (size_t)c->shard_len;
+  if (mark) mark(marg, ex == DDQ_EXCHANGE_SHARDED ? "reduce_scatter" : "all_to_all");
+  if (ex == DDQ_EXCHANGE_SHARDED)
+    NCCL_TRY(c, ncclReduceScatter(nb.grad, c->gsl, len, ncclFloat, ncclSum, c->comm, c->stream));
+  else
+    NCCL_TRY(c, ncclAllToAll(nb.grad, c->gsl, len, ncclFloat, c->comm, c->stream));
+  if (mark) mark(marg, "apply_shard");
+  HIP_TRY(c, launch_apply_shard(nb, u.rule, u.lr, u.decay, u.eps, u.momentum, u.weight_decay,
+                                c->gsl, (int64_t)c->rank * len, (int64_t)len, (int64_t)len,
+                                ex == DDQ_EXCHANGE_SHARDED ? 1 : W, c->stream));
+  if (mark) mark(marg, "all_gather");
+  NCCL_TRY(c, ncclAllGather(nb.theta[0] + (size_t)c->rank * len, nb.theta[0], len, ncclFloat,
+                            c->comm, c->stream));
+  if (mark) mark(marg, "refresh");
+  HIP_TRY(c, launch_refresh(nb, c->stream));
+  return DDQ_OK;
+}
+
+// fwd/bwd -> exchange -> apply on the minibatch held by `nb`; when `pre` is
+// given, the NEXT step's sample + gather into `pre`'s minibatch set run on
+// the side stream under this step's forward (the replay ring is not written
+// inside a step, and the device RNG counter advances in the same order, so
+// the index stream equals the sequential one).
+static int enqueue_train(ddq_ctx* c, const ddq_step_cfg* cfg, const NetBuffers& nb_in,
                          const NetBuffers* pre, void (*mark)(void*, const char*), void* marg,
                          ReplayMeta* bump = nullptr) {
+  NetBuffers nb = nb_in;
+  nb.book_inc = step_inc(c, cfg);
   if (pre) {
     HIP_TRY(c, hipEventRecord(nb.ev[6], c->stream));
     HIP_TRY(c, hipStreamWaitEvent(nb.side, nb.ev[6], 0));
@@ -858,16 +993,11 @@ static int enqueue_train(ddq_ctx* c, const ddq_step_cfg* cfg, const NetBuffers& 
                              nb.side));
     HIP_TRY(c, hipEventRecord(nb.ev[7], nb.side));
   }
-  TRY(enqueue_fwd_bwd(c, nb, mark, marg, cfg->target_period > 0 ? cfg->target_period : 0, bump));
-  if (cfg->allreduce && c->nranks > 1) {
-    if (mark) mark(marg, "allreduce");
-    NCCL_TRY(c, ncclAllReduce(nb.grad, nb.grad, (size_t)nb.L.total, ncclFloat, ncclSum, c->comm,
-                              c->stream));
-  }
-  if (mark) mark(marg, "apply");
-  const ddq_update_cfg& u = cfg->update;
-  HIP_TRY(c, launch_apply(nb, u.rule, u.lr, u.decay, u.eps, u.momentum, u.weight_decay,
-                          cfg->target_period, true, c->stream));
+  const bool overlap = has_exchange(c, cfg) && cfg->exchange == DDQ_EXCHANGE_ALLREDUCE &&
+                       cfg->overlap && c->comm && mark == nullptr;
+  TRY(enqueue_fwd_bwd_x(c, nb, mark, marg, cfg->target_period > 0 ? cfg->target_period : 0, bump,
+                        overlap));
+  TRY(enqueue_exchange_apply(c, cfg, nb, mark, marg, overlap));
   if (pre) HIP_TRY(c, hipStreamWaitEvent(c->stream, nb.ev[7], 0));
   return DDQ_OK;
 }
@@ -918,7 +1048,10 @@ static int check_step(ddq_ctx* c, const ddq_step_cfg* cfg) {
   if (c->nb.B >= c->valid)
     return fail(c, DDQ_EINVAL, "Can't draw sample of size %d from replay dataset of size %lld",
                 c->nb.B, (long long)c->valid);
-  if (cfg->allreduce && c->nranks > 1 && !c->comm) return fail(c, DDQ_ESTATE, "no communicator");
+  if (cfg->exchange < DDQ_EXCHANGE_NONE || cfg->exchange > DDQ_EXCHANGE_SERVER)
+    return fail(c, DDQ_EINVAL, "unknown exchange %d", cfg->exchange);
+  if (cfg->exchange != DDQ_EXCHANGE_NONE && c->nranks > 1 && !c->comm && !c->local)
+    return fail(c, DDQ_ESTATE, "no communicator");
   return DDQ_OK;
 }
 
@@ -928,7 +1061,7 @@ int ddq_step_async(ddq_ctx* c, const ddq_step_cfg* cfg) {
   if (c->steps == 0) TRY(initial_target_sync(c, cfg));
   TRY(enqueue_step(c, cfg, nullptr, nullptr));
   c->steps++;
-  c->applied++;
+  c->applied += step_inc(c, cfg);
   return DDQ_OK;
 }
 
@@ -968,7 +1101,7 @@ int ddq_step_graph_async(ddq_ctx* c, const ddq_step_cfg* cfg, int32_t nsteps) {
     HIP_TRY(c, hipGraphLaunch(c->gexec_k, c->stream));
   for (; i < nsteps; ++i) HIP_TRY(c, hipGraphLaunch(c->gexec, c->stream));
   c->steps += nsteps;
-  c->applied += nsteps;
+  c->applied += (int64_t)nsteps * step_inc(c, cfg);
   return DDQ_OK;
 }
 
@@ -1017,10 +1150,153 @@ int ddq_step_pipelined_async(ddq_ctx* c, const ddq_step_cfg* cfg, int32_t nsteps
   for (int i = 0; i < nsteps; ++i) {
     HIP_TRY(c, hipGraphLaunch(c->pexec[p][i + 1 < nsteps ? 1 : 0], c->stream));
     c->steps++;
-    c->applied++;
+    c->applied += step_inc(c, cfg);
     p ^= 1;
   }
   return DDQ_OK;
+}
+
+// ---------------- in-process groups ----------------
+int ddq_group_init(ddq_ctx** ctxs, int32_t W) {
+  if (!ctxs || W < 1 || W > kMaxRanks) return fail(nullptr, DDQ_EINVAL, "bad group");
+  for (int r = 0; r < W; ++r) {
+    ddq_ctx* c = ctxs[r];
+    if (!c) return fail(nullptr, DDQ_EINVAL, "null ctx in group");
+    if (c->comm) return fail(c, DDQ_ESTATE, "ctx already has an RCCL communicator");
+    if (c->nb.S != ctxs[0]->nb.S || c->nb.B != ctxs[0]->nb.B)
+      return fail(c, DDQ_EINVAL, "group members must share batch and frame");
+  }
+  for (int r = 0; r < W; ++r) {
+    ddq_ctx* c = ctxs[r];
+    TRY(set_dev(c));
+    c->local = true;
+    c->nranks = W;
+    c->rank = r;
+    TRY(setup_shards(c, W));
+    if (!c->gstage) TRY(dalloc(c, &c->gstage, (size_t)W * (c->nb.L.total + kShardPad)));
+    invalidate_graph(c);
+  }
+  return DDQ_OK;
+}
+
+// One synchronous data-parallel step of an in-process group: the same
+// kernels and exchange semantics as RCCL ranks, with the collectives done as
+// device copies between the members' buffers, phase by phase.
+int ddq_group_step(ddq_ctx** ctxs, int32_t W, const ddq_step_cfg* cfg) {
+  if (!ctxs || !cfg || W < 1) return fail(nullptr, DDQ_EINVAL, "bad argument");
+  for (int r = 0; r < W; ++r) {
+    ddq_ctx* c = ctxs[r];
+    if (!c || !c->local || c->nranks != W || c->rank != r)
+      return fail(c, DDQ_ESTATE, "ctx %d is not rank %d of a %d-member group", r, r, W);
+    TRY(check_step(c, cfg));
+  }
+  const int ex = cfg->exchange;
+  const ddq_update_cfg& u = cfg->update;
+  const int64_t P = ctxs[0]->nb.L.total;
+  std::vector<hipEvent_t> ev(W);
+  auto record_all = [&](void) -> int {
+    for (int r = 0; r < W; ++r) {
+      ddq_ctx* c = ctxs[r];
+      TRY(set_dev(c));
+      if (ev[r] == nullptr) HIP_TRY(c, hipEventCreateWithFlags(&ev[r], hipEventDisableTiming));
+      HIP_TRY(c, hipEventRecord(ev[r], c->stream));
+    }
+    return DDQ_OK;
+  };
+  auto wait_all = [&](ddq_ctx* c) -> int {
+    for (int j = 0; j < W; ++j) HIP_TRY(c, hipStreamWaitEvent(c->stream, ev[j], 0));
+    return DDQ_OK;
+  };
+  int rc = [&]() -> int {
+    // phase 1: sample + gather + forward/backward (+ bookkeeping) per member
+    for (int r = 0; r < W; ++r) {
+      ddq_ctx* c = ctxs[r];
+      TRY(set_dev(c));
+      if (c->steps == 0) TRY(initial_target_sync(c, cfg));
+      NetBuffers nb = c->nb;
+      nb.book_inc = step_inc(c, cfg);
+      ReplayMeta* bump = nullptr;
+      if (nb.B <= 256) {
+        HIP_TRY(c, launch_sample_gather(nb, c->r_state, c->r_action, c->r_reward, c->r_nonterm,
+                                        c->r_meta, cfg->seed, c->stream));
+        bump = c->r_meta;
+      } else {
+        HIP_TRY(c, launch_sample(nb, c->r_meta, cfg->seed, c->stream));
+        HIP_TRY(c, launch_gather(nb, c->r_state, c->r_action, c->r_reward, c->r_nonterm,
+                                 c->r_meta, c->stream));
+      }
+      TRY(enqueue_fwd_bwd_x(c, nb, nullptr, nullptr,
+                            cfg->target_period > 0 ? cfg->target_period : 0, bump, false));
+    }
+    TRY(record_all());
+    // phase 2: exchange + (owner) apply
+    for (int r = 0; r < W; ++r) {
+      ddq_ctx* c = ctxs[r];
+      TRY(set_dev(c));
+      TRY(wait_all(c));
+      const NetBuffers& nb = c->nb;
+      const int64_t len = c->shard_len;
+      if (ex == DDQ_EXCHANGE_NONE) {
+        HIP_TRY(c, launch_apply(nb, u.rule, u.lr, u.decay, u.eps, u.momentum, u.weight_decay,
+                                cfg->target_period, true, c->stream));
+        continue;
+      }
+      if (ex == DDQ_EXCHANGE_ALLREDUCE) {   // gather every gradient first (summed below)
+        for (int j = 0; j < W; ++j)
+          HIP_TRY(c, hipMemcpyAsync(c->gstage + (size_t)j * P, ctxs[j]->nb.grad, P * 4,
+                                    hipMemcpyDeviceToDevice, c->stream));
+        continue;
+      }
+      for (int j = 0; j < W; ++j)
+        HIP_TRY(c, hipMemcpyAsync(c->gsl + (size_t)j * len, ctxs[j]->nb.grad + (size_t)r * len,
+                                  len * 4, hipMemcpyDeviceToDevice, c->stream));
+      int nsl = W;
+      if (ex == DDQ_EXCHANGE_SHARDED) {
+        HIP_TRY(c, launch_sum_slices(c->gsl, c->gsl, W, len, len, c->stream));
+        nsl = 1;
+      }
+      HIP_TRY(c, launch_apply_shard(nb, u.rule, u.lr, u.decay, u.eps, u.momentum, u.weight_decay,
+                                    c->gsl, (int64_t)r * len, len, len, nsl, c->stream));
+    }
+    if (ex == DDQ_EXCHANGE_ALLREDUCE) {
+      TRY(record_all());       // every member holds all W gradients: sum in rank order, apply
+      for (int r = 0; r < W; ++r) {
+        ddq_ctx* c = ctxs[r];
+        TRY(set_dev(c));
+        TRY(wait_all(c));
+        HIP_TRY(c, launch_sum_slices(c->nb.grad, c->gstage, W, P, P, c->stream));
+        HIP_TRY(c, launch_apply(c->nb, u.rule, u.lr, u.decay, u.eps, u.momentum, u.weight_decay,
+                                cfg->target_period, true, c->stream));
+      }
+    }
+    if (ex == DDQ_EXCHANGE_SHARDED || ex == DDQ_EXCHANGE_SERVER) {
+      TRY(record_all());
+      // phase 3: all-gather of the owners' shards + refresh
+      for (int r = 0; r < W; ++r) {
+        ddq_ctx* c = ctxs[r];
+        TRY(set_dev(c));
+        TRY(wait_all(c));
+        const int64_t len = c->shard_len;
+        for (int j = 0; j < W; ++j)
+          if (j != r)
+            HIP_TRY(c, hipMemcpyAsync(c->nb.theta[0] + (size_t)j * len,
+                                      ctxs[j]->nb.theta[0] + (size_t)j * len, len * 4,
+                                      hipMemcpyDeviceToDevice, c->stream));
+        HIP_TRY(c, launch_refresh(c->nb, c->stream));
+      }
+    }
+    for (int r = 0; r < W; ++r) {
+      ddq_ctx* c = ctxs[r];
+      TRY(set_dev(c));
+      HIP_TRY(c, hipStreamSynchronize(c->stream));
+      c->steps++;
+      c->applied += step_inc(c, cfg);
+    }
+    return DDQ_OK;
+  }();
+  for (auto& e : ev)
+    if (e) hipEventDestroy(e);
+  return rc;
 }
 
 int64_t ddq_step_count(const ddq_ctx* c) { return c ? c->steps : -1; }
@@ -1049,7 +1325,7 @@ int ddq_profile_step(ddq_ctx* c, const ddq_step_cfg* cfg, char* names, float* us
   TRY(enqueue_step(c, cfg, mark_cb, c));
   mark_cb(c, "end");
   c->steps++;
-  c->applied++;
+  c->applied += step_inc(c, cfg);
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   const int k = (int)c->marks.size() - 1;
   *n = k;

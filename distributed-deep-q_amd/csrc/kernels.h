@@ -57,6 +57,7 @@ struct NetBuffers {
   float gamma;
   int conv_impl;                    // 0 = implicit-GEMM engine, 1 = direct (patch-in-LDS)
   int variant;                      // tuning experiments (DDQ_VARIANT bits), 0 = default
+  int book_inc;                     // param-server iterations per apply (1, or W: server mode)
 };
 
 // fused device draw + gather for the step (B <= 256); counter advanced by the
@@ -74,11 +75,21 @@ hipError_t launch_head(const NetBuffers& nb, hipStream_t s);
 // concurrent: run the weight-gradient GEMMs on nb.side beside the data-gradient chain.
 hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(void*, const char*),
                            void* mark_arg, bool concurrent, bool book = false, int book_period = 0,
-                           ReplayMeta* bump = nullptr);
+                           ReplayMeta* bump = nullptr, hipError_t (*fc4_done)(void*) = nullptr,
+                           void* fc4_done_arg = nullptr);
 // period > 0: also copy Q -> P when the next pull sees iteration % period == 0.
 hipError_t launch_apply(const NetBuffers& nb, int rule, float lr, float decay, float eps,
                         float momentum, float wd, int period, bool booked, hipStream_t s);
 hipError_t launch_relayout(const NetBuffers& nb, int z, hipStream_t s);
+// owner apply of shard [off, off+len) with W gradient slices (stride `slice`)
+// applied in rank order; then, after the theta all-gather, launch_refresh
+// rebuilds the conv kernel layouts and performs a latched P <- Q sync.
+hipError_t launch_apply_shard(const NetBuffers& nb, int rule, float lr, float decay, float eps,
+                              float momentum, float wd, const float* gsl, int64_t off,
+                              int64_t len, int64_t slice, int W, hipStream_t s);
+hipError_t launch_refresh(const NetBuffers& nb, hipStream_t s);
+hipError_t launch_sum_slices(float* out, const float* in, int W, int64_t len, int64_t slice,
+                             hipStream_t s);
 // Q-tower forward of n states (NHWC f32 in `in`) into scratch, argmax into out.
 hipError_t launch_act(const NetBuffers& nb, const float* in, int n, float* pool1, float* pool2,
                       float* pool3, float* h4, float* part, float* qout, int32_t* actions,

@@ -698,13 +698,15 @@ struct HeadSums {
   float *loss, *gw5, *gb5, *gb4;
 };
 
+// inc: gradients the apply consumes (param-server iterations: 1, or W in
+// the ordered server exchange, server.py:200 INCR per received gradient)
 __device__ __forceinline__ void apply_book(int64_t* iter, int32_t* opt_init, int period,
-                                           ReplayMeta* bump = nullptr) {
+                                           ReplayMeta* bump = nullptr, int inc = 1) {
   if (bump) bump->counter += 1;     // the step's fused draw (sample_gather_kernel)
   const int64_t it = *iter;
   opt_init[2] = (opt_init[0] == 0);
-  opt_init[3] = period > 0 && ((it + 1) % period) == 0;
-  *iter = it + 1;
+  opt_init[3] = period > 0 && ((it + inc) % period) == 0;
+  *iter = it + inc;
   opt_init[0] = 1;
 }
 
@@ -713,10 +715,11 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
                                                            WredDims d1, WredDims d2,
                                                            int64_t* iter, int32_t* opt_init,
                                                            int book_period, ReplayMeta* bump,
-                                                           HeadSums hs) {
+                                                           int book_inc, HeadSums hs) {
   __shared__ float red[4][64];
   const int bid = blockIdx.x;
-  if (opt_init && bid == 0 && threadIdx.x == 0) apply_book(iter, opt_init, book_period, bump);
+  if (opt_init && bid == 0 && threadIdx.x == 0)
+    apply_book(iter, opt_init, book_period, bump, book_inc);
   if (bid >= hs.blk0) {
     head_sums(bid - hs.blk0, hs.B, hs.dqbuf, hs.lpart, hs.h4q, hs.dh4, hs.loss, hs.gw5, hs.gb5,
               hs.gb4);
@@ -838,6 +841,114 @@ __global__ __launch_bounds__(256) void apply_kernel(
 // into the step's wgrad slab reduce or as this one-thread kernel.
 __global__ void apply_book_kernel(int64_t* iter, int32_t* opt_init, int period) {
   apply_book(iter, opt_init, period);
+}
+
+// Owner apply of one parameter shard [off, off+len) (sharded / server
+// exchanges): the W gradient slices gsl[w][0..len) are applied one after the
+// other in rank (ticket) order -- server.py:196-209 applies every received
+// gradient on arrival (apply_descent :49-78) -- with theta and the optimizer
+// state held in registers across the W updates.  Only the first gradient of
+// the first apply takes the rules' first-call branch.  Conv kernel layouts and
+// the P tower are refreshed after the all-gather (refresh_kernel).
+__global__ __launch_bounds__(256) void apply_shard_kernel(
+    float* __restrict__ theta, const float* __restrict__ gsl, float* __restrict__ opt,
+    const int32_t* __restrict__ opt_init, int64_t off, int64_t len, int64_t slice, int W,
+    ApplyArgs a) {
+  const bool first = opt_init[2] != 0;
+  const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (j >= len) return;
+  const int64_t i = off + j;
+  const float4 t4 = *reinterpret_cast<const float4*>(theta + i);
+  float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (a.rule != 0 && !first) s4 = *reinterpret_cast<const float4*>(opt + i);
+  float th[4] = {t4.x, t4.y, t4.z, t4.w};
+  float st[4] = {s4.x, s4.y, s4.z, s4.w};
+  for (int w = 0; w < W; ++w) {
+    const float4 g4 = *reinterpret_cast<const float4*>(gsl + (int64_t)w * slice + j);
+    const float g[4] = {g4.x, g4.y, g4.z, g4.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      th[e] = (i + e < a.n) ? apply_one(a, first && w == 0, i + e, th[e], g[e], st[e]) : 0.f;
+  }
+  *reinterpret_cast<float4*>(theta + i) = make_float4(th[0], th[1], th[2], th[3]);
+  if (a.rule != 0) *reinterpret_cast<float4*>(opt + i) = make_float4(st[0], st[1], st[2], st[3]);
+}
+
+// After the theta all-gather: conv kernel layouts of Q, and P <- Q (weights
+// and kernel layouts) when the step's bookkeeping latched a target sync.
+__global__ __launch_bounds__(256) void refresh_kernel(const float* __restrict__ theta,
+                                                      const int32_t* __restrict__ opt_init,
+                                                      float* __restrict__ wk,
+                                                      float* __restrict__ thetaP,
+                                                      float* __restrict__ wkP, ApplyArgs a) {
+  const bool sync = opt_init[3] != 0;
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i >= a.n || (!sync && i >= a.conv[2].w_off + (int64_t)a.conv[2].cout * a.conv[2].cin * 9))
+    return;
+  const float4 o4 = *reinterpret_cast<const float4*>(theta + i);
+  if (sync) *reinterpret_cast<float4*>(thetaP + i) = o4;
+  const float th[4] = {o4.x, o4.y, o4.z, o4.w};
+#pragma unroll
+  for (int l = 0; l < 3; ++l) {
+    const ConvDims& d = a.conv[l];
+    const int64_t e0 = i - d.w_off;
+    if (e0 >= 0 && e0 < (int64_t)d.cout * d.cin * d.ks * d.ks) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = wk_local(d, (int)e0 + e);
+        wk[d.wk_off + k] = th[e];
+        if (sync) wkP[d.wk_off + k] = th[e];
+      }
+    }
+  }
+}
+
+// out[0..len) = sum_w in[w][0..len) in rank order (in-process group exchange)
+__global__ __launch_bounds__(256) void sum_slices_kernel(float* __restrict__ out,
+                                                         const float* __restrict__ in, int W,
+                                                         int64_t len, int64_t slice) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= len) return;
+  float acc = in[j];
+  for (int w = 1; w < W; ++w) acc += in[(int64_t)w * slice + j];
+  out[j] = acc;
+}
+
+static ApplyArgs apply_args(const NetBuffers& nb, int rule, float lr, float decay, float eps,
+                            float momentum, float wd, int period) {
+  ApplyArgs a;
+  a.n = nb.L.total;
+  a.rule = rule; a.period = period;
+  a.lr = lr; a.decay = decay; a.eps = eps; a.momentum = momentum; a.wd = wd;
+  a.one_minus_decay = (float)(1.0 - (double)decay);
+  for (int l = 0; l < 5; ++l) { a.bias_lo[l] = nb.L.b[l]; a.bias_hi[l] = nb.L.b[l] + nb.L.bn[l]; }
+  conv_dims(nb.L, a.conv);
+  return a;
+}
+
+hipError_t launch_apply_shard(const NetBuffers& nb, int rule, float lr, float decay, float eps,
+                              float momentum, float wd, const float* gsl, int64_t off,
+                              int64_t len, int64_t slice, int W, hipStream_t s) {
+  const ApplyArgs a = apply_args(nb, rule, lr, decay, eps, momentum, wd, 0);
+  const int64_t blocks = (len / 4 + 255) / 256;
+  if (blocks > 0)
+    hipLaunchKernelGGL(apply_shard_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, nb.theta[0],
+                       gsl, nb.opt, nb.opt_init, off, len, slice, W, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_refresh(const NetBuffers& nb, hipStream_t s) {
+  const ApplyArgs a = apply_args(nb, 0, 0.f, 0.f, 0.f, 0.f, 0.f, 0);
+  hipLaunchKernelGGL(refresh_kernel, dim3((uint32_t)((a.n / 4 + 255) / 256)), dim3(256), 0, s,
+                     nb.theta[0], nb.opt_init, nb.wk[0], nb.theta[1], nb.wk[1], a);
+  return hipGetLastError();
+}
+
+hipError_t launch_sum_slices(float* out, const float* in, int W, int64_t len, int64_t slice,
+                             hipStream_t s) {
+  hipLaunchKernelGGL(sum_slices_kernel, dim3((uint32_t)((len + 255) / 256)), dim3(256), 0, s, out,
+                     in, W, len, slice);
+  return hipGetLastError();
 }
 
 hipError_t launch_apply(const NetBuffers& nb, int rule, float lr, float decay, float eps,
@@ -1034,7 +1145,7 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
 
 hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(void*, const char*),
                            void* marg, bool concurrent, bool book, int book_period,
-                           ReplayMeta* bump) {
+                           ReplayMeta* bump, hipError_t (*fc4_done)(void*), void* fc4_done_arg) {
   const ParamLayout& L = nb.L;
   const int B = nb.B, S = nb.S;
   const int s4 = S / 8;
@@ -1072,6 +1183,9 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     p.dh4 = nb.dh4; p.x = nb.pool3[0]; p.gw4 = nb.grad + L.w[3];
     M("fc4_wgrad");
     CHECK_LAUNCH(launch_gemm<CfgFcW>(p, 1, 1, sw));
+    // the fc4 weight gradient (the bulk of the flat gradient) is final here:
+    // the caller may start reducing it under the conv backward
+    if (fc4_done) CHECK_LAUNCH(fc4_done(fc4_done_arg));
     CHECK_LAUNCH(fork());   // side waits for fc4 dgrad (dconv3)
   }
   {  // conv3 wgrad
@@ -1173,7 +1287,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
                 nb.grad + L.b[4], nb.grad + L.b[3]};
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blk + kFc4 / 64), dim3(256), 0, s, nb.wpart,
                        nb.grad, d[0], d[1], d[2], nb.iter, book ? nb.opt_init : nullptr,
-                       book_period, book ? bump : nullptr, hs);
+                       book_period, book ? bump : nullptr, nb.book_inc, hs);
     CHECK_LAUNCH(hipGetLastError());
   }
   return hipSuccess;

@@ -44,7 +44,12 @@ class UpdateCfg(ctypes.Structure):
 
 class StepCfg(ctypes.Structure):
     _fields_ = [("update", UpdateCfg), ("target_period", ctypes.c_int32),
-                ("allreduce", ctypes.c_int32), ("seed", ctypes.c_uint64)]
+                ("exchange", ctypes.c_int32), ("seed", ctypes.c_uint64),
+                ("overlap", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+ABI_VERSION = 2
+EXCHANGES = {"none": 0, "allreduce": 1, "sharded": 2, "server": 3}
 
 
 _P = ctypes.c_void_p
@@ -100,6 +105,8 @@ _SIGS = {
     "ddq_step_graph_async": (ctypes.c_int, [_P, ctypes.POINTER(StepCfg), _i32]),
     "ddq_step_pipelined_async": (ctypes.c_int, [_P, ctypes.POINTER(StepCfg), _i32]),
     "ddq_step_count": (_i64, [_P]),
+    "ddq_group_init": (ctypes.c_int, [ctypes.POINTER(_P), _i32]),
+    "ddq_group_step": (ctypes.c_int, [ctypes.POINTER(_P), _i32, ctypes.POINTER(StepCfg)]),
     "ddq_profile_step": (ctypes.c_int, [_P, ctypes.POINTER(StepCfg), _P, _fp, _i32,
                                         ctypes.POINTER(_i32)]),
     "ddq_step_flops": (ctypes.c_double, [_P]),
@@ -126,6 +133,9 @@ def load(path=LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.ddq_abi_version() != ABI_VERSION:
+        raise ImportError("libddq_hip.so ABI %d != binding ABI %d (rebuild)"
+                          % (lib.ddq_abi_version(), ABI_VERSION))
     _lib = lib
     return lib
 

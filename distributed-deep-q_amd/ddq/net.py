@@ -306,9 +306,14 @@ class DeepQNet:
 
     # -------------------------------------------------------------------- step
     def step_cfg(self, rule="rmsprop", lr=1e-4, target_period=10, allreduce=False, seed=0,
-                 **kw):
-        return _lib.StepCfg(_lib.update_cfg(rule, lr, **kw), int(target_period),
-                            int(bool(allreduce)), int(seed))
+                 exchange=None, overlap=False, **kw):
+        """exchange: "none" | "allreduce" | "sharded" | "server" (include/ddq_hip.h
+        enum ddq_exchange); allreduce=True is shorthand for "allreduce"."""
+        if exchange is None:
+            exchange = "allreduce" if allreduce else "none"
+        ex = _lib.EXCHANGES[exchange] if isinstance(exchange, str) else int(exchange)
+        return _lib.StepCfg(_lib.update_cfg(rule, lr, **kw), int(target_period), ex, int(seed),
+                            int(bool(overlap)), 0)
 
     def step(self, cfg):
         self._check(self.lib.ddq_step_async(self.ctx, ctypes.byref(cfg)))
@@ -344,6 +349,23 @@ class DeepQNet:
     def comm_init(self, uid, nranks, rank):
         buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
         self._check(self.lib.ddq_comm_init(self.ctx, buf, int(nranks), int(rank)))
+
+    @staticmethod
+    def group_init(nets):
+        """In-process data-parallel group (ddq_group_init): nets[r] is rank r."""
+        lib = _lib.load()
+        arr = (ctypes.c_void_p * len(nets))(*[n.ctx.value for n in nets])
+        check(lib.ddq_group_init(arr, len(nets)))
+        return arr
+
+    @staticmethod
+    def group_step(nets, cfg, arr=None):
+        lib = _lib.load()
+        if arr is None:
+            arr = (ctypes.c_void_p * len(nets))(*[n.ctx.value for n in nets])
+        rc = lib.ddq_group_step(arr, len(nets), ctypes.byref(cfg))
+        if rc != 0:
+            check(rc, nets[0].ctx)
 
     def allreduce_grads(self):
         self._check(self.lib.ddq_allreduce_grads(self.ctx))

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define DDQ_ABI_VERSION 1
+#define DDQ_ABI_VERSION 2
 
 enum ddq_status {
   DDQ_OK = 0,
@@ -86,15 +86,39 @@ typedef struct ddq_update_cfg {
   float weight_decay;    /* momentum rule only (0.0005)                       */
 } ddq_update_cfg;
 
+/* Gradient exchange of a data-parallel step (replaces the HTTP gradient POST
+ * + server apply + model GET round trip, baristanet.py:85-133,
+ * server.py:181-209).  Used when the ctx has a communicator (ddq_comm_init)
+ * or belongs to an in-process group (ddq_group_init); ignored otherwise. */
+enum ddq_exchange {
+  DDQ_EXCHANGE_NONE = 0,
+  /* W gradients computed at the same theta, summed, applied once (replicated
+   * apply on every rank).  Equals the server applying W equally-stale SGD
+   * gradients; a documented deviation for rmsprop/adagrad. */
+  DDQ_EXCHANGE_ALLREDUCE = 1,
+  /* Same semantics, sharded: reduce-scatter(sum) -> each rank applies its
+   * 1/W shard (optimizer state sharded) -> all-gather of theta. */
+  DDQ_EXCHANGE_SHARDED = 2,
+  /* Param-server semantics (server.py:196-209): every rank owns a 1/W shard
+   * and its optimizer state; gradient slices go all-to-all and the owner
+   * applies the W gradients one by one in rank (ticket) order, exactly as
+   * the server applies gradients on arrival; iteration += W per step; then
+   * all-gather of theta.  Staleness within a step: 0..W-1 updates. */
+  DDQ_EXCHANGE_SERVER = 3
+};
+
 /* One fused training step (main.py:61-103 debug_process_connection body,
  * minus acting): sample B indices (device RNG) -> gather -> P/Q forward ->
- * Bellman target + loss -> Q backward -> [grad all-reduce] -> apply ->
- * [P <- Q every target_period steps]. */
+ * Bellman target + loss -> Q backward -> [exchange] -> apply ->
+ * [P <- Q when the next pull sees iteration % target_period == 0]. */
 typedef struct ddq_step_cfg {
   ddq_update_cfg update;
   int32_t target_period;   /* server.py:274 --special-update (10); 0 = never */
-  int32_t allreduce;       /* 1: sum grads over the RCCL communicator        */
+  int32_t exchange;        /* enum ddq_exchange                              */
   uint64_t seed;           /* device index-stream seed (per rank)            */
+  int32_t overlap;         /* ALLREDUCE over RCCL: reduce the fc4 weight
+                              bucket on a comm stream under the conv backward */
+  int32_t reserved;        /* 0 */
 } ddq_step_cfg;
 
 /* ---------------- context ---------------------------------------------- */
@@ -222,6 +246,12 @@ int ddq_step_graph_async(ddq_ctx* ctx, const ddq_step_cfg* cfg, int32_t nsteps);
  * overlapped with step t (double-buffered minibatch).  Same results, indices
  * and counters as nsteps sequential ddq_step_async calls.  Enqueued, no sync. */
 int ddq_step_pipelined_async(ddq_ctx* ctx, const ddq_step_cfg* cfg, int32_t nsteps);
+/* In-process data parallelism: W ctxs (W workers sharing a GPU, or peer-
+ * enabled devices) exchange through device copies instead of RCCL, with the
+ * same exchanges, shard layout and kernels as ddq_comm_init ranks.  The
+ * group step is synchronous and runs phase by phase over the members. */
+int ddq_group_init(ddq_ctx** ctxs, int32_t nranks);
+int ddq_group_step(ddq_ctx** ctxs, int32_t nranks, const ddq_step_cfg* cfg);
 /* Steps taken so far (drives the target-sync period). */
 int64_t ddq_step_count(const ddq_ctx* ctx);
 

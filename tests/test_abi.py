@@ -51,11 +51,12 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_lib.BlobDesc) == 16 + 4 + 16 + 4 + 8 + 8   # incl. padding
     assert _lib.BlobDesc.offset.offset == 40
     assert ctypes.sizeof(_lib.UpdateCfg) == 24
-    assert ctypes.sizeof(_lib.StepCfg) == 24 + 4 + 4 + 8
+    assert ctypes.sizeof(_lib.StepCfg) == 24 + 4 + 4 + 8 + 4 + 4
+    assert _lib.StepCfg.seed.offset == 32 and _lib.StepCfg.overlap.offset == 40
 
 
 def test_abi_version(lib):
-    assert lib.ddq_abi_version() == 1
+    assert lib.ddq_abi_version() == 2
 
 
 def test_no_gpu_fails_loudly(lib):
