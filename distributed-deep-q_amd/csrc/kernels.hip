@@ -1212,7 +1212,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     p.dconv = nb.dconv3; p.wk = nb.wk[0] + L.wk_off[2]; p.pmask = nb.mask2; p.pdconv = nb.dconv2;
     M("conv3_dgrad");
     if (nb.conv_impl == 1) {
-      const DirectArgs d = direct_dgrad_args(nb.dconv3, p.wk, nb.mask2, nb.dconv2, B, H, 1);
+      DirectArgs d = direct_dgrad_args(nb.dconv3, p.wk, nb.mask2, nb.dconv2, B, H, 1);
       CHECK_LAUNCH((launch_direct<64, 64, 3, 8, 8, 2, 2, true, false, 3>(d, 1, s)));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgD3>(p, 1, 1, s));
@@ -1244,7 +1244,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     M("conv2_dgrad");
     if (nb.conv_impl == 1) {
       // 2 tap groups: two waves per SIMD over the 1024 output blocks
-      const DirectArgs d = direct_dgrad_args(nb.dconv2, p.wk, nb.mask1, nb.dconv1, B, H, 2);
+      DirectArgs d = direct_dgrad_args(nb.dconv2, p.wk, nb.mask1, nb.dconv1, B, H, 2);
       CHECK_LAUNCH((launch_direct<64, 32, 5, 8, 16, 4, 1, true, false, 2>(d, 1, s)));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgD2>(p, 1, 1, s));

@@ -1,0 +1,48 @@
+"""Summarise a rocprofv3 kernel-trace directory: median device time of each
+step kernel over the graph-replayed steps, plus the bench JSON value.
+
+Usage: python tools/trace_summary.py <rocprof out dir> [label]"""
+import collections
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+
+SHORT = [("sample_gather_kernel", "sample"), ("direct_conv_kernel<4, 32, 7", "c1f"),
+         ("direct_conv_kernel<32, 64, 5", "c2f"), ("direct_conv_kernel<64, 64, 3, 8, 8, 2, 2, false", "c3f"),
+         ("fc4_fwd_direct", "fc4f"), ("fc4_head", "head"), ("fc4_dgrad_direct", "fc4d"),
+         ("FcWgrad", "fc4w"), ("wgradd_kernel<64, 64, 3", "c3w"),
+         ("direct_conv_kernel<64, 64, 3, 8, 8, 2, 2, true", "c3d"), ("wgradd_kernel<32, 64, 5", "c2w"),
+         ("direct_conv_kernel<64, 32, 5", "c2d"), ("wgrad1_kernel", "c1w"),
+         ("wgrad_reduce_kernel", "wred"), ("apply_kernel", "apply")]
+
+
+def main():
+    d = sys.argv[1]
+    label = sys.argv[2] if len(sys.argv) > 2 else ""
+    f = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)[0]
+    per = collections.defaultdict(list)
+    for r in csv.DictReader(open(f)):
+        name = r["Kernel_Name"]
+        for key, short in SHORT:
+            if key in name:
+                per[short].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+                break
+    out = {k: round(statistics.median(v), 2) for k, v in per.items() if v}
+    tot = sum(out.values())
+    js = d.rstrip("/") + ".json"
+    val = ""
+    if os.path.exists(js):
+        try:
+            b = json.load(open(js))
+            val = "%s upd/s %.4f ms" % (b["value"], b["ms_per_step"])
+        except Exception:
+            pass
+    print("variant %s: %s | sum %.1f us | %s" % (label, val, tot,
+          " ".join("%s=%.1f" % (k, out[k]) for _, k in SHORT if k in out)))
+
+
+if __name__ == "__main__":
+    main()
