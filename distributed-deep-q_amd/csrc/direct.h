@@ -87,43 +87,84 @@ template <class C, int CP, int N>
 struct WStage {
   static constexpr int kF4 = N * CP / 4;                       // float4 per tap
   static constexpr int kPer = (kF4 + C::kGroup - 1) / C::kGroup;   // one tap group stages a tap
-  float4 r[kPer];
+  static_assert(kPer <= 8, "weight staging slots");
+  // Eight NAMED registers, every access through a compile-time slot: with a
+  // float4 array member hipcc kept the staging set in scratch memory (48 B /
+  // lane on conv2 fwd, seen in the .s), so the next tap's weight loads were
+  // spilled the moment they landed instead of staying in flight.
+  float4 r0, r1, r2, r3, r4, r5, r6, r7;
+
+  template <int S>
+  __device__ __forceinline__ float4& slot() {
+    if constexpr (S == 0) return r0;
+    else if constexpr (S == 1) return r1;
+    else if constexpr (S == 2) return r2;
+    else if constexpr (S == 3) return r3;
+    else if constexpr (S == 4) return r4;
+    else if constexpr (S == 5) return r5;
+    else if constexpr (S == 6) return r6;
+    else return r7;
+  }
+  template <int S>
+  __device__ __forceinline__ const float4& slot() const {
+    if constexpr (S == 0) return r0;
+    else if constexpr (S == 1) return r1;
+    else if constexpr (S == 2) return r2;
+    else if constexpr (S == 3) return r3;
+    else if constexpr (S == 4) return r4;
+    else if constexpr (S == 5) return r5;
+    else if constexpr (S == 6) return r6;
+    else return r7;
+  }
 
   // fwd: wb[n=co][k=ci] = Wk[co][t][ci], float4 along k.  dgrad (TRANS):
   // wb[n=ci][k=co] = Wk[co][T-1-t][ci], float4 along ci, transposed on store.
-  template <bool TRANS>
-  __device__ __forceinline__ void load(const float* __restrict__ wk, int t, int tid) {
-#pragma unroll
-    for (int s = 0; s < kPer; ++s) {
-      const int f = tid + s * C::kGroup;
-      if (kF4 % C::kGroup != 0 && f >= kF4) continue;
+  template <bool TRANS, int S>
+  __device__ __forceinline__ void load1(const float* __restrict__ wk, int t, int tid) {
+    if constexpr (S < kPer) {
+      const int f = tid + S * C::kGroup;
+      if (kF4 % C::kGroup != 0 && f >= kF4) return;
       if (!TRANS) {
         const int n = f / (CP / 4), c4 = f % (CP / 4);
-        r[s] = *reinterpret_cast<const float4*>(wk + ((size_t)n * C::T + t) * CP + 4 * c4);
-      } else {               // wb[n=ci][k=co] = Wk[co][T-1-t][ci], float4 along ci
+        slot<S>() = *reinterpret_cast<const float4*>(wk + ((size_t)n * C::T + t) * CP + 4 * c4);
+      } else {
         const int co = f / (N / 4), n4 = f % (N / 4);
-        r[s] = *reinterpret_cast<const float4*>(wk + ((size_t)co * C::T + (C::T - 1 - t)) * N +
-                                                4 * n4);
+        slot<S>() = *reinterpret_cast<const float4*>(
+            wk + ((size_t)co * C::T + (C::T - 1 - t)) * N + 4 * n4);
+      }
+    }
+  }
+  template <bool TRANS, int S>
+  __device__ __forceinline__ void store1(float* wb, int tid) const {
+    if constexpr (S < kPer) {
+      const int f = tid + S * C::kGroup;
+      if (kF4 % C::kGroup != 0 && f >= kF4) return;
+      const float4 v = slot<S>();
+      if (!TRANS) {
+        const int n = f / (CP / 4), c4 = f % (CP / 4);
+        *reinterpret_cast<float4*>(wb + n * C::CW + 4 * c4) = v;
+      } else {
+        const int co = f / (N / 4), n4 = f % (N / 4);
+        wb[(4 * n4 + 0) * C::CW + co] = v.x;
+        wb[(4 * n4 + 1) * C::CW + co] = v.y;
+        wb[(4 * n4 + 2) * C::CW + co] = v.z;
+        wb[(4 * n4 + 3) * C::CW + co] = v.w;
       }
     }
   }
   template <bool TRANS>
+  __device__ __forceinline__ void load(const float* __restrict__ wk, int t, int tid) {
+    load1<TRANS, 0>(wk, t, tid); load1<TRANS, 1>(wk, t, tid);
+    load1<TRANS, 2>(wk, t, tid); load1<TRANS, 3>(wk, t, tid);
+    load1<TRANS, 4>(wk, t, tid); load1<TRANS, 5>(wk, t, tid);
+    load1<TRANS, 6>(wk, t, tid); load1<TRANS, 7>(wk, t, tid);
+  }
+  template <bool TRANS>
   __device__ __forceinline__ void store(float* wb, int tid) const {
-#pragma unroll
-    for (int s = 0; s < kPer; ++s) {
-      const int f = tid + s * C::kGroup;
-      if (kF4 % C::kGroup != 0 && f >= kF4) continue;
-      if (!TRANS) {
-        const int n = f / (CP / 4), c4 = f % (CP / 4);
-        *reinterpret_cast<float4*>(wb + n * C::CW + 4 * c4) = r[s];
-      } else {
-        const int co = f / (N / 4), n4 = f % (N / 4);
-        wb[(4 * n4 + 0) * C::CW + co] = r[s].x;
-        wb[(4 * n4 + 1) * C::CW + co] = r[s].y;
-        wb[(4 * n4 + 2) * C::CW + co] = r[s].z;
-        wb[(4 * n4 + 3) * C::CW + co] = r[s].w;
-      }
-    }
+    store1<TRANS, 0>(wb, tid); store1<TRANS, 1>(wb, tid);
+    store1<TRANS, 2>(wb, tid); store1<TRANS, 3>(wb, tid);
+    store1<TRANS, 4>(wb, tid); store1<TRANS, 5>(wb, tid);
+    store1<TRANS, 6>(wb, tid); store1<TRANS, 7>(wb, tid);
   }
 };
 
@@ -153,15 +194,15 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void direct_conv_kernel(const Di
   // ---- stage the halo patch (zero outside the image) and the first weights ----
   WStage<C, CP, N> ws;
   if constexpr (WALL) {
-    // all taps' weights (conv1: 25 KB) and the patch: every global load is
-    // issued before the first LDS store, so the prologue pays one memory
-    // latency instead of one per staging round (measured -7.5 us on conv1;
-    // the per-round loop below is faster for the per-tap kernels)
-    static_assert(!DGRAD, "WALL staging is forward-only");
+    // every global load (patch, and the weights: all taps for WALL, the
+    // group's first tap otherwise) is issued before the first LDS store, so
+    // the prologue pays one memory latency instead of one per staging round
+    // (conv1: -12 us in the kernel trace)
     constexpr int kPF4 = C::PH * C::PW * (CP / 4);
     constexpr int kPIt = (kPF4 + C::kThreads - 1) / C::kThreads;
-    constexpr int kWF4 = C::T * N * (CP / 4);
+    constexpr int kWF4 = WALL ? C::T * N * (CP / 4) : 1;
     constexpr int kWIt = (kWF4 + C::kThreads - 1) / C::kThreads;
+    static_assert(!(WALL && DGRAD), "WALL staging is forward-only");
     float4 pv[kPIt], wv[kWIt];
 #pragma unroll
     for (int it = 0; it < kPIt; ++it) {
@@ -176,29 +217,32 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void direct_conv_kernel(const Di
                                                      4 * c4);
       }
     }
+    if constexpr (WALL) {
 #pragma unroll
-    for (int it = 0; it < kWIt; ++it) {
-      const int f = tid + it * C::kThreads;
-      wv[it] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (kWF4 % C::kThreads == 0 || f < kWF4)
-        wv[it] = reinterpret_cast<const float4*>(wk)[f];
-    }
-    {
-#pragma unroll
-      for (int it = 0; it < kPIt; ++it) {
+      for (int it = 0; it < kWIt; ++it) {
         const int f = tid + it * C::kThreads;
-        if (kPF4 % C::kThreads == 0 || f < kPF4) {
-          const int pix = f / (CP / 4), c4 = f % (CP / 4);
-          const int py = pix / C::PW, px = pix % C::PW;
-          float* dst = patch + py * C::RS + px * C::CS + 4 * c4;
-          if (CP >= 8) {
-            *reinterpret_cast<float4*>(dst) = pv[it];
-          } else {
-            reinterpret_cast<float2*>(dst)[0] = make_float2(pv[it].x, pv[it].y);
-            reinterpret_cast<float2*>(dst)[1] = make_float2(pv[it].z, pv[it].w);
-          }
+        wv[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (kWF4 % C::kThreads == 0 || f < kWF4) wv[it] = reinterpret_cast<const float4*>(wk)[f];
+      }
+    } else {
+      if (wkg < C::T) ws.template load<DGRAD>(wk, wkg, gtid);
+    }
+#pragma unroll
+    for (int it = 0; it < kPIt; ++it) {
+      const int f = tid + it * C::kThreads;
+      if (kPF4 % C::kThreads == 0 || f < kPF4) {
+        const int pix = f / (CP / 4), c4 = f % (CP / 4);
+        const int py = pix / C::PW, px = pix % C::PW;
+        float* dst = patch + py * C::RS + px * C::CS + 4 * c4;
+        if (CP >= 8) {
+          *reinterpret_cast<float4*>(dst) = pv[it];
+        } else {
+          reinterpret_cast<float2*>(dst)[0] = make_float2(pv[it].x, pv[it].y);
+          reinterpret_cast<float2*>(dst)[1] = make_float2(pv[it].z, pv[it].w);
         }
       }
+    }
+    if constexpr (WALL) {
 #pragma unroll
       for (int it = 0; it < kWIt; ++it) {
         const int f = tid + it * C::kThreads;
@@ -208,6 +252,8 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void direct_conv_kernel(const Di
           *reinterpret_cast<float4*>(wbuf + (t * N + n) * C::CW + 4 * c4) = wv[it];
         }
       }
+    } else {
+      if (wkg < C::T) ws.template store<DGRAD>(wbuf + wkg * N * C::CW, gtid);
     }
   } else {
     for (int f = tid; f < C::PH * C::PW * (CP / 4); f += C::kThreads) {
@@ -265,7 +311,13 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void direct_conv_kernel(const Di
     const float* wb = wbuf + (WALL ? t : ((s & 1) * WK + wkg)) * N * C::CW;
     // next tap's weights in flight under this tap's MFMAs (clamped index: the
     // load is unconditional so the staging registers never go through scratch)
-    if (!WALL && s + 1 < NSTEP) ws.template load<DGRAD>(wk, tn < C::T ? tn : C::T - 1, gtid);
+    if (!WALL && s + 1 < NSTEP) {
+      ws.template load<DGRAD>(wk, tn < C::T ? tn : C::T - 1, gtid);
+      // pin the loads here: without the barrier hipcc sinks them to the LDS
+      // store after the MFMAs and waits on them at once (one exposed L2
+      // round trip per tap, seen in the .s)
+      __builtin_amdgcn_sched_barrier(0);
+    }
     if (t < C::T) {
       const int ky = t / KS, kx = t % KS;
       const float* pa = patch + ky * C::RS + kx * C::CS;

@@ -7,6 +7,7 @@ import csv
 import glob
 import json
 import os
+import re
 import statistics
 import sys
 
@@ -26,6 +27,15 @@ def main():
     per = collections.defaultdict(list)
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
+        m = re.search(r"direct_conv_kernel<(\d+), (\d+), (\d+),.*?(true|false), (true|false)", name)
+        if m:   # any tile config: classify by (CP, N, KS, DGRAD)
+            cp, n, ks, dg = int(m.group(1)), int(m.group(2)), int(m.group(3)), m.group(4) == "true"
+            short = {(4, 32, 7): "c1f", (32, 64, 5): "c2f", (64, 32, 5): "c2d"}.get((cp, n, ks))
+            if ks == 3:
+                short = "c3d" if dg else "c3f"
+            if short:
+                per[short].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+            continue
         for key, short in SHORT:
             if key in name:
                 per[short].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
