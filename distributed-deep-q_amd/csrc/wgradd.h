@@ -124,17 +124,51 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
   // ---- MFMA: k-step s = pixels (2s, 2s+1); lane half h takes pixel 2s+h ----
+  // The KS input pixels of step s are a window that slides by two pixels per
+  // step: keep it in registers, load only the two new pixels (and the next
+  // dconv value) per step, and issue those loads before this step's MFMAs
+  // (pinned by a scheduling barrier) -- the plain load/wait/MFMA loop left
+  // three LDS round trips exposed per step.
   auto compute = [&]() {
     const float* pa = rd + h * 32 + l31;
     const float* pb = rin + h * CIN + l31;
+    float bw[KS][NCB];
+    float av = pa[0];
+#pragma unroll
+    for (int kx = 0; kx < KS; ++kx)
+#pragma unroll
+      for (int c = 0; c < NCB; ++c) bw[kx][c] = pb[kx * CIN + c * 32];
     for (int s = 0; s < W2; ++s) {
-      const float av = pa[s * 64];
+      float an = 0.f, n0[NCB], n1[NCB];
+      const bool more = s + 1 < W2;
+      if (more) {
+        an = pa[(s + 1) * 64];
+#pragma unroll
+        for (int c = 0; c < NCB; ++c) {
+          n0[c] = pb[(2 * s + KS) * CIN + c * 32];
+          n1[c] = pb[(2 * s + KS + 1) * CIN + c * 32];
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int kx = 0; kx < KS; ++kx)
 #pragma unroll
         for (int c = 0; c < NCB; ++c)
-          acc[kx * NCB + c] = __builtin_amdgcn_mfma_f32_32x32x2f32(
-              av, pb[(2 * s + kx) * CIN + c * 32], acc[kx * NCB + c], 0, 0, 0);
+          acc[kx * NCB + c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bw[kx][c],
+                                                                  acc[kx * NCB + c], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (more) {
+#pragma unroll
+        for (int kx = 0; kx + 2 < KS; ++kx)
+#pragma unroll
+          for (int c = 0; c < NCB; ++c) bw[kx][c] = bw[kx + 2][c];
+#pragma unroll
+        for (int c = 0; c < NCB; ++c) {
+          bw[KS - 2][c] = n0[c];
+          bw[KS - 1][c] = n1[c];
+        }
+        av = an;
+      }
     }
     __builtin_amdgcn_wave_barrier();
   };
