@@ -92,19 +92,22 @@ def fill_replay(net, N, S, seed):
                       np.tile(rw, reps)[:N], np.tile(nt, reps)[:N].astype(np.uint8), 0, N)
 
 
-def cpu_baseline(B, S, seed, budget_s=12.0, max_steps=16):
-    """Oracle C restatement (Caffe CPU algorithm) of the same update step."""
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _cpu_updates(lib, B, S, seed, threads, budget_s, max_steps):
+    """Time sample->gather->P/Q fwd->target->Q bwd->rmsprop apply updates of the
+    oracle's C restatement (Caffe CPU algorithm) on `threads` OpenMP threads."""
     from oracle import ref_numpy as ref
     from ddq.expgain import synthetic_transitions
-    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "libddq_cpu.so"))
     fp = ctypes.POINTER(ctypes.c_float)
-    lib.ddq_cpu_full_pass.restype = ctypes.c_int
-    lib.ddq_cpu_apply.restype = ctypes.c_int
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count()
-    cores = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores))))
     N = 1024
     st, ac, rw, nt = synthetic_transitions(N, S, seed=seed)
     theta = ref.flatten(ref.init_params(S, seed=42))
@@ -113,9 +116,9 @@ def cpu_baseline(B, S, seed, budget_s=12.0, max_steps=16):
     grad = np.zeros_like(theta)
     rng = np.random.default_rng(seed)
     img = 4 * S * S
+    P = lambda a: a.ctypes.data_as(fp)
     t0 = time.perf_counter()
     steps = 0
-    P = lambda a: a.ctypes.data_as(fp)
     while steps < max_steps and (steps == 0 or time.perf_counter() - t0 < budget_s):
         idx = ref.draw_indices(rng, N, 0, B)
         nxt = np.where(idx + 1 == N, 0, idx + 1)
@@ -126,17 +129,44 @@ def cpu_baseline(B, S, seed, budget_s=12.0, max_steps=16):
         r = rw[nxt].astype(np.float32)
         n = nt[nxt].astype(np.float32)
         rc = lib.ddq_cpu_full_pass(B, S, P(theta), P(thetaP), P(s), P(a), P(r), P(s2), P(n),
-                                   ctypes.c_float(0.85), P(grad), None, cores)
+                                   ctypes.c_float(0.85), P(grad), None, threads)
         assert rc == 0
         lib.ddq_cpu_apply(1, ctypes.c_long(theta.size), P(theta), P(grad), P(cache),
                           int(steps == 0), ctypes.c_float(1e-4), ctypes.c_float(0.9),
                           ctypes.c_float(1e-8))
         steps += 1
-    dt = time.perf_counter() - t0
-    return {"value": round(steps / dt, 4), "unit": "updates/s", "cores": cores, "kind": "port",
-            "sample": "%d updates (sample->gather->P/Q fwd->target->Q bwd->rmsprop apply) "
-                      "at B=%d, %dx%d, oracle/ddq_cpu.c im2col+SGEMM fp32, %d OpenMP threads, "
-                      "%.1f s" % (steps, B, S, S, cores, dt)}
+    return steps, time.perf_counter() - t0
+
+
+def cpu_baseline(B, S, seed, budget_s=12.0, max_steps=64):
+    """Oracle C restatement (Caffe CPU algorithm: im2col + SGEMM, fp32, OpenMP)
+    of the same update step, on all host cores and on one core (BASELINE.md
+    section 2), with the reference's own published 2015 Caffe CPU time for
+    context (results/cost-vs-image-size.txt:4, hardware unstated)."""
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "libddq_cpu.so"))
+    lib.ddq_cpu_full_pass.restype = ctypes.c_int
+    lib.ddq_cpu_apply.restype = ctypes.c_int
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count()
+    cores = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores))))
+    steps, dt = _cpu_updates(lib, B, S, seed, cores, budget_s, max_steps)
+    s1, d1 = _cpu_updates(lib, B, S, seed, 1, budget_s / 2, max(2, max_steps // 8))
+    published = {16: 81.7, 32: 252.8, 64: 981.5, 128: 4044.0}.get(S)
+    out = {"value": round(steps / dt, 4), "unit": "updates/s", "cores": cores, "kind": "port",
+           "sample": "%d updates (sample->gather->P/Q fwd->target->Q bwd->rmsprop apply) "
+                     "at B=%d, %dx%d, oracle/ddq_cpu.c im2col+SGEMM fp32, %d OpenMP threads, "
+                     "%.1f s" % (steps, B, S, S, cores, dt),
+           "cpu_model": cpu_model(),
+           "single_core": {"value": round(s1 / d1, 4), "cores": 1,
+                           "sample": "%d updates, %.1f s" % (s1, d1)}}
+    if published:
+        out["reference_published"] = {
+            "value": round(1000.0 / published, 4), "unit": "updates/s (fwd+bwd only)",
+            "source": "results/cost-vs-image-size.txt (Caffe CPU, %.1f ms fwd+bwd at %dx%d "
+                      "B=32, hardware unstated)" % (published, S, S)}
+    return out
 
 
 def dev_timer(net):
