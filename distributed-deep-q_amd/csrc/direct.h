@@ -32,7 +32,8 @@
 
 namespace ddq {
 
-template <int CP, int N, int KS, int TY, int TX, int WM, int WN, bool DGRAD, bool WALL, int WK = 1>
+template <int CP, int N, int KS, int TY, int TX, int WM, int WN, bool DGRAD, bool WALL, int WK = 1,
+          bool RB = false>
 struct DirectCfg {
   static constexpr int V = CP >= 8 ? 4 : CP / 2;     // floats per lane per LDS read
   static constexpr int G = 2 * V;                     // channels per read group
@@ -47,7 +48,7 @@ struct DirectCfg {
   static constexpr int TM = TY * TX / WM / 32;        // 32-pixel blocks per wave
   static constexpr int TN = N / WN / 32;              // 32-channel blocks per wave
   static constexpr int kPatch = PH * RS;
-  static constexpr int kW = WSLOTS * N * CW;
+  static constexpr int kW = RB ? 0 : WSLOTS * N * CW;   // RB: weights never touch LDS
   static constexpr int kRed = (WK - 1) * WM * WN * TM * TN * 1024;   // tap-group sums
   static constexpr int kSmem = kPatch + kW > kRed ? kPatch + kW : kRed;
   static_assert(TM >= 1 && TN >= 1, "wave tile");
@@ -168,9 +169,11 @@ struct WStage {
   }
 };
 
-template <int CP, int N, int KS, int TY, int TX, int WM, int WN, bool DGRAD, bool WALL, int WK>
+template <int CP, int N, int KS, int TY, int TX, int WM, int WN, bool DGRAD, bool WALL, int WK,
+          bool RB>
 __global__ __launch_bounds__(64 * WM * WN * WK) void direct_conv_kernel(const DirectArgs a) {
-  using C = DirectCfg<CP, N, KS, TY, TX, WM, WN, DGRAD, WALL, WK>;
+  using C = DirectCfg<CP, N, KS, TY, TX, WM, WN, DGRAD, WALL, WK, RB>;
+  static_assert(!(RB && WALL), "register-B is per-tap");
   using VT = typename VecT<C::V>::T;
   constexpr int TM = C::TM, TN = C::TN, V = C::V;
   __shared__ __attribute__((aligned(16))) float smem[C::kSmem];
@@ -271,7 +274,7 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void direct_conv_kernel(const Di
         reinterpret_cast<float2*>(dst)[1] = make_float2(v.z, v.w);
       }
     }
-    if (wkg < C::T) {
+    if (!RB && wkg < C::T) {
       ws.template load<DGRAD>(wk, wkg, gtid);
       ws.template store<DGRAD>(wbuf + wkg * N * C::CW, gtid);
     }
@@ -305,6 +308,63 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void direct_conv_kernel(const Di
   // Tap steps: group wkg takes tap s*WK + wkg; non-WALL weights live in a
   // two-slot ring per group (slot (s&1)*WK + wkg), one barrier per step.
   constexpr int NSTEP = (C::T + WK - 1) / WK;
+  if constexpr (RB) {
+    // Register-B: every lane loads its own B operand of the next tap straight
+    // from the (L2-resident) weights while this tap's MFMAs run -- no weight
+    // staging, no LDS weight reads, no barrier in the tap loop, and LDS holds
+    // only the patch (more workgroups per CU).
+    //   fwd  : B[k = ci][n = co] = Wk[co][t][ci]      (one VT load per group)
+    //   dgrad: B[k = co][n = ci] = Wk[co][T-1-t][ci]  (V dword loads, lanes
+    //          along ci: 128-byte rows)
+    constexpr int NG = CP / C::G;
+    float bq[2][TN][NG][V];
+    auto load_b = [&](float (&dst)[TN][NG][V], int t) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = wni * TN * 32 + 32 * j + l31;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          const int k0 = g * C::G + h * V;
+          if (!DGRAD) {
+            const VT q = *reinterpret_cast<const VT*>(wk + ((size_t)n * C::T + t) * CP + k0);
+#pragma unroll
+            for (int v = 0; v < V; ++v) dst[j][g][v] = vget(q, v);
+          } else {
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+              dst[j][g][v] = wk[((size_t)(k0 + v) * C::T + (C::T - 1 - t)) * N + n];
+          }
+        }
+      }
+    };
+    load_b(bq[0], wkg < C::T ? wkg : C::T - 1);
+#pragma unroll
+    for (int s = 0; s < NSTEP; ++s) {
+      const int t = s * WK + wkg;
+      const int tn = t + WK;
+      if (s + 1 < NSTEP) load_b(bq[(s + 1) & 1], tn < C::T ? tn : C::T - 1);
+      __builtin_amdgcn_sched_barrier(0);
+      if (t < C::T) {
+        const int ky = t / KS, kx = t % KS;
+        const float* pa = patch + ky * C::RS + kx * C::CS;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          VT av[TM];
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            av[i] = *reinterpret_cast<const VT*>(pa + abase[i] + g * C::G);
+#pragma unroll
+          for (int v = 0; v < V; ++v)
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+              for (int j = 0; j < TN; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+                    vget(av[i], v), bq[s & 1][j][g][v], acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+  } else
   for (int s = 0; s < NSTEP; ++s) {
     const int t = s * WK + wkg;
     const int tn = t + WK;
@@ -422,12 +482,13 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void direct_conv_kernel(const Di
   }
 }
 
-template <int CP, int N, int KS, int TY, int TX, int WM, int WN, bool DGRAD, bool WALL, int WK = 1>
+template <int CP, int N, int KS, int TY, int TX, int WM, int WN, bool DGRAD, bool WALL, int WK = 1,
+          bool RB = false>
 inline hipError_t launch_direct(DirectArgs a, int nz, hipStream_t st) {
   a.tiles_x = (a.W + TX - 1) / TX;
   const int tiles_y = (a.H + TY - 1) / TY;
   dim3 grid(tiles_y * a.tiles_x, a.B, nz);
-  hipLaunchKernelGGL((direct_conv_kernel<CP, N, KS, TY, TX, WM, WN, DGRAD, WALL, WK>), grid,
+  hipLaunchKernelGGL((direct_conv_kernel<CP, N, KS, TY, TX, WM, WN, DGRAD, WALL, WK, RB>), grid,
                      dim3(64 * WM * WN * WK), 0, st, a);
   return hipGetLastError();
 }
