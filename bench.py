@@ -169,6 +169,54 @@ def cpu_baseline(B, S, seed, budget_s=12.0, max_steps=64):
     return out
 
 
+def kernel_roofline(avg_us, B, S, P):
+    """Per-kernel fraction of its roofline: MFMA kernels vs the
+    f32 MFMA peak; the replay gather and the apply vs HBM (algorithmic bytes:
+    gather 2*B*4*S^2 u8 read + f32 write; rmsprop apply 20*P, +8P on sync
+    steps not counted).  Device times are the eager HIP-event times."""
+    fl = kernel_flops(B, S)
+    out = {}
+    for k, us in avg_us.items():
+        if us <= 0:
+            continue
+        if k in fl:
+            tf = fl[k] / (us * 1e-6) / 1e12
+            out[k] = {"TFLOPs": round(tf, 2), "frac": round(tf * 1e12 / F32_MFMA_PEAK, 3)}
+        elif k == "sample_gather":
+            by = 2 * B * 4 * S * S * 5 + B * 24
+            out[k] = {"GBps": round(by / (us * 1e-6) / 1e9, 1),
+                      "frac": round(by / (us * 1e-6) / HBM_PEAK, 3)}
+        elif k == "apply":
+            by = 20 * P
+            out[k] = {"GBps": round(by / (us * 1e-6) / 1e9, 1),
+                      "frac": round(by / (us * 1e-6) / HBM_PEAK, 3)}
+    return out
+
+
+def acting_rate(net, cfg, S, iters=200, seed=5):
+    """SURVEY 8(d) 'including acting' variant: per update one batch-1 greedy
+    action (ddq_select_action on the newest state) and one synthetic-frame
+    add_experience, then the fused training step (host-synchronous loop)."""
+    from ddq.expgain import synthetic_transitions
+    st, ac, rw, nt = synthetic_transitions(64, S, seed=seed)
+    for i in range(5):
+        net.select_action(st[i:i + 1])
+        net.replay_add(int(ac[i]), int(rw[i]), st[i])
+        net.step(cfg)
+    net.synchronize()
+    t0 = time.perf_counter()
+    for i in range(iters):
+        j = i % 64
+        net.select_action(st[j:j + 1])
+        net.replay_add(int(ac[j]), int(rw[j]), st[j] if nt[j] else None)
+        net.step(cfg)
+    net.synchronize()
+    dt = time.perf_counter() - t0
+    return {"value": round(iters / dt, 2), "unit": "updates/s",
+            "note": "eager step + batch-1 select_action + add_experience per update, "
+                    "host-synchronous (%d updates)" % iters}
+
+
 def dev_timer(net):
     """HIP-event timer on the ctx stream (torch events on an ExternalStream)."""
     import torch
@@ -275,6 +323,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather-stress", action="store_true",
                     help="skip the C5 1M-slot gather stress (rank 0, N=1 only)")
+    ap.add_argument("--chunks", type=int, default=20,
+                    help="timed chunks for the step-time median/p10/p90 (0: skip)")
+    ap.add_argument("--chunk-steps", type=int, default=24)
+    ap.add_argument("--acting", action="store_true",
+                    help="also time updates including acting (select_action + add_experience)")
     ap.add_argument("--sweep", action="store_true",
                     help="C3: also run the batch-256 frame-size sweep 16..128 (slow)")
     ap.add_argument("--eager", action="store_true", help="no hipGraph (debug)")
@@ -331,6 +384,18 @@ def main():
     dt = ddist.max_over_ranks(time.perf_counter() - t0)
     loss = float(net.blob("loss"))
 
+    # step-time distribution: chunks of graph steps bracketed by HIP events on
+    # the ctx stream (no host sync inside a chunk)
+    dist_ms = None
+    if not args.eager and args.chunks > 0:
+        timer = dev_timer(net)
+        per = sorted(timer(lambda: run(args.chunk_steps), 1) / args.chunk_steps / 1e3
+                     for _ in range(args.chunks))
+        dist_ms = {"median": round(float(np.median(per)), 4),
+                   "p10": round(float(np.percentile(per, 10)), 4),
+                   "p90": round(float(np.percentile(per, 90)), 4),
+                   "chunks": args.chunks, "steps_per_chunk": args.chunk_steps}
+
     # per-kernel device times (HIP events on the ctx stream), averaged
     prof = {}
     for _ in range(args.profile_steps):
@@ -373,8 +438,12 @@ def main():
                          "step_tflops": round(step_flops / (dt / args.steps) / 1e12, 3),
                          "step_frac": round(step_flops / (dt / args.steps) / F32_MFMA_PEAK, 4)},
             "kernels_us": {k: round(v, 2) for k, v in avg.items()},
+            "kernel_roofline": kernel_roofline(avg, B, S, net.num_params),
+            "step_ms_distribution": dist_ms,
             "final_loss": loss,
         }
+        if args.acting and world == 1:
+            out["with_acting"] = acting_rate(net, cfg, S)
         if not args.no_gather_stress and world == 1:
             out["gather_stress"] = gather_stress()
         if args.sweep and world == 1:
