@@ -80,3 +80,89 @@ def test_world2_gloo_sync_dp_semantics():
     assert m0 > 0
     assert t0 == t1 == 2.0                    # max over ranks
     assert s0 != s1                           # distinct per-rank index streams
+
+
+def _shard_len(P, W):
+    """Shard geometry of ddq_comm_init / ddq_group_init (api.hip setup_shards)."""
+    return ((P + W * 64 - 1) // (W * 64)) * 64
+
+
+def _exchange_worker(rank, world, port, out):
+    """The SERVER and SHARDED exchanges restated over gloo with the library's
+    shard geometry: gradient slices to their owners (all-gather + slicing
+    stands in for RCCL's all-to-all / reduce-scatter), the owner applies its
+    slice (W gradients one by one in rank order, or their sum), then the
+    owners' shards are all-gathered into every replica."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "distributed-deep-q_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    from ddq import dist as ddist
+    from oracle import ref_numpy as ref
+    ddist.init_process_group(rank, world, "gloo")
+    S = 16
+    P = ref.num_params(S)
+    L = _shard_len(P, world)
+    theta = ref.flatten(ref.init_params(S, seed=3))
+    rng = np.random.default_rng(100 + rank)
+    g = rng.normal(0, 1e-2, P).astype(np.float32)
+    gp = np.zeros(world * L, np.float32)
+    gp[:P] = g
+    allg = [torch.zeros(world * L) for _ in range(world)]
+    dist.all_gather(allg, torch.from_numpy(gp))
+    mine = slice(rank * L, (rank + 1) * L)
+    th = np.zeros(world * L, np.float32)
+    th[:P] = theta
+    res = {}
+    for mode in ("server", "sharded"):
+        shard, cache = th[mine].copy(), None
+        slices = [a.numpy()[mine] for a in allg]        # what the all-to-all delivers
+        if mode == "server":
+            for s in slices:                           # ticket (rank) order
+                shard, cache = ref.rmsprop_update(shard, s, cache, 1e-3)
+        else:
+            shard, cache = ref.rmsprop_update(shard, np.sum(slices, axis=0,
+                                                            dtype=np.float32), None, 1e-3)
+        parts = [torch.zeros(L) for _ in range(world)]
+        dist.all_gather(parts, torch.from_numpy(np.ascontiguousarray(shard)))
+        res[mode] = torch.cat(parts).numpy()[:P]
+    out.put((rank, res["server"], res["sharded"],
+             np.stack([a.numpy()[:P] for a in allg])))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_server_and_sharded_exchange_semantics(world):
+    """Every replica ends with the same theta, equal to the param server
+    applying the W gradients on arrival in rank order (server.py:196-209,
+    rmsprop lagged cache across them) resp. applying their sum once; shards
+    of ceil(P/(64W))*64 cover P for W not dividing P."""
+    from oracle import ref_numpy as ref
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=300) for _ in range(world)), key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    S = 16
+    theta = ref.flatten(ref.init_params(S, seed=3))
+    grads = res[0][3]
+    want_srv, cache = theta.copy(), None
+    for g in grads:
+        want_srv, cache = ref.rmsprop_update(want_srv, g, cache, 1e-3)
+    want_sh, _ = ref.rmsprop_update(theta, grads.sum(axis=0, dtype=np.float32), None, 1e-3)
+    for r, srv, sh, _ in res:
+        np.testing.assert_array_equal(srv, res[0][1])
+        np.testing.assert_array_equal(sh, res[0][2])
+        np.testing.assert_allclose(srv, want_srv, rtol=0, atol=1e-6)
+        np.testing.assert_allclose(sh, want_sh, rtol=0, atol=1e-6)
+    # the two semantics differ (rmsprop: W lagged applies != one summed apply)
+    assert np.abs(res[0][1] - res[0][2]).max() > 1e-5
