@@ -28,6 +28,8 @@
 //          layer's pre-pool gradient.  (Staging from a pre-transposed copy
 //          kept by the apply kernel measured slower: 51.9 vs 40.4 us.)
 #pragma once
+#include <type_traits>
+
 #include "common.h"
 
 namespace ddq {
@@ -169,6 +171,13 @@ struct WStage {
   }
 };
 
+struct NoStage {
+  template <bool TRANS>
+  __device__ __forceinline__ void load(const float*, int, int) {}
+  template <bool TRANS>
+  __device__ __forceinline__ void store(float*, int) const {}
+};
+
 template <int CP, int N, int KS, int TY, int TX, int WM, int WN, bool DGRAD, bool WALL, int WK,
           bool RB>
 __global__ __launch_bounds__(64 * WM * WN * WK) void direct_conv_kernel(const DirectArgs a) {
@@ -195,7 +204,8 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void direct_conv_kernel(const Di
   uint8_t* __restrict__ maskz = z ? a.mask[1] : a.mask[0];
 
   // ---- stage the halo patch (zero outside the image) and the first weights ----
-  WStage<C, CP, N> ws;
+  // (register-B kernels never stage weights: a stand-in keeps the code shared)
+  std::conditional_t<RB, NoStage, WStage<C, CP, N>> ws;
   if constexpr (WALL) {
     // every global load (patch, and the weights: all taps for WALL, the
     // group's first tap otherwise) is issued before the first LDS store, so

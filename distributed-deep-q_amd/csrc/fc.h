@@ -137,11 +137,12 @@ struct Fc4DgradArgs {
   float* dconv3;                   // NHWC (B, 2S4, 2S4, 64)
 };
 
-__global__ __launch_bounds__(512) void fc4_dgrad_direct_kernel(const Fc4DgradArgs a) {
-  __shared__ float red[8][1024];
+// Body on block (bx, by) with an 8 x 1024-float LDS image; 512 threads.
+__device__ __forceinline__ void fc4_dgrad_body(const Fc4DgradArgs& a, float (*red)[1024], int bx,
+                                               int by) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int l31 = lane & 31, h = lane >> 5;
-  const int kc0 = blockIdx.x * 32, b0 = blockIdx.y * 32;
+  const int kc0 = bx * 32, b0 = by * 32;
   const int K = a.K;
   const int nbase = w * 64 + h * 16;
   const __amdgpu_buffer_rsrc_t ra = fc_rsrc(a.dh4, (uint32_t)(a.B * 512 * 4));
@@ -193,6 +194,11 @@ __global__ __launch_bounds__(512) void fc4_dgrad_direct_kernel(const Fc4DgradArg
     base[(size_t)H3 * 64] = (mk == 2) ? v : 0.f;
     base[(size_t)H3 * 64 + 64] = (mk == 3) ? v : 0.f;
   }
+}
+
+__global__ __launch_bounds__(512) void fc4_dgrad_direct_kernel(const Fc4DgradArgs a) {
+  __shared__ float red[8][1024];
+  fc4_dgrad_body(a, red, blockIdx.x, blockIdx.y);
 }
 
 inline hipError_t launch_fc4_dgrad_direct(const Fc4DgradArgs& a, hipStream_t st) {

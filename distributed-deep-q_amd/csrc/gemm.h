@@ -60,15 +60,18 @@ struct Slots {
   static constexpr int kPer = (kElems + C::kThreads - 1) / C::kThreads;
 };
 
+// The GEMM body on block (bx, by = split, bz = tower) with an LDS image of
+// C::kSmem floats; callable from fused launches (fc4_bwd_kernel) as well as
+// from gemm_f32_kernel.  Threads >= C::kThreads must not enter.
 template <class C, class P>
-__global__ __launch_bounds__(C::kThreads) void gemm_f32_kernel(const P prob) {
+__device__ __forceinline__ void gemm_f32_body(const P& prob, float* smem, int bx, int by,
+                                              int bz) {
   constexpr int BM = C::BM, BN = C::BN, BK = C::BK;
   constexpr int TM = C::TM, TN = C::TN;
   constexpr int LDA = C::LDA, LDB = C::LDB;
   using SA = Slots<C, BM>;
   using SB = Slots<C, BN>;
 
-  __shared__ __attribute__((aligned(16))) float smem[C::kSmem];
   float* As = smem;                    // [2][BK][LDA]
   float* Bs = smem + 2 * BK * LDA;     // [2][BK][LDB]
 
@@ -80,11 +83,11 @@ __global__ __launch_bounds__(C::kThreads) void gemm_f32_kernel(const P prob) {
   const int wm = (w2 / C::WN) * (BM / C::WM);
   const int wn = (w2 % C::WN) * (BN / C::WN);
 
-  const int z = blockIdx.z;
-  const int split = blockIdx.y;
+  const int z = bz;
+  const int split = by;
   const int tiles_n = (prob.N + BN - 1) / BN;
-  const int tm = blockIdx.x / tiles_n;
-  const int tn = blockIdx.x % tiles_n;
+  const int tm = bx / tiles_n;
+  const int tn = bx % tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int kbeg = split * prob.ksplit_len;
   const int kend = min(prob.K, kbeg + prob.ksplit_len);
@@ -227,6 +230,12 @@ __global__ __launch_bounds__(C::kThreads) void gemm_f32_kernel(const P prob) {
 #pragma unroll
     for (int j = 0; j < TN; ++j)
       prob.epilogue(z, split, m0 + wm + 32 * i, n0 + wn + 32 * j, acc[i][j], lane);
+}
+
+template <class C, class P>
+__global__ __launch_bounds__(C::kThreads) void gemm_f32_kernel(const P prob) {
+  __shared__ __attribute__((aligned(16))) float smem[C::kSmem];
+  gemm_f32_body<C, P>(prob, smem, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
 // Row of accumulator register r for a lane (see above).

@@ -1051,6 +1051,22 @@ static WgradDArgs wgradd_args(const P& p, int B, int G) {
   return a;
 }
 
+// fc4 data gradient (blocks [0, nd): fc4_dgrad_body, 512 threads) beside the
+// fc4 weight gradient (blocks [nd, ...): the GEMM engine's FcWgrad, 256
+// threads; the other 4 waves end at once, which s_barrier does not wait for)
+__global__ __launch_bounds__(512) void fc4_bwd_kernel(const Fc4DgradArgs d, const FcWgrad w, int nd,
+                                                      int ndx) {
+  constexpr int kLds = 8 * 1024 > CfgFcW::kSmem ? 8 * 1024 : CfgFcW::kSmem;
+  __shared__ __attribute__((aligned(16))) float smem[kLds];
+  const int bid = blockIdx.x;
+  if (bid < nd) {
+    fc4_dgrad_body(d, reinterpret_cast<float(*)[1024]>(smem), bid % ndx, bid / ndx);
+    return;
+  }
+  if (threadIdx.x >= CfgFcW::kThreads) return;
+  gemm_f32_body<CfgFcW, FcWgrad>(w, smem, bid - nd, 0, 0);
+}
+
 hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
                           void (*mark)(void*, const char*), void* marg, bool out) {
   const ParamLayout& L = nb.L;
@@ -1161,7 +1177,24 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     ++nev;
     return e;
   };
-  {  // fc4 dgrad -> dconv3
+  // fc4 dgrad and fc4 wgrad both need only dh4 (the head's output): one
+  // launch runs them side by side (dgrad blocks first -- they feed conv3),
+  // instead of two serial latency-bound launches.
+  const bool fc4_fused = !concurrent && !mark && !(nb.variant & 8);
+  if (fc4_fused) {
+    Fc4DgradArgs f;
+    f.B = B; f.K = 64 * s4 * s4; f.s4 = s4; f.fS4sq = FastDiv(s4 * s4); f.fS4 = FastDiv(s4);
+    f.dh4 = nb.dh4; f.w4 = nb.theta[0] + L.w[3]; f.mask3 = nb.mask3; f.dconv3 = nb.dconv3;
+    FcWgrad w;
+    w.M = kFc4; w.N = 64 * s4 * s4; w.K = B; w.ksplit_len = ((B + 31) / 32) * 32;
+    w.dh4 = nb.dh4; w.x = nb.pool3[0]; w.gw4 = nb.grad + L.w[3];
+    const int ndx = f.K / 32, nd = ndx * ((B + 31) / 32);
+    const int nw = ((kFc4 + CfgFcW::BM - 1) / CfgFcW::BM) * ((w.N + CfgFcW::BN - 1) / CfgFcW::BN);
+    hipLaunchKernelGGL(fc4_bwd_kernel, dim3(nd + nw), dim3(512), 0, s, f, w, nd, ndx);
+    CHECK_LAUNCH(hipGetLastError());
+    if (fc4_done) CHECK_LAUNCH(fc4_done(fc4_done_arg));
+  }
+  if (!fc4_fused) {  // fc4 dgrad -> dconv3
     FcDgrad p;
     p.M = B; p.N = 64 * s4 * s4; p.K = kFc4; p.ksplit_len = kFc4;
     p.s4 = s4; p.s4sq = s4 * s4; p.fS4sq = FastDiv(s4 * s4); p.fS4 = FastDiv(s4);
@@ -1177,7 +1210,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
       CHECK_LAUNCH(launch_gemm<CfgFcD>(p, 1, 1, s));
     }
   }
-  {  // fc4 wgrad
+  if (!fc4_fused) {  // fc4 wgrad
     FcWgrad p;
     p.M = kFc4; p.N = 64 * s4 * s4; p.K = B; p.ksplit_len = ((B + 31) / 32) * 32;
     p.dh4 = nb.dh4; p.x = nb.pool3[0]; p.gw4 = nb.grad + L.w[3];

@@ -14,7 +14,7 @@ import sys
 SHORT = [("sample_gather_kernel", "sample"), ("direct_conv_kernel<4, 32, 7", "c1f"),
          ("direct_conv_kernel<32, 64, 5", "c2f"), ("direct_conv_kernel<64, 64, 3, 8, 8, 2, 2, false", "c3f"),
          ("fc4_fwd_direct", "fc4f"), ("fc4_head", "head"), ("fc4_dgrad_direct", "fc4d"),
-         ("FcWgrad", "fc4w"), ("wgradd_kernel<64, 64, 3", "c3w"),
+         ("fc4_bwd_kernel", "fc4bwd"), ("FcWgrad", "fc4w"), ("wgradd_kernel<64, 64, 3", "c3w"),
          ("direct_conv_kernel<64, 64, 3, 8, 8, 2, 2, true", "c3d"), ("wgradd_kernel<32, 64, 5", "c2w"),
          ("direct_conv_kernel<64, 32, 5", "c2d"), ("wgrad1_kernel", "c1w"),
          ("wgrad_reduce_kernel", "wred"), ("apply_kernel", "apply")]
