@@ -241,10 +241,19 @@ class DeepQNet:
         self._check(self.lib.ddq_replay_import(self.ctx, ptr(st), ptr(ac), ptr(rw), ptr(nt),
                                                ac.size, int(head), int(valid)))
 
-    def replay_export(self):
+    def replay_export(self, state_out=None):
+        """Ring contents; ``state_out`` (e.g. a memory map of the replay file's
+        state block) receives the states in place."""
         _, _, cap = self.replay_info()
         S = self.frame
-        st = np.empty((cap, NFRAME, S, S), np.uint8)
+        if state_out is not None:
+            if state_out.shape != (cap, NFRAME, S, S) or state_out.dtype != np.uint8 or \
+                    not state_out.flags.c_contiguous:
+                raise ValueError("state_out must be a C-contiguous u8 array of shape %s"
+                                 % ((cap, NFRAME, S, S),))
+            st = state_out
+        else:
+            st = np.empty((cap, NFRAME, S, S), np.uint8)
         ac = np.empty(cap, np.uint8)
         rw = np.empty(cap, np.int16)
         nt = np.empty(cap, np.uint8)

@@ -16,8 +16,15 @@ When the dataset is attached to a ``BaristaNet`` (``net.add_dataset``) the
 ring moves into that net's GPU context and ``sample_direct`` on the net's own
 minibatch arrays gathers straight into the network's device input (no host
 round trip), which is what the reference's zero-copy MEMORY_DATA binding did.
-Persistence: ``save()`` / ``__del__`` write ``filename`` (npz with the
-reference's dataset names) and a non-overwrite open reloads it.
+Persistence (replay.py:23-45 reopen, :185-192 persist on ``__del__``):
+``save()`` / ``close()`` / ``__del__`` write ``filename`` as the reference's
+HDF5 file (``ddq.h5lite``: same datasets, dtypes and head/valid attributes,
+readable by h5py and by the reference itself), the state block exported
+straight into a memory map of the file; a non-overwrite open of an existing
+file -- one the reference wrote, or one written here -- resumes from it,
+keeping the file's size with the reference's warning.  A file holding none of
+the four datasets is replaced, as the reference creates them.  (An ``.npz``
+written by earlier versions of this package is still read.)
 """
 from __future__ import annotations
 
@@ -26,6 +33,7 @@ import random
 
 import numpy as np
 
+from . import h5lite
 from .net import DeepQNet
 
 
@@ -39,8 +47,11 @@ class ReplayDataset:
             raise ValueError("state_shape must be (4, S, S), got %s" % (self.state_shape,))
         loaded = None
         if filename and not overwrite and os.path.exists(filename):
-            with np.load(filename, allow_pickle=False) as f:
-                loaded = {k: f[k] for k in f.files}
+            loaded = _load_ring(filename)
+        if loaded is not None:
+            if loaded["state"].shape[1:] != self.state_shape:
+                raise ValueError("%s holds states of shape %s, not %s"
+                                 % (filename, loaded["state"].shape[1:], self.state_shape))
             if loaded["state"].shape[0] != dset_size:
                 print("Warning: dataset loaded from %s is of size %d, not %d as requested. "
                       "Using existing size." % (filename, loaded["state"].shape[0], dset_size))
@@ -127,12 +138,14 @@ class ReplayDataset:
         return st, ac, rw, ns, nt
 
     def save(self):
+        """Persist the ring as the reference's HDF5 file (replay.py:185-192)."""
         if not self.filename:
             return
-        st, ac, rw, nt = self._net.replay_export()
-        head, valid, _ = self._net.replay_info()
-        with open(self.filename, "wb") as fp:
-            np.savez(fp, state=st, action=ac, reward=rw, non_terminal=nt, head=head, valid=valid)
+        head, valid, cap = self._net.replay_info()
+        S = self.state_shape[1]
+        # states: device -> memory map of the file's state block, one copy
+        h5lite.write_replay(self.filename, lambda mm: self._net.replay_export(state_out=mm)[1:],
+                            head=head, valid=valid, shape=(cap, 4, S, S))
 
     def close(self):
         if getattr(self, "_net", None) is not None and self._net.ctx:
@@ -148,3 +161,14 @@ class ReplayDataset:
             self.close()
         except Exception:
             pass
+
+
+def _load_ring(filename):
+    """The reference's HDF5 replay file (or a legacy npz) -> ring dict, or None
+    when the file holds no replay datasets."""
+    with open(filename, "rb") as fp:
+        magic = fp.read(8)
+    if magic[:2] == b"PK":
+        with np.load(filename, allow_pickle=False) as f:
+            return {k: f[k] for k in f.files}
+    return h5lite.read_replay(filename, mmap_state=True)

@@ -57,6 +57,87 @@ def test_replay_dataset_dropin_matches_oracle(tmp_path):
     ds2.close()
 
 
+def test_replay_dataset_resumes_reference_files(tmp_path):
+    """F1: the drop-in opens files the reference's replay.py persisted
+    (fixtures: oracle/gen_hdf5_golden.py), gathers exactly what the reference
+    gathered from them, and persists a file that reads back identically."""
+    import shutil
+    from ddq import h5lite
+    from ddq.replay import ReplayDataset
+    S = 16
+    want = np.load(os.path.join(GOLD, "h5_ref_s16.npz"))
+    p = str(tmp_path / "ref.hdf5")
+    shutil.copy(os.path.join(GOLD, "h5_ref_s16.hdf5"), p)
+    ds = ReplayDataset(p, (4, S, S), dset_size=12, batch_size=4)
+    assert (ds.head, ds.valid) == (int(want["head"]), int(want["valid"]))
+    st, ac, rw, nt = ds._net.replay_export()
+    for got, k in ((st, "state"), (ac, "action"), (rw, "reward"), (nt, "non_terminal")):
+        np.testing.assert_array_equal(got, want[k], err_msg=k)
+    ds.close()
+
+    f = np.load(os.path.join(GOLD, "h5_resume.npz"))
+    p = str(tmp_path / "resume.hdf5")
+    shutil.copy(os.path.join(GOLD, "h5_resume_out.hdf5"), p)
+    B = len(f["idx"])
+    ds = ReplayDataset(p, (4, S, S), dset_size=10, batch_size=B)
+    assert (ds.head, ds.valid) == (int(f["fin_head"]), int(f["fin_valid"]))
+    ds.draw_indices = lambda n: [int(i) for i in f["idx"]]     # the reference's scripted draw
+    out = [np.zeros((B, 4, S, S), np.float32), np.zeros((B, 4, 1, 1), np.float32),
+           np.zeros((B, 1, 1, 1), np.float32), np.zeros((B, 4, S, S), np.float32),
+           np.zeros((B, 1, 1, 1), np.float32)]
+    ds.sample_direct(*out, B)
+    for got, k in zip(out, ("state", "action", "reward", "next_state", "non_terminal")):
+        np.testing.assert_array_equal(got, f["out_" + k], err_msg=k)
+    ds.close()                                   # persists (replay.py:185-192)
+    got = h5lite.read_replay(p)
+    for k in ("state", "action", "reward", "non_terminal", "head", "valid"):
+        np.testing.assert_array_equal(got[k], f["fin_" + k], err_msg=k)
+
+
+def test_policy_evaluator_and_q_convergence_match_oracle(tmp_path):
+    """F4: evaluation.py's greedy evaluation (batched select_action on the
+    GPU) scores exactly what the float64 oracle's action choices score, and
+    q_convergence's mean Q_out matches the oracle forward on the same draws."""
+    from ddq import evaluation
+    from ddq.barista.baristanet import BaristaNet
+    from ddq.replay import ReplayDataset
+    from ddq.expgain import synthetic_transitions
+
+    class OracleNet:
+        def __init__(self, B, S, pQ):
+            self.batch_size, self.pQ = B, pQ
+            self.state = np.zeros((B, 4, S, S), np.float32)
+
+        def select_action(self, states, batch_size=1):
+            return ref.select_action(np.asarray(states, np.float32), self.pQ)
+
+    S = 16
+    net = BaristaNet(os.path.join(GOLD, "deepq16.prototxt"), None, None)
+    B = net.batch_size
+    pQ = ref.init_params(S, seed=21)
+    gpu = evaluation.PolicyEvaluator(None, None, net=net, seed=9, max_moves=300)
+    cpu = evaluation.PolicyEvaluator(None, None, net=OracleNet(B, S, pQ), seed=9, max_moves=300)
+    assert gpu.evaluate(pQ, 40) == cpu.evaluate(None, 40)
+
+    ds = ReplayDataset(str(tmp_path / "q.hdf5"), (4, S, S), dset_size=300, batch_size=B)
+    st, ac, rw, nt = synthetic_transitions(300, S, seed=4)
+    r = ref.ReplayRef((4, S, S), 300)
+    for i in range(300):
+        ds.add_experience(int(ac[i]), int(rw[i]), st[i] if nt[i] else None)
+        r.add_experience(int(ac[i]), int(rw[i]), st[i] if nt[i] else None)
+    net.add_dataset(ds)
+    random.seed(13)
+    got = evaluation.evaluate_model(net, pQ, 3)
+    random.seed(13)
+    want = 0.0
+    p64 = {k: [np.asarray(w, np.float64) for w in v] for k, v in pQ.items()}
+    for _ in range(3):
+        x = r.gather(ds.draw_indices(B))[0]
+        want += ref.net_forward(np.asarray(x, np.float64), p64, "Q")["out"].mean()
+    assert got == pytest.approx(want / 3, rel=1e-4, abs=1e-7)
+    ds.close()
+
+
 @pytest.fixture
 def param_server():
     from ddq.param_server import ParamServer
