@@ -59,9 +59,9 @@ KERNEL_SYMBOL = {
     "head": "ddq::fc4_head_kernel",
     "fc4_dgrad": "ddq::fc4_dgrad_direct_kernel",
     "fc4_wgrad": "void ddq::gemm_f32_kernel<ddq::GemmCfg<64, 64, 32, 2, 2, 1>, ddq::FcWgrad>",
-    "conv3_wgrad": "void ddq::wgradd_kernel<64, 64, 3, 1>",
+    "conv3_wgrad": "void ddq::wgradd_kernel<64, 64, 3, 1",
     "conv3_dgrad": "void ddq::direct_conv_kernel<64, 64, 3, 4, 8, 1, 2, true",
-    "conv2_wgrad": "void ddq::wgradd_kernel<32, 64, 5, 2>",
+    "conv2_wgrad": "void ddq::wgradd_kernel<32, 64, 5, 2",
     "conv2_dgrad": "void ddq::direct_conv_kernel<64, 32, 5,",
     "conv1_wgrad": "ddq::wgrad1_kernel",
     "wgrad_reduce": "ddq::wgrad_reduce_kernel",

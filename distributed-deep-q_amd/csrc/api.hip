@@ -751,7 +751,7 @@ int ddq_read_pool_mask(ddq_ctx* c, int32_t layer, uint8_t* dst, int64_t n) {
   const uint8_t* src = layer == 1 ? c->nb.mask1 : (layer == 2 ? c->nb.mask2 : c->nb.mask3);
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   HIP_TRY(c, scopy(c, tmp.data(), src, cnt, hipMemcpyDeviceToHost));
-  if (layer == 3) {            // pool3 routing is stored in Caffe order already
+  if (layer == 3 && c->nb.conv_impl != 1) {   // GEMM engine: pool3 routing in Caffe order
     memcpy(dst, tmp.data(), cnt);
     return DDQ_OK;
   }

@@ -66,8 +66,13 @@ struct DirectArgs {
   const float* wk[2];        // Wk[co][tap][ci] of the layer
   const float* bias[2];      // fwd only
   float* out[2];             // fwd: pooled NHWC (B,H/2,W/2,N), or NCHW if nchw
-  int nchw;                  // fwd: 1 = pooled output / mask in Caffe (B,N,H/2,W/2) order
+  int nchw;                  // fwd: 1 = pooled output in Caffe (B,N,H/2,W/2) order
+  int mask_nhwc;             // fwd, nchw: routing bytes stay NHWC (B,H/2,W/2,N)
   uint8_t* mask[2];          // fwd: routing bytes (nullable)
+  // dgrad source given pooled: in = (B,H/2,W/2,CP) gradient of the pool
+  // output, in_route = its NHWC routing bytes; the patch is staged as the
+  // un-pooled gradient (value at the routed quadrant, 0 elsewhere)
+  const uint8_t* in_route;
   const uint8_t* pmask;      // dgrad: previous pool's routing bytes (B,H,W,N)
   float* pdconv;             // dgrad: previous layer's pre-pool gradient (B,2H,2W,N)
 };
@@ -274,8 +279,22 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void direct_conv_kernel(const Di
       const int py = pix / C::PW, px = pix % C::PW;
       const int gy = y0 - a.pad + py, gx = x0 - a.pad + px;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if ((unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W)
-        v = *reinterpret_cast<const float4*>(in + (((size_t)b * a.H + gy) * a.W + gx) * CP + 4 * c4);
+      if ((unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W) {
+        if (DGRAD && a.in_route) {   // pooled source: expand through the routing bytes
+          const size_t o =
+              (((size_t)b * (a.H >> 1) + (gy >> 1)) * (a.W >> 1) + (gx >> 1)) * CP + 4 * c4;
+          const float4 u = *reinterpret_cast<const float4*>(in + o);
+          const uint32_t m = *reinterpret_cast<const uint32_t*>(a.in_route + o);
+          const uint32_t q = ((gy & 1) << 1) | (gx & 1);
+          v.x = (m & 0xff) == q ? u.x : 0.f;
+          v.y = ((m >> 8) & 0xff) == q ? u.y : 0.f;
+          v.z = ((m >> 16) & 0xff) == q ? u.z : 0.f;
+          v.w = (m >> 24) == q ? u.w : 0.f;
+        } else {
+          v = *reinterpret_cast<const float4*>(in + (((size_t)b * a.H + gy) * a.W + gx) * CP +
+                                               4 * c4);
+        }
+      }
       float* dst = patch + py * C::RS + px * C::CS + 4 * c4;
       if (CP >= 8) {
         *reinterpret_cast<float4*>(dst) = v;
@@ -464,10 +483,10 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void direct_conv_kernel(const Di
           if (v2 > mx) { mx = v2; arg = 2; }
           if (v3 > mx) { mx = v3; arg = 3; }
           const bool pos = mx > 0.f;
-          const size_t o = a.nchw ? (((size_t)b * N + n) * Hp + pyy) * Wp + pxx
-                                  : (((size_t)b * Hp + pyy) * Wp + pxx) * N + n;
+          const size_t onhwc = (((size_t)b * Hp + pyy) * Wp + pxx) * N + n;
+          const size_t o = a.nchw ? (((size_t)b * N + n) * Hp + pyy) * Wp + pxx : onhwc;
           outz[o] = pos ? mx : 0.f;
-          if (maskz) maskz[o] = (uint8_t)(pos ? arg : 4);
+          if (maskz) maskz[a.mask_nhwc ? onhwc : o] = (uint8_t)(pos ? arg : 4);
         }
       } else {
         const int W2 = 2 * a.W;

@@ -74,30 +74,39 @@ __device__ void draw_sorted(const ReplayMeta* meta, int B, uint64_t seed, uint64
   const int t = threadIdx.x;
   const int64_t valid = meta->valid;
   const int64_t forbid = meta->head - 1;   // -1 when head == 0: nothing forbidden
-  auto draw = [&](int round) -> int64_t {
-    uint64_t r = splitmix64(seed ^ splitmix64(ctr * 0x100000001B3ull + (uint64_t)t * 0x9E37ull +
+  // draw for sorted position `pos` in redraw round `round`
+  auto draw_at = [&](int round, int pos) -> int64_t {
+    uint64_t r = splitmix64(seed ^ splitmix64(ctr * 0x100000001B3ull + (uint64_t)pos * 0x9E37ull +
                                               ((uint64_t)round << 40)));
     return (int64_t)__umul64hi(r, (uint64_t)valid);
   };
+  auto draw = [&](int round) -> int64_t { return draw_at(round, t); };
   if (B <= 64) {
-    // one wave, registers + cross-lane shuffles: no workgroup barriers.  The
-    // sorted set equals the general path's (padding sorts to the end and the
-    // redraw of sorted position t uses the same hash input t).
+    // One wave, no sort network: lane t keeps its draw and computes its
+    // sorted position by comparing against every lane (readlane, no LDS
+    // round trips -- the 21-stage shuffle bitonic sort it replaces was a
+    // chain of ds_bpermute latencies).  Ties rank by lane, so the positions
+    // a duplicate group occupies are the bitonic path's; the later ones are
+    // redrawn with their position as hash input, exactly as there (and as
+    // the multi-wave path below), so the sorted set is unchanged.  Indices
+    // fit 32 bits (valid < 2^31); head-1 = -1 never matches a draw.
     if (t < 64) {
-      int64_t v = (t < B) ? draw(0) : INT64_MAX;
+      uint32_t v = (t < B) ? (uint32_t)draw_at(0, t) : 0xFFFFFFFFu;
+      const uint32_t fb = (uint32_t)forbid;
+      int r = t;
       for (int round = 1; round < 256; ++round) {
-        for (int k = 2; k <= 64; k <<= 1)
-          for (int j = k >> 1; j > 0; j >>= 1) {
-            const int64_t o = __shfl_xor(v, j);
-            const bool up = (t & k) == 0, lo = (t & j) == 0;
-            v = (lo == up) ? (v < o ? v : o) : (v < o ? o : v);
-          }
-        const int64_t prev = __shfl_up(v, 1);
-        const bool bad = t < B && (v == forbid || (t > 0 && v == prev));
+        int less = 0, eqlo = 0;
+        for (int k = 0; k < B; ++k) {
+          const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)v, k);
+          less += o < v;
+          eqlo += (o == v) & (k < t);
+        }
+        r = less + eqlo;
+        const bool bad = t < B && (v == fb || eqlo > 0);
         if (__ballot(bad) == 0) break;
-        if (bad) v = draw(round);
+        if (bad) v = (uint32_t)draw_at(round, r);
       }
-      cand[t] = v;
+      if (t < B) cand[r] = (int64_t)v;
     }
     __syncthreads();
     return;
@@ -1048,6 +1057,7 @@ static WgradDArgs wgradd_args(const P& p, int B, int G) {
   a.B = B; a.H = p.H; a.W = p.W; a.G = G;
   a.RPG = (B * p.H + G - 1) / G;
   a.NP = p.NP; a.dconv = p.dconv; a.in = p.in; a.part = p.part;
+  a.droute = nullptr;
   return a;
 }
 
@@ -1125,6 +1135,7 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     if (nb.conv_impl == 1) {
       DirectArgs d = direct_fwd_args(p.in, p.wk, p.bias, p.out, p.mask, B, H, 1);
       d.nchw = 1;
+      d.mask_nhwc = 1;   // routing bytes NHWC: the backward expands dpool3 through them
       // 3 tap groups: 512 output blocks per tower would leave one wave per SIMD
       CHECK_LAUNCH((launch_direct<64, 64, 3, 8, 8, 2, 2, false, false, 3>(d, nz, s)));
     } else {
@@ -1185,6 +1196,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     Fc4DgradArgs f;
     f.B = B; f.K = 64 * s4 * s4; f.s4 = s4; f.fS4sq = FastDiv(s4 * s4); f.fS4 = FastDiv(s4);
     f.dh4 = nb.dh4; f.w4 = nb.theta[0] + L.w[3]; f.mask3 = nb.mask3; f.dconv3 = nb.dconv3;
+    f.pooled = nb.conv_impl == 1;
     FcWgrad w;
     w.M = kFc4; w.N = 64 * s4 * s4; w.K = B; w.ksplit_len = ((B + 31) / 32) * 32;
     w.dh4 = nb.dh4; w.x = nb.pool3[0]; w.gw4 = nb.grad + L.w[3];
@@ -1199,12 +1211,14 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     p.M = B; p.N = 64 * s4 * s4; p.K = kFc4; p.ksplit_len = kFc4;
     p.s4 = s4; p.s4sq = s4 * s4; p.fS4sq = FastDiv(s4 * s4); p.fS4 = FastDiv(s4);
     p.dh4 = nb.dh4; p.w4 = nb.theta[0] + L.w[3]; p.mask3 = nb.mask3; p.dconv3 = nb.dconv3;
+    p.pooled = nb.conv_impl == 1;
     CHECK_LAUNCH(fork());   // side: fc4 wgrad needs only dh4 (head) -> fork before dgrad
     M("fc4_dgrad");
     if (!(nb.variant & 8)) {   // register-direct (bit 8: LDS GEMM engine, A/B)
       Fc4DgradArgs f;
       f.B = B; f.K = p.N; f.s4 = s4; f.fS4sq = p.fS4sq; f.fS4 = p.fS4;
       f.dh4 = nb.dh4; f.w4 = p.w4; f.mask3 = nb.mask3; f.dconv3 = nb.dconv3;
+      f.pooled = p.pooled;
       CHECK_LAUNCH(launch_fc4_dgrad_direct(f, s));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgFcD>(p, 1, 1, s));
@@ -1232,7 +1246,11 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     p.NP = nb.wnp[2]; p.dconv = nb.dconv3; p.in = nb.pool2[0]; p.part = nb.wpart + nb.wpart_off[2];
     M("conv3_wgrad");
     if (nb.conv_impl == 1) {
-      CHECK_LAUNCH((launch_wgradd<64, 64, 3, 1>(wgradd_args(p, B, nb.wsplits[2]), sw)));
+      // dconv3 holds the pooled gradient (fc4 dgrad, pooled mode): expanded
+      // through pool3's routing bytes while the rows are staged
+      WgradDArgs wa = wgradd_args(p, B, nb.wsplits[2]);
+      wa.droute = nb.mask3;
+      CHECK_LAUNCH((launch_wgradd<64, 64, 3, 1, true>(wa, sw)));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgW3>(p, 1, ns, sw));
     }
@@ -1246,6 +1264,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     M("conv3_dgrad");
     if (nb.conv_impl == 1) {
       DirectArgs d = direct_dgrad_args(nb.dconv3, p.wk, nb.mask2, nb.dconv2, B, H, 1);
+      d.in_route = nb.mask3;   // pooled dconv3, expanded while the patch is staged
       // 4x8-pixel tiles (256 workgroups instead of 128: -2.5 us) with the B
       // operand straight from L2 (register-B, no weight ring: -2.5 us more)
       CHECK_LAUNCH((launch_direct<64, 64, 3, 4, 8, 1, 2, true, false, 3, true>(d, 1, s)));

@@ -293,8 +293,9 @@ struct FcDgrad {
   FastDiv fS4sq, fS4;
   const float* dh4;                 // (B,512)
   const float* w4;                  // (512, N)
-  const uint8_t* mask3;             // NCHW (B,64,S4,S4)
-  float* dconv3;                    // NHWC (B,2S4,2S4,64)
+  const uint8_t* mask3;             // NCHW (B,64,S4,S4); unused when pooled
+  float* dconv3;                    // NHWC (B,2S4,2S4,64), or pooled NHWC (B,S4,S4,64)
+  int pooled;                       // as Fc4DgradArgs::pooled
 
   struct ACtx { int b; bool ok; };
   __device__ ACtx actx(int, int m) const { return {m, m < M}; }
@@ -319,6 +320,10 @@ struct FcDgrad {
     for (int r = 0; r < 16; ++r) {
       const int b = mb + acc_row(r, lane);
       if (b >= M) continue;
+      if (pooled) {
+        dconv3[((size_t)b * s4sq + p) * 64 + ch] = acc[r];
+        continue;
+      }
       const int mk = mask3[(size_t)b * N + kc];          // NCHW: kc = ch*S4^2 + p
       const float v = acc[r];
       float* base = dconv3 + (((size_t)b * H3 + 2 * py) * H3 + 2 * px) * 64 + ch;

@@ -26,9 +26,10 @@ struct WgradDArgs {
   int B, H, W;              // layer grid (input and dconv share H x W)
   int G, RPG;               // row groups (= slabs) and rows per group
   int NP;                   // slab pitch
-  const float* dconv;       // NHWC (B,H,W,COUT)
+  const float* dconv;       // NHWC (B,H,W,COUT); PSRC: pooled (B,H/2,W/2,COUT)
   const float* in;          // NHWC (B,H,W,CIN)
   float* part;              // [G][COUT][NP]
+  const uint8_t* droute;    // PSRC: NHWC routing bytes of the pooled gradient
 };
 
 template <int CIN, int PAD>
@@ -38,7 +39,10 @@ struct WgradDGeom {
   static __host__ __device__ int region(int W) { return in_floats(W) + ((W + 1) >> 1) * 64; }
 };
 
-template <int CIN, int COUT, int KS, int PAD>
+// PSRC: dconv is given pooled (the gradient of the 2x2 max-pool output plus
+// its routing bytes, as fc4's data gradient leaves it) and expanded while the
+// rows are staged: value at the routed quadrant, 0 at the other three.
+template <int CIN, int COUT, int KS, int PAD, bool PSRC = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void wgradd_kernel(
     const WgradDArgs a) {
   constexpr int NCB = CIN / 32;
@@ -87,36 +91,53 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
   const int rows_total = a.B * H;
   const __amdgpu_buffer_rsrc_t rs_in =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.in, (short)0, rows_total * W * CIN * 4, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rs_d = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.dconv, (short)0, rows_total * W * COUT * 4, 0x00020000);
+  const int dsz = PSRC ? (rows_total / 2) * (W / 2) * COUT : rows_total * W * COUT;
+  const __amdgpu_buffer_rsrc_t rs_d =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.dconv, (short)0, dsz * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_m =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.droute, (short)0, PSRC ? dsz : 0, 0x00020000);
   constexpr int kOOB = 0x7ff00000;   // beyond any tensor here: reads 0
-  struct Regs { float4 i[4], d[4]; };
+  struct Regs { float4 i[4], d[4]; uint32_t m[4]; };
   auto load = [&](Regs& g, int row, int base) {
     const int b = row / H, yi = row - b * H + ky - PAD;
     const bool vin = (unsigned)yi < (unsigned)H && row < rows_total;
     const int ib = vin ? (b * H + yi) * W * CIN * 4 : kOOB;
-    const int db = row < rows_total ? (row * W * COUT + cb * 32) * 4 : kOOB;
+    // PSRC: pooled row (b, y/2) of width W/2
+    const int db = row >= rows_total ? kOOB
+                   : PSRC ? ((b * (H >> 1) + ((row - b * H) >> 1)) * (W >> 1) * COUT + cb * 32) * 4
+                          : (row * W * COUT + cb * 32) * 4;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int i = base + lane + 64 * j;
       const int oi = i < nin ? ib + i * 16 : kOOB;
-      const int od = i < nd ? db + ((i >> 3) * COUT + (i & 7) * 4) * 4 : kOOB;
+      const int px = PSRC ? (i >> 4) : (i >> 3);
+      const int od = i < nd ? db + (px * COUT + (i & 7) * 4) * 4 : kOOB;
       auto vi = __builtin_amdgcn_raw_buffer_load_b128(rs_in, oi, 0, 0);
       auto vd = __builtin_amdgcn_raw_buffer_load_b128(rs_d, od, 0, 0);
       g.i[j] = *reinterpret_cast<float4*>(&vi);
       g.d[j] = *reinterpret_cast<float4*>(&vd);
+      if (PSRC) g.m[j] = __builtin_amdgcn_raw_buffer_load_b32(rs_m, od == kOOB ? kOOB : od >> 2, 0, 0);
     }
   };
-  auto store = [&](const Regs& g, int base) {
+  auto store = [&](const Regs& g, int base, int row) {
     float4* dst = reinterpret_cast<float4*>(rin + PAD * CIN);
     float4* dd = reinterpret_cast<float4*>(rd);
+    const uint32_t qy = PSRC ? (((row - (row / H) * H) & 1) << 1) : 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int i = base + lane + 64 * j;
       if (i < nin) dst[i] = g.i[j];
       if (i < nd) {
-        dd[i] = g.d[j];
-        bsum.x += g.d[j].x; bsum.y += g.d[j].y; bsum.z += g.d[j].z; bsum.w += g.d[j].w;
+        float4 d = g.d[j];
+        if (PSRC) {
+          const uint32_t q = qy | ((i >> 3) & 1), m = g.m[j];
+          d.x = (m & 0xff) == q ? d.x : 0.f;
+          d.y = ((m >> 8) & 0xff) == q ? d.y : 0.f;
+          d.z = ((m >> 16) & 0xff) == q ? d.z : 0.f;
+          d.w = (m >> 24) == q ? d.w : 0.f;
+        }
+        dd[i] = d;
+        bsum.x += d.x; bsum.y += d.y; bsum.z += d.z; bsum.w += d.w;
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -178,11 +199,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
     int row = r0 + w;
     if (row < r1) load(ga, row, 0);
     for (; row < r1; row += 8) {
-      store(ga, 0);
+      store(ga, 0, row);
       load(gb, row + 4, 0);          // rows past r1 only read (bounded), never staged
       compute();
       if (row + 4 >= r1) break;
-      store(gb, 0);
+      store(gb, 0, row + 4);
       load(ga, row + 8, 0);
       compute();
     }
@@ -190,7 +211,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void w
     Regs g;
     const int nmax = nin > nd ? nin : nd;
     for (int row = r0 + w; row < r1; row += 4) {
-      for (int base = 0; base < nmax; base += 256) { load(g, row, base); store(g, base); }
+      for (int base = 0; base < nmax; base += 256) { load(g, row, base); store(g, base, row); }
       compute();
     }
   }
@@ -245,12 +266,12 @@ inline void wgradd_groups(int rows, int nts, int* G, int* RPG) {
   *G = (rows + rpg - 1) / rpg;
 }
 
-template <int CIN, int COUT, int KS, int PAD>
+template <int CIN, int COUT, int KS, int PAD, bool PSRC = false>
 inline hipError_t launch_wgradd(const WgradDArgs& a, hipStream_t st) {
   const size_t shm = wgradd_smem_bytes<CIN, PAD>(a.W);
   const int g8 = (a.G + 7) / 8 * 8;
-  hipLaunchKernelGGL((wgradd_kernel<CIN, COUT, KS, PAD>), dim3(g8 * (COUT / 32) * KS), dim3(256),
-                     shm, st, a);
+  hipLaunchKernelGGL((wgradd_kernel<CIN, COUT, KS, PAD, PSRC>), dim3(g8 * (COUT / 32) * KS),
+                     dim3(256), shm, st, a);
   return hipGetLastError();
 }
 
