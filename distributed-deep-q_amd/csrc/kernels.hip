@@ -573,17 +573,30 @@ __global__ __launch_bounds__(512) void fc4_head_kernel(
   const size_t stride = (size_t)2 * B * kFc4;
   float h[2];
   float q[8];
+  // split-K partial sums of both towers: 16 independent loads per round
+  float acc2[2] = {0.f, 0.f};
+  {
+    const float* p0 = part + (size_t)b * kFc4 + n;
+    const float* p1 = part + ((size_t)B + b) * kFc4 + n;
+    for (int s = 0; s < splits; s += 8) {
+      float v[2][8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {            // clamped, unconditional loads
+        const int su = min(s + u, splits - 1);
+        v[0][u] = p0[su * stride];
+        v[1][u] = p1[su * stride];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const bool in = s + u < splits;
+        acc2[0] += in ? v[0][u] : 0.f;
+        acc2[1] += in ? v[1][u] : 0.f;
+      }
+    }
+  }
 #pragma unroll
   for (int z = 0; z < 2; ++z) {
-    const float* p = part + ((size_t)z * B + b) * kFc4 + n;
-    float acc = 0.f;
-    int s = 0;
-    for (; s + 4 <= splits; s += 4) {
-      const float v0 = p[(s + 0) * stride], v1 = p[(s + 1) * stride];
-      const float v2 = p[(s + 2) * stride], v3 = p[(s + 3) * stride];
-      acc += v0; acc += v1; acc += v2; acc += v3;
-    }
-    for (; s < splits; ++s) acc += p[s * stride];
+    const float acc = acc2[z];
     const float* th = z ? thp : thq;
     const float v = acc + th[b4_off + n];
     h[z] = v > 0.f ? v : 0.f;
@@ -655,12 +668,27 @@ __device__ void head_sums(int hb, int B, const float* __restrict__ dqbuf,
   }
   const int j = hb * 64 + lane;
   float db = 0.f, dw[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int b = g; b < B; b += 4) {
-    const float* d = dqbuf + b * 4;
-    const float hv = h4q[(size_t)b * kFc4 + j];
-    db += dh4[(size_t)b * kFc4 + j];
+  // rounds of 8 batch rows with every load issued first (clamped indices,
+  // dropped in the sums); the sums run in the same order as a plain loop
+  for (int b0 = g; b0 < B; b0 += 32) {
+    float hv[8], dv[8];
+    float4 dq[8];
 #pragma unroll
-    for (int a = 0; a < 4; ++a) dw[a] += d[a] * hv;
+    for (int u = 0; u < 8; ++u) {
+      const int bb = min(b0 + 4 * u, B - 1);
+      hv[u] = h4q[(size_t)bb * kFc4 + j];
+      dv[u] = dh4[(size_t)bb * kFc4 + j];
+      dq[u] = *reinterpret_cast<const float4*>(dqbuf + bb * 4);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (b0 + 4 * u >= B) break;
+      db += dv[u];
+      dw[0] += dq[u].x * hv[u];
+      dw[1] += dq[u].y * hv[u];
+      dw[2] += dq[u].z * hv[u];
+      dw[3] += dq[u].w * hv[u];
+    }
   }
   float* r = red + (g * 64 + lane) * 5;
   r[0] = db;
@@ -719,17 +747,21 @@ __device__ __forceinline__ void apply_book(int64_t* iter, int32_t* opt_init, int
   opt_init[0] = 1;
 }
 
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part,
-                                                           float* __restrict__ grad, WredDims d0,
-                                                           WredDims d1, WredDims d2,
-                                                           int64_t* iter, int32_t* opt_init,
-                                                           int book_period, ReplayMeta* bump,
-                                                           int book_inc, HeadSums hs) {
-  __shared__ float red[4][64];
+// kWredG split groups x 64 columns, four slab loads in flight per thread
+// (8-load rounds and 8 groups in 512-thread blocks both measured slower).
+// Head-sum blocks use the first 256 threads.
+constexpr int kWredG = 4;
+static_assert(kWredG == 4 || kWredG == 8, "slab-reduce groups");
+__global__ __launch_bounds__(64 * kWredG) void wgrad_reduce_kernel(
+    const float* __restrict__ part, float* __restrict__ grad, WredDims d0, WredDims d1,
+    WredDims d2, int64_t* iter, int32_t* opt_init, int book_period, ReplayMeta* bump,
+    int book_inc, HeadSums hs) {
+  __shared__ float red[kWredG][64];
   const int bid = blockIdx.x;
   if (opt_init && bid == 0 && threadIdx.x == 0)
     apply_book(iter, opt_init, book_period, bump, book_inc);
   if (bid >= hs.blk0) {
+    if (threadIdx.x >= 256) return;   // ended waves do not hold up s_barrier
     head_sums(bid - hs.blk0, hs.B, hs.dqbuf, hs.lpart, hs.h4q, hs.dh4, hs.loss, hs.gw5, hs.gb5,
               hs.gb4);
     return;
@@ -744,17 +776,18 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   const size_t stride = (size_t)d.cout * d.np;
   float acc = 0.f;
   int s = g;
-  for (; s + 12 < d.splits; s += 16) {
-    const float v0 = p[s * stride], v1 = p[(s + 4) * stride];
-    const float v2 = p[(s + 8) * stride], v3 = p[(s + 12) * stride];
+  for (; s + 3 * kWredG < d.splits; s += 4 * kWredG) {
+    const float v0 = p[s * stride], v1 = p[(s + kWredG) * stride];
+    const float v2 = p[(s + 2 * kWredG) * stride], v3 = p[(s + 3 * kWredG) * stride];
     acc += v0; acc += v1; acc += v2; acc += v3;
   }
-  for (; s < d.splits; s += 4) acc += p[s * stride];
+  for (; s < d.splits; s += kWredG) acc += p[s * stride];
   red[g][threadIdx.x & 63] = acc;
   __syncthreads();
   if (g == 0 && n <= kc) {
     const int l = threadIdx.x;
-    const float v = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
+    float v = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
+    if (kWredG == 8) v += (red[4][l] + red[5][l]) + (red[6][l] + red[7][l]);
     if (n < kc) {
       const int tap = n / d.cin, ci = n % d.cin;
       grad[d.w_off + ((size_t)co * d.cin + ci) * kk + tap] = v;
@@ -1339,7 +1372,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     M("wgrad_reduce");
     HeadSums hs{blk, B, nb.dqbuf, nb.lpart, nb.h4[0], nb.dh4, nb.loss, nb.grad + L.w[4],
                 nb.grad + L.b[4], nb.grad + L.b[3]};
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blk + kFc4 / 64), dim3(256), 0, s, nb.wpart,
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blk + kFc4 / 64), dim3(64 * kWredG), 0, s, nb.wpart,
                        nb.grad, d[0], d[1], d[2], nb.iter, book ? nb.opt_init : nullptr,
                        book_period, book ? bump : nullptr, nb.book_inc, hs);
     CHECK_LAUNCH(hipGetLastError());

@@ -5,9 +5,9 @@
 //
 // conv1 has Cin = 4, so the implicit-GEMM form expands every input pixel 49x
 // through global loads (15 VALU per MFMA measured).  Here one workgroup takes
-// one image band of R rows: the band's dconv rows (R x W x 32) and the input
-// halo (R+6) x (W+6) x 4 are staged in LDS once, then 8 waves run MFMAs
-// straight from LDS: wave ky (0..6) computes the 32 x 28 block
+// one image band of R rows: the input halo (R+6) x (W+6) x 4 is staged in LDS
+// once and the band's dconv rows (W x 32 each) stream through two LDS slots,
+// and 8 waves run MFMAs straight from LDS: wave ky (0..6) computes the 32 x 28 block
 // (co) x (kx, ci) of tap row ky (lane n = kx*4 + ci; lanes 28..31 are padding
 // whose products are dropped), wave 7 the bias column (B = 1).  K = the band's
 // pixels, two per MFMA step.  Output: one fp32 slab per band in the layout
@@ -25,6 +25,13 @@ struct Wgrad1Args {
   float* part;                 // [B * H / R][32][NP]
 };
 
+// The band's dconv rows are streamed through two LDS row slots per half: row
+// r+1 is loaded into registers before row r's MFMAs and stored after them,
+// so only the first row's load is exposed (staging the whole band up front
+// left every CU idle for the band's 64 KB load -- one workgroup per CU and a
+// single wave of workgroups).  Sums run in the same order as before.
+constexpr int kWgrad1Pre = 4;                // float4 of a dconv row per thread (W <= 256)
+
 template <int NH>
 __global__ __launch_bounds__(512 * NH) void wgrad1_kernel(const Wgrad1Args a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -32,11 +39,34 @@ __global__ __launch_bounds__(512 * NH) void wgrad1_kernel(const Wgrad1Args a) {
   const int PW = W + 6;
   const int RS = PW * 4 + 2;                 // odd-ish row stride: rows land on other banks
   float* patch = sm;                         // (R+6) x RS
-  float* dbuf = sm + (((R + 6) * RS + 3) & ~3);   // R*W x 32 (16-B aligned)
   const int tid = threadIdx.x, lane = tid & 63, w = (tid >> 6) & 7, half = tid >> 9;
+  const int ht = tid & 511;                  // thread within the half
+  // this half's two dconv row slots, W x 32 each (16-B aligned)
+  float* dslot = sm + (((R + 6) * RS + 3) & ~3) + half * 2 * W * 32;
   const int split = blockIdx.x;
   const int bands = a.H / R;
   const int b = split / bands, y0 = (split % bands) * R;
+  const int rh = R / NH, rlo = half * rh;   // this half's rows of the band
+  const int nd4 = W * 8;                    // float4 per dconv row
+  const float4* drow = reinterpret_cast<const float4*>(a.dconv + ((size_t)b * a.H + y0) * W * 32);
+  // named registers: a float4 array here was kept in scratch (80 B/lane)
+  float4 p0 = f4zero(), p1 = f4zero(), p2 = f4zero(), p3 = f4zero();
+  static_assert(kWgrad1Pre == 4, "prefetch registers");
+  auto load_row = [&](int r) {
+    const float4* s = drow + (size_t)r * nd4 + ht;
+    if (ht < nd4) p0 = s[0];
+    if (ht + 512 < nd4) p1 = s[512];
+    if (ht + 1024 < nd4) p2 = s[1024];
+    if (ht + 1536 < nd4) p3 = s[1536];
+  };
+  auto store_row = [&](float* dst) {
+    float4* d = reinterpret_cast<float4*>(dst) + ht;
+    if (ht < nd4) d[0] = p0;
+    if (ht + 512 < nd4) d[512] = p1;
+    if (ht + 1024 < nd4) d[1024] = p2;
+    if (ht + 1536 < nd4) d[1536] = p3;
+  };
+  load_row(rlo);
 
   // ---- stage the input halo (zero outside the image) ----
   for (int f = tid; f < (R + 6) * PW; f += 512 * NH) {
@@ -49,10 +79,7 @@ __global__ __launch_bounds__(512 * NH) void wgrad1_kernel(const Wgrad1Args a) {
     d[0] = make_float2(v.x, v.y);
     d[1] = make_float2(v.z, v.w);
   }
-  // ---- stage the band's dconv rows (contiguous in NHWC) ----
-  const float4* src = reinterpret_cast<const float4*>(a.dconv + ((size_t)b * a.H + y0) * W * 32);
-  for (int f = tid; f < R * W * 8; f += 512 * NH)
-    reinterpret_cast<float4*>(dbuf)[f] = src[f];
+  store_row(dslot);
   __syncthreads();
 
   const int l31 = lane & 31, h = lane >> 5;
@@ -60,25 +87,27 @@ __global__ __launch_bounds__(512 * NH) void wgrad1_kernel(const Wgrad1Args a) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   // A[co][k] = dconv[k][co]: lane (co = l31, half h) reads pixel 2s + h
-  const float* pa = dbuf + h * 32 + l31;
-  const int rh = R / NH, rlo = half * rh;           // this half's rows of the band
-  if (w < 7) {
-    // B[k][n] = in[pixel + (ky, kx)][ci], n = kx*4 + ci = l31
-    const float* pb = patch + w * RS + 4 * h + l31;
-    for (int r = rlo; r < rlo + rh; ++r) {
-      const float* ar = pa + r * W * 32;
+  // B[k][n] = in[pixel + (ky, kx)][ci], n = kx*4 + ci = l31 (waves 0..6 = ky);
+  // wave 7: the bias column (B = 1)
+  const float* pb = patch + w * RS + 4 * h + l31;
+  for (int i = 0; i < rh; ++i) {
+    const int r = rlo + i;
+    if (i + 1 < rh) load_row(r + 1);
+    __builtin_amdgcn_sched_barrier(0);   // keep the next row's loads ahead of the MFMAs
+    const float* ar = dslot + (i & 1) * W * 32 + h * 32 + l31;
+    if (w < 7) {
       const float* br = pb + r * RS;
 #pragma unroll 4
       for (int xs = 0; xs < W / 2; ++xs)
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[xs * 64], br[xs * 8], acc, 0, 0, 0);
-    }
-  } else {
-    for (int r = rlo; r < rlo + rh; ++r) {
-      const float* ar = pa + r * W * 32;
+    } else {
 #pragma unroll 4
       for (int xs = 0; xs < W / 2; ++xs)
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[xs * 64], 1.0f, acc, 0, 0, 0);
     }
+    // the other slot was last read in iteration i-1, fenced by its barrier
+    if (i + 1 < rh) store_row(dslot + ((i + 1) & 1) * W * 32);
+    __syncthreads();
   }
   // ---- the two halves' partial sums meet in LDS (fixed order) ----
   if (NH == 2) {
@@ -107,7 +136,8 @@ __global__ __launch_bounds__(512 * NH) void wgrad1_kernel(const Wgrad1Args a) {
 
 inline size_t wgrad1_smem_bytes(int W, int R) {
   const int RS = (W + 6) * 4 + 2;
-  return (size_t)((((R + 6) * RS + 3) & ~3) + R * W * 32) * 4;
+  const int NH = R == 8 ? 2 : 1;             // two row slots per half
+  return (size_t)((((R + 6) * RS + 3) & ~3) + NH * 2 * W * 32) * 4;
 }
 
 // Band height: largest power of two <= 8 dividing H whose LDS image fits
@@ -120,6 +150,7 @@ inline int wgrad1_band(int H, int W) {
 }
 
 inline hipError_t launch_wgrad1(const Wgrad1Args& a, hipStream_t st) {
+  if (a.W * 8 > 512 * kWgrad1Pre) return hipErrorInvalidValue;   // row prefetch registers
   size_t shm = wgrad1_smem_bytes(a.W, a.R);
   if (a.R == 8 && shm < 8 * 16 * 64 * 4) shm = 8 * 16 * 64 * 4;   // halves' LDS sum
   if (a.R == 8)
