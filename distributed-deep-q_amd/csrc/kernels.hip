@@ -657,14 +657,22 @@ __device__ void head_sums(int hb, int B, const float* __restrict__ dqbuf,
   __shared__ float red[4 * 64 * 5];
   const int t = threadIdx.x, lane = t & 63, g = t >> 6;
   if (hb == 0 && t < 5) {
+    // sequential sums over b, loads issued 16 at a time (clamped indices,
+    // dropped): the plain loop was a chain of dependent loads that made
+    // these five threads the reduce kernel's critical path (~9 us)
+    const float* src = t < 4 ? dqbuf + t : lpart;
+    const int es = t < 4 ? 4 : 1;
     float acc = 0.f;
-    if (t < 4) {
-      for (int b = 0; b < B; ++b) acc += dqbuf[b * 4 + t];
-      gb5[t] = acc;
-    } else {
-      for (int b = 0; b < B; ++b) acc += lpart[b];
-      *loss_o = acc / (float)B / 2.f;
+    for (int b0 = 0; b0 < B; b0 += 16) {
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = src[min(b0 + u, B - 1) * es];
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (b0 + u < B) acc += v[u];
     }
+    if (t < 4) gb5[t] = acc;
+    else *loss_o = acc / (float)B / 2.f;
   }
   const int j = hb * 64 + lane;
   float db = 0.f, dw[4] = {0.f, 0.f, 0.f, 0.f};
@@ -747,53 +755,71 @@ __device__ __forceinline__ void apply_book(int64_t* iter, int32_t* opt_init, int
   opt_init[0] = 1;
 }
 
-// kWredG split groups x 64 columns, four slab loads in flight per thread
-// (8-load rounds and 8 groups in 512-thread blocks both measured slower).
-// Head-sum blocks use the first 256 threads.
-constexpr int kWredG = 4;
-static_assert(kWredG == 4 || kWredG == 8, "slab-reduce groups");
-__global__ __launch_bounds__(64 * kWredG) void wgrad_reduce_kernel(
-    const float* __restrict__ part, float* __restrict__ grad, WredDims d0, WredDims d1,
-    WredDims d2, int64_t* iter, int32_t* opt_init, int book_period, ReplayMeta* bump,
-    int book_inc, HeadSums hs) {
-  __shared__ float red[kWredG][64];
-  const int bid = blockIdx.x;
-  if (opt_init && bid == 0 && threadIdx.x == 0)
-    apply_book(iter, opt_init, book_period, bump, book_inc);
-  if (bid >= hs.blk0) {
-    if (threadIdx.x >= 256) return;   // ended waves do not hold up s_barrier
-    head_sums(bid - hs.blk0, hs.B, hs.dqbuf, hs.lpart, hs.h4q, hs.dh4, hs.loss, hs.gw5, hs.gb5,
-              hs.gb4);
-    return;
-  }
-  const WredDims d = bid >= d2.blk0 ? d2 : (bid >= d1.blk0 ? d1 : d0);
-  const int lb = bid - d.blk0;
+// Slab reduce: a unit = 64 slab columns n of one (layer, co).  Persistent
+// 256-thread blocks (kWredBlocks, two per CU) walk the units, longest layer
+// first; the 4 waves are split groups g summing slabs s = g, g+4, ... (the
+// order of a plain loop) with up to kWredCh loads in flight per thread, then
+// meet in LDS in fixed order.  Measured: an (almost) empty launch of ~8000
+// waves alone costs ~4.7 us on this chip, and a 4-load-per-round loop left
+// conv1's units (256 slabs) 16 dependent memory rounds deep; one block per
+// unit (1600 blocks) or 1024-thread blocks were both slower.
+constexpr int kWredBlocks = 512;
+constexpr int kWredCh = 32;
+
+__device__ __forceinline__ void wred_unit(const float* __restrict__ part, float* __restrict__ grad,
+                                          const WredDims& d, int lu, float (*red)[64]) {
+  const int col = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int nblk = d.np / 64;
-  const int co = lb / nblk, n = (lb % nblk) * 64 + (threadIdx.x & 63);
-  const int g = threadIdx.x >> 6;
+  const int co = lu / nblk, n = (lu % nblk) * 64 + col;
   const int kk = d.ks * d.ks, kc = kk * d.cin;
-  const float* p = part + d.part_off + (size_t)co * d.np + n;
-  const size_t stride = (size_t)d.cout * d.np;
   float acc = 0.f;
-  int s = g;
-  for (; s + 3 * kWredG < d.splits; s += 4 * kWredG) {
-    const float v0 = p[s * stride], v1 = p[(s + kWredG) * stride];
-    const float v2 = p[(s + 2 * kWredG) * stride], v3 = p[(s + 3 * kWredG) * stride];
-    acc += v0; acc += v1; acc += v2; acc += v3;
+  if (n <= kc) {   // slab padding columns (n > kc) are never read
+    const float* p = part + d.part_off + (size_t)co * d.np + n;
+    const size_t stride = (size_t)d.cout * d.np;
+    const int cnt = (d.splits - g + 3) >> 2;          // this group's slabs g + 4i
+    for (int i0 = 0; i0 < cnt; i0 += kWredCh) {
+      float v[kWredCh];
+#pragma unroll
+      for (int u = 0; u < kWredCh; ++u)               // clamped, unconditional
+        v[u] = p[(size_t)(g + 4 * min(i0 + u, cnt - 1)) * stride];
+#pragma unroll
+      for (int u = 0; u < kWredCh; ++u)
+        if (i0 + u < cnt) acc += v[u];
+    }
   }
-  for (; s < d.splits; s += kWredG) acc += p[s * stride];
-  red[g][threadIdx.x & 63] = acc;
+  red[g][col] = acc;
   __syncthreads();
   if (g == 0 && n <= kc) {
-    const int l = threadIdx.x;
-    float v = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
-    if (kWredG == 8) v += (red[4][l] + red[5][l]) + (red[6][l] + red[7][l]);
+    const float v = (red[0][col] + red[1][col]) + (red[2][col] + red[3][col]);
     if (n < kc) {
       const int tap = n / d.cin, ci = n % d.cin;
       grad[d.w_off + ((size_t)co * d.cin + ci) * kk + tap] = v;
     } else {
       grad[d.b_off + co] = v;
     }
+  }
+  __syncthreads();   // red is reused by the block's next unit
+}
+
+// Units [d.blk0, ...) of each layer (conv1, conv3, conv2 order: d0 < d2 <
+// d1), blocks [0, nub) persistent over the units, blocks [nub, nub + 8) the
+// head sums; block 0 also latches the apply bookkeeping.
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(
+    const float* __restrict__ part, float* __restrict__ grad, WredDims d0, WredDims d1,
+    WredDims d2, int nunits, int nub, int64_t* iter, int32_t* opt_init, int book_period,
+    ReplayMeta* bump, int book_inc, HeadSums hs) {
+  __shared__ float red[4][64];
+  const int bid = blockIdx.x;
+  if (opt_init && bid == 0 && threadIdx.x == 0)
+    apply_book(iter, opt_init, book_period, bump, book_inc);
+  if (bid >= nub) {
+    head_sums(bid - nub, hs.B, hs.dqbuf, hs.lpart, hs.h4q, hs.dh4, hs.loss, hs.gw5, hs.gb5,
+              hs.gb4);
+    return;
+  }
+  for (int u = bid; u < nunits; u += nub) {
+    const WredDims d = u >= d1.blk0 ? d1 : (u >= d2.blk0 ? d2 : d0);
+    wred_unit(part, grad, d, u - d.blk0, red);
   }
 }
 
@@ -1337,6 +1363,15 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
       CHECK_LAUNCH(launch_gemm<CfgD2>(p, 1, 1, s));
     }
   }
+  // slab-reduce geometry: layer l's blocks start at d[l].blk0
+  WredDims d[3];
+  const int cout[3] = {32, 64, 64}, cin[3] = {4, 32, 64}, ks[3] = {7, 5, 3};
+  int blk = 0;
+  for (int l : {0, 2, 1}) {           // unit order: longest slab stacks first
+    d[l] = {L.w[l], L.b[l], nb.wpart_off[l], cout[l], cin[l], ks[l], nb.wsplits[l], nb.wnp[l],
+            blk};
+    blk += cout[l] * (nb.wnp[l] / 64);
+  }
   {  // conv1 wgrad
     ConvWgrad<4, 32, 7, 3> p;
     p.M = 32; p.N = 197; p.K = B * S * S;
@@ -1350,31 +1385,27 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
       Wgrad1Args w;
       w.B = B; w.H = S; w.W = S; w.R = wgrad1_band(S, S); w.NP = nb.wnp[0];
       w.dconv = nb.dconv1; w.in = nb.state; w.part = p.part;
+      // (running the conv2/conv3 slab reduces as extra blocks of this launch
+      // measured 1.7 us slower than the separate reduce kernel)
       CHECK_LAUNCH(launch_wgrad1(w, s));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgW1>(p, 1, ns, s));
     }
   }
   {  // slab reduce -> grads (Caffe layout)
-    WredDims d[3];
-    const int cout[3] = {32, 64, 64}, cin[3] = {4, 32, 64}, ks[3] = {7, 5, 3};
-    int blk = 0;
-    for (int l = 0; l < 3; ++l) {
-      d[l] = {L.w[l], L.b[l], nb.wpart_off[l], cout[l], cin[l], ks[l], nb.wsplits[l], nb.wnp[l],
-              blk};
-      blk += cout[l] * (nb.wnp[l] / 64);
-    }
     if (concurrent) {       // join the side stream
       CHECK_LAUNCH(hipEventRecord(nb.ev[nev], nb.side));
       CHECK_LAUNCH(hipStreamWaitEvent(s, nb.ev[nev], 0));
       ++nev;
     }
     M("wgrad_reduce");
-    HeadSums hs{blk, B, nb.dqbuf, nb.lpart, nb.h4[0], nb.dh4, nb.loss, nb.grad + L.w[4],
+    HeadSums hs{0, B, nb.dqbuf, nb.lpart, nb.h4[0], nb.dh4, nb.loss, nb.grad + L.w[4],
                 nb.grad + L.b[4], nb.grad + L.b[3]};
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blk + kFc4 / 64), dim3(64 * kWredG), 0, s, nb.wpart,
-                       nb.grad, d[0], d[1], d[2], nb.iter, book ? nb.opt_init : nullptr,
-                       book_period, book ? bump : nullptr, nb.book_inc, hs);
+    const int nub = blk < kWredBlocks ? blk : kWredBlocks;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(nub + kFc4 / 64), dim3(256), 0, s, nb.wpart,
+                       nb.grad, d[0], d[1], d[2], blk, nub, nb.iter,
+                       book ? nb.opt_init : nullptr, book_period, book ? bump : nullptr,
+                       nb.book_inc, hs);
     CHECK_LAUNCH(hipGetLastError());
   }
   return hipSuccess;

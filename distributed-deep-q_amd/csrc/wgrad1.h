@@ -32,9 +32,9 @@ struct Wgrad1Args {
 // single wave of workgroups).  Sums run in the same order as before.
 constexpr int kWgrad1Pre = 4;                // float4 of a dconv row per thread (W <= 256)
 
+// Body of band `split` on 512 * NH threads with the dynamic LDS image `sm`.
 template <int NH>
-__global__ __launch_bounds__(512 * NH) void wgrad1_kernel(const Wgrad1Args a) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
+__device__ __forceinline__ void wgrad1_body(const Wgrad1Args& a, float* sm, int split) {
   const int W = a.W, R = a.R;
   const int PW = W + 6;
   const int RS = PW * 4 + 2;                 // odd-ish row stride: rows land on other banks
@@ -43,7 +43,6 @@ __global__ __launch_bounds__(512 * NH) void wgrad1_kernel(const Wgrad1Args a) {
   const int ht = tid & 511;                  // thread within the half
   // this half's two dconv row slots, W x 32 each (16-B aligned)
   float* dslot = sm + (((R + 6) * RS + 3) & ~3) + half * 2 * W * 32;
-  const int split = blockIdx.x;
   const int bands = a.H / R;
   const int b = split / bands, y0 = (split % bands) * R;
   const int rh = R / NH, rlo = half * rh;   // this half's rows of the band
@@ -134,6 +133,12 @@ __global__ __launch_bounds__(512 * NH) void wgrad1_kernel(const Wgrad1Args a) {
   }
 }
 
+template <int NH>
+__global__ __launch_bounds__(512 * NH) void wgrad1_kernel(const Wgrad1Args a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  wgrad1_body<NH>(a, sm, blockIdx.x);
+}
+
 inline size_t wgrad1_smem_bytes(int W, int R) {
   const int RS = (W + 6) * 4 + 2;
   const int NH = R == 8 ? 2 : 1;             // two row slots per half
@@ -149,10 +154,15 @@ inline int wgrad1_band(int H, int W) {
   return R;
 }
 
-inline hipError_t launch_wgrad1(const Wgrad1Args& a, hipStream_t st) {
-  if (a.W * 8 > 512 * kWgrad1Pre) return hipErrorInvalidValue;   // row prefetch registers
+inline size_t wgrad1_launch_smem(const Wgrad1Args& a) {
   size_t shm = wgrad1_smem_bytes(a.W, a.R);
   if (a.R == 8 && shm < 8 * 16 * 64 * 4) shm = 8 * 16 * 64 * 4;   // halves' LDS sum
+  return shm;
+}
+
+inline hipError_t launch_wgrad1(const Wgrad1Args& a, hipStream_t st) {
+  if (a.W * 8 > 512 * kWgrad1Pre) return hipErrorInvalidValue;   // row prefetch registers
+  const size_t shm = wgrad1_launch_smem(a);
   if (a.R == 8)
     hipLaunchKernelGGL(wgrad1_kernel<2>, dim3(a.B * (a.H / a.R)), dim3(1024), shm, st, a);
   else
