@@ -1358,6 +1358,8 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     if (nb.conv_impl == 1) {
       // 2 tap groups: two waves per SIMD over the 1024 output blocks
       DirectArgs d = direct_dgrad_args(nb.dconv2, p.wk, nb.mask1, nb.dconv1, B, H, 2);
+      // (8x8 tiles -- two 74 KB workgroups per CU -- measured 39.3 us, and
+      // 8x8 register-B 42.9 us, against 36.8 us for this configuration)
       CHECK_LAUNCH((launch_direct<64, 32, 5, 8, 16, 4, 1, true, false, 2>(d, 1, s)));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgD2>(p, 1, 1, s));
