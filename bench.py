@@ -5,7 +5,9 @@ One step = one minibatch update of the deepq network on one GPU:
   device index draw -> replay gather -> P/Q forward -> Bellman target + loss ->
   Q backward -> [RCCL sum all-reduce of the gradient] -> rmsprop apply
   (param-server default rule) -> P <- Q every 10 updates,
-captured once into a hipGraph and replayed.  Workload at N=1: BASELINE.json
+captured into hipGraphs (8 steps per graph) and replayed; by default the next
+step's draw + gather ride on each step's apply launch into a second minibatch
+buffer (``ddq_step_pipelined_async``: bit-identical to sequential steps).  Workload at N=1: BASELINE.json
 configs[1] -- deepq Snake, batch 32, 4-frame 64x64 history, 30 000-slot HBM
 replay filled with synthetic Snake frames.
 
@@ -335,10 +337,12 @@ def main():
                     help="N>1 gradient exchange (include/ddq_hip.h enum ddq_exchange)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="allreduce: do not reduce the fc4 bucket under the conv backward")
-    ap.add_argument("--pipeline", action="store_true",
-                    help="prefetch the next minibatch on a side stream (slower on MI355X: "
-                         "the cross-stream graph edges cost more than the overlap)")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="plain graph steps, each drawing + gathering its own minibatch at its "
+                         "head (default: the next step's draw + gather ride on this step's "
+                         "apply launch into a second minibatch buffer -- bit-identical results)")
     args = ap.parse_args()
+    args.pipeline = not args.no_pipeline
 
     from ddq import dist as ddist
     rank, world, local = ddist.env_ranks()
@@ -378,8 +382,10 @@ def main():
     except ddq.DDQError as e:
         if world == 1 or args.eager:
             raise
-        print("bench: graph step failed (%s); retrying without overlap" % e, file=sys.stderr)
+        print("bench: graph step failed (%s); retrying plain graph steps without overlap" % e,
+              file=sys.stderr)
         cfg.overlap = 0
+        args.pipeline = False
         try:
             run(args.warmup)
         except ddq.DDQError as e2:

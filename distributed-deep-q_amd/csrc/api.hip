@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <functional>
 #include <vector>
 
 #include "../../include/ddq_hip.h"
@@ -69,6 +70,7 @@ struct ddq_ctx {
   float *mb2_reward = nullptr, *mb2_nonterm = nullptr;
   int32_t* mb2_idx = nullptr;
   hipGraphExec_t pexec[2][2] = {};
+  hipGraphExec_t pexec_k[2] = {};   // kGraphSteps prefetching steps starting on set p
   ddq_step_cfg pcfg{};
   bool have_pipe = false;
   int64_t steps = 0;
@@ -153,6 +155,10 @@ static void invalidate_graph(ddq_ctx* c) {
       if (g) hipGraphExecDestroy(g);
       g = nullptr;
     }
+  for (auto& g : c->pexec_k) {
+    if (g) hipGraphExecDestroy(g);
+    g = nullptr;
+  }
   c->have_pipe = false;
 }
 
@@ -928,7 +934,8 @@ static int enqueue_fwd_bwd_x(ddq_ctx* c, const NetBuffers& nb, void (*mark)(void
 //             one by one in rank order (server.py:196-209 on arrival) ->
 //             all-gather -> refresh.
 static int enqueue_exchange_apply(ddq_ctx* c, const ddq_step_cfg* cfg, const NetBuffers& nb,
-                                  void (*mark)(void*, const char*), void* marg, bool overlap) {
+                                  void (*mark)(void*, const char*), void* marg, bool overlap,
+                                  const Prefetch* pf = nullptr) {
   const ddq_update_cfg& u = cfg->update;
   const ParamLayout& L = nb.L;
   const int ex = has_exchange(c, cfg) ? cfg->exchange : DDQ_EXCHANGE_NONE;
@@ -953,7 +960,7 @@ static int enqueue_exchange_apply(ddq_ctx* c, const ddq_step_cfg* cfg, const Net
     }
     if (mark) mark(marg, "apply");
     HIP_TRY(c, launch_apply(nb, u.rule, u.lr, u.decay, u.eps, u.momentum, u.weight_decay,
-                            cfg->target_period, true, c->stream));
+                            cfg->target_period, true, c->stream, pf));
     return DDQ_OK;
   }
   const int W = c->nranks;
@@ -980,11 +987,29 @@ static int enqueue_exchange_apply(ddq_ctx* c, const ddq_step_cfg* cfg, const Net
 // the side stream under this step's forward (the replay ring is not written
 // inside a step, and the device RNG counter advances in the same order, so
 // the index stream equals the sequential one).
+// Pipelined steps whose next draw + gather ride on the apply launch (no side
+// stream): exchanges that end in the plain apply kernel, B <= 256.
+static bool fused_prefetch(const ddq_ctx* c, const ddq_step_cfg* cfg) {
+  const int ex = has_exchange(c, cfg) ? cfg->exchange : DDQ_EXCHANGE_NONE;
+  return (ex == DDQ_EXCHANGE_NONE || ex == DDQ_EXCHANGE_ALLREDUCE) && c->nb.B <= 256;
+}
+
 static int enqueue_train(ddq_ctx* c, const ddq_step_cfg* cfg, const NetBuffers& nb_in,
                          const NetBuffers* pre, void (*mark)(void*, const char*), void* marg,
                          ReplayMeta* bump = nullptr) {
   NetBuffers nb = nb_in;
   nb.book_inc = step_inc(c, cfg);
+  if (pre && fused_prefetch(c, cfg)) {
+    // the step's bookkeeping advances the draw counter (bump) before the apply
+    // launch draws the next minibatch with it
+    const Prefetch pf = make_prefetch(*pre, c->r_state, c->r_action, c->r_reward, c->r_nonterm,
+                                      c->r_meta, cfg->seed);
+    const bool overlap = has_exchange(c, cfg) && cfg->exchange == DDQ_EXCHANGE_ALLREDUCE &&
+                         cfg->overlap && c->comm && mark == nullptr;
+    TRY(enqueue_fwd_bwd_x(c, nb, mark, marg, cfg->target_period > 0 ? cfg->target_period : 0,
+                          c->r_meta, overlap));
+    return enqueue_exchange_apply(c, cfg, nb, mark, marg, overlap, &pf);
+  }
   if (pre) {
     HIP_TRY(c, hipEventRecord(nb.ev[6], c->stream));
     HIP_TRY(c, hipStreamWaitEvent(nb.side, nb.ev[6], 0));
@@ -1110,6 +1135,24 @@ int ddq_step_graph_async(ddq_ctx* c, const ddq_step_cfg* cfg, int32_t nsteps) {
 // and (f = 1) prefetches into set 1-p; the chain starts on the parity that
 // makes the LAST step train on set 0, so afterwards the ctx's minibatch,
 // indices and counters are exactly those of nsteps sequential steps.
+// With fused_prefetch the prefetch is extra blocks of the apply launch (no
+// side stream), the first draw is the fused sample_gather kernel (which does
+// not advance the counter) and every step's bookkeeping advances it, as in
+// the plain graph step; chains longer than kGraphSteps + 1 replay
+// kGraphSteps-step graphs (an even count: they start and end on set p).
+static int capture_exec(ddq_ctx* c, hipGraphExec_t* out, const std::function<int()>& body) {
+  HIP_TRY(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+  int rc = body();
+  hipGraph_t g = nullptr;
+  hipError_t e = hipStreamEndCapture(c->stream, &g);
+  if (rc != DDQ_OK) { if (g) hipGraphDestroy(g); return rc; }
+  if (e != hipSuccess) return fail(c, DDQ_EHIP, "hipStreamEndCapture: %s", hipGetErrorString(e));
+  e = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
+  hipGraphDestroy(g);
+  if (e != hipSuccess) return fail(c, DDQ_EHIP, "hipGraphInstantiate: %s", hipGetErrorString(e));
+  return DDQ_OK;
+}
+
 int ddq_step_pipelined_async(ddq_ctx* c, const ddq_step_cfg* cfg, int32_t nsteps) {
   TRY(check_step(c, cfg));
   TRY(set_dev(c));
@@ -1123,35 +1166,54 @@ int ddq_step_pipelined_async(ddq_ctx* c, const ddq_step_cfg* cfg, int32_t nsteps
     TRY(dalloc(c, &c->mb2_nonterm, (size_t)B));
     TRY(dalloc(c, &c->mb2_idx, (size_t)B));
   }
+  const bool fpf = fused_prefetch(c, cfg);
+  ReplayMeta* bump = fpf ? c->r_meta : nullptr;
   if (!c->have_pipe || memcmp(&c->pcfg, cfg, sizeof(*cfg)) != 0) {
     invalidate_graph(c);
-    for (int p = 0; p < 2; ++p)
+    for (int p = 0; p < 2; ++p) {
       for (int f = 0; f < 2; ++f) {
         const NetBuffers cur = mb_view(c, p), nxt = mb_view(c, 1 - p);
-        HIP_TRY(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-        int rc = enqueue_train(c, cfg, cur, f ? &nxt : nullptr, nullptr, nullptr);
-        hipGraph_t g = nullptr;
-        hipError_t e = hipStreamEndCapture(c->stream, &g);
-        if (rc != DDQ_OK) { if (g) hipGraphDestroy(g); return rc; }
-        if (e != hipSuccess) return fail(c, DDQ_EHIP, "hipStreamEndCapture: %s", hipGetErrorString(e));
-        e = hipGraphInstantiate(&c->pexec[p][f], g, nullptr, nullptr, 0);
-        hipGraphDestroy(g);
-        if (e != hipSuccess) return fail(c, DDQ_EHIP, "hipGraphInstantiate: %s", hipGetErrorString(e));
+        TRY(capture_exec(c, &c->pexec[p][f], [&]() -> int {
+          return enqueue_train(c, cfg, cur, f ? &nxt : nullptr, nullptr, nullptr, bump);
+        }));
       }
+      if (fpf)
+        TRY(capture_exec(c, &c->pexec_k[p], [&]() -> int {
+          for (int k = 0; k < kGraphSteps; ++k) {
+            const int q = p ^ (k & 1);
+            const NetBuffers cur = mb_view(c, q), nxt = mb_view(c, 1 - q);
+            TRY(enqueue_train(c, cfg, cur, &nxt, nullptr, nullptr, bump));
+          }
+          return DDQ_OK;
+        }));
+    }
     c->pcfg = *cfg;
     c->have_pipe = true;
   }
   if (c->steps == 0) TRY(initial_target_sync(c, cfg));
   int p = (nsteps - 1) & 1;
   const NetBuffers first = mb_view(c, p);
-  HIP_TRY(c, launch_sample(first, c->r_meta, cfg->seed, c->stream));
-  HIP_TRY(c, launch_gather(first, c->r_state, c->r_action, c->r_reward, c->r_nonterm, c->r_meta,
-                           c->stream));
-  for (int i = 0; i < nsteps; ++i) {
+  if (fpf) {
+    HIP_TRY(c, launch_sample_gather(first, c->r_state, c->r_action, c->r_reward, c->r_nonterm,
+                                    c->r_meta, cfg->seed, c->stream));
+  } else {
+    HIP_TRY(c, launch_sample(first, c->r_meta, cfg->seed, c->stream));
+    HIP_TRY(c, launch_gather(first, c->r_state, c->r_action, c->r_reward, c->r_nonterm, c->r_meta,
+                             c->stream));
+  }
+  for (int i = 0; i < nsteps;) {
+    if (fpf && nsteps - i > kGraphSteps) {
+      HIP_TRY(c, hipGraphLaunch(c->pexec_k[p], c->stream));   // ends on set p again
+      c->steps += kGraphSteps;
+      c->applied += (int64_t)kGraphSteps * step_inc(c, cfg);
+      i += kGraphSteps;
+      continue;
+    }
     HIP_TRY(c, hipGraphLaunch(c->pexec[p][i + 1 < nsteps ? 1 : 0], c->stream));
     c->steps++;
     c->applied += step_inc(c, cfg);
     p ^= 1;
+    ++i;
   }
   return DDQ_OK;
 }

@@ -78,8 +78,23 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
                            ReplayMeta* bump = nullptr, hipError_t (*fc4_done)(void*) = nullptr,
                            void* fc4_done_arg = nullptr);
 // period > 0: also copy Q -> P when the next pull sees iteration % period == 0.
+// Next step's draw + gather carried by the apply launch (pipelined stepping)
+struct Prefetch {
+  const uint8_t* st;
+  const uint8_t* act;
+  const int16_t* rew;
+  const uint8_t* nt;
+  ReplayMeta* meta;
+  uint64_t seed;
+  int B, S, gx, ng;                 // ng = 0: no prefetch blocks
+  int32_t* idx;
+  float *sQ, *sP, *action, *reward, *nonterm;
+};
+Prefetch make_prefetch(const NetBuffers& next, const uint8_t* st, const uint8_t* act,
+                       const int16_t* rew, const uint8_t* nt, ReplayMeta* meta, uint64_t seed);
 hipError_t launch_apply(const NetBuffers& nb, int rule, float lr, float decay, float eps,
-                        float momentum, float wd, int period, bool booked, hipStream_t s);
+                        float momentum, float wd, int period, bool booked, hipStream_t s,
+                        const Prefetch* pre = nullptr);
 hipError_t launch_relayout(const NetBuffers& nb, int z, hipStream_t s);
 // owner apply of shard [off, off+len) with W gradient slices (stride `slice`)
 // applied in rank order; then, after the theta all-gather, launch_refresh

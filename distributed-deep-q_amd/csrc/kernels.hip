@@ -161,13 +161,12 @@ __device__ __forceinline__ void gather_body(
     const uint8_t* __restrict__ st, const uint8_t* __restrict__ act,
     const int16_t* __restrict__ rew, const uint8_t* __restrict__ nt, ReplayMeta* meta, int64_t i,
     int S, float* __restrict__ sQ, float* __restrict__ sP, float* __restrict__ action,
-    float* __restrict__ reward, float* __restrict__ nonterm) {
-  const int b = blockIdx.y, z = blockIdx.z;
+    float* __restrict__ reward, float* __restrict__ nonterm, int bx, int b, int z) {
   const int64_t N = meta->capacity;
   const int64_t nxt = (i + 1 == N) ? 0 : i + 1;
   const int64_t slot = z ? nxt : i;
   const int SS = S * S;
-  const int p4 = blockIdx.x * 256 + threadIdx.x;     // group of 4 pixels
+  const int p4 = bx * 256 + threadIdx.x;             // group of 4 pixels
   if (p4 * 4 < SS) {
     const uint8_t* src = st + slot * 4 * SS + p4 * 4;
     const uchar4 c0 = *reinterpret_cast<const uchar4*>(src);
@@ -180,7 +179,7 @@ __device__ __forceinline__ void gather_body(
     dst[2] = f4(c0.z, c1.z, c2.z, c3.z);
     dst[3] = f4(c0.w, c1.w, c2.w, c3.w);
   }
-  if (z == 1 && blockIdx.x == 0 && threadIdx.x < 4) {
+  if (z == 1 && bx == 0 && threadIdx.x < 4) {
     const int a = act[nxt];
     if (a >= kActions) meta->err = 1;
     action[b * 4 + threadIdx.x] = (threadIdx.x == a) ? 1.f : 0.f;
@@ -197,7 +196,8 @@ __global__ __launch_bounds__(256) void gather_kernel(
     const int16_t* __restrict__ rew, const uint8_t* __restrict__ nt, ReplayMeta* meta,
     const int32_t* __restrict__ idx, int S, float* __restrict__ sQ, float* __restrict__ sP,
     float* __restrict__ action, float* __restrict__ reward, float* __restrict__ nonterm) {
-  gather_body(st, act, rew, nt, meta, idx[blockIdx.y], S, sQ, sP, action, reward, nonterm);
+  gather_body(st, act, rew, nt, meta, idx[blockIdx.y], S, sQ, sP, action, reward, nonterm,
+              blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
 // Fused draw + gather for the training step (B <= 256): every workgroup
@@ -215,7 +215,8 @@ __global__ __launch_bounds__(256) void sample_gather_kernel(
   draw_sorted(meta, B, seed, meta->counter, cand, &bad_any);
   if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x < B)
     idx_out[threadIdx.x] = (int32_t)cand[threadIdx.x];
-  gather_body(st, act, rew, nt, meta, cand[blockIdx.y], S, sQ, sP, action, reward, nonterm);
+  gather_body(st, act, rew, nt, meta, cand[blockIdx.y], S, sQ, sP, action, reward, nonterm,
+              blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
 hipError_t launch_sample(const NetBuffers& nb, ReplayMeta* meta, uint64_t seed, hipStream_t s) {
@@ -866,13 +867,29 @@ __device__ __forceinline__ float apply_one(const ApplyArgs& a, bool first, int64
   }
 }
 
+// Blocks [0, pf.ng) of the apply launch draw + gather the NEXT step's
+// minibatch into the other buffer set (pipelined stepping, B <= 256): the
+// sample_gather kernel's work rides on the HBM-bound apply instead of being a
+// serial latency-bound launch at the head of the next step.  The counter it
+// draws with was advanced by this step's bookkeeping (the reduce kernel), so
+// the draws are the ones sequential steps make.
 __global__ __launch_bounds__(256) void apply_kernel(
     float* __restrict__ theta, const float* __restrict__ grad, float* __restrict__ opt,
     const int32_t* __restrict__ opt_init, float* __restrict__ wk, float* __restrict__ thetaP,
-    float* __restrict__ wkP, ApplyArgs a) {
+    float* __restrict__ wkP, ApplyArgs a, Prefetch pf) {
+  if ((int)blockIdx.x < pf.ng) {
+    __shared__ int64_t cand[256];
+    __shared__ int bad_any;
+    const int g = blockIdx.x, bx = g % pf.gx, b = (g / pf.gx) % pf.B, z = g / (pf.gx * pf.B);
+    draw_sorted(pf.meta, pf.B, pf.seed, pf.meta->counter, cand, &bad_any);
+    if (g == 0 && threadIdx.x < pf.B) pf.idx[threadIdx.x] = (int32_t)cand[threadIdx.x];
+    gather_body(pf.st, pf.act, pf.rew, pf.nt, pf.meta, cand[b], pf.S, pf.sQ, pf.sP, pf.action,
+                pf.reward, pf.nonterm, bx, b, z);
+    return;
+  }
   const bool first = opt_init[2] != 0;      // latched by apply_book
   const bool sync = opt_init[3] != 0;
-  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const int64_t i = ((int64_t)(blockIdx.x - pf.ng) * blockDim.x + threadIdx.x) * 4;
   if (i < a.n) {
     const float4 g4 = *reinterpret_cast<const float4*>(grad + i);
     const float4 t4 = *reinterpret_cast<const float4*>(theta + i);
@@ -1019,8 +1036,23 @@ hipError_t launch_sum_slices(float* out, const float* in, int W, int64_t len, in
   return hipGetLastError();
 }
 
+Prefetch make_prefetch(const NetBuffers& next, const uint8_t* st, const uint8_t* act,
+                       const int16_t* rew, const uint8_t* nt, ReplayMeta* meta, uint64_t seed) {
+  Prefetch pf;
+  pf.st = st; pf.act = act; pf.rew = rew; pf.nt = nt; pf.meta = meta; pf.seed = seed;
+  pf.B = next.B; pf.S = next.S;
+  pf.gx = (next.S * next.S / 4 + 255) / 256;
+  pf.ng = pf.gx * next.B * 2;
+  pf.idx = next.idx; pf.sQ = next.state; pf.sP = next.next_state;
+  pf.action = next.action; pf.reward = next.reward; pf.nonterm = next.nonterm;
+  return pf;
+}
+
 hipError_t launch_apply(const NetBuffers& nb, int rule, float lr, float decay, float eps,
-                        float momentum, float wd, int period, bool booked, hipStream_t s) {
+                        float momentum, float wd, int period, bool booked, hipStream_t s,
+                        const Prefetch* pre) {
+  Prefetch pf{};
+  if (pre) pf = *pre;
   ApplyArgs a;
   a.n = nb.L.total;
   a.rule = rule; a.period = period;
@@ -1030,8 +1062,8 @@ hipError_t launch_apply(const NetBuffers& nb, int rule, float lr, float decay, f
   conv_dims(nb.L, a.conv);
   const int blocks = (int)((a.n / 4 + 255) / 256);
   if (!booked) hipLaunchKernelGGL(apply_book_kernel, dim3(1), dim3(1), 0, s, nb.iter, nb.opt_init, period);
-  hipLaunchKernelGGL(apply_kernel, dim3(blocks), dim3(256), 0, s, nb.theta[0], nb.grad, nb.opt,
-                     nb.opt_init, nb.wk[0], nb.theta[1], nb.wk[1], a);
+  hipLaunchKernelGGL(apply_kernel, dim3(blocks + pf.ng), dim3(256), 0, s, nb.theta[0], nb.grad,
+                     nb.opt, nb.opt_init, nb.wk[0], nb.theta[1], nb.wk[1], a, pf);
   return hipGetLastError();
 }
 

@@ -286,7 +286,7 @@ def test_pipelined_step_matches_graph(ddq, ref):
         n.replay_create(N)
         n.replay_import(st, acts, rws, nts, 0, N)
     cfg = nets[0].step_cfg("sgd", lr=1e-4, target_period=3, seed=5)
-    for k in (1, 4, 3):
+    for k in (1, 4, 3, 19):      # 19: two 8-step prefetching graphs + singles
         nets[0].step_pipelined(cfg, k)
         nets[1].step_graph(cfg, k)
     for n in nets:
