@@ -1232,6 +1232,7 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
       d.nchw = 1;
       d.mask_nhwc = 1;   // routing bytes NHWC: the backward expands dpool3 through them
       // 3 tap groups: 512 output blocks per tower would leave one wave per SIMD
+      // (register-B variants measured slower: 8x8 15.6 us, 4x8 17.5, against 14.5)
       CHECK_LAUNCH((launch_direct<64, 64, 3, 8, 8, 2, 2, false, false, 3>(d, nz, s)));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgConv3F>(p, nz, 1, s));
