@@ -42,8 +42,8 @@ struct WgradDGeom {
 // PSRC: dconv is given pooled (the gradient of the 2x2 max-pool output plus
 // its routing bytes, as fc4's data gradient leaves it) and expanded while the
 // rows are staged: value at the routed quadrant, 0 at the other three.
-template <int CIN, int COUT, int KS, int PAD, bool PSRC = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void wgradd_kernel(
+template <int CIN, int COUT, int KS, int PAD, bool PSRC = false, int WPE = 2>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void wgradd_kernel(
     const WgradDArgs a) {
   constexpr int NCB = CIN / 32;
   constexpr int T = KS * NCB;
@@ -256,8 +256,8 @@ inline size_t wgradd_smem_bytes(int W) {
 }
 
 // Row groups: about two 4-wave workgroups per CU over all (cb, ky) pairs.
-inline void wgradd_groups(int rows, int nts, int* G, int* RPG) {
-  int g = 512 / nts;
+inline void wgradd_groups(int rows, int nts, int* G, int* RPG, int target = 512) {
+  int g = target / nts;
   if (g >= 16) g &= ~7;            // whole XCD rounds (see the kernel's decode)
   if (g < 1) g = 1;
   if (g > rows) g = rows;
@@ -266,11 +266,11 @@ inline void wgradd_groups(int rows, int nts, int* G, int* RPG) {
   *G = (rows + rpg - 1) / rpg;
 }
 
-template <int CIN, int COUT, int KS, int PAD, bool PSRC = false>
+template <int CIN, int COUT, int KS, int PAD, bool PSRC = false, int WPE = 2>
 inline hipError_t launch_wgradd(const WgradDArgs& a, hipStream_t st) {
   const size_t shm = wgradd_smem_bytes<CIN, PAD>(a.W);
   const int g8 = (a.G + 7) / 8 * 8;
-  hipLaunchKernelGGL((wgradd_kernel<CIN, COUT, KS, PAD, PSRC>), dim3(g8 * (COUT / 32) * KS),
+  hipLaunchKernelGGL((wgradd_kernel<CIN, COUT, KS, PAD, PSRC, WPE>), dim3(g8 * (COUT / 32) * KS),
                      dim3(256), shm, st, a);
   return hipGetLastError();
 }
