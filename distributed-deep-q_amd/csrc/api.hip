@@ -1403,6 +1403,34 @@ int ddq_profile_step(ddq_ctx* c, const ddq_step_cfg* cfg, char* names, float* us
   return DDQ_OK;
 }
 
+int ddq_time_layer(ddq_ctx* c, const char* name, int32_t reps, float* usec) {
+  if (!c) return DDQ_EINVAL;
+  if (!name || !usec || reps < 1) return fail(c, DDQ_EINVAL, "time_layer: bad arguments");
+  int l = 0;
+  if (!strcmp(name, "conv1_fwd")) l = 1;
+  else if (!strcmp(name, "conv2_fwd")) l = 2;
+  else if (!strcmp(name, "conv3_fwd")) l = 3;
+  else return fail(c, DDQ_EINVAL, "time_layer: unknown layer %s", name);
+  TRY(set_dev(c));
+  NetBuffers nb = c->nb;
+  nb.fwd_only = l;
+  hipEvent_t e0, e1;
+  HIP_TRY(c, hipEventCreate(&e0));
+  HIP_TRY(c, hipEventCreate(&e1));
+  hipError_t e = launch_forward(nb, 2, c->stream, nullptr, nullptr);   // warm
+  if (e == hipSuccess) e = hipEventRecord(e0, c->stream);
+  for (int i = 0; i < reps && e == hipSuccess; ++i) e = launch_forward(nb, 2, c->stream, nullptr, nullptr);
+  if (e == hipSuccess) e = hipEventRecord(e1, c->stream);
+  if (e == hipSuccess) e = hipEventSynchronize(e1);
+  float ms = 0.f;
+  if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  HIP_TRY(c, e);
+  *usec = ms * 1000.f / reps;
+  return DDQ_OK;
+}
+
 double ddq_step_flops(const ddq_ctx* c) { return c ? step_flops(c->nb.B, c->nb.S) : 0.0; }
 
 }  // extern "C"

@@ -185,20 +185,20 @@ struct NoStage {
 
 template <int CP, int N, int KS, int TY, int TX, int WM, int WN, bool DGRAD, bool WALL, int WK,
           bool RB>
-__global__ __launch_bounds__(64 * WM * WN * WK) void direct_conv_kernel(const DirectArgs a) {
+__device__ __forceinline__ void direct_conv_body(const DirectArgs& a, float* smem, int bx, int by,
+                                                 int bz) {
   using C = DirectCfg<CP, N, KS, TY, TX, WM, WN, DGRAD, WALL, WK, RB>;
   static_assert(!(RB && WALL), "register-B is per-tap");
   using VT = typename VecT<C::V>::T;
   constexpr int TM = C::TM, TN = C::TN, V = C::V;
-  __shared__ __attribute__((aligned(16))) float smem[C::kSmem];
   float* patch = smem;
   float* wbuf = smem + C::kPatch;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wkg = wid / (WM * WN);                 // tap group: taps t = s*WK + wkg
   const int gtid = tid - wkg * C::kGroup;
-  const int z = blockIdx.z, b = blockIdx.y;
-  const int ty = blockIdx.x / a.tiles_x, tx = blockIdx.x % a.tiles_x;
+  const int z = bz, b = by;
+  const int ty = bx / a.tiles_x, tx = bx % a.tiles_x;
   const int y0 = ty * TY, x0 = tx * TX;
   // select, never index, the per-tower kernel arguments: a runtime index into
   // a kernarg array makes the compiler copy the struct to scratch memory
@@ -509,6 +509,15 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void direct_conv_kernel(const Di
       }
     }
   }
+}
+
+template <int CP, int N, int KS, int TY, int TX, int WM, int WN, bool DGRAD, bool WALL, int WK,
+          bool RB>
+__global__ __launch_bounds__(64 * WM * WN * WK) void direct_conv_kernel(const DirectArgs a) {
+  using C = DirectCfg<CP, N, KS, TY, TX, WM, WN, DGRAD, WALL, WK, RB>;
+  __shared__ __attribute__((aligned(16))) float smem[C::kSmem];
+  direct_conv_body<CP, N, KS, TY, TX, WM, WN, DGRAD, WALL, WK, RB>(a, smem, blockIdx.x, blockIdx.y,
+                                                                  blockIdx.z);
 }
 
 template <int CP, int N, int KS, int TY, int TX, int WM, int WN, bool DGRAD, bool WALL, int WK = 1,

@@ -57,6 +57,7 @@ struct NetBuffers {
   float gamma;
   int conv_impl;                    // 0 = implicit-GEMM engine, 1 = direct (patch-in-LDS)
   int variant;                      // tuning experiments (DDQ_VARIANT bits), 0 = default
+  int fwd_only;                     // launch_forward: 0 = every layer, l + 1 = conv layer l only
   int book_inc;                     // param-server iterations per apply (1, or W: server mode)
 };
 

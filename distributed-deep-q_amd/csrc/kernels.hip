@@ -1173,7 +1173,7 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
   const ParamLayout& L = nb.L;
   const int B = nb.B, S = nb.S;
   auto M = [&](const char* n) { if (mark) mark(marg, n); };
-  {
+  if (!nb.fwd_only || nb.fwd_only == 1) {
     ConvFwd<4, 32, 7, 3> p;
     p.nchw = 0;
     p.M = B * S * S; p.N = 32; p.K = 196; p.ksplit_len = 196;
@@ -1193,7 +1193,7 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
       CHECK_LAUNCH(launch_gemm<CfgConv1F>(p, nz, 1, s));
     }
   }
-  {
+  if (!nb.fwd_only || nb.fwd_only == 2) {
     const int H = S / 2;
     ConvFwd<32, 64, 5, 2> p;
     p.nchw = 0;
@@ -1215,7 +1215,7 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
       CHECK_LAUNCH(launch_gemm<CfgConv2F>(p, nz, 1, s));
     }
   }
-  {
+  if (!nb.fwd_only || nb.fwd_only == 3) {
     const int H = S / 4;
     ConvFwd<64, 64, 3, 1> p;
     p.M = B * H * H; p.N = 64; p.K = 576; p.ksplit_len = 576;
@@ -1238,6 +1238,7 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
       CHECK_LAUNCH(launch_gemm<CfgConv3F>(p, nz, 1, s));
     }
   }
+  if (nb.fwd_only) return hipSuccess;   // ddq_time_layer: one conv layer
   {
     const int s4 = S / 8;
     FcFwd p;
@@ -1264,6 +1265,27 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     CHECK_LAUNCH(hipGetLastError());
   }
   return hipSuccess;
+}
+
+// conv3 weight gradient (blocks [0, nw): wgradd body, 4 waves) beside the
+// conv3 data gradient (blocks [nw, ...): register-B direct dgrad, 6 waves;
+// wgrad blocks end their extra 2 waves at once).  Both only need dpool3 and
+// are latency-bound alone (about 25 % of the MFMA roof each); the shared
+// launch was meant to overlap their prologues and tails (A/B only, see the
+// launch site).
+using Conv3DgradCfg = DirectCfg<64, 64, 3, 4, 8, 1, 2, true, false, 3, true>;
+__global__ __launch_bounds__(Conv3DgradCfg::kThreads) void conv3_bwd_kernel(const WgradDArgs w,
+                                                                            const DirectArgs d,
+                                                                            int nw, int ntiles) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int bid = blockIdx.x;
+  if (bid < nw) {
+    if (threadIdx.x >= 256) return;
+    wgradd_body<64, 64, 3, 1, true>(w, sm, bid);
+    return;
+  }
+  const int i = bid - nw;
+  direct_conv_body<64, 64, 3, 4, 8, 1, 2, true, false, 3, true>(d, sm, i % ntiles, i / ntiles, 0);
 }
 
 hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(void*, const char*),
@@ -1331,7 +1353,34 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     if (fc4_done) CHECK_LAUNCH(fc4_done(fc4_done_arg));
     CHECK_LAUNCH(fork());   // side waits for fc4 dgrad (dconv3)
   }
-  {  // conv3 wgrad
+  // conv3 wgrad and dgrad in one launch: opt-in A/B (DDQ_VARIANT bit 32).
+  // Measured slower: 32.6 us against 15.2 + 15.3 separately -- the shared
+  // launch runs both bodies at the larger register count (199 VGPRs, 2 waves
+  // per SIMD), so a 6-wave dgrad workgroup leaves no room beside it.
+  const bool conv3_fused = !concurrent && !mark && nb.conv_impl == 1 && (nb.variant & 32);
+  if (conv3_fused) {
+    const int H = S / 4;
+    ConvWgrad<64, 64, 3, 1> p;
+    p.M = 64; p.N = 577; p.K = B * H * H;
+    int ns;
+    p.ksplit_len = split_len(p.K, kWgradBK[2], kWgradSplitLen[2], &ns);
+    p.rowtile = (H % kWgradBK[2]) == 0;
+    p.H = H; p.W = H; p.fW = FastDiv(H); p.fH = FastDiv(H);
+    p.NP = nb.wnp[2]; p.dconv = nb.dconv3; p.in = nb.pool2[0]; p.part = nb.wpart + nb.wpart_off[2];
+    WgradDArgs wa = wgradd_args(p, B, nb.wsplits[2]);
+    wa.droute = nb.mask3;
+    const int nw = (wa.G + 7) / 8 * 8 * 2 * 3;
+    DirectArgs d = direct_dgrad_args(nb.dconv3, nb.wk[0] + L.wk_off[2], nb.mask2, nb.dconv2, B, H, 1);
+    d.in_route = nb.mask3;
+    d.tiles_x = (H + 7) / 8;
+    const int ntiles = d.tiles_x * ((H + 3) / 4);
+    const size_t wsm = wgradd_smem_bytes<64, 1>(H);
+    const size_t dsm = (size_t)Conv3DgradCfg::kSmem * 4;
+    hipLaunchKernelGGL(conv3_bwd_kernel, dim3(nw + ntiles * B), dim3(Conv3DgradCfg::kThreads),
+                       wsm > dsm ? wsm : dsm, s, wa, d, nw, ntiles);
+    CHECK_LAUNCH(hipGetLastError());
+  }
+  if (!conv3_fused) {  // conv3 wgrad
     const int H = S / 4;
     ConvWgrad<64, 64, 3, 1> p;
     p.M = 64; p.N = 577; p.K = B * H * H;
@@ -1351,7 +1400,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
       CHECK_LAUNCH(launch_gemm<CfgW3>(p, 1, ns, sw));
     }
   }
-  {  // conv3 dgrad -> dconv2
+  if (!conv3_fused) {  // conv3 dgrad -> dconv2
     const int H = S / 4;
     ConvDgrad<64, 64, 3, 1> p;
     p.M = B * H * H; p.N = 64; p.K = 576; p.ksplit_len = 576;

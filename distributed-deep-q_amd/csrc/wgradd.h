@@ -42,14 +42,14 @@ struct WgradDGeom {
 // PSRC: dconv is given pooled (the gradient of the 2x2 max-pool output plus
 // its routing bytes, as fc4's data gradient leaves it) and expanded while the
 // rows are staged: value at the routed quadrant, 0 at the other three.
-template <int CIN, int COUT, int KS, int PAD, bool PSRC = false, int WPE = 2>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void wgradd_kernel(
-    const WgradDArgs a) {
+// Body of one 4-wave workgroup L of the 1-D grid (a fused launch with wider
+// workgroups ends the extra waves first; s_barrier does not wait for them).
+template <int CIN, int COUT, int KS, int PAD, bool PSRC>
+__device__ __forceinline__ void wgradd_body(const WgradDArgs& a, float* sm, int L) {
   constexpr int NCB = CIN / 32;
   constexpr int T = KS * NCB;
   constexpr int KC = KS * KS * CIN;
   using Geo = WgradDGeom<CIN, PAD>;
-  extern __shared__ __attribute__((aligned(16))) float sm[];
   const int W = a.W, H = a.H;
   const int W2 = (W + 1) >> 1;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   // round-robin, so give every (cb, ky) workgroup of row group g the same
   // L % 8 and the group's rows stay in one XCD's L2.
   constexpr int NTS = (COUT / 32) * KS;
-  const int L = blockIdx.x, xcd = L & 7, q = L >> 3;
+  const int xcd = L & 7, q = L >> 3;
   const int ts = q % NTS, g = xcd + 8 * (q / NTS);
   if (g >= a.G) return;
   const int cb = ts / KS, ky = ts % KS;
@@ -247,6 +247,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       slab[(size_t)co * a.NP + KC] = v;
     }
   }
+}
+
+template <int CIN, int COUT, int KS, int PAD, bool PSRC = false, int WPE = 2>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void wgradd_kernel(
+    const WgradDArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  wgradd_body<CIN, COUT, KS, PAD, PSRC>(a, sm, blockIdx.x);
 }
 
 template <int CIN, int PAD>

@@ -109,6 +109,7 @@ _SIGS = {
     "ddq_group_step": (ctypes.c_int, [ctypes.POINTER(_P), _i32, ctypes.POINTER(StepCfg)]),
     "ddq_profile_step": (ctypes.c_int, [_P, ctypes.POINTER(StepCfg), _P, _fp, _i32,
                                         ctypes.POINTER(_i32)]),
+    "ddq_time_layer": (ctypes.c_int, [_P, ctypes.c_char_p, _i32, _fp]),
     "ddq_step_flops": (ctypes.c_double, [_P]),
 }
 

@@ -344,6 +344,13 @@ class DeepQNet:
         return [(raw[16 * i:16 * i + 16].split(b"\0")[0].decode(), float(us[i]))
                 for i in range(min(n.value, cap))]
 
+    def time_layer(self, name, reps=100):
+        """Average device microseconds of one launch of a forward conv layer
+        ("conv1_fwd" / "conv2_fwd" / "conv3_fwd"), reps launches back to back."""
+        us = ctypes.c_float()
+        self._check(self.lib.ddq_time_layer(self.ctx, name.encode(), int(reps), ctypes.byref(us)))
+        return float(us.value)
+
     def step_flops(self):
         return float(self.lib.ddq_step_flops(self.ctx))
 

@@ -262,6 +262,11 @@ int64_t ddq_step_count(const ddq_ctx* ctx);
  * fills names (16 chars each, NUL padded) and device-time microseconds. */
 int ddq_profile_step(ddq_ctx* ctx, const ddq_step_cfg* cfg, char* names, float* usec,
                      int32_t cap, int32_t* n);
+/* Launch one forward conv layer ("conv1_fwd", "conv2_fwd" or "conv3_fwd",
+ * both towers, the step's own kernel and arguments) reps times back to back
+ * between two HIP events on the ctx stream; *usec = average device time per
+ * launch (no per-launch event overhead: the roofline's kernel time). */
+int ddq_time_layer(ddq_ctx* ctx, const char* name, int32_t reps, float* usec);
 /* Algorithmic FLOPs of one step (SURVEY.md 8(d) model, for the roofline). */
 double ddq_step_flops(const ddq_ctx* ctx);
 
