@@ -41,8 +41,18 @@ struct DirectCfg {
   static constexpr int G = 2 * V;                     // channels per read group
   static constexpr int CS = CP >= 8 ? CP + 4 : CP;    // patch pixel stride (floats)
   static constexpr int PH = TY + KS - 1, PW = TX + KS - 1;
-  static constexpr int RS = PW * CS + (CP >= 8 ? 0 : 2);   // patch row stride
-  static constexpr int CW = CP >= 8 ? CP + 4 : CP;    // weight row stride (one row per n)
+  // Patch row stride.  ds_read_b128 serves a wave in four 16-lane groups
+  // (lanes {0-3,12-15,20-27}, {4-11,16-19,28-31}, +32) on 64 banks; a group
+  // spans two pixel rows of the window-major block, so RS = 32 (mod 64)
+  // puts the two rows in opposite bank halves: conflict-free (RS = 16 mod
+  // 64 was 2-way, conv3's 40 mod 64 3-way).  CP < 8 (ds_read_b64, 32-lane
+  // groups) is conflict-free at PW*CP + 2.
+  static constexpr int RS0 = PW * CS + (CP >= 8 ? 0 : 2);
+  static constexpr int RS = CP >= 8 ? RS0 + (96 - RS0 % 64) % 64 : RS0;
+  // weight row stride (one row per n).  CP = 4 keeps stride 4 (2-way on the
+  // ds_read_b64 B reads): stride 6 is conflict-free but its 37 KB weight
+  // image costs conv1 a workgroup per CU (38.7 us against 30.7)
+  static constexpr int CW = CP >= 8 ? CP + 4 : CP;
   static constexpr int T = KS * KS;
   static constexpr int WSLOTS = WALL ? T : 2 * WK;
   static constexpr int kGroup = 64 * WM * WN;         // threads of one tap group
@@ -267,7 +277,13 @@ __device__ __forceinline__ void direct_conv_body(const DirectArgs& a, float* sme
         if (kWF4 % C::kThreads == 0 || f < kWF4) {
           const int n = f / (C::T * (CP / 4)), rem = f % (C::T * (CP / 4));
           const int t = rem / (CP / 4), c4 = rem % (CP / 4);
-          *reinterpret_cast<float4*>(wbuf + (t * N + n) * C::CW + 4 * c4) = wv[it];
+          float* dst = wbuf + (t * N + n) * C::CW + 4 * c4;
+          if (CP >= 8) {
+            *reinterpret_cast<float4*>(dst) = wv[it];
+          } else {
+            reinterpret_cast<float2*>(dst)[0] = make_float2(wv[it].x, wv[it].y);
+            reinterpret_cast<float2*>(dst)[1] = make_float2(wv[it].z, wv[it].w);
+          }
         }
       }
     } else {
