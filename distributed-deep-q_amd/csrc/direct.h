@@ -85,6 +85,8 @@ struct DirectArgs {
   const uint8_t* in_route;
   const uint8_t* pmask;      // dgrad: previous pool's routing bytes (B,H,W,N)
   float* pdconv;             // dgrad: previous layer's pre-pool gradient (B,2H,2W,N)
+  int pd_pooled;             // dgrad: 1 = store the pool-output gradient pooled, NHWC
+                             // (B,H,W,N); the consumer routes it through pmask
 };
 
 template <int V>
@@ -514,8 +516,12 @@ __device__ __forceinline__ void direct_conv_body(const DirectArgs& a, float* sme
           const int x = x0 + 2 * (win % (TX / 2)) + (m & 1);
           if (y >= a.H || x >= a.W) continue;
           const size_t pix = ((size_t)b * a.H + y) * a.W + x;
-          const int mk = a.pmask[pix * N + n];
           const float v = acc[i][j][r];
+          if (a.pd_pooled) {   // one store per element: lanes along n, 128-B runs
+            a.pdconv[pix * N + n] = v;
+            continue;
+          }
+          const int mk = a.pmask[pix * N + n];
           float* base = a.pdconv + (((size_t)b * 2 * a.H + 2 * y) * W2 + 2 * x) * N + n;
           base[0] = (mk == 0) ? v : 0.f;
           base[N] = (mk == 1) ? v : 0.f;

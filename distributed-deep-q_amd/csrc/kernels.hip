@@ -1446,6 +1446,9 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     if (nb.conv_impl == 1) {
       // 2 tap groups: two waves per SIMD over the 1024 output blocks
       DirectArgs d = direct_dgrad_args(nb.dconv2, p.wk, nb.mask1, nb.dconv1, B, H, 2);
+      // pool1-output gradient stored pooled (4.2 MB instead of the 16.8 MB
+      // un-pooled image, 3/4 zeros); conv1 wgrad expands it through mask1
+      d.pd_pooled = 1;
       // (8x8 tiles -- two 74 KB workgroups per CU -- measured 39.3 us, and
       // 8x8 register-B 42.9 us, against 36.8 us for this configuration)
       // (two 32-pixel blocks per wave over 4 tap groups: 40.6 us)
@@ -1476,6 +1479,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
       Wgrad1Args w;
       w.B = B; w.H = S; w.W = S; w.R = wgrad1_band(S, S); w.NP = nb.wnp[0];
       w.dconv = nb.dconv1; w.in = nb.state; w.part = p.part;
+      w.droute = nb.mask1;   // dconv1 holds conv2 dgrad's pooled output
       // (running the conv2/conv3 slab reduces as extra blocks of this launch
       // measured 1.7 us slower than the separate reduce kernel)
       CHECK_LAUNCH(launch_wgrad1(w, s));

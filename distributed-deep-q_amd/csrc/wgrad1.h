@@ -20,7 +20,9 @@ namespace ddq {
 struct Wgrad1Args {
   int B, H, W, R;              // conv1 grid (H = W = S), band height
   int NP;                      // slab pitch (>= 197)
-  const float* dconv;          // NHWC (B,H,W,32)
+  const float* dconv;          // NHWC (B,H,W,32); droute: pooled (B,H/2,W/2,32)
+  const uint8_t* droute;       // nullable: NHWC routing bytes of a pooled dconv (pool1's:
+                               // 0..3 = routed quadrant dy*2+dx, 4 = ReLU'd window)
   const float* in;             // NHWC (B,H,W,4)  (the gathered state)
   float* part;                 // [B * H / R][32][NP]
 };
@@ -50,20 +52,50 @@ __device__ __forceinline__ void wgrad1_body(const Wgrad1Args& a, float* sm, int 
   const float4* drow = reinterpret_cast<const float4*>(a.dconv + ((size_t)b * a.H + y0) * W * 32);
   // named registers: a float4 array here was kept in scratch (80 B/lane)
   float4 p0 = f4zero(), p1 = f4zero(), p2 = f4zero(), p3 = f4zero();
+  uint32_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;
   static_assert(kWgrad1Pre == 4, "prefetch registers");
-  auto load_row = [&](int r) {
-    const float4* s = drow + (size_t)r * nd4 + ht;
-    if (ht < nd4) p0 = s[0];
-    if (ht + 512 < nd4) p1 = s[512];
-    if (ht + 1024 < nd4) p2 = s[1024];
-    if (ht + 1536 < nd4) p3 = s[1536];
+  // Pooled source (conv2's data gradient leaves the pool1-output gradient,
+  // a quarter of the bytes): float4 f of full-res row y = pixel x = f/8,
+  // channels 4*(f%8).. read pooled pixel (y/2, x/2) and its routing bytes,
+  // and keep each channel only where the window routed quadrant (y&1, x&1).
+  const uint8_t* __restrict__ route = a.droute;
+  const int Wp = W >> 1;
+  auto src_off = [&](int r, int f) -> size_t {
+    return (((size_t)b * (a.H >> 1) + ((y0 + r) >> 1)) * Wp + ((f >> 3) >> 1)) * 32 + 4 * (f & 7);
   };
-  auto store_row = [&](float* dst) {
-    float4* d = reinterpret_cast<float4*>(dst) + ht;
-    if (ht < nd4) d[0] = p0;
-    if (ht + 512 < nd4) d[512] = p1;
-    if (ht + 1024 < nd4) d[1024] = p2;
-    if (ht + 1536 < nd4) d[1536] = p3;
+  auto load1 = [&](float4& p, uint32_t& m, int r, int f) {
+    if (f >= nd4) return;
+    if (!route) {
+      p = drow[(size_t)r * nd4 + f];
+    } else {
+      const size_t o = src_off(r, f);
+      p = *reinterpret_cast<const float4*>(a.dconv + o);
+      m = *reinterpret_cast<const uint32_t*>(route + o);
+    }
+  };
+  auto load_row = [&](int r) {
+    load1(p0, m0, r, ht);
+    load1(p1, m1, r, ht + 512);
+    load1(p2, m2, r, ht + 1024);
+    load1(p3, m3, r, ht + 1536);
+  };
+  auto store1 = [&](float4* d, float4 p, uint32_t m, int r, int f) {
+    if (f >= nd4) return;
+    if (route) {
+      const uint32_t q = (((y0 + r) & 1) << 1) | ((f >> 3) & 1);
+      p.x = (m & 0xff) == q ? p.x : 0.f;
+      p.y = ((m >> 8) & 0xff) == q ? p.y : 0.f;
+      p.z = ((m >> 16) & 0xff) == q ? p.z : 0.f;
+      p.w = (m >> 24) == q ? p.w : 0.f;
+    }
+    d[f] = p;
+  };
+  auto store_row = [&](float* dst, int r) {
+    float4* d = reinterpret_cast<float4*>(dst);
+    store1(d, p0, m0, r, ht);
+    store1(d, p1, m1, r, ht + 512);
+    store1(d, p2, m2, r, ht + 1024);
+    store1(d, p3, m3, r, ht + 1536);
   };
   load_row(rlo);
 
@@ -78,7 +110,7 @@ __device__ __forceinline__ void wgrad1_body(const Wgrad1Args& a, float* sm, int 
     d[0] = make_float2(v.x, v.y);
     d[1] = make_float2(v.z, v.w);
   }
-  store_row(dslot);
+  store_row(dslot, rlo);
   __syncthreads();
 
   const int l31 = lane & 31, h = lane >> 5;
@@ -105,7 +137,7 @@ __device__ __forceinline__ void wgrad1_body(const Wgrad1Args& a, float* sm, int 
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ar[xs * 64], 1.0f, acc, 0, 0, 0);
     }
     // the other slot was last read in iteration i-1, fenced by its barrier
-    if (i + 1 < rh) store_row(dslot + ((i + 1) & 1) * W * 32);
+    if (i + 1 < rh) store_row(dslot + ((i + 1) & 1) * W * 32, r + 1);
     __syncthreads();
   }
   // ---- the two halves' partial sums meet in LDS (fixed order) ----
