@@ -1373,6 +1373,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     const int nw = (wa.G + 7) / 8 * 8 * 2 * 3;
     DirectArgs d = direct_dgrad_args(nb.dconv3, nb.wk[0] + L.wk_off[2], nb.mask2, nb.dconv2, B, H, 1);
     d.in_route = nb.mask3;
+    d.pd_pooled = 1;
     d.tiles_x = (H + 7) / 8;
     const int ntiles = d.tiles_x * ((H + 3) / 4);
     const size_t wsm = wgradd_smem_bytes<64, 1>(H);
@@ -1413,6 +1414,9 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
       d.in_route = nb.mask3;   // pooled dconv3, expanded while the patch is staged
       // 4x8-pixel tiles (256 workgroups instead of 128: -2.5 us) with the B
       // operand straight from L2 (register-B, no weight ring: -2.5 us more)
+      // pool2-output gradient stored pooled (2.1 MB instead of 8.4 MB); the
+      // conv2 wgrad / dgrad expand it through mask2 while staging
+      d.pd_pooled = 1;
       CHECK_LAUNCH((launch_direct<64, 64, 3, 4, 8, 1, 2, true, false, 3, true>(d, 1, s)));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgD3>(p, 1, 1, s));
@@ -1431,7 +1435,9 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     M("conv2_wgrad");
     if (nb.conv_impl == 1) {
       // (3 waves per SIMD -- 168 VGPRs, 720 workgroups -- measured the same 39.0 us)
-      CHECK_LAUNCH((launch_wgradd<32, 64, 5, 2>(wgradd_args(p, B, nb.wsplits[1]), sw)));
+      WgradDArgs wa = wgradd_args(p, B, nb.wsplits[1]);
+      wa.droute = nb.mask2;   // dconv2 pooled (conv3 dgrad)
+      CHECK_LAUNCH((launch_wgradd<32, 64, 5, 2, true>(wa, sw)));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgW2>(p, 1, ns, sw));
     }
@@ -1446,6 +1452,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     if (nb.conv_impl == 1) {
       // 2 tap groups: two waves per SIMD over the 1024 output blocks
       DirectArgs d = direct_dgrad_args(nb.dconv2, p.wk, nb.mask1, nb.dconv1, B, H, 2);
+      d.in_route = nb.mask2;   // dconv2 pooled (conv3 dgrad), expanded while staged
       // pool1-output gradient stored pooled (4.2 MB instead of the 16.8 MB
       // un-pooled image, 3/4 zeros); conv1 wgrad expands it through mask1
       d.pd_pooled = 1;
