@@ -873,6 +873,7 @@ __device__ __forceinline__ float apply_one(const ApplyArgs& a, bool first, int64
 // serial latency-bound launch at the head of the next step.  The counter it
 // draws with was advanced by this step's bookkeeping (the reduce kernel), so
 // the draws are the ones sequential steps make.
+template <int U>
 __global__ __launch_bounds__(256) void apply_kernel(
     float* __restrict__ theta, const float* __restrict__ grad, float* __restrict__ opt,
     const int32_t* __restrict__ opt_init, float* __restrict__ wk, float* __restrict__ thetaP,
@@ -889,12 +890,24 @@ __global__ __launch_bounds__(256) void apply_kernel(
   }
   const bool first = opt_init[2] != 0;      // latched by apply_book
   const bool sync = opt_init[3] != 0;
-  const int64_t i = ((int64_t)(blockIdx.x - pf.ng) * blockDim.x + threadIdx.x) * 4;
-  if (i < a.n) {
-    const float4 g4 = *reinterpret_cast<const float4*>(grad + i);
-    const float4 t4 = *reinterpret_cast<const float4*>(theta + i);
-    float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (a.rule != 0 && !first) s4 = *reinterpret_cast<const float4*>(opt + i);
+  // U float4 per thread, every load issued before the first update
+  const int64_t i0 = ((int64_t)(blockIdx.x - pf.ng) * blockDim.x * U + threadIdx.x) * 4;
+  float4 gv[U], tv[U], sv[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = i0 + (int64_t)u * blockDim.x * 4;
+    gv[u] = tv[u] = sv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < a.n) {
+      gv[u] = *reinterpret_cast<const float4*>(grad + i);
+      tv[u] = *reinterpret_cast<const float4*>(theta + i);
+      if (a.rule != 0 && !first) sv[u] = *reinterpret_cast<const float4*>(opt + i);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = i0 + (int64_t)u * blockDim.x * 4;
+    if (i >= a.n) continue;
+    const float4 g4 = gv[u], t4 = tv[u], s4 = sv[u];
     float th[4] = {t4.x, t4.y, t4.z, t4.w};
     const float g[4] = {g4.x, g4.y, g4.z, g4.w};
     float st[4] = {s4.x, s4.y, s4.z, s4.w};
@@ -1060,9 +1073,10 @@ hipError_t launch_apply(const NetBuffers& nb, int rule, float lr, float decay, f
   a.one_minus_decay = (float)(1.0 - (double)decay);   // numpy: (1 - rmsprop_decay) in double
   for (int l = 0; l < 5; ++l) { a.bias_lo[l] = nb.L.b[l]; a.bias_hi[l] = nb.L.b[l] + nb.L.bn[l]; }
   conv_dims(nb.L, a.conv);
-  const int blocks = (int)((a.n / 4 + 255) / 256);
   if (!booked) hipLaunchKernelGGL(apply_book_kernel, dim3(1), dim3(1), 0, s, nb.iter, nb.opt_init, period);
-  hipLaunchKernelGGL(apply_kernel, dim3(blocks + pf.ng), dim3(256), 0, s, nb.theta[0], nb.grad,
+  // one float4 per thread (two, loads first: 12.0 us against 11.3 in the trace)
+  const int blocks = (int)((a.n / 4 + 255) / 256);
+  hipLaunchKernelGGL(apply_kernel<1>, dim3(blocks + pf.ng), dim3(256), 0, s, nb.theta[0], nb.grad,
                      nb.opt, nb.opt_init, nb.wk[0], nb.theta[1], nb.wk[1], a, pf);
   return hipGetLastError();
 }
@@ -1111,7 +1125,11 @@ int wgrad_splits_for(int layer, int B, int S, int* np, int impl) {
   if (impl == 1) {                                                    // direct: one slab per row group
     const int nts[3] = {0, 2 * 5, 2 * 3};
     int G, RPG;
-    wgradd_groups(B * H, nts[layer], &G, &RPG);
+    int target = 512;
+    // tuning sweeps; conv3 measured 128: 25.0 us, 256: 16.0, 512: 15.2, 1024: 18.8
+    const char* e = layer == 2 ? getenv("DDQ_WG3_TARGET") : nullptr;
+    if (e && atoi(e) > 0) target = atoi(e);
+    wgradd_groups(B * H, nts[layer], &G, &RPG, target);
     return G;
   }
   int ns;
