@@ -909,12 +909,14 @@ static hipError_t fc4_bucket_start(void* arg) {
 }
 
 static int enqueue_fwd_bwd_x(ddq_ctx* c, const NetBuffers& nb, void (*mark)(void*, const char*),
-                             void* marg, int book, ReplayMeta* bump, bool overlap) {
+                             void* marg, int book, ReplayMeta* bump, bool overlap,
+                             const Prefetch* pf = nullptr) {
   HIP_TRY(c, launch_forward(nb, 2, c->stream, mark, marg, false));
   if (mark) mark(marg, "head");
-  HIP_TRY(c, launch_head(nb, c->stream));
+  HIP_TRY(c, launch_head(nb, c->stream, bump));   // fused apply: the draw counter advances here
   hipError_t e = launch_backward(nb, c->stream, mark, marg, mark == nullptr && (nb.variant & 16),
-                                 book >= 0, book, bump, overlap ? fc4_bucket_start : nullptr, c);
+                                 book >= 0, book, bump, overlap ? fc4_bucket_start : nullptr, c,
+                                 pf);
   if (e != hipSuccess && !c->comm_err.empty()) {
     std::string m = c->comm_err;
     c->comm_err.clear();
@@ -999,6 +1001,18 @@ static int enqueue_train(ddq_ctx* c, const ddq_step_cfg* cfg, const NetBuffers& 
                          ReplayMeta* bump = nullptr) {
   NetBuffers nb = nb_in;
   nb.book_inc = step_inc(c, cfg);
+  // exchange-free steps: fc4's weight update rides on the slab-reduce launch
+  // (DDQ_VARIANT bit 512: off, A/B); per-kernel profiling keeps it separate
+  const int ex = has_exchange(c, cfg) ? cfg->exchange : DDQ_EXCHANGE_NONE;
+  if (ex == DDQ_EXCHANGE_NONE && mark == nullptr && nb.conv_impl == 1 && !(nb.variant & 16) &&
+      !(nb.variant & 512) && fused_apply_ok(nb.L)) {
+    const ddq_update_cfg& u = cfg->update;
+    nb.fa.on = 1;
+    nb.fa.rule = u.rule;
+    nb.fa.period = cfg->target_period > 0 ? cfg->target_period : 0;
+    nb.fa.lr = u.lr; nb.fa.decay = u.decay; nb.fa.eps = u.eps;
+    nb.fa.momentum = u.momentum; nb.fa.wd = u.weight_decay;
+  }
   if (pre && fused_prefetch(c, cfg)) {
     // the step's bookkeeping advances the draw counter (bump) before the apply
     // launch draws the next minibatch with it
@@ -1006,9 +1020,10 @@ static int enqueue_train(ddq_ctx* c, const ddq_step_cfg* cfg, const NetBuffers& 
                                       c->r_meta, cfg->seed);
     const bool overlap = has_exchange(c, cfg) && cfg->exchange == DDQ_EXCHANGE_ALLREDUCE &&
                          cfg->overlap && c->comm && mark == nullptr;
+    // fused apply: the slab-reduce launch carries the draw + gather too
     TRY(enqueue_fwd_bwd_x(c, nb, mark, marg, cfg->target_period > 0 ? cfg->target_period : 0,
-                          c->r_meta, overlap));
-    return enqueue_exchange_apply(c, cfg, nb, mark, marg, overlap, &pf);
+                          c->r_meta, overlap, nb.fa.on ? &pf : nullptr));
+    return enqueue_exchange_apply(c, cfg, nb, mark, marg, overlap, nb.fa.on ? nullptr : &pf);
   }
   if (pre) {
     HIP_TRY(c, hipEventRecord(nb.ev[6], c->stream));

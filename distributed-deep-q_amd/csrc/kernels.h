@@ -27,6 +27,13 @@ struct ReplayMeta {
   int32_t pad;
 };
 
+// Fused fc4-weight apply (exchange-free steps): the update rule of the step.
+struct FusedApplyCfg {
+  int on;
+  int rule, period;
+  float lr, decay, eps, momentum, wd;
+};
+
 struct NetBuffers {
   int B, S;
   // minibatch (NHWC frames; action one-hot (B,4); reward / non_terminal (B))
@@ -58,6 +65,8 @@ struct NetBuffers {
   int conv_impl;                    // 0 = implicit-GEMM engine, 1 = direct (patch-in-LDS)
   int variant;                      // tuning experiments (DDQ_VARIANT bits), 0 = default
   int fwd_only;                     // launch_forward: 0 = every layer, l + 1 = conv layer l only
+  FusedApplyCfg fa;                 // on: head latches the apply flags, the slab reduce
+                                    // applies fc4's weights, launch_apply the rest
   int book_inc;                     // param-server iterations per apply (1, or W: server mode)
 };
 
@@ -72,12 +81,17 @@ hipError_t launch_gather(const NetBuffers& nb, const uint8_t* st, const uint8_t*
 hipError_t launch_sample(const NetBuffers& nb, ReplayMeta* meta, uint64_t seed, hipStream_t s);
 hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s, void (*mark)(void*, const char*), void* mark_arg,
                           bool out = true);
-hipError_t launch_head(const NetBuffers& nb, hipStream_t s);
+// bump (fused apply only): the step's draw-counter advance, done here so the
+// slab-reduce launch can carry the next step's draw + gather
+hipError_t launch_head(const NetBuffers& nb, hipStream_t s, ReplayMeta* bump = nullptr);
+bool fused_apply_ok(const ParamLayout& L);
+struct Prefetch;
 // concurrent: run the weight-gradient GEMMs on nb.side beside the data-gradient chain.
+// pf (fused apply only): the next step's draw + gather as blocks of the slab-reduce launch.
 hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(void*, const char*),
                            void* mark_arg, bool concurrent, bool book = false, int book_period = 0,
                            ReplayMeta* bump = nullptr, hipError_t (*fc4_done)(void*) = nullptr,
-                           void* fc4_done_arg = nullptr);
+                           void* fc4_done_arg = nullptr, const Prefetch* pf = nullptr);
 // period > 0: also copy Q -> P when the next pull sees iteration % period == 0.
 // Next step's draw + gather carried by the apply launch (pipelined stepping)
 struct Prefetch {

@@ -567,10 +567,19 @@ __global__ __launch_bounds__(512) void fc4_head_kernel(
     const float* __restrict__ nonterm, float* __restrict__ h4q, float* __restrict__ h4p,
     float* __restrict__ outq, float* __restrict__ outp, float* q_sa_o, float* p_sa_o,
     float* target_o, float* __restrict__ dqbuf, float* __restrict__ lpart,
-    float* __restrict__ dh4) {
+    float* __restrict__ dh4, int32_t* latch, const int64_t* iter, int period, int inc,
+    ReplayMeta* bump) {
   __shared__ float red[8][8];
   __shared__ float qp[8];
   const int b = blockIdx.x, n = threadIdx.x, w = n >> 6;
+  // fused apply: latch the step's apply flags now (the values apply_book
+  // latches again in the slab reduce), so the fc4 apply blocks of that launch
+  // never read them while its block 0 advances the counters
+  if (latch && b == 0 && n == 0) {
+    latch[2] = (latch[0] == 0);
+    latch[3] = period > 0 && ((*iter + inc) % period) == 0;
+    if (bump) bump->counter += 1;   // the step's draw (apply_book's bump, moved here)
+  }
   const size_t stride = (size_t)2 * B * kFc4;
   float h[2];
   float q[8];
@@ -718,12 +727,14 @@ __device__ void head_sums(int hb, int B, const float* __restrict__ dqbuf,
   }
 }
 
-hipError_t launch_head(const NetBuffers& nb, hipStream_t s) {
+hipError_t launch_head(const NetBuffers& nb, hipStream_t s, ReplayMeta* bump) {
   const ParamLayout& L = nb.L;
   hipLaunchKernelGGL(fc4_head_kernel, dim3(nb.B), dim3(kFc4), 0, s, nb.fc4_part, nb.fc4_splits,
                      nb.B, nb.gamma, nb.theta[0], nb.theta[1], L.b[3], L.w[4], L.b[4], nb.action,
                      nb.reward, nb.nonterm, nb.h4[0], nb.h4[1], nb.q_out, nb.p_out, nb.q_sa,
-                     nb.p_sa, nb.target, nb.dqbuf, nb.lpart, nb.dh4);
+                     nb.p_sa, nb.target, nb.dqbuf, nb.lpart, nb.dh4,
+                     nb.fa.on ? nb.opt_init : nullptr, nb.iter, nb.fa.period, nb.book_inc,
+                     nb.fa.on ? bump : nullptr);
   return hipGetLastError();
 }
 
@@ -754,6 +765,111 @@ __device__ __forceinline__ void apply_book(int64_t* iter, int32_t* opt_init, int
   opt_init[3] = period > 0 && ((it + inc) % period) == 0;
   *iter = it + inc;
   opt_init[0] = 1;
+}
+
+// ---------------------------------------------------------------------------
+// apply: server.py update rules on the flat Q tower, float4 per thread, with
+//  - the conv kernel-layout copy refreshed from the new values,
+//  - the target sync P <- Q fused in when the NEXT pull will see
+//    iteration % period == 0 (server.py:188-189),
+// ---------------------------------------------------------------------------
+struct ApplyArgs {
+  int64_t n;
+  int64_t lo, hi, skip_lo, skip_len;   // elements [lo, hi) minus [skip_lo, skip_lo + skip_len)
+  int rule, period;
+  float lr, decay, one_minus_decay, eps, momentum, wd;
+  int64_t bias_lo[5], bias_hi[5];   // [lo,hi) element ranges of biases (momentum multipliers)
+  ConvDims conv[3];
+};
+
+__device__ __forceinline__ float apply_one(const ApplyArgs& a, bool first, int64_t i, float th,
+                                           float g, float& st) {
+  switch (a.rule) {
+    case 0:   // sgd: theta - lr*g  (server.py:81-83, apply_descent :66-68)
+      return th - a.lr * g;
+    case 1: { // rmsprop with the one-step-lagged cache (server.py:86-105)
+      const float g2 = g * g;
+      const float c_use = first ? g2 : st;
+      st = first ? g2 : (a.decay * st + a.one_minus_decay * g2);
+      return th - (a.lr * g) / sqrtf(c_use + a.eps);
+    }
+    case 2: { // adagrad with the current accumulator (server.py:108-124)
+      const float acc = first ? g * g : st + g * g;
+      st = acc;
+      return th - (a.lr * g) / sqrtf(acc + a.eps);
+    }
+    default: { // Caffe SGDSolver momentum (blobs_lr {1,2}, weight_decay {1,0})
+      bool is_bias = false;
+#pragma unroll
+      for (int l = 0; l < 5; ++l) is_bias |= (i >= a.bias_lo[l] && i < a.bias_hi[l]);
+      const float lr = a.lr * (is_bias ? 2.f : 1.f);
+      const float wd = is_bias ? 0.f : a.wd;
+      const float v = a.momentum * (first ? 0.f : st) + lr * (g + wd * th);
+      st = v;
+      return th - v;
+    }
+  }
+}
+
+// Update operands of the apply (the apply launch, or the fused fc4-weight
+// apply blocks of the slab-reduce launch).
+struct ApplyTail {
+  float* theta;
+  const float* grad;
+  float* opt;
+  const int32_t* opt_init;   // [2] first call, [3] P<-Q sync due: latched before the launch
+  float* wk;
+  float* thetaP;
+  float* wkP;
+  int blk0;                  // first apply block of the launch
+};
+
+// One float4 of parameters per thread: block blk covers elements
+// lo + blk*1024 ..., with the skipped range jumped over (float4-aligned).
+__device__ __forceinline__ void apply_elems(const ApplyTail& t, const ApplyArgs& a, int64_t blk) {
+  const bool first = t.opt_init[2] != 0;
+  const bool sync = t.opt_init[3] != 0;
+  int64_t i = a.lo + (blk * 256 + threadIdx.x) * 4;
+  if (i >= a.skip_lo) i += a.skip_len;
+  if (i >= a.hi) return;
+  const float4 g4 = *reinterpret_cast<const float4*>(t.grad + i);
+  const float4 t4 = *reinterpret_cast<const float4*>(t.theta + i);
+  float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (a.rule != 0 && !first) s4 = *reinterpret_cast<const float4*>(t.opt + i);
+  float th[4] = {t4.x, t4.y, t4.z, t4.w};
+  const float g[4] = {g4.x, g4.y, g4.z, g4.w};
+  float st[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) th[e] = apply_one(a, first, i + e, th[e], g[e], st[e]);
+  const float4 o4 = make_float4(th[0], th[1], th[2], th[3]);
+  *reinterpret_cast<float4*>(t.theta + i) = o4;
+  if (a.rule != 0) *reinterpret_cast<float4*>(t.opt + i) = make_float4(st[0], st[1], st[2], st[3]);
+  if (sync) *reinterpret_cast<float4*>(t.thetaP + i) = o4;
+#pragma unroll
+  for (int l = 0; l < 3; ++l) {
+    const ConvDims& d = a.conv[l];
+    const int64_t e0 = i - d.w_off;
+    if (e0 >= 0 && e0 < (int64_t)d.cout * d.cin * d.ks * d.ks) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = wk_local(d, (int)e0 + e);
+        t.wk[d.wk_off + k] = th[e];
+        if (sync) t.wkP[d.wk_off + k] = th[e];
+      }
+    }
+  }
+}
+
+// Prefetch block g: every block draws the (same) sorted index set of the next
+// step with the already-advanced counter, then gathers its slice.
+__device__ __forceinline__ void prefetch_body(const Prefetch& pf, int g) {
+  __shared__ int64_t cand[256];
+  __shared__ int bad_any;
+  const int bx = g % pf.gx, b = (g / pf.gx) % pf.B, z = g / (pf.gx * pf.B);
+  draw_sorted(pf.meta, pf.B, pf.seed, pf.meta->counter, cand, &bad_any);
+  if (g == 0 && threadIdx.x < pf.B) pf.idx[threadIdx.x] = (int32_t)cand[threadIdx.x];
+  gather_body(pf.st, pf.act, pf.rew, pf.nt, pf.meta, cand[b], pf.S, pf.sQ, pf.sP, pf.action,
+              pf.reward, pf.nonterm, bx, b, z);
 }
 
 // Slab reduce: a unit = 64 slab columns n of one (layer, co).  Persistent
@@ -808,9 +924,17 @@ __device__ __forceinline__ void wred_unit(const float* __restrict__ part, float*
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(
     const float* __restrict__ part, float* __restrict__ grad, WredDims d0, WredDims d1,
     WredDims d2, int nunits, int nub, int64_t* iter, int32_t* opt_init, int book_period,
-    ReplayMeta* bump, int book_inc, HeadSums hs) {
+    ReplayMeta* bump, int book_inc, HeadSums hs, ApplyTail fat, ApplyArgs faa, Prefetch pf) {
   __shared__ float red[4][64];
-  const int bid = blockIdx.x;
+  if ((int)blockIdx.x < pf.ng) {   // fused apply: the next step's draw + gather first
+    prefetch_body(pf, blockIdx.x);
+    return;
+  }
+  const int bid = blockIdx.x - pf.ng;
+  if (fat.blk0 > 0 && bid >= fat.blk0) {   // fused fc4-weight apply blocks
+    apply_elems(fat, faa, bid - fat.blk0);
+    return;
+  }
   if (opt_init && bid == 0 && threadIdx.x == 0)
     apply_book(iter, opt_init, book_period, bump, book_inc);
   if (bid >= nub) {
@@ -824,113 +948,19 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(
   }
 }
 
-// ---------------------------------------------------------------------------
-// apply: server.py update rules on the flat Q tower, float4 per thread, with
-//  - the conv kernel-layout copy refreshed from the new values,
-//  - the target sync P <- Q fused in when the NEXT pull will see
-//    iteration % period == 0 (server.py:188-189),
-// ---------------------------------------------------------------------------
-struct ApplyArgs {
-  int64_t n;
-  int rule, period;
-  float lr, decay, one_minus_decay, eps, momentum, wd;
-  int64_t bias_lo[5], bias_hi[5];   // [lo,hi) element ranges of biases (momentum multipliers)
-  ConvDims conv[3];
-};
-
-__device__ __forceinline__ float apply_one(const ApplyArgs& a, bool first, int64_t i, float th,
-                                           float g, float& st) {
-  switch (a.rule) {
-    case 0:   // sgd: theta - lr*g  (server.py:81-83, apply_descent :66-68)
-      return th - a.lr * g;
-    case 1: { // rmsprop with the one-step-lagged cache (server.py:86-105)
-      const float g2 = g * g;
-      const float c_use = first ? g2 : st;
-      st = first ? g2 : (a.decay * st + a.one_minus_decay * g2);
-      return th - (a.lr * g) / sqrtf(c_use + a.eps);
-    }
-    case 2: { // adagrad with the current accumulator (server.py:108-124)
-      const float acc = first ? g * g : st + g * g;
-      st = acc;
-      return th - (a.lr * g) / sqrtf(acc + a.eps);
-    }
-    default: { // Caffe SGDSolver momentum (blobs_lr {1,2}, weight_decay {1,0})
-      bool is_bias = false;
-#pragma unroll
-      for (int l = 0; l < 5; ++l) is_bias |= (i >= a.bias_lo[l] && i < a.bias_hi[l]);
-      const float lr = a.lr * (is_bias ? 2.f : 1.f);
-      const float wd = is_bias ? 0.f : a.wd;
-      const float v = a.momentum * (first ? 0.f : st) + lr * (g + wd * th);
-      st = v;
-      return th - v;
-    }
-  }
-}
-
 // Blocks [0, pf.ng) of the apply launch draw + gather the NEXT step's
 // minibatch into the other buffer set (pipelined stepping, B <= 256): the
 // sample_gather kernel's work rides on the HBM-bound apply instead of being a
 // serial latency-bound launch at the head of the next step.  The counter it
 // draws with was advanced by this step's bookkeeping (the reduce kernel), so
 // the draws are the ones sequential steps make.
-template <int U>
-__global__ __launch_bounds__(256) void apply_kernel(
-    float* __restrict__ theta, const float* __restrict__ grad, float* __restrict__ opt,
-    const int32_t* __restrict__ opt_init, float* __restrict__ wk, float* __restrict__ thetaP,
-    float* __restrict__ wkP, ApplyArgs a, Prefetch pf) {
+__global__ __launch_bounds__(256) void apply_kernel(ApplyTail t, ApplyArgs a, Prefetch pf) {
   if ((int)blockIdx.x < pf.ng) {
-    __shared__ int64_t cand[256];
-    __shared__ int bad_any;
-    const int g = blockIdx.x, bx = g % pf.gx, b = (g / pf.gx) % pf.B, z = g / (pf.gx * pf.B);
-    draw_sorted(pf.meta, pf.B, pf.seed, pf.meta->counter, cand, &bad_any);
-    if (g == 0 && threadIdx.x < pf.B) pf.idx[threadIdx.x] = (int32_t)cand[threadIdx.x];
-    gather_body(pf.st, pf.act, pf.rew, pf.nt, pf.meta, cand[b], pf.S, pf.sQ, pf.sP, pf.action,
-                pf.reward, pf.nonterm, bx, b, z);
+    prefetch_body(pf, blockIdx.x);
     return;
   }
-  const bool first = opt_init[2] != 0;      // latched by apply_book
-  const bool sync = opt_init[3] != 0;
-  // U float4 per thread, every load issued before the first update
-  const int64_t i0 = ((int64_t)(blockIdx.x - pf.ng) * blockDim.x * U + threadIdx.x) * 4;
-  float4 gv[U], tv[U], sv[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int64_t i = i0 + (int64_t)u * blockDim.x * 4;
-    gv[u] = tv[u] = sv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (i < a.n) {
-      gv[u] = *reinterpret_cast<const float4*>(grad + i);
-      tv[u] = *reinterpret_cast<const float4*>(theta + i);
-      if (a.rule != 0 && !first) sv[u] = *reinterpret_cast<const float4*>(opt + i);
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int64_t i = i0 + (int64_t)u * blockDim.x * 4;
-    if (i >= a.n) continue;
-    const float4 g4 = gv[u], t4 = tv[u], s4 = sv[u];
-    float th[4] = {t4.x, t4.y, t4.z, t4.w};
-    const float g[4] = {g4.x, g4.y, g4.z, g4.w};
-    float st[4] = {s4.x, s4.y, s4.z, s4.w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) th[e] = apply_one(a, first, i + e, th[e], g[e], st[e]);
-    const float4 o4 = make_float4(th[0], th[1], th[2], th[3]);
-    *reinterpret_cast<float4*>(theta + i) = o4;
-    if (a.rule != 0) *reinterpret_cast<float4*>(opt + i) = make_float4(st[0], st[1], st[2], st[3]);
-    if (sync) *reinterpret_cast<float4*>(thetaP + i) = o4;
-#pragma unroll
-    for (int l = 0; l < 3; ++l) {
-      const ConvDims& d = a.conv[l];
-      const int64_t e0 = i - d.w_off;
-      if (e0 >= 0 && e0 < (int64_t)d.cout * d.cin * d.ks * d.ks) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int k = wk_local(d, (int)e0 + e);
-          wk[d.wk_off + k] = th[e];
-          if (sync) wkP[d.wk_off + k] = th[e];
-        }
-      }
-    }
-  }
+  // (two float4 per thread with every load first measured 12.0 us against 11.3)
+  apply_elems(t, a, (int)blockIdx.x - pf.ng);
 }
 
 // param-server iteration / first-call bookkeeping of one apply: latch the
@@ -1016,12 +1046,24 @@ static ApplyArgs apply_args(const NetBuffers& nb, int rule, float lr, float deca
                             float momentum, float wd, int period) {
   ApplyArgs a;
   a.n = nb.L.total;
+  a.lo = 0; a.hi = a.n; a.skip_lo = a.n; a.skip_len = 0;
   a.rule = rule; a.period = period;
   a.lr = lr; a.decay = decay; a.eps = eps; a.momentum = momentum; a.wd = wd;
-  a.one_minus_decay = (float)(1.0 - (double)decay);
+  a.one_minus_decay = (float)(1.0 - (double)decay);   // numpy: (1 - rmsprop_decay) in double
   for (int l = 0; l < 5; ++l) { a.bias_lo[l] = nb.L.b[l]; a.bias_hi[l] = nb.L.b[l] + nb.L.bn[l]; }
   conv_dims(nb.L, a.conv);
   return a;
+}
+
+static ApplyTail apply_tail(const NetBuffers& nb) {
+  return ApplyTail{nb.theta[0], nb.grad, nb.opt, nb.opt_init, nb.wk[0], nb.theta[1], nb.wk[1], 0};
+}
+
+// The fused fc4-weight apply (NetBuffers::fa): fc4's weight gradient is final
+// after the fc4 backward, so its update runs as extra blocks of the slab-
+// reduce launch and the apply launch keeps the rest of the parameters.
+bool fused_apply_ok(const ParamLayout& L) {
+  return L.w[3] % 4 == 0 && L.b[3] % 4 == 0 && L.b[3] > L.w[3];
 }
 
 hipError_t launch_apply_shard(const NetBuffers& nb, int rule, float lr, float decay, float eps,
@@ -1066,18 +1108,14 @@ hipError_t launch_apply(const NetBuffers& nb, int rule, float lr, float decay, f
                         const Prefetch* pre) {
   Prefetch pf{};
   if (pre) pf = *pre;
-  ApplyArgs a;
-  a.n = nb.L.total;
-  a.rule = rule; a.period = period;
-  a.lr = lr; a.decay = decay; a.eps = eps; a.momentum = momentum; a.wd = wd;
-  a.one_minus_decay = (float)(1.0 - (double)decay);   // numpy: (1 - rmsprop_decay) in double
-  for (int l = 0; l < 5; ++l) { a.bias_lo[l] = nb.L.b[l]; a.bias_hi[l] = nb.L.b[l] + nb.L.bn[l]; }
-  conv_dims(nb.L, a.conv);
+  ApplyArgs a = apply_args(nb, rule, lr, decay, eps, momentum, wd, period);
+  if (nb.fa.on) {   // fc4 weights were applied by the slab-reduce launch
+    a.skip_lo = nb.L.w[3];
+    a.skip_len = nb.L.b[3] - nb.L.w[3];
+  }
   if (!booked) hipLaunchKernelGGL(apply_book_kernel, dim3(1), dim3(1), 0, s, nb.iter, nb.opt_init, period);
-  // one float4 per thread (two, loads first: 12.0 us against 11.3 in the trace)
-  const int blocks = (int)((a.n / 4 + 255) / 256);
-  hipLaunchKernelGGL(apply_kernel<1>, dim3(blocks + pf.ng), dim3(256), 0, s, nb.theta[0], nb.grad,
-                     nb.opt, nb.opt_init, nb.wk[0], nb.theta[1], nb.wk[1], a, pf);
+  const int blocks = (int)(((a.n - a.skip_len) / 4 + 255) / 256);
+  hipLaunchKernelGGL(apply_kernel, dim3(blocks + pf.ng), dim3(256), 0, s, apply_tail(nb), a, pf);
   return hipGetLastError();
 }
 
@@ -1309,7 +1347,8 @@ __global__ __launch_bounds__(Conv3DgradCfg::kThreads) void conv3_bwd_kernel(cons
 
 hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(void*, const char*),
                            void* marg, bool concurrent, bool book, int book_period,
-                           ReplayMeta* bump, hipError_t (*fc4_done)(void*), void* fc4_done_arg) {
+                           ReplayMeta* bump, hipError_t (*fc4_done)(void*), void* fc4_done_arg,
+                           const Prefetch* pre) {
   const ParamLayout& L = nb.L;
   const int B = nb.B, S = nb.S;
   const int s4 = S / 8;
@@ -1522,10 +1561,23 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     HeadSums hs{0, B, nb.dqbuf, nb.lpart, nb.h4[0], nb.dh4, nb.loss, nb.grad + L.w[4],
                 nb.grad + L.b[4], nb.grad + L.b[3]};
     const int nub = blk < kWredBlocks ? blk : kWredBlocks;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(nub + kFc4 / 64), dim3(256), 0, s, nb.wpart,
-                       nb.grad, d[0], d[1], d[2], blk, nub, nb.iter,
-                       book ? nb.opt_init : nullptr, book_period, book ? bump : nullptr,
-                       nb.book_inc, hs);
+    ApplyTail fat = apply_tail(nb);
+    ApplyArgs faa = apply_args(nb, nb.fa.rule, nb.fa.lr, nb.fa.decay, nb.fa.eps, nb.fa.momentum,
+                               nb.fa.wd, nb.fa.period);
+    int nfa = 0;
+    fat.blk0 = 0;
+    if (nb.fa.on) {   // fc4 weights [w4, b4): its gradient is final since fc4_bwd
+      faa.lo = L.w[3];
+      faa.hi = L.b[3];
+      nfa = (int)(((L.b[3] - L.w[3]) / 4 + 255) / 256);
+      fat.blk0 = nub + kFc4 / 64;
+    }
+    Prefetch pf{};
+    if (pre && nb.fa.on) pf = *pre;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(pf.ng + nub + kFc4 / 64 + nfa), dim3(256), 0, s,
+                       nb.wpart, nb.grad, d[0], d[1], d[2], blk, nub, nb.iter,
+                       book ? nb.opt_init : nullptr, book_period,
+                       book && !nb.fa.on ? bump : nullptr, nb.book_inc, hs, fat, faa, pf);
     CHECK_LAUNCH(hipGetLastError());
   }
   return hipSuccess;

@@ -199,3 +199,33 @@ def test_barista_tcp_loop_with_dummy_client(param_server, tmp_path, monkeypatch)
         c.close()
     th.join(timeout=60)
     assert ps.iteration == 3
+
+
+def test_time_layer_times_the_step_kernels_without_side_effects():
+    """ddq_time_layer (the bench's roofline timing) relaunches one forward conv
+    layer of the step: positive times, the next full pass unchanged, and an
+    unknown layer name is an error, not a launch."""
+    import ddq
+    S, B = 16, 32
+    rng = np.random.default_rng(7)
+    net = ddq.DeepQNet(batch=B, frame=S, device=0)
+    theta = ref.flatten(ref.init_params(S, seed=2))
+    net.set_flat(0, theta)
+    net.set_flat(1, theta)
+    st = rng.integers(0, 256, (B, 4, S, S)).astype(np.float32)
+    ns = rng.integers(0, 256, (B, 4, S, S)).astype(np.float32)
+    ac = np.eye(4, dtype=np.float32)[rng.integers(0, 4, B)].reshape(B, 4, 1, 1)
+    rw = rng.integers(-1, 2, (B, 1, 1, 1)).astype(np.float32)
+    nt = np.ones((B, 1, 1, 1), np.float32)
+    net.write_minibatch(st, ac, rw, ns, nt)
+    loss0 = net.forward_backward()
+    g0 = net.get_grads_flat()
+    for name in ("conv1_fwd", "conv2_fwd", "conv3_fwd"):
+        us = net.time_layer(name, 5)
+        assert 0.0 < us < 1e5, (name, us)
+    with pytest.raises(Exception):
+        net.time_layer("fc9_fwd", 1)
+    loss1 = net.forward_backward()
+    assert loss1 == loss0
+    np.testing.assert_array_equal(net.get_grads_flat(), g0)
+    net.close()
