@@ -1165,7 +1165,7 @@ int wgrad_splits_for(int layer, int B, int S, int* np, int impl) {
     int G, RPG;
     int target = 512;
     // tuning sweeps; conv3 measured 128: 25.0 us, 256: 16.0, 512: 15.2, 1024: 18.8
-    const char* e = layer == 2 ? getenv("DDQ_WG3_TARGET") : nullptr;
+    const char* e = getenv(layer == 2 ? "DDQ_WG3_TARGET" : "DDQ_WG2_TARGET");
     if (e && atoi(e) > 0) target = atoi(e);
     wgradd_groups(B * H, nts[layer], &G, &RPG, target);
     return G;
@@ -1491,9 +1491,10 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     p.NP = nb.wnp[1]; p.dconv = nb.dconv2; p.in = nb.pool1[0]; p.part = nb.wpart + nb.wpart_off[1];
     M("conv2_wgrad");
     if (nb.conv_impl == 1) {
-      // (3 waves per SIMD -- 168 VGPRs, 720 workgroups -- measured the same 39.0 us)
       WgradDArgs wa = wgradd_args(p, B, nb.wsplits[1]);
       wa.droute = nb.mask2;   // dconv2 pooled (conv3 dgrad)
+      // (3 waves per SIMD, 168 VGPRs: 43.3 us; with 4-row-per-wave balanced
+      // groups, DDQ_WG2_TARGET=640: 41.6 us; against 39.8 us)
       CHECK_LAUNCH((launch_wgradd<32, 64, 5, 2, true>(wa, sw)));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgW2>(p, 1, ns, sw));
