@@ -1245,7 +1245,10 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
       DirectArgs d = direct_fwd_args(p.in, p.wk, p.bias, p.out, p.mask, B, S, 3);
       // (8 waves of one 32-pixel block each measured 39.9 us against 30.7)
       // (register-B, patch-only LDS: 34.8 us)
-      CHECK_LAUNCH((launch_direct<4, 32, 7, 16, 16, 4, 1, false, true>(d, nz, s)));
+      // 16x32 tiles, 8 waves of two 32-pixel blocks: the 25 KB weight image is
+      // staged once per 512 pixels instead of 256 (29.3 us against 30.6 for
+      // 16x16 tiles / 4 waves; 32x16: 29.4; 16x32 / 4 waves of 4 blocks: 39.1)
+      CHECK_LAUNCH((launch_direct<4, 32, 7, 16, 32, 8, 1, false, true>(d, nz, s)));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgConv1F>(p, nz, 1, s));
     }
