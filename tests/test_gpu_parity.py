@@ -324,3 +324,39 @@ def test_rccl_world1_allreduce_and_step(ddq, ref):
         n.step_graph(cfg, 3)
         n.synchronize()
     np.testing.assert_array_equal(nets[0].get_flat(0), nets[1].get_flat(0))
+
+
+@pytest.mark.parametrize("rule", ["rmsprop", "adagrad", "momentum"])
+def test_fused_apply_matches_separate_apply(ddq, ref, rule, monkeypatch):
+    """The fused fc4-weight apply (slab-reduce launch, draw counter advanced by
+    the head kernel) against the separate apply launch (DDQ_VARIANT bit 512):
+    identical parameters, optimizer effect and P<-Q syncs over pipelined and
+    graph chains that cross sync steps."""
+    S, B, N = 16, 16, 300
+    rng = np.random.default_rng(31)
+    theta = ref.flatten(ref.init_params(S, seed=8))
+    st = rng.integers(0, 256, (N, 4, S, S)).astype(np.uint8)
+    acts = rng.integers(0, 4, N).astype(np.uint8)
+    rws = rng.integers(-1, 2, N).astype(np.int16)
+    nts = (rng.random(N) > 0.1).astype(np.uint8)
+    nets = []
+    for var in ("0", "512"):
+        monkeypatch.setenv("DDQ_VARIANT", var)   # read when the ctx is created
+        n = ddq.DeepQNet(batch=B, frame=S)
+        n.set_flat(0, theta)
+        n.set_flat(1, theta)
+        n.replay_create(N)
+        n.replay_import(st, acts, rws, nts, 0, N)
+        nets.append(n)
+    cfg = nets[0].step_cfg(rule, lr=1e-4, target_period=3, seed=9)
+    for n in nets:
+        n.step(cfg)
+        n.step_pipelined(cfg, 9)
+        n.step_graph(cfg, 4)
+        n.synchronize()
+    a, b = nets
+    np.testing.assert_array_equal(a.read_indices(), b.read_indices())
+    np.testing.assert_array_equal(a.get_flat(0), b.get_flat(0))
+    np.testing.assert_array_equal(a.get_flat(1), b.get_flat(1))
+    np.testing.assert_array_equal(a.get_grads_flat(), b.get_grads_flat())
+    assert not np.array_equal(a.get_flat(0), theta)
