@@ -257,10 +257,11 @@ def gather_stress(S=64, N=1_000_000, sizes=(256, 4096, 32768), seed=3):
         # gather alone over 16 pre-drawn index sets in rotation, so the slots
         # read are not still in the 256 MB Infinity Cache from the last call
         sets = []
+        import torch
         for _ in range(16):
-            net.replay_sample_batch(bufs, seed=seed)          # synchronises
-            sets.append(bufs["idx"].clone())
-        net.synchronize()
+            net.replay_sample_batch(bufs, seed=seed)          # synchronises the ctx stream
+            sets.append(bufs["idx"].clone())                  # on torch's current stream
+        torch.cuda.synchronize()                              # clones done before the ctx reads them
         rot = [0]
 
         def gather_next():
@@ -374,24 +375,22 @@ def main():
         else:
             net.step_graph(cfg, k)
 
-    # Robustness of the multi-rank graph: if capturing the exchange on the comm
-    # stream is refused, fall back to the exchange on the main stream, then to
-    # eager steps (same kernels; every rank takes the same deterministic path).
-    try:
-        run(args.warmup)
-    except ddq.DDQError as e:
-        if world == 1 or args.eager:
-            raise
-        print("bench: graph step failed (%s); retrying plain graph steps without overlap" % e,
-              file=sys.stderr)
-        cfg.overlap = 0
-        args.pipeline = False
-        try:
-            run(args.warmup)
-        except ddq.DDQError as e2:
-            print("bench: graph step failed again (%s); eager steps" % e2, file=sys.stderr)
-            args.eager = True
-            run(args.warmup)
+    # Step mode: capture every graph first (nothing launched), then agree on
+    # the first mode every rank prepared (gloo MIN): a rank whose capture of the
+    # comm-stream exchange is refused falls back TOGETHER with the others, so
+    # no rank waits in an RCCL collective the rest abandoned.
+    if args.eager:
+        modes = [("eager", False)]
+    elif args.pipeline:
+        modes = [("pipelined", not args.no_overlap), ("graph", False), ("eager", False)]
+    else:
+        modes = [("graph", not args.no_overlap), ("graph", False), ("eager", False)]
+    mode, ov = ddist.choose_step_mode(net, cfg, modes,
+                                      log=lambda m: print("bench: " + m, file=sys.stderr))
+    args.eager = mode == "eager"
+    args.pipeline = mode == "pipelined"
+    args.no_overlap = not ov
+    run(args.warmup)
     net.synchronize()
     if world > 1:
         dist.barrier()

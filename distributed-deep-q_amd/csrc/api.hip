@@ -49,6 +49,9 @@ struct ddq_ctx {
   float *act_in = nullptr, *act_p1 = nullptr, *act_p2 = nullptr, *act_p3 = nullptr;
   float *act_h4 = nullptr, *act_part = nullptr, *act_q = nullptr;
   int32_t* act_out = nullptr;
+  // index log (ddq_index_log_enable)
+  int32_t* log_buf = nullptr;
+  int64_t log_buf_cap = 0;
   // comm (RCCL ranks, or an in-process group of ctxs exchanging by device copies)
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
@@ -69,8 +72,10 @@ struct ddq_ctx {
   float *mb2_state = nullptr, *mb2_next = nullptr, *mb2_action = nullptr;
   float *mb2_reward = nullptr, *mb2_nonterm = nullptr;
   int32_t* mb2_idx = nullptr;
-  hipGraphExec_t pexec[2][2] = {};
+  hipGraphExec_t pexec[2][2] = {};  // one step on set p, [f] = prefetching
   hipGraphExec_t pexec_k[2] = {};   // kGraphSteps prefetching steps starting on set p
+  hipGraphExec_t ptail[2][9] = {};  // r = 1..kGraphSteps steps from set p, the last one
+                                    // not prefetching (the end of a fused chain)
   ddq_step_cfg pcfg{};
   bool have_pipe = false;
   int64_t steps = 0;
@@ -159,6 +164,11 @@ static void invalidate_graph(ddq_ctx* c) {
     if (g) hipGraphExecDestroy(g);
     g = nullptr;
   }
+  for (auto& row : c->ptail)
+    for (auto& g : row) {
+      if (g) hipGraphExecDestroy(g);
+      g = nullptr;
+    }
   c->have_pipe = false;
 }
 
@@ -198,12 +208,16 @@ int ddq_create(ddq_ctx** out, int device, const ddq_net_desc* desc) {
     for (auto& e : nb.ev) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     const int B = desc->batch, S = desc->frame;
     nb.B = B; nb.S = S; nb.gamma = desc->gamma;
-    {
+    nb.conv_impl = 1;   // direct (patch-in-LDS) conv kernels
+    nb.variant = 0;
+#ifdef DDQ_EXPERIMENTS
+    {   // A/B tuning knobs: experiment builds only (make EXPERIMENTS=1)
       const char* impl = getenv("DDQ_CONV_IMPL");
-      nb.conv_impl = (impl && strcmp(impl, "gemm") == 0) ? 0 : 1;
+      if (impl && strcmp(impl, "gemm") == 0) nb.conv_impl = 0;
       const char* var = getenv("DDQ_VARIANT");
       nb.variant = var ? atoi(var) : 0;
     }
+#endif
     nb.L = make_layout(S);
     const int64_t P = nb.L.total;
     const int S2 = S / 2, S3 = S / 4, S4 = S / 8;
@@ -623,6 +637,55 @@ int ddq_replay_gather_batch_async(ddq_ctx* c, const int32_t* idx, int32_t n, flo
   HIP_TRY(c, launch_gather_nchw(c->r_state, c->r_action, c->r_reward, c->r_nonterm, c->r_meta,
                                 idx, n, c->nb.S, state, next_state, action, reward, nonterm,
                                 c->stream));
+  return DDQ_OK;
+}
+
+int ddq_index_log_enable(ddq_ctx* c, int64_t draws) {
+  if (!c) return fail(nullptr, DDQ_EINVAL, "null ctx");
+  if (draws < 0 || draws > (1ll << 24)) return fail(c, DDQ_EINVAL, "draws must be in [0, 2^24]");
+  TRY(set_dev(c));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (draws == 0) {
+    c->nb.idx_log = nullptr;
+    c->nb.log_cap = 0;
+  } else if (draws > c->log_buf_cap) {
+    TRY(dalloc(c, &c->log_buf, (size_t)draws * c->nb.B));
+    c->log_buf_cap = draws;
+    c->nb.idx_log = c->log_buf;
+    c->nb.log_cap = draws;
+  } else {
+    c->nb.idx_log = c->log_buf;
+    c->nb.log_cap = draws;
+  }
+  invalidate_graph(c);   // captured kernels hold the log pointer
+  return DDQ_OK;
+}
+
+int ddq_replay_draws(ddq_ctx* c, int64_t* draws) {
+  if (!c || !draws) return fail(c, DDQ_EINVAL, "null argument");
+  if (!c->r_state) return fail(c, DDQ_ESTATE, "no replay buffer");
+  TRY(set_dev(c));
+  ReplayMeta m;
+  HIP_TRY(c, hipMemcpyAsync(&m, c->r_meta, sizeof(m), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  *draws = (int64_t)m.counter;
+  return DDQ_OK;
+}
+
+int ddq_index_log_read(ddq_ctx* c, int64_t first, int64_t n, int32_t* out) {
+  if (!c || !out) return fail(c, DDQ_EINVAL, "null argument");
+  if (!c->nb.idx_log) return fail(c, DDQ_ESTATE, "index log not enabled");
+  int64_t drawn = 0;
+  TRY(ddq_replay_draws(c, &drawn));
+  if (first < 0 || n < 0 || first + n > drawn || drawn - first > c->nb.log_cap)
+    return fail(c, DDQ_EINVAL, "draws [%lld, %lld) not in the log (drawn %lld, cap %lld)",
+                (long long)first, (long long)(first + n), (long long)drawn,
+                (long long)c->nb.log_cap);
+  const int B = c->nb.B;
+  for (int64_t d = first; d < first + n; ++d)
+    HIP_TRY(c, hipMemcpyAsync(out + (d - first) * B, c->nb.idx_log + (d % c->nb.log_cap) * B,
+                              (size_t)B * 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
   return DDQ_OK;
 }
 
@@ -1116,6 +1179,9 @@ static int capture_steps(ddq_ctx* c, const ddq_step_cfg* cfg, int k, hipGraphExe
   e = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
   hipGraphDestroy(g);
   if (e != hipSuccess) return fail(c, DDQ_EHIP, "hipGraphInstantiate: %s", hipGetErrorString(e));
+  // upload now: the first launch of a never-uploaded exec pays the upload on
+  // the stream (measured ~0.3 ms in the first timed chunk otherwise)
+  HIP_TRY(c, hipGraphUpload(*out, c->stream));
   return DDQ_OK;
 }
 
@@ -1125,9 +1191,7 @@ static int capture_steps(ddq_ctx* c, const ddq_step_cfg* cfg, int k, hipGraphExe
 // make every captured step read its own iteration / RNG state.
 static constexpr int kGraphSteps = 8;
 
-int ddq_step_graph_async(ddq_ctx* c, const ddq_step_cfg* cfg, int32_t nsteps) {
-  TRY(check_step(c, cfg));
-  TRY(set_dev(c));
+static int ensure_graph(ddq_ctx* c, const ddq_step_cfg* cfg) {
   if (!c->have_graph || memcmp(&c->gcfg, cfg, sizeof(*cfg)) != 0) {
     invalidate_graph(c);
     TRY(capture_steps(c, cfg, 1, &c->gexec));
@@ -1135,6 +1199,13 @@ int ddq_step_graph_async(ddq_ctx* c, const ddq_step_cfg* cfg, int32_t nsteps) {
     c->gcfg = *cfg;
     c->have_graph = true;
   }
+  return DDQ_OK;
+}
+
+int ddq_step_graph_async(ddq_ctx* c, const ddq_step_cfg* cfg, int32_t nsteps) {
+  TRY(check_step(c, cfg));
+  TRY(set_dev(c));
+  TRY(ensure_graph(c, cfg));
   if (c->steps == 0 && nsteps > 0) TRY(initial_target_sync(c, cfg));
   int i = 0;
   for (; i + kGraphSteps <= nsteps; i += kGraphSteps)
@@ -1165,13 +1236,13 @@ static int capture_exec(ddq_ctx* c, hipGraphExec_t* out, const std::function<int
   e = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
   hipGraphDestroy(g);
   if (e != hipSuccess) return fail(c, DDQ_EHIP, "hipGraphInstantiate: %s", hipGetErrorString(e));
+  // upload now: the first launch of a never-uploaded exec pays the upload on
+  // the stream (measured ~0.3 ms in the first timed chunk otherwise)
+  HIP_TRY(c, hipGraphUpload(*out, c->stream));
   return DDQ_OK;
 }
 
-int ddq_step_pipelined_async(ddq_ctx* c, const ddq_step_cfg* cfg, int32_t nsteps) {
-  TRY(check_step(c, cfg));
-  TRY(set_dev(c));
-  if (nsteps <= 0) return DDQ_OK;
+static int ensure_pipe(ddq_ctx* c, const ddq_step_cfg* cfg) {
   if (!c->mb2_state) {
     const int B = c->nb.B, S = c->nb.S;
     TRY(dalloc(c, &c->mb2_state, (size_t)B * S * S * 4));
@@ -1192,7 +1263,7 @@ int ddq_step_pipelined_async(ddq_ctx* c, const ddq_step_cfg* cfg, int32_t nsteps
           return enqueue_train(c, cfg, cur, f ? &nxt : nullptr, nullptr, nullptr, bump);
         }));
       }
-      if (fpf)
+      if (fpf) {
         TRY(capture_exec(c, &c->pexec_k[p], [&]() -> int {
           for (int k = 0; k < kGraphSteps; ++k) {
             const int q = p ^ (k & 1);
@@ -1201,10 +1272,38 @@ int ddq_step_pipelined_async(ddq_ctx* c, const ddq_step_cfg* cfg, int32_t nsteps
           }
           return DDQ_OK;
         }));
+        for (int r = 2; r <= kGraphSteps; ++r)
+          TRY(capture_exec(c, &c->ptail[p][r], [&]() -> int {
+            for (int k = 0; k < r; ++k) {
+              const int q = p ^ (k & 1);
+              const NetBuffers cur = mb_view(c, q), nxt = mb_view(c, 1 - q);
+              TRY(enqueue_train(c, cfg, cur, k + 1 < r ? &nxt : nullptr, nullptr, nullptr, bump));
+            }
+            return DDQ_OK;
+          }));
+      }
     }
     c->pcfg = *cfg;
     c->have_pipe = true;
   }
+  return DDQ_OK;
+}
+
+int ddq_step_prepare(ddq_ctx* c, const ddq_step_cfg* cfg, int32_t mode) {
+  TRY(check_step(c, cfg));
+  TRY(set_dev(c));
+  if (mode == 1) return ensure_graph(c, cfg);
+  if (mode == 2) return ensure_pipe(c, cfg);
+  if (mode != 0) return fail(c, DDQ_EINVAL, "mode must be 0 (eager), 1 (graph) or 2 (pipelined)");
+  return DDQ_OK;
+}
+
+int ddq_step_pipelined_async(ddq_ctx* c, const ddq_step_cfg* cfg, int32_t nsteps) {
+  TRY(check_step(c, cfg));
+  TRY(set_dev(c));
+  if (nsteps <= 0) return DDQ_OK;
+  TRY(ensure_pipe(c, cfg));
+  const bool fpf = fused_prefetch(c, cfg);
   if (c->steps == 0) TRY(initial_target_sync(c, cfg));
   int p = (nsteps - 1) & 1;
   const NetBuffers first = mb_view(c, p);
@@ -1222,6 +1321,15 @@ int ddq_step_pipelined_async(ddq_ctx* c, const ddq_step_cfg* cfg, int32_t nsteps
       c->steps += kGraphSteps;
       c->applied += (int64_t)kGraphSteps * step_inc(c, cfg);
       i += kGraphSteps;
+      continue;
+    }
+    if (fpf && nsteps - i > 1) {   // the chain's last r steps: one graph
+      const int r = nsteps - i;
+      HIP_TRY(c, hipGraphLaunch(c->ptail[p][r], c->stream));
+      c->steps += r;
+      c->applied += (int64_t)r * step_inc(c, cfg);
+      p ^= (r - 1) & 1;   // == 0: every chain ends on set 0
+      i += r;
       continue;
     }
     HIP_TRY(c, hipGraphLaunch(c->pexec[p][i + 1 < nsteps ? 1 : 0], c->stream));

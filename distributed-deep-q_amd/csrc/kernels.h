@@ -23,7 +23,8 @@ ParamLayout make_layout(int S);
 struct ReplayMeta {
   int64_t head, valid, capacity;
   uint64_t counter;        // device index-stream draws so far
-  int32_t err;             // sticky: stored action >= num_actions seen
+  int32_t err;             // sticky: 1 = stored action >= num_actions seen,
+                           //         2 = a draw found no distinct index set
   int32_t pad;
 };
 
@@ -44,6 +45,9 @@ struct NetBuffers {
   uint8_t *mask1, *mask2, *mask3;   // Q tower only
   float* fc4_part;                  // [splits][2][B][512]
   int fc4_splits;
+  // optional device index log: draw d's sorted indices at [(d % log_cap) * B]
+  int32_t* idx_log;
+  int64_t log_cap;
   // blobs
   float *q_out, *p_out, *q_sa, *p_sa, *target, *loss;
   // backward scratch
@@ -103,6 +107,8 @@ struct Prefetch {
   uint64_t seed;
   int B, S, gx, ng;                 // ng = 0: no prefetch blocks
   int32_t* idx;
+  int32_t* idx_log;                 // NetBuffers::idx_log / log_cap of the step
+  int64_t log_cap;
   float *sQ, *sP, *action, *reward, *nonterm;
 };
 Prefetch make_prefetch(const NetBuffers& next, const uint8_t* st, const uint8_t* act,

@@ -69,7 +69,9 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 // round; the process is symmetric in the population, so the final set is
 // uniform.  Deterministic in (seed, ctr): every workgroup that runs it gets
 // the same set, which lets the gather workgroups draw for themselves.
-__device__ void draw_sorted(const ReplayMeta* meta, int B, uint64_t seed, uint64_t ctr,
+constexpr int kDrawRounds = 4096;
+
+__device__ void draw_sorted(ReplayMeta* meta, int B, uint64_t seed, uint64_t ctr,
                             int64_t* cand, int* bad_any) {
   const int t = threadIdx.x;
   const int64_t valid = meta->valid;
@@ -94,7 +96,8 @@ __device__ void draw_sorted(const ReplayMeta* meta, int B, uint64_t seed, uint64
       uint32_t v = (t < B) ? (uint32_t)draw_at(0, t) : 0xFFFFFFFFu;
       const uint32_t fb = (uint32_t)forbid;
       int r = t;
-      for (int round = 1; round < 256; ++round) {
+      bool done = false;
+      for (int round = 1; round <= kDrawRounds; ++round) {
         int less = 0, eqlo = 0;
         for (int k = 0; k < B; ++k) {
           const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)v, k);
@@ -103,9 +106,12 @@ __device__ void draw_sorted(const ReplayMeta* meta, int B, uint64_t seed, uint64
         }
         r = less + eqlo;
         const bool bad = t < B && (v == fb || eqlo > 0);
-        if (__ballot(bad) == 0) break;
-        if (bad) v = (uint32_t)draw_at(round, r);
+        if (__ballot(bad) == 0) { done = true; break; }
+        if (round < kDrawRounds && bad) v = (uint32_t)draw_at(round, r);
       }
+      // no distinct set after kDrawRounds checked rounds (valid barely above
+      // B): flag it (ddq_replay_status) instead of gathering a bad set silently
+      if (!done && t == 0) meta->err = 2;
       if (t < B) cand[r] = (int64_t)v;
     }
     __syncthreads();
@@ -114,7 +120,7 @@ __device__ void draw_sorted(const ReplayMeta* meta, int B, uint64_t seed, uint64
   int P2 = 1;
   while (P2 < B) P2 <<= 1;
   if (t < P2) cand[t] = (t < B) ? draw(0) : INT64_MAX;
-  for (int round = 1; round < 256; ++round) {
+  for (int round = 1; round <= kDrawRounds; ++round) {
     __syncthreads();
     // bitonic sort of cand[0..P2)
     for (int k = 2; k <= P2; k <<= 1) {
@@ -137,19 +143,31 @@ __device__ void draw_sorted(const ReplayMeta* meta, int B, uint64_t seed, uint64
     if (bad) *bad_any = 1;
     __syncthreads();
     if (!*bad_any) break;
+    if (round == kDrawRounds) {   // checked and still bad: flag it (see above)
+      if (t == 0) meta->err = 2;
+      break;
+    }
     if (bad) cand[t] = draw(round);
   }
   __syncthreads();
 }
 
+// Index log (ddq_index_log_enable): draw `ctr`'s sorted set, B entries.
+__device__ __forceinline__ void log_draw(int32_t* log, int64_t cap, uint64_t ctr, int B, int t,
+                                         int32_t v) {
+  if (log && t < B) log[(int64_t)(ctr % (uint64_t)cap) * B + t] = v;
+}
+
 __global__ __launch_bounds__(1024) void sample_kernel(ReplayMeta* meta, int B, uint64_t seed,
-                                                      int32_t* idx_out) {
+                                                      int32_t* idx_out, int32_t* log,
+                                                      int64_t log_cap) {
   __shared__ int64_t cand[1024];
   __shared__ int bad_any;
   const uint64_t ctr = meta->counter;
   draw_sorted(meta, B, seed, ctr, cand, &bad_any);
   const int t = threadIdx.x;
   if (t < B) idx_out[t] = (int32_t)cand[t];
+  log_draw(log, log_cap, ctr, B, t, (int32_t)cand[t < B ? t : 0]);
   if (t == 0) meta->counter = ctr + 1;
 }
 
@@ -209,12 +227,15 @@ __global__ __launch_bounds__(256) void sample_gather_kernel(
     const int16_t* __restrict__ rew, const uint8_t* __restrict__ nt, ReplayMeta* meta, int B,
     uint64_t seed, int32_t* __restrict__ idx_out, int S, float* __restrict__ sQ,
     float* __restrict__ sP, float* __restrict__ action, float* __restrict__ reward,
-    float* __restrict__ nonterm) {
+    float* __restrict__ nonterm, int32_t* log, int64_t log_cap) {
   __shared__ int64_t cand[256];
   __shared__ int bad_any;
-  draw_sorted(meta, B, seed, meta->counter, cand, &bad_any);
-  if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x < B)
+  const uint64_t ctr = meta->counter;
+  draw_sorted(meta, B, seed, ctr, cand, &bad_any);
+  if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x < B) {
     idx_out[threadIdx.x] = (int32_t)cand[threadIdx.x];
+    log_draw(log, log_cap, ctr, B, threadIdx.x, (int32_t)cand[threadIdx.x]);
+  }
   gather_body(st, act, rew, nt, meta, cand[blockIdx.y], S, sQ, sP, action, reward, nonterm,
               blockIdx.x, blockIdx.y, blockIdx.z);
 }
@@ -222,7 +243,8 @@ __global__ __launch_bounds__(256) void sample_gather_kernel(
 hipError_t launch_sample(const NetBuffers& nb, ReplayMeta* meta, uint64_t seed, hipStream_t s) {
   int threads = 64;                 // one wave for B <= 64: cheap barriers
   while (threads < nb.B) threads <<= 1;
-  hipLaunchKernelGGL(sample_kernel, dim3(1), dim3(threads), 0, s, meta, nb.B, seed, nb.idx);
+  hipLaunchKernelGGL(sample_kernel, dim3(1), dim3(threads), 0, s, meta, nb.B, seed, nb.idx,
+                     nb.idx_log, nb.log_cap);
   return hipGetLastError();
 }
 
@@ -233,7 +255,7 @@ hipError_t launch_sample_gather(const NetBuffers& nb, const uint8_t* st, const u
   dim3 grid((SS / 4 + 255) / 256, nb.B, 2);
   hipLaunchKernelGGL(sample_gather_kernel, grid, dim3(256), 0, s, st, act, rew, nt, meta, nb.B,
                      seed, nb.idx, nb.S, nb.state, nb.next_state, nb.action, nb.reward,
-                     nb.nonterm);
+                     nb.nonterm, nb.idx_log, nb.log_cap);
   return hipGetLastError();
 }
 
@@ -866,8 +888,12 @@ __device__ __forceinline__ void prefetch_body(const Prefetch& pf, int g) {
   __shared__ int64_t cand[256];
   __shared__ int bad_any;
   const int bx = g % pf.gx, b = (g / pf.gx) % pf.B, z = g / (pf.gx * pf.B);
-  draw_sorted(pf.meta, pf.B, pf.seed, pf.meta->counter, cand, &bad_any);
-  if (g == 0 && threadIdx.x < pf.B) pf.idx[threadIdx.x] = (int32_t)cand[threadIdx.x];
+  const uint64_t ctr = pf.meta->counter;
+  draw_sorted(pf.meta, pf.B, pf.seed, ctr, cand, &bad_any);
+  if (g == 0 && threadIdx.x < pf.B) {
+    pf.idx[threadIdx.x] = (int32_t)cand[threadIdx.x];
+    log_draw(pf.idx_log, pf.log_cap, ctr, pf.B, threadIdx.x, (int32_t)cand[threadIdx.x]);
+  }
   gather_body(pf.st, pf.act, pf.rew, pf.nt, pf.meta, cand[b], pf.S, pf.sQ, pf.sP, pf.action,
               pf.reward, pf.nonterm, bx, b, z);
 }
@@ -1099,6 +1125,7 @@ Prefetch make_prefetch(const NetBuffers& next, const uint8_t* st, const uint8_t*
   pf.gx = (next.S * next.S / 4 + 255) / 256;
   pf.ng = pf.gx * next.B * 2;
   pf.idx = next.idx; pf.sQ = next.state; pf.sP = next.next_state;
+  pf.idx_log = next.idx_log; pf.log_cap = next.log_cap;
   pf.action = next.action; pf.reward = next.reward; pf.nonterm = next.nonterm;
   return pf;
 }
@@ -1165,8 +1192,10 @@ int wgrad_splits_for(int layer, int B, int S, int* np, int impl) {
     int G, RPG;
     int target = 512;
     // tuning sweeps; conv3 measured 128: 25.0 us, 256: 16.0, 512: 15.2, 1024: 18.8
+#ifdef DDQ_EXPERIMENTS
     const char* e = getenv(layer == 2 ? "DDQ_WG3_TARGET" : "DDQ_WG2_TARGET");
     if (e && atoi(e) > 0) target = atoi(e);
+#endif
     wgradd_groups(B * H, nts[layer], &G, &RPG, target);
     return G;
   }

@@ -48,7 +48,7 @@ class StepCfg(ctypes.Structure):
                 ("overlap", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 EXCHANGES = {"none": 0, "allreduce": 1, "sharded": 2, "server": 3}
 
 
@@ -87,6 +87,9 @@ _SIGS = {
     "ddq_replay_sample_batch_async": (ctypes.c_int, [_P, _i32, _u64, _P, _P, _P, _P, _P, _P]),
     "ddq_replay_gather_batch_async": (ctypes.c_int, [_P, _P, _i32, _P, _P, _P, _P, _P]),
     "ddq_replay_status": (ctypes.c_int, [_P]),
+    "ddq_replay_draws": (ctypes.c_int, [_P, ctypes.POINTER(_i64)]),
+    "ddq_index_log_enable": (ctypes.c_int, [_P, _i64]),
+    "ddq_index_log_read": (ctypes.c_int, [_P, _i64, _i64, _P]),
     "ddq_forward_backward": (ctypes.c_int, [_P, _fp]),
     "ddq_forward_backward_async": (ctypes.c_int, [_P]),
     "ddq_forward_q": (ctypes.c_int, [_P]),
@@ -104,6 +107,7 @@ _SIGS = {
     "ddq_step_async": (ctypes.c_int, [_P, ctypes.POINTER(StepCfg)]),
     "ddq_step_graph_async": (ctypes.c_int, [_P, ctypes.POINTER(StepCfg), _i32]),
     "ddq_step_pipelined_async": (ctypes.c_int, [_P, ctypes.POINTER(StepCfg), _i32]),
+    "ddq_step_prepare": (ctypes.c_int, [_P, ctypes.POINTER(StepCfg), _i32]),
     "ddq_step_count": (_i64, [_P]),
     "ddq_group_init": (ctypes.c_int, [ctypes.POINTER(_P), _i32]),
     "ddq_group_step": (ctypes.c_int, [ctypes.POINTER(_P), _i32, ctypes.POINTER(StepCfg)]),

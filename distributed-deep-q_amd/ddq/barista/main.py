@@ -5,7 +5,7 @@ acting through the GPU Q tower), sample a minibatch from the HBM replay, run
 the forward/backward pass on the GPU, push the Q gradients, reply.
 
     python -m ddq.barista.main <train_val.prototxt> <model.npz|none>
-        [--port 50001] [--driver 127.0.0.1:5500|None] [--dataset replay.npz]
+        [--port 50001] [--driver 127.0.0.1:5500|None] [--dataset replay-dataset.hdf5]
         [--dset-size 1000] [--overwrite] [--debug] [--initial-replay 20000]
 
 ``--mode`` accepts only ``gpu``: there is no CPU compute path.
@@ -72,7 +72,7 @@ def get_args(argv=None):
     ap.add_argument("--mode", default="gpu", choices=["gpu"])
     ap.add_argument("--port", type=int, default=50001)
     ap.add_argument("--driver", default="127.0.0.1:5500")
-    ap.add_argument("--dataset", default="replay-dataset.npz")
+    ap.add_argument("--dataset", default="replay-dataset.hdf5")   # main.py:131
     ap.add_argument("--dset-size", dest="dset_size", type=int, default=1000)
     ap.add_argument("--overwrite", action="store_true")
     ap.add_argument("--debug", action="store_true")

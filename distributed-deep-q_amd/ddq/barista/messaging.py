@@ -79,6 +79,32 @@ def create_model_message(net, compress=False):
     return create_net_message(_net_params(net, "data"), "data", compress)
 
 
+class _HeaderUnpickler(pickle.Unpickler):
+    """Headers arrive from the network: resolve no global except OrderedDict
+    (lists, tuples, strings and ints need none).  A reference header (Python 2
+    cPickle protocol 2) decodes unchanged; anything else -- a pickle that would
+    call a function or build another class -- is refused instead of run."""
+
+    def find_class(self, module, name):
+        if (module, name) in (("collections", "OrderedDict"), ("builtins", "list"),
+                              ("builtins", "tuple")):
+            return super().find_class(module, name)
+        raise pickle.UnpicklingError("message header refers to %s.%s: refused" % (module, name))
+
+
+def _load_header(raw):
+    import io
+    header = _HeaderUnpickler(io.BytesIO(raw), encoding="latin1").load()
+    if not isinstance(header, dict):
+        raise ValueError("message header is not a mapping")
+    for name, shapes in header.items():
+        if not isinstance(name, str) or not isinstance(shapes, (list, tuple)) or not all(
+                isinstance(sh, (list, tuple)) and all(isinstance(d, int) and d >= 0 for d in sh)
+                for sh in shapes):
+            raise ValueError("malformed message header entry %r" % (name,))
+    return header
+
+
 def _parse(message, with_iteration, compressed):
     if with_iteration:
         iteration_num, hlen = struct.unpack("ii", message[:8])
@@ -86,7 +112,7 @@ def _parse(message, with_iteration, compressed):
     else:
         iteration_num, (hlen,) = None, struct.unpack("i", message[:4])
         off = 4
-    header = pickle.loads(message[off:off + hlen])
+    header = _load_header(message[off:off + hlen])
     data = message[off + hlen:]
     if compressed:
         data = zlib.decompress(data)

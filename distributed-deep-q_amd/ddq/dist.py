@@ -63,3 +63,36 @@ def max_over_ranks(value):
     t = torch.tensor([float(value)], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def all_ranks_ok(ok):
+    """True only if ``ok`` holds on every rank (gloo MIN all-reduce): a
+    fallback decision every rank takes together, so no rank proceeds into a
+    collective the others have abandoned."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return bool(ok)
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+def choose_step_mode(net, cfg, modes, log=None):
+    """Prepare (capture + instantiate, nothing launched) the first step mode
+    of ``modes`` -- (name, overlap) pairs, name in "pipelined" / "graph" /
+    "eager" -- that succeeds on EVERY rank; the decision is collective.
+    Returns the chosen (name, overlap)."""
+    from ._lib import DDQError
+    for name, overlap in modes:
+        cfg.overlap = int(bool(overlap))
+        ok = True
+        try:
+            net.step_prepare(cfg, name)
+        except DDQError as e:
+            ok = False
+            if log:
+                log("step mode %s%s failed to prepare: %s" % (name, "+overlap" if overlap else "", e))
+        if all_ranks_ok(ok):
+            return name, overlap
+    raise RuntimeError("no step mode could be prepared on every rank")

@@ -308,6 +308,22 @@ class DeepQNet:
         if check:
             self._check(self.lib.ddq_replay_status(self.ctx))
 
+    def replay_draws(self):
+        """Device index draws made so far (device RNG stream position)."""
+        d = _lib._i64()
+        self._check(self.lib.ddq_replay_draws(self.ctx, ctypes.byref(d)))
+        return int(d.value)
+
+    def index_log_enable(self, draws):
+        """Log every device-drawn index set in a ring of ``draws`` entries."""
+        self._check(self.lib.ddq_index_log_enable(self.ctx, int(draws)))
+
+    def index_log(self, first, n):
+        """(n, B) sorted index sets of device draws first .. first+n-1."""
+        out = np.empty((int(n), self.batch), np.int32)
+        self._check(self.lib.ddq_index_log_read(self.ctx, int(first), int(n), ptr(out)))
+        return out
+
     def read_indices(self):
         out = np.empty(self.batch, np.int32)
         self._check(self.lib.ddq_read_indices(self.ctx, ptr(out), self.batch))
@@ -329,6 +345,12 @@ class DeepQNet:
 
     def step_graph(self, cfg, nsteps):
         self._check(self.lib.ddq_step_graph_async(self.ctx, ctypes.byref(cfg), int(nsteps)))
+
+    def step_prepare(self, cfg, mode="pipelined"):
+        """Capture and instantiate the graphs of a step mode ("eager", "graph",
+        "pipelined") without launching anything."""
+        m = {"eager": 0, "graph": 1, "pipelined": 2}[mode]
+        self._check(self.lib.ddq_step_prepare(self.ctx, ctypes.byref(cfg), m))
 
     def step_pipelined(self, cfg, nsteps):
         """nsteps graph steps with step t+1's sample + gather overlapped with step t."""

@@ -24,6 +24,8 @@ The apply runs in ``apply_kernel`` on the device (``ddq_set_grads`` +
 """
 from __future__ import annotations
 
+import pickle
+import struct
 import threading
 
 import numpy as np
@@ -96,25 +98,23 @@ class ParamServer:
     def update_params(self, message):
         """POST /api/v1/update_model (server.py:196-209) -> b"Updated"."""
         grads = messaging.load_gradient_message(message)
+        missing = [k for k in self.net.q_names if k not in grads]
+        if missing:
+            # server.py:86-124 would touch only the received keys; workers
+            # always send every Q blob (messaging.py:43-79), and the device
+            # apply updates the whole tower -- a partial message is refused
+            # rather than zero-filled (which would still decay the rmsprop
+            # cache / consume adagrad's first call of the missing blobs)
+            raise ValueError("gradient message lacks %s" % ", ".join(missing))
         with self.model_lock:
             self.iteration += 1
-            flat = self.net.join({k: v for k, v in grads.items()}, "Q") \
-                if all(k in grads for k in self.net.q_names) else self._partial(grads)
+            flat = self.net.join({k: v for k, v in grads.items()}, "Q")
             self.net.set_grads_flat(flat)
             self.net.apply(self.update, lr=self.learning_rate, decay=self.rmsprop_decay)
             if self.snapshot_frequency and self.iteration % self.snapshot_frequency == 0 \
                     and self.on_snapshot is not None:
                 self.on_snapshot(get_snapshot_name(self.iteration), self.model_params())
         return b"Updated"
-
-    def _partial(self, grads):
-        # a gradient message carrying a subset of the Q blobs: others get 0
-        flat = np.zeros(self.net.num_params, np.float32)
-        cur = self.net.split(flat, "Q")
-        for k, v in grads.items():
-            for dst, src in zip(cur[k], v):
-                dst.flat[:] = src
-        return self.net.join(cur, "Q")
 
     # ---------------------------------------------------------------- HTTP
     def serve(self, port=5500, host="127.0.0.1"):
@@ -145,7 +145,11 @@ class ParamServer:
                 if self.path != "/api/v1/update_model":
                     return self._reply(b"not found", 404)
                 n = int(self.headers.get("Content-Length", "0"))
-                self._reply(ps.update_params(self.rfile.read(n)))
+                try:
+                    body = ps.update_params(self.rfile.read(n))
+                except (ValueError, KeyError, struct.error, pickle.UnpicklingError) as e:
+                    return self._reply(("bad gradient message: %s" % e).encode(), 400)
+                self._reply(body)
 
             def log_message(self, *args):
                 pass

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define DDQ_ABI_VERSION 2
+#define DDQ_ABI_VERSION 3
 
 enum ddq_status {
   DDQ_OK = 0,
@@ -202,6 +202,19 @@ int ddq_replay_gather_batch_async(ddq_ctx* ctx, const int32_t* idx, int32_t n, f
 int ddq_replay_status(ddq_ctx* ctx);
 /* Last sorted index list used by the gather (device -> host). */
 int ddq_read_indices(ddq_ctx* ctx, int32_t* idx, int32_t batch);
+/* Device index draws made so far (the device RNG stream position; reset by
+ * ddq_replay_create).  Draw d is the minibatch of the (d+1)-th device-drawn
+ * step of this ctx. */
+int ddq_replay_draws(ddq_ctx* ctx, int64_t* draws);
+/* Debug / parity log of the device draws: every device-drawn sorted index
+ * set d (sample kernels, fused step draws, pipelined prefetches) is also
+ * written to a device ring of `draws` entries of B int32 (0 disables).  Lets a
+ * checker replay exactly the minibatches a graph-captured chain trained on
+ * (the role of replay.py:152-159's host index list).  Invalidates graphs. */
+int ddq_index_log_enable(ddq_ctx* ctx, int64_t draws);
+/* Copy draws [first, first+n) (each B sorted int32) out of the log; they must
+ * be among the last `draws` made. */
+int ddq_index_log_read(ddq_ctx* ctx, int64_t first, int64_t n, int32_t* out);
 
 /* ---------------- compute ---------------------------------------------- */
 /* net.forward(); net.backward() (baristanet.py:138-140).  loss may be NULL. */
@@ -246,6 +259,11 @@ int ddq_step_graph_async(ddq_ctx* ctx, const ddq_step_cfg* cfg, int32_t nsteps);
  * overlapped with step t (double-buffered minibatch).  Same results, indices
  * and counters as nsteps sequential ddq_step_async calls.  Enqueued, no sync. */
 int ddq_step_pipelined_async(ddq_ctx* ctx, const ddq_step_cfg* cfg, int32_t nsteps);
+/* Capture + instantiate (and upload) the graphs of a step mode without
+ * launching anything: mode 0 = eager (no-op), 1 = ddq_step_graph_async,
+ * 2 = ddq_step_pipelined_async.  Lets multi-rank callers agree on a mode
+ * (every rank prepared it) before any rank enters a collective. */
+int ddq_step_prepare(ddq_ctx* ctx, const ddq_step_cfg* cfg, int32_t mode);
 /* In-process data parallelism: W ctxs (W workers sharing a GPU, or peer-
  * enabled devices) exchange through device copies instead of RCCL, with the
  * same exchanges, shard layout and kernels as ddq_comm_init ranks.  The

@@ -303,6 +303,105 @@ def full_pass(pQ, pP, state, action, reward, next_state, non_terminal, routes=No
     return blobs, grads
 
 
+def magnitudes(pQ, pP, state, action, reward, next_state, non_terminal, routes=None):
+    """Per-element magnitude M of every blob and gradient of ``full_pass``:
+    the same computation with every operand replaced by its absolute value
+    (|W|, |x|, |b|, |dQ| ...) along the same ReLU / max-pool routing.  M is the
+    sum of |terms| an output element accumulates -- its condition: fp32
+    rounding of the terms (and relative errors of the inputs) perturb the
+    element by a small multiple of eps32 * M however much the terms cancel.
+    The parity tests bound each element by rtol * |ref| + c * M (tests/_parity.py),
+    an elementwise tolerance with no tensor-wide floor.  Returns
+    (blob_mags, grad_mags) keyed like full_pass's outputs."""
+    f64 = lambda a: np.abs(np.asarray(a, np.float64))
+    B = np.asarray(state).shape[0]
+    act = f64(action).reshape(B, NUM_ACTIONS)
+    r = f64(reward).reshape(B)
+    nt = f64(non_terminal).reshape(B)
+    pQa = {k: [f64(w) for w in v] for k, v in pQ.items()}
+    pPa = {k: [f64(w) for w in v] for k, v in pP.items()}
+    # signed forward for the routing / ReLU decisions
+    cq = net_forward(np.asarray(state, np.float64),
+                     {k: [np.asarray(w, np.float64) for w in v] for k, v in pQ.items()}, "Q")
+    cp = net_forward(np.asarray(next_state, np.float64),
+                     {k: [np.asarray(w, np.float64) for w in v] for k, v in pP.items()}, "P")
+
+    def fwd_mag(x, pa, cache, prefix, rts):
+        names = layer_names(prefix)
+        h = f64(x)
+        ins = []
+        for i, ((_, _, k, pad), lname) in enumerate(zip(CONVS, names[:3])):
+            W, b = pa[lname]
+            ins.append(h)
+            m = conv_forward(h, W, b.reshape(-1), pad)
+            a_s = cache["act%d" % (i + 1)]
+            m = np.where(a_s > 0, m, 0.0)
+            if rts is not None and prefix == "Q":
+                code = np.asarray(rts[i + 1])
+                keep = code < 4
+                win = m.reshape(B, m.shape[1], m.shape[2] // 2, 2, m.shape[3] // 2, 2).transpose(
+                    0, 1, 2, 4, 3, 5).reshape(B, m.shape[1], m.shape[2] // 2, m.shape[3] // 2, 4)
+                h = np.take_along_axis(win, np.where(keep, code, 0)[..., None], -1)[..., 0] * keep
+            else:
+                arg = cache["arg%d" % (i + 1)]
+                win = m.reshape(B, m.shape[1], m.shape[2] // 2, 2, m.shape[3] // 2, 2).transpose(
+                    0, 1, 2, 4, 3, 5).reshape(B, m.shape[1], m.shape[2] // 2, m.shape[3] // 2, 4)
+                h = np.take_along_axis(win, arg[..., None], -1)[..., 0]
+        flat = h.reshape(B, -1)
+        W4, b4 = pa[names[3]]
+        mh4 = (flat @ W4.reshape(FC4, -1).T + b4.reshape(-1)) * (cache["h4"] > 0)
+        W5, b5 = pa[names[4]]
+        mout = mh4 @ W5.reshape(NUM_ACTIONS, -1).T + b5.reshape(-1)
+        return ins, flat, mh4, mout
+
+    insq, mflat, mh4, mQ = fwd_mag(state, pQa, cq, "Q", routes)
+    _, _, _, mP = fwd_mag(next_state, pPa, cp, "P", None)
+    Q, P = cq["out"], cp["out"]
+    m_qsa = (mQ * act).sum(axis=1)
+    m_psa = mP[np.arange(B), P.argmax(axis=1)] * nt
+    m_target = GAMMA * m_psa + r
+    m_diff = m_qsa + m_target
+    diff = np.abs((Q * np.asarray(action, np.float64).reshape(B, -1)).sum(1)
+                  - (GAMMA * P.max(1) * np.asarray(non_terminal, np.float64).reshape(B)
+                     + np.asarray(reward, np.float64).reshape(B)))
+    m_loss = float((diff * m_diff).sum() / B)
+    blobs = dict(Q_out=mQ, P_out=mP, Q_sa=m_qsa, P_sa=m_psa, target_Q_sa=m_target, loss=m_loss)
+    # backward on magnitudes
+    names = layer_names("Q")
+    mdQ = act * (m_diff / B)[:, None]
+    W5 = pQa[names[4]][0].reshape(NUM_ACTIONS, -1)
+    g = collections.OrderedDict()
+    gW5 = mdQ.T @ mh4                    # products of magnitudes bound both error terms
+    gb5 = mdQ.sum(0)
+    mdh4 = (mdQ @ W5) * (cq["h4"] > 0)
+    W4 = pQa[names[3]][0].reshape(FC4, -1)
+    gW4 = mdh4.T @ mflat
+    gb4 = mdh4.sum(0)
+    dpool = (mdh4 @ W4).reshape(cq["pool3"].shape)
+    conv_g = []
+    for i in (3, 2, 1):
+        act_i = cq["act%d" % i]
+        if routes is None:
+            dpre = maxpool_backward(dpool, cq["arg%d" % i], act_i.shape[2], act_i.shape[3])
+            dpre = dpre * (act_i > 0)
+        else:
+            code = np.asarray(routes[i])
+            keep = code < 4
+            dpre = maxpool_backward(dpool * keep, np.where(keep, code, 0), act_i.shape[2],
+                                    act_i.shape[3])
+        W = pQa[names[i - 1]][0]
+        gW, gb, dx = conv_backward(insq[i - 1], W, dpre, CONVS[i - 1][3], need_bottom=(i > 1))
+        conv_g.append((gW, gb))
+        dpool = dx
+    conv_g.reverse()
+    shapes = param_shapes(np.asarray(state).shape[2], "Q")
+    for (gW, gb), lname in zip(conv_g, names[:3]):
+        g[lname] = [gW.reshape(shapes[lname][0]), gb.reshape(shapes[lname][1])]
+    g[names[3]] = [gW4.reshape(shapes[names[3]][0]), gb4.reshape(shapes[names[3]][1])]
+    g[names[4]] = [gW5.reshape(shapes[names[4]][0]), gb5.reshape(shapes[names[4]][1])]
+    return blobs, g
+
+
 def select_action(state_f32, pQ):
     """BaristaNet.select_action (baristanet.py:142-146): argmax of Q_out (first max)."""
     return np.argmax(net_forward(np.asarray(state_f32, np.float64),

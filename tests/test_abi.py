@@ -56,7 +56,7 @@ def test_struct_layouts_match_header():
 
 
 def test_abi_version(lib):
-    assert lib.ddq_abi_version() == 2
+    assert lib.ddq_abi_version() == 3
 
 
 def test_no_gpu_fails_loudly(lib):

@@ -166,3 +166,46 @@ def test_gloo_server_and_sharded_exchange_semantics(world):
         np.testing.assert_allclose(sh, want_sh, rtol=0, atol=1e-6)
     # the two semantics differ (rmsprop: W lagged applies != one summed apply)
     assert np.abs(res[0][1] - res[0][2]).max() > 1e-5
+
+
+def _mode_worker(rank, world, port, fail, out):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "distributed-deep-q_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    from ddq import dist as ddist
+    from ddq._lib import DDQError
+    ddist.init_process_group(rank, world, "gloo")
+
+    class Cfg:
+        overlap = 0
+
+    class FakeNet:   # step_prepare refuses the modes listed for this rank
+        def step_prepare(self, cfg, mode):
+            if (mode, bool(cfg.overlap)) in fail.get(rank, ()):
+                raise DDQError(-3, "capture refused on rank %d" % rank)
+
+    modes = [("pipelined", True), ("graph", False), ("eager", False)]
+    out.put((rank, ddist.choose_step_mode(FakeNet(), Cfg(), modes)))
+    import torch.distributed as dist
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail,want", [({}, ("pipelined", True)),
+                                       ({1: {("pipelined", True)}}, ("graph", False)),
+                                       ({0: {("pipelined", True)}, 2: {("graph", False)}},
+                                        ("eager", False))])
+def test_step_mode_fallback_is_collective(fail, want):
+    """bench.py's graph-capture fallback: one rank failing to prepare a mode
+    moves EVERY rank to the next mode (no rank left waiting in a collective)."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_mode_worker, args=(r, world, port, fail, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    assert all(res[r] == want for r in range(world)), res

@@ -174,6 +174,28 @@ def test_worker_param_server_round_trip(param_server):
     np.testing.assert_array_equal(net.dqn.get_flat(1), theta0)
 
 
+def test_partial_gradient_message_is_refused(param_server):
+    """A gradient message lacking Q blobs is refused (the device apply would
+    otherwise decay the rmsprop cache of the missing blobs); the server state
+    is untouched and the HTTP route answers 400."""
+    import urllib.request
+    from ddq.barista import messaging
+    ps, driver = param_server
+    theta0 = ps.net.get_flat(0)
+    p = ref.init_params(16, seed=4)
+    del p["Qconv2"]
+    msg = messaging.create_net_message(p, "diff")
+    with pytest.raises(ValueError, match="Qconv2"):
+        ps.update_params(msg)
+    req = urllib.request.Request("http://%s/api/v1/update_model" % driver, data=msg,
+                                 headers={"Content-Type": "application/deepQ"})
+    with pytest.raises(urllib.error.HTTPError) as ei:
+        urllib.request.urlopen(req, timeout=10)
+    assert ei.value.code == 400
+    assert ps.iteration == 0
+    np.testing.assert_array_equal(ps.net.get_flat(0), theta0)
+
+
 def test_barista_tcp_loop_with_dummy_client(param_server, tmp_path, monkeypatch):
     """Config 1 plumbing: dummy client -> Barista TCP 'G' -> param server."""
     from ddq.barista import main as bmain

@@ -52,6 +52,55 @@ def test_header_is_python2_readable_protocol():
     assert msg[8:10] == b"\x80\x02"          # pickle protocol 2 (cPickle -1 in Py2)
 
 
+class _Evil:
+    def __reduce__(self):
+        return (os.system, ("echo pwned > /dev/null",))
+
+
+@pytest.mark.parametrize("kind", ["model", "gradient"])
+def test_malicious_header_is_refused(kind, monkeypatch):
+    """Headers come off the network: a pickle naming any global but
+    OrderedDict is refused before anything runs (messaging.py:89)."""
+    from ddq.barista import messaging
+    header = pickle.dumps(collections_od([("Qconv1", _Evil())]), 2)   # names os.system
+    called = []
+    monkeypatch.setattr(os, "system", lambda *a: called.append(a))
+    data = np.zeros(4, np.float32).tobytes()
+    if kind == "model":
+        msg = struct.pack("ii", 0, len(header)) + header + data
+        with pytest.raises(pickle.UnpicklingError):
+            messaging.load_model_params(msg)
+    else:
+        msg = struct.pack("i", len(header)) + header + data
+        with pytest.raises(pickle.UnpicklingError):
+            messaging.load_gradient_message(msg)
+    assert not called
+    # a malformed (but harmless) header is rejected too
+    bad = pickle.dumps({"Qconv1": "not shapes"}, 2)
+    with pytest.raises(ValueError):
+        messaging.load_gradient_message(struct.pack("i", len(bad)) + bad + data)
+
+
+def test_python2_style_header_still_loads():
+    """A header as Python 2 cPickle.dumps(OrderedDict, -1) writes it (str names
+    as SHORT_BINSTRING, tuples of ints) decodes with the restricted loader."""
+    from ddq.barista import messaging
+    # protocol-2 pickle of OrderedDict([('Qconv1', [(2, 2), (1, 1, 1, 2)])]) with
+    # Python 2 byte strings ('U' opcodes), as cPickle writes it
+    raw = (b"\x80\x02ccollections\nOrderedDict\nq\x00)Rq\x01U\x06Qconv1q\x02]q\x03"
+           b"(K\x02K\x02\x86q\x04(K\x01K\x01K\x01K\x02tq\x05es.")
+    data = np.arange(6, dtype=np.float32).tobytes()
+    g = messaging.load_gradient_message(struct.pack("i", len(raw)) + raw + data)
+    assert list(g) == ["Qconv1"]
+    np.testing.assert_array_equal(g["Qconv1"][0], [[0, 1], [2, 3]])
+    np.testing.assert_array_equal(g["Qconv1"][1].ravel(), [4, 5])
+
+
+def collections_od(items):
+    import collections
+    return collections.OrderedDict(items)
+
+
 def test_parse_architecture():
     from ddq.barista.baristanet import parse_architecture
     assert parse_architecture(os.path.join(GOLD, "deepq16.prototxt")) == (32, 16, 0.85)

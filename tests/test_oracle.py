@@ -216,3 +216,30 @@ def test_rmsprop_uses_lagged_cache():
     th2, c2 = ref.rmsprop_update(th1, g2, c1, 0.1)
     np.testing.assert_allclose(th2, th1 - 0.1 * g2 / np.sqrt(c1 + 1e-8), rtol=1e-6)
     np.testing.assert_allclose(c2, 0.9 * c1 + 0.1 * g2 ** 2, rtol=1e-6)
+
+
+def test_magnitudes_bound_every_output():
+    """oracle.magnitudes (the per-element sum of |terms| the parity tolerance
+    scales with) bounds |value| of every blob and gradient element, and is
+    routing-consistent (same result when the oracle's own routing is passed)."""
+    S, B = 16, 4
+    rng = np.random.default_rng(12)
+    pQ, pP = ref.init_params(S, seed=1), ref.init_params(S, seed=2, prefix="P")
+    st = rng.integers(0, 256, (B, 4, S, S)).astype(np.float32)
+    ns = rng.integers(0, 256, (B, 4, S, S)).astype(np.float32)
+    act = np.zeros((B, 4, 1, 1), np.float32)
+    act[np.arange(B), rng.integers(0, 4, B)] = 1
+    rw = rng.integers(-1, 2, (B, 1, 1, 1)).astype(np.float32)
+    nt = np.ones((B, 1, 1, 1), np.float32)
+    blobs, grads, cache = ref.full_pass(pQ, pP, st, act, rw, ns, nt, return_cache=True)
+    mb, mg = ref.magnitudes(pQ, pP, st, act, rw, ns, nt)
+    for k in blobs:
+        assert np.all(np.abs(blobs[k]) <= np.asarray(mb[k]) * (1 + 1e-12) + 1e-300), k
+    for k in grads:
+        for i in range(2):
+            assert np.all(np.abs(grads[k][i]) <= mg[k][i] * (1 + 1e-12) + 1e-300), (k, i)
+    routes = {i: ref.route_codes(cache["act%d" % i], cache["arg%d" % i]) for i in (1, 2, 3)}
+    mb2, mg2 = ref.magnitudes(pQ, pP, st, act, rw, ns, nt, routes=routes)
+    for k in grads:
+        for i in range(2):
+            np.testing.assert_allclose(mg2[k][i], mg[k][i], rtol=1e-12)
