@@ -48,6 +48,7 @@ struct ddq_ctx {
   uint8_t* act_u8 = nullptr;
   float *act_in = nullptr, *act_p1 = nullptr, *act_p2 = nullptr, *act_p3 = nullptr;
   float *act_h4 = nullptr, *act_part = nullptr, *act_q = nullptr;
+  __bf16 *act_p1s = nullptr, *act_p2s = nullptr;
   int32_t* act_out = nullptr;
   // index log (ddq_index_log_enable)
   int32_t* log_buf = nullptr;
@@ -234,6 +235,9 @@ int ddq_create(ddq_ctx** out, int device, const ddq_net_desc* desc) {
       TRY(dalloc(c, &nb.h4[z], (size_t)B * 512));
       TRY(dalloc(c, &nb.theta[z], (size_t)P + kShardPad));
       TRY(dalloc(c, &nb.wk[z], (size_t)nb.L.wk_total));
+      TRY(dalloc(c, &nb.wks[z], (size_t)3 * nb.L.wks_total));   // zero: conv1's kx 7 stays 0
+      TRY(dalloc(c, &nb.pool1s[z], (size_t)3 * B * S2 * S2 * 32));
+      TRY(dalloc(c, &nb.pool2s[z], (size_t)3 * B * S3 * S3 * 64));
     }
     TRY(dalloc(c, &nb.mask1, (size_t)B * S2 * S2 * 32));
     TRY(dalloc(c, &nb.mask2, (size_t)B * S3 * S3 * 64));
@@ -272,6 +276,8 @@ int ddq_create(ddq_ctx** out, int device, const ddq_net_desc* desc) {
     TRY(dalloc(c, &c->act_in, (size_t)B * S * S * 4));
     TRY(dalloc(c, &c->act_p1, (size_t)B * S2 * S2 * 32));
     TRY(dalloc(c, &c->act_p2, (size_t)B * S3 * S3 * 64));
+    TRY(dalloc(c, &c->act_p1s, (size_t)3 * B * S2 * S2 * 32));
+    TRY(dalloc(c, &c->act_p2s, (size_t)3 * B * S3 * S3 * 64));
     TRY(dalloc(c, &c->act_p3, (size_t)B * S4 * S4 * 64));
     TRY(dalloc(c, &c->act_h4, (size_t)B * 512));
     TRY(dalloc(c, &c->act_part, (size_t)nb.fc4_splits * 2 * B * 512));
@@ -422,6 +428,8 @@ int ddq_sync_target(ddq_ctx* c) {
   HIP_TRY(c, hipMemcpyAsync(c->nb.theta[1], c->nb.theta[0], c->nb.L.total * 4,
                             hipMemcpyDeviceToDevice, c->stream));
   HIP_TRY(c, hipMemcpyAsync(c->nb.wk[1], c->nb.wk[0], c->nb.L.wk_total * 4,
+                            hipMemcpyDeviceToDevice, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(c->nb.wks[1], c->nb.wks[0], c->nb.L.wks_total * 3 * 2,
                             hipMemcpyDeviceToDevice, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return DDQ_OK;
@@ -787,7 +795,7 @@ int ddq_forward_q(ddq_ctx* c) {
   if (!c) return fail(nullptr, DDQ_EINVAL, "null ctx");
   TRY(set_dev(c));
   HIP_TRY(c, launch_act(c->nb, c->nb.state, c->nb.B, c->act_p1, c->act_p2, c->act_p3, c->act_h4,
-                        c->act_part, c->nb.q_out, nullptr, c->stream));
+                        c->act_part, c->nb.q_out, nullptr, c->act_p1s, c->act_p2s, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return DDQ_OK;
 }
@@ -839,7 +847,7 @@ int ddq_select_action(ddq_ctx* c, const uint8_t* states, int32_t n, int32_t* act
   HIP_TRY(c, hipMemcpyAsync(c->act_u8, states, bytes, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(c, launch_u8_to_nhwc(c->act_u8, n, c->nb.S, c->act_in, c->stream));
   HIP_TRY(c, launch_act(c->nb, c->act_in, n, c->act_p1, c->act_p2, c->act_p3, c->act_h4,
-                        c->act_part, c->act_q, c->act_out, c->stream));
+                        c->act_part, c->act_q, c->act_out, c->act_p1s, c->act_p2s, c->stream));
   HIP_TRY(c, hipMemcpyAsync(actions, c->act_out, n * 4, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return DDQ_OK;
@@ -1138,6 +1146,8 @@ static int initial_target_sync(ddq_ctx* c, const ddq_step_cfg* cfg) {
     HIP_TRY(c, hipMemcpyAsync(c->nb.theta[1], c->nb.theta[0], c->nb.L.total * 4,
                               hipMemcpyDeviceToDevice, c->stream));
     HIP_TRY(c, hipMemcpyAsync(c->nb.wk[1], c->nb.wk[0], c->nb.L.wk_total * 4,
+                              hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->nb.wks[1], c->nb.wks[0], c->nb.L.wks_total * 3 * 2,
                               hipMemcpyDeviceToDevice, c->stream));
   }
   return DDQ_OK;

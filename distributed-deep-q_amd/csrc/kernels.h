@@ -15,6 +15,8 @@ struct ParamLayout {
   int64_t total;
   int64_t wk_off[3];       // offsets of conv kernel-layout copies in the wk buffer
   int64_t wk_total;
+  int64_t wks_off[3];      // offsets of the split (3 x bf16) forward weights in a wks plane
+  int64_t wks_total;       // elements per wks plane (conv1 padded to kx = 8)
 };
 ParamLayout make_layout(int S);
 
@@ -40,8 +42,10 @@ struct NetBuffers {
   // minibatch (NHWC frames; action one-hot (B,4); reward / non_terminal (B))
   float *state, *next_state, *action, *reward, *nonterm;
   int32_t* idx;
-  // activations per tower z (0 = Q on state, 1 = P on next_state)
+  // activations per tower z (0 = Q on state, 1 = P on next_state); the
+  // forward convs read their input split (split.h), the Q backward fp32
   float *pool1[2], *pool2[2], *pool3[2], *h4[2];
+  __bf16 *pool1s[2], *pool2s[2];    // split pool1 / pool2 (3 planes, NHWC)
   uint8_t *mask1, *mask2, *mask3;   // Q tower only
   float* fc4_part;                  // [splits][2][B][512]
   int fc4_splits;
@@ -56,8 +60,11 @@ struct NetBuffers {
   int64_t wpart_off[3];
   int wsplits[3];
   int wnp[3];
-  // parameters: theta[z] flat Caffe layout; wk[z] conv kernel layout; grad; opt state
+  // parameters: theta[z] flat Caffe layout; wk[z] conv kernel layout (fp32,
+  // the data gradients); wks[z] split kernel layout (the forward convs);
+  // grad; opt state
   float *theta[2], *wk[2], *grad, *opt;
+  __bf16* wks[2];
   float *dqbuf, *lpart;             // head: per-sample dQ (B,4) and squared error (B)
   int32_t* opt_init;                // 0 until the first apply after a reset
   int64_t* iter;                    // applied updates (param-server iteration)
@@ -129,7 +136,7 @@ hipError_t launch_sum_slices(float* out, const float* in, int W, int64_t len, in
 // Q-tower forward of n states (NHWC f32 in `in`) into scratch, argmax into out.
 hipError_t launch_act(const NetBuffers& nb, const float* in, int n, float* pool1, float* pool2,
                       float* pool3, float* h4, float* part, float* qout, int32_t* actions,
-                      hipStream_t s);
+                      __bf16* pool1s, __bf16* pool2s, hipStream_t s);
 // large-batch device draw (bitmap claim + ordered compaction) into idx[0..n)
 // and the Caffe-layout (n,4,S,S) f32 gather of replay.py:167-183
 hipError_t launch_sample_batch(ReplayMeta* meta, int64_t valid, int n, uint64_t seed,

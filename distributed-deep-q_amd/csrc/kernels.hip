@@ -6,6 +6,7 @@
 #include "wgrad1.h"
 #include "wgradd.h"
 #include "fc.h"
+#include "split.h"
 
 namespace ddq {
 
@@ -41,6 +42,11 @@ ParamLayout make_layout(int S) {
   int64_t q = 0;
   for (int i = 0; i < 3; ++i) { L.wk_off[i] = q; q += wn[i]; }
   L.wk_total = q;
+  // split forward weights: conv1 [n][7][8][4] (kx 7 zero), conv2/3 [co][tap][ci]
+  L.wks_off[0] = 0;
+  L.wks_off[1] = kConv1WPlane;
+  L.wks_off[2] = L.wks_off[1] + wn[1];
+  L.wks_total = L.wks_off[2] + wn[2];
   return L;
 }
 
@@ -491,7 +497,7 @@ hipError_t launch_u8_to_nhwc(const uint8_t* src, int n, int S, float* dst, hipSt
 // ---------------------------------------------------------------------------
 // Caffe (co,ci,ky,kx) -> kernel layout (co,ky,kx,ci) for the three convs
 // ---------------------------------------------------------------------------
-struct ConvDims { int64_t w_off, wk_off; int cout, cin, ks; };
+struct ConvDims { int64_t w_off, wk_off, wks_off; int cout, cin, ks; };
 
 // e: Caffe-order element (co, ci, ky, kx) of the layer's weight (< 2^31);
 // returns its offset in the kernel layout Wk[co][tap][ci].
@@ -502,26 +508,47 @@ __device__ __forceinline__ int wk_local(const ConvDims& d, int e) {
   return (co * kk + tap) * d.cin + ci;
 }
 
+// e as in wk_local; its offset in the split forward layout (split.h):
+// conv1 [co][ky][kx 0..7][ci] (kx 7 stays zero), conv2/3 [co][tap][ci]
+__device__ __forceinline__ int wks_local(const ConvDims& d, int e) {
+  const int kk = d.ks * d.ks, per = d.cin * kk;
+  const int co = e / per, rem = e - co * per;
+  const int ci = rem / kk, tap = rem - ci * kk;
+  if (d.ks == 7) {
+    const int ky = tap / 7, kx = tap - 7 * ky;
+    return ((co * 7 + ky) * 8 + kx) * 4 + ci;
+  }
+  return (co * kk + tap) * d.cin + ci;
+}
+
+// conv weight element k (of layer d) now holds v: refresh the fp32 kernel
+// layout and the split forward layout
+__device__ __forceinline__ void put_conv_weight(const ConvDims& d, int e, float v, float* wk,
+                                                __bf16* wks, int64_t wks_plane) {
+  wk[d.wk_off + wk_local(d, e)] = v;
+  store_split(wks, wks_plane, d.wks_off + wks_local(d, e), v);
+}
+
 __global__ void relayout_kernel(const float* __restrict__ theta, float* __restrict__ wk,
-                                ConvDims d0, ConvDims d1, ConvDims d2) {
+                                __bf16* __restrict__ wks, int64_t wks_plane, ConvDims d0,
+                                ConvDims d1, ConvDims d2) {
   const int l = blockIdx.y;
   const ConvDims d = l == 0 ? d0 : (l == 1 ? d1 : d2);
   const int n = d.cout * d.cin * d.ks * d.ks;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
-    wk[d.wk_off + wk_local(d, e)] = theta[d.w_off + e];
-  }
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x)
+    put_conv_weight(d, e, theta[d.w_off + e], wk, wks, wks_plane);
 }
 
 static void conv_dims(const ParamLayout& L, ConvDims* d) {
   const int cout[3] = {32, 64, 64}, cin[3] = {4, 32, 64}, ks[3] = {7, 5, 3};
-  for (int i = 0; i < 3; ++i) d[i] = {L.w[i], L.wk_off[i], cout[i], cin[i], ks[i]};
+  for (int i = 0; i < 3; ++i) d[i] = {L.w[i], L.wk_off[i], L.wks_off[i], cout[i], cin[i], ks[i]};
 }
 
 hipError_t launch_relayout(const NetBuffers& nb, int z, hipStream_t s) {
   ConvDims d[3];
   conv_dims(nb.L, d);
-  hipLaunchKernelGGL(relayout_kernel, dim3(64, 3), dim3(256), 0, s, nb.theta[z], nb.wk[z], d[0],
-                     d[1], d[2]);
+  hipLaunchKernelGGL(relayout_kernel, dim3(64, 3), dim3(256), 0, s, nb.theta[z], nb.wk[z],
+                     nb.wks[z], nb.L.wks_total, d[0], d[1], d[2]);
   return hipGetLastError();
 }
 
@@ -843,6 +870,9 @@ struct ApplyTail {
   float* wk;
   float* thetaP;
   float* wkP;
+  __bf16* wks;               // split forward weights of Q / P (plane stride wks_plane)
+  __bf16* wksP;
+  int64_t wks_plane;
   int blk0;                  // first apply block of the launch
 };
 
@@ -874,9 +904,8 @@ __device__ __forceinline__ void apply_elems(const ApplyTail& t, const ApplyArgs&
     if (e0 >= 0 && e0 < (int64_t)d.cout * d.cin * d.ks * d.ks) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int k = wk_local(d, (int)e0 + e);
-        t.wk[d.wk_off + k] = th[e];
-        if (sync) t.wkP[d.wk_off + k] = th[e];
+        put_conv_weight(d, (int)e0 + e, th[e], t.wk, t.wks, t.wks_plane);
+        if (sync) put_conv_weight(d, (int)e0 + e, th[e], t.wkP, t.wksP, t.wks_plane);
       }
     }
   }
@@ -1034,7 +1063,9 @@ __global__ __launch_bounds__(256) void refresh_kernel(const float* __restrict__ 
                                                       const int32_t* __restrict__ opt_init,
                                                       float* __restrict__ wk,
                                                       float* __restrict__ thetaP,
-                                                      float* __restrict__ wkP, ApplyArgs a) {
+                                                      float* __restrict__ wkP, __bf16* wks,
+                                                      __bf16* wksP, int64_t wks_plane,
+                                                      ApplyArgs a) {
   const bool sync = opt_init[3] != 0;
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i >= a.n || (!sync && i >= a.conv[2].w_off + (int64_t)a.conv[2].cout * a.conv[2].cin * 9))
@@ -1049,9 +1080,8 @@ __global__ __launch_bounds__(256) void refresh_kernel(const float* __restrict__ 
     if (e0 >= 0 && e0 < (int64_t)d.cout * d.cin * d.ks * d.ks) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int k = wk_local(d, (int)e0 + e);
-        wk[d.wk_off + k] = th[e];
-        if (sync) wkP[d.wk_off + k] = th[e];
+        put_conv_weight(d, (int)e0 + e, th[e], wk, wks, wks_plane);
+        if (sync) put_conv_weight(d, (int)e0 + e, th[e], wkP, wksP, wks_plane);
       }
     }
   }
@@ -1082,7 +1112,8 @@ static ApplyArgs apply_args(const NetBuffers& nb, int rule, float lr, float deca
 }
 
 static ApplyTail apply_tail(const NetBuffers& nb) {
-  return ApplyTail{nb.theta[0], nb.grad, nb.opt, nb.opt_init, nb.wk[0], nb.theta[1], nb.wk[1], 0};
+  return ApplyTail{nb.theta[0], nb.grad,  nb.opt,    nb.opt_init,      nb.wk[0],
+                   nb.theta[1], nb.wk[1], nb.wks[0], nb.wks[1], nb.L.wks_total, 0};
 }
 
 // The fused fc4-weight apply (NetBuffers::fa): fc4's weight gradient is final
@@ -1106,7 +1137,8 @@ hipError_t launch_apply_shard(const NetBuffers& nb, int rule, float lr, float de
 hipError_t launch_refresh(const NetBuffers& nb, hipStream_t s) {
   const ApplyArgs a = apply_args(nb, 0, 0.f, 0.f, 0.f, 0.f, 0.f, 0);
   hipLaunchKernelGGL(refresh_kernel, dim3((uint32_t)((a.n / 4 + 255) / 256)), dim3(256), 0, s,
-                     nb.theta[0], nb.opt_init, nb.wk[0], nb.theta[1], nb.wk[1], a);
+                     nb.theta[0], nb.opt_init, nb.wk[0], nb.theta[1], nb.wk[1], nb.wks[0],
+                     nb.wks[1], nb.L.wks_total, a);
   return hipGetLastError();
 }
 
@@ -1271,13 +1303,24 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     p.mask[0] = nb.mask1; p.mask[1] = nullptr;
     M("conv1_fwd");
     if (nb.conv_impl == 1) {
-      DirectArgs d = direct_fwd_args(p.in, p.wk, p.bias, p.out, p.mask, B, S, 3);
-      // (8 waves of one 32-pixel block each measured 39.9 us against 30.7)
-      // (register-B, patch-only LDS: 34.8 us)
-      // 16x32 tiles, 8 waves of two 32-pixel blocks: the 25 KB weight image is
-      // staged once per 512 pixels instead of 256 (29.3 us against 30.6 for
-      // 16x16 tiles / 4 waves; 32x16: 29.4; 16x32 / 4 waves of 4 blocks: 39.1)
-      CHECK_LAUNCH((launch_direct<4, 32, 7, 16, 32, 8, 1, false, true>(d, nz, s)));
+      // bf16 matrix cores, fp32-exact (split.h): frames are exact in bf16, so
+      // 3 MFMAs per 32x32x16 block; the pooled output goes out split (conv2's
+      // input) and, for the Q tower, fp32 (conv2's weight gradient).
+      // (ubench, both towers: 32x32 tiles / 16 waves 14.5 us, 16x32 / 8 waves
+      // 15.0, against 29.3 us for the f32-MFMA direct kernel)
+      Conv1Args c1{};
+      c1.B = B; c1.H = S; c1.W = S;
+      for (int z = 0; z < 2; ++z) {
+        c1.in[z] = p.in[z];
+        c1.wk[z] = nb.wks[z] + L.wks_off[0];
+        c1.bias[z] = p.bias[z];
+        c1.out_split[z] = nb.pool1s[z];
+      }
+      c1.out[0] = nb.pool1[0];   // the P tower needs no fp32 copy
+      c1.out[1] = nullptr;
+      c1.out_elems = (int64_t)B * (S / 2) * (S / 2) * 32;
+      c1.mask[0] = nb.mask1; c1.mask[1] = nullptr;
+      CHECK_LAUNCH((launch_split_conv1<32, 32, 16>(c1, nz, s, L.wks_total)));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgConv1F>(p, nz, 1, s));
     }
@@ -1295,11 +1338,24 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     p.mask[0] = nb.mask2; p.mask[1] = nullptr;
     M("conv2_fwd");
     if (nb.conv_impl == 1) {
-      DirectArgs d = direct_fwd_args(p.in, p.wk, p.bias, p.out, p.mask, B, H, 2);
-      // 8 waves, each one 32-channel half of a 32-pixel block: 53.9 us against
-      // 55.7 with 4 waves of both halves (16x16 tiles: 53.8; 8x8: 56.6; two
-      // tap groups: 57.6)
-      CHECK_LAUNCH((launch_direct<32, 64, 5, 8, 16, 4, 2, false, false>(d, nz, s)));
+      // split bf16 (split.h): 16x16 tiles, 16 waves of one 32x32 block each
+      // (ubench, both towers: 33.9 us against 53.9 for the f32-MFMA kernel;
+      // 8 waves of 32x64: 34.3; 8x16 tiles: 43)
+      SplitArgs a2{};
+      a2.B = B; a2.H = H; a2.W = H; a2.pad = 2;
+      for (int z = 0; z < 2; ++z) {
+        a2.in[z] = nb.pool1s[z];
+        a2.wk[z] = nb.wks[z] + L.wks_off[1];
+        a2.bias[z] = p.bias[z];
+        a2.out_split[z] = nb.pool2s[z];
+      }
+      a2.in_elems = (int64_t)B * H * H * 32;
+      a2.wk_elems = L.wks_total;
+      a2.out[0] = nb.pool2[0];   // fp32 for the Q tower only (conv3's weight gradient)
+      a2.out[1] = nullptr;
+      a2.out_elems = (int64_t)B * (H / 2) * (H / 2) * 64;
+      a2.mask[0] = nb.mask2; a2.mask[1] = nullptr;
+      CHECK_LAUNCH((launch_split_conv<32, 32, 64, 5, 16, 16, 8, 2, false>(a2, nz, s)));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgConv2F>(p, nz, 1, s));
     }
@@ -1317,12 +1373,22 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     p.nchw = 1; p.fHWp = FastDiv((H / 2) * (H / 2));   // pool3 = fc4 input in Caffe order
     M("conv3_fwd");
     if (nb.conv_impl == 1) {
-      DirectArgs d = direct_fwd_args(p.in, p.wk, p.bias, p.out, p.mask, B, H, 1);
-      d.nchw = 1;
-      d.mask_nhwc = 1;   // routing bytes NHWC: the backward expands dpool3 through them
-      // 3 tap groups: 512 output blocks per tower would leave one wave per SIMD
-      // (register-B variants measured slower: 8x8 15.6 us, 4x8 17.5, against 14.5)
-      CHECK_LAUNCH((launch_direct<64, 64, 3, 8, 8, 2, 2, false, false, 3>(d, nz, s)));
+      // split bf16: 8x8 tiles, 4 waves (ubench 12.1 us against 14.5 f32);
+      // pool3 (= fc4's input) fp32 in Caffe order, routing bytes NHWC (the
+      // backward expands dpool3 through them)
+      SplitArgs a3{};
+      a3.B = B; a3.H = H; a3.W = H; a3.pad = 1;
+      for (int z = 0; z < 2; ++z) {
+        a3.in[z] = nb.pool2s[z];
+        a3.wk[z] = nb.wks[z] + L.wks_off[2];
+        a3.bias[z] = p.bias[z];
+        a3.out[z] = nb.pool3[z];
+      }
+      a3.in_elems = (int64_t)B * H * H * 64;
+      a3.wk_elems = L.wks_total;
+      a3.nchw = 1;
+      a3.mask[0] = nb.mask3; a3.mask[1] = nullptr;
+      CHECK_LAUNCH((launch_split_conv<64, 64, 64, 3, 8, 8, 2, 2, false>(a3, nz, s)));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgConv3F>(p, nz, 1, s));
     }
@@ -1631,13 +1697,14 @@ __global__ void argmax_kernel(int n, const float* __restrict__ qout, int32_t* __
 
 hipError_t launch_act(const NetBuffers& nb, const float* in, int n, float* pool1, float* pool2,
                       float* pool3, float* h4, float* part, float* qout, int32_t* actions,
-                      hipStream_t s) {
+                      __bf16* pool1s, __bf16* pool2s, hipStream_t s) {
   NetBuffers a = nb;
   a.B = n;
   a.state = const_cast<float*>(in);
   a.next_state = const_cast<float*>(in);
   a.pool1[0] = pool1; a.pool2[0] = pool2; a.pool3[0] = pool3; a.h4[0] = h4;
   a.pool1[1] = pool1; a.pool2[1] = pool2; a.pool3[1] = pool3; a.h4[1] = h4;
+  a.pool1s[0] = a.pool1s[1] = pool1s; a.pool2s[0] = a.pool2s[1] = pool2s;
   a.mask1 = a.mask2 = a.mask3 = nullptr;
   a.fc4_part = part;
   a.q_out = qout; a.p_out = qout;

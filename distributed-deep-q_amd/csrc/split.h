@@ -1,0 +1,563 @@
+// fp32-exact convolutions on the bf16 matrix cores (gfx950).
+//
+// gfx950 runs v_mfma_f32_32x32x16_bf16 at 16x the rate of the f32-input
+// v_mfma_f32_32x32x2_f32 (2 vs 32 cycles per unit of K per SIMD).  An fp32
+// value splits EXACTLY into three bf16 values, x = x0 + x1 + x2 (x0 = bf16(x),
+// x1 = bf16(x - x0), x2 = bf16(x - x0 - x1): 3 x 8 significant bits = the 24
+// of fp32; the remainder is below 2^-24 |x|).  A product of two split values
+// is the sum of nine bf16 x bf16 products, each exact in fp32; the six with
+// i + j <= 2 carry everything above 2^-24 |ab| (the three dropped ones are
+// 2^-24, 2^-24 and 2^-32 of it, the size of fp32's own rounding), so
+//
+//   a . b  ~=  a0b0 + (a1b0 + a0b1 + a2b0 + a1b1 + a0b2)
+//
+// costs 6 bf16 MFMAs per 16 K instead of 8 f32 MFMAs at 4x the cycles:
+// 192 against 512 cycles per 32x32x16 block, with fp32 accuracy (the big
+// term and the five corrections accumulate in separate fp32 registers and
+// are added once at the end).  The parity tests hold these kernels to the
+// same per-element bound as the f32 MFMA path (tests/_parity.py).
+//
+// Storage: a "split tensor" of E elements is 3 bf16 planes of E (plane p at
+// +p*E), each in the layout of the fp32 tensor it stands for.  Producers
+// split once in their epilogue (activations: the pool epilogue; gradients:
+// the dgrad epilogue; weights: the apply / relayout) so the MFMA loops only
+// load: no conversion in any K loop.
+//
+// Direct convolution (fwd and dgrad), one workgroup = one image b x a TY x TX
+// tile of output pixels x all N output channels, as in direct.h: the halo
+// patch of all 3 planes is staged in LDS once, the weights tap by tap through
+// a two-slot ring; lane (row r, k-half h) of the 32x32x16 operand reads the 8
+// consecutive channels [16g + 8h, +8) of its pixel (A) or weight row (B) with
+// one ds_read_b128 per plane.
+#pragma once
+#include <type_traits>
+
+#include "common.h"
+
+namespace ddq {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));   // native vector: promotable
+
+// x -> (x0, x1, x2) bf16, x0 + x1 + x2 == x to 2^-24 |x| (RNE conversions)
+__device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
+  h = (__bf16)x;
+  const float r = x - (float)h;
+  m = (__bf16)r;
+  l = (__bf16)(r - (float)m);
+}
+
+// Store the split of v at element e of a split tensor of E elements.
+__device__ __forceinline__ void store_split(__bf16* t, int64_t E, int64_t e, float v) {
+  __bf16 h, m, l;
+  split3(v, h, m, l);
+  t[e] = h;
+  t[E + e] = m;
+  t[2 * E + e] = l;
+}
+
+// bank-conflict-free strides for the 32x32x16 operand reads (tools/lds_banks.py):
+// pixel stride CP + 8 bf16 (an odd number of 16-byte units), patch row stride
+// == 128 (mod 256) bytes: the four 16-lane groups of a ds_read_b128 then hit
+// 16 distinct 16-byte bank quads for TX = 16 tiles (two pixel rows per
+// 32-pixel block); weight rows CP + 8 bf16 likewise.
+// CPT input channels are processed in NCH = CPT / CP chunks of CP (the patch
+// of one chunk is resident at a time: conv2 dgrad's 64-channel patch of a
+// 16 x 16 tile would not fit LDS with its 3 planes).
+template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN>
+struct SplitCfg {
+  static constexpr int NCH = CPT / CP;
+  static constexpr int PH = TY + KS - 1, PW = TX + KS - 1;
+  static constexpr int CS = CP + 8;                                   // bf16 per pixel
+  static constexpr int RS0 = PW * CS;
+  static constexpr int RS = RS0 + ((64 - (RS0 % 128)) + 128) % 128;   // == 64 (mod 128) bf16
+  static constexpr int CW = CP + 8;                                   // bf16 per weight row
+  static constexpr int T = KS * KS;
+  static constexpr int KSTEP = CP / 16;
+  static constexpr int kGroup = 64 * WM * WN;
+  static constexpr int kThreads = kGroup;
+  static constexpr int TM = TY * TX / WM / 32;
+  static constexpr int TN = N / WN / 32;
+  static constexpr int kPlane = PH * RS;                              // bf16 per patch plane
+  static constexpr int kWSlot = N * CW;                               // bf16 per weight plane
+  static constexpr int kPatchB = 3 * kPlane * 2;
+  static constexpr int kWB = 2 * 3 * kWSlot * 2;                      // two-slot ring
+  static constexpr int kSmemB = kPatchB + kWB;
+  static_assert(CPT % CP == 0 && CP % 16 == 0 && TY % 2 == 0 && TX % 2 == 0, "shape");
+  static_assert(TM >= 1 && TN >= 1 && TY * TX == WM * TM * 32 && N == WN * TN * 32, "wave tile");
+  static_assert(kSmemB <= 160 * 1024, "LDS budget");
+};
+
+// Weight staging of one (chunk, tap) (3 planes of N x CP bf16): a global ->
+// register load issued two steps ahead, a register -> LDS store after the
+// MFMAs of the step before it.  Native vector registers in an array indexed
+// only by unrolled constants: HIP's uint4 struct (or registers captured by a
+// lambda) were kept in scratch memory and every load waited on at once.
+template <class C, int CPT, int CP, int N>
+struct SplitWStage {
+  static constexpr int WV = N * CP / 8;                         // 16-byte vectors per plane
+  static constexpr int kPer = (3 * WV + C::kGroup - 1) / C::kGroup;
+  static_assert(kPer <= 12, "weight staging registers");
+  u32x4 r[kPer];
+
+  __device__ __forceinline__ void load(const __bf16* __restrict__ wk, int64_t E, int ch, int t,
+                                       int tid) {
+#pragma unroll
+    for (int S = 0; S < kPer; ++S) {   // clamped, unconditional: the store drops extra lanes
+      const int f0 = tid + S * C::kGroup;
+      const int f = (3 * WV) % C::kGroup == 0 || f0 < 3 * WV ? f0 : 3 * WV - 1;
+      const int p = f / WV, q = f - p * WV;
+      const int n = q / (CP / 8), c8 = q % (CP / 8);
+      r[S] = *reinterpret_cast<const u32x4*>(wk + p * E + ((size_t)n * C::T + t) * CPT + ch * CP +
+                                             8 * c8);
+    }
+  }
+  __device__ __forceinline__ void store(__bf16* dst, int tid) const {
+#pragma unroll
+    for (int S = 0; S < kPer; ++S) {   // clamped lanes rewrite the last vector: no branch
+      const int f0 = tid + S * C::kGroup;
+      const int f = (3 * WV) % C::kGroup == 0 || f0 < 3 * WV ? f0 : 3 * WV - 1;
+      const int p = f / WV, q = f - p * WV;
+      const int n = q / (CP / 8), c8 = q % (CP / 8);
+      *reinterpret_cast<u32x4*>(dst + p * C::kWSlot + n * C::CW + 8 * c8) = r[S];
+    }
+  }
+};
+
+struct SplitArgs {
+  int B, H, W;               // conv grid (stride 1, same padding)
+  int tiles_x;
+  int pad;
+  const __bf16* in[2];       // split NHWC (B,H,W,CPT); dgrad pooled: (B,H/2,W/2,CPT)
+  int64_t in_elems;          // E of the input split tensor
+  const __bf16* wk[2];       // split weights [n][tap][CPT] (dgrad: transposed + flipped)
+  int64_t wk_elems;          // E of the weight split tensor (plane stride)
+  const float* bias[2];      // fwd
+  float* out[2];             // fwd: fp32 pooled output (nullable), NHWC or NCHW (nchw)
+  __bf16* out_split[2];      // fwd: split pooled NHWC output (nullable)
+  int64_t out_elems;         // E of the pooled output
+  int nchw;                  // fwd: fp32 output in Caffe (B,N,H/2,W/2) order
+  uint8_t* mask[2];          // fwd: NHWC routing bytes (nullable)
+  const uint8_t* in_route;   // dgrad: routing bytes of the pooled source (NHWC)
+  float* pd;                 // dgrad: fp32 gradient of the previous pool output (nullable)
+  __bf16* pd_split;          // dgrad: split gradient of the previous pool output (nullable)
+  int64_t pd_elems;
+};
+
+// Epilogue of a direct conv tile (accumulator rows window-major: a lane's 4
+// consecutive rows are one 2x2 pooling window).
+//  fwd  : bias + ReLU + 2x2 max-pool + first-max routing byte; the pooled value
+//         goes to the fp32 output (NHWC, or NCHW with nchw) and / or the split
+//         NHWC output, the routing byte (0..3, 4 = ReLU'd window) to mask.
+//  dgrad: the gradient of the previous layer's pool output, NHWC, fp32 and / or
+//         split (the consumer routes it through that pool's mask).
+template <int TM, int TN, int TX, int N, bool DGRAD>
+__device__ __forceinline__ void split_epilogue(const SplitArgs& a, const f32x16 (&acc)[TM][TN],
+                                               int b, int z, int y0, int x0, int wmi, int wni,
+                                               int l31, int h) {
+  const float* __restrict__ biasz = z ? a.bias[1] : a.bias[0];
+  float* __restrict__ outz = z ? a.out[1] : a.out[0];
+  __bf16* __restrict__ osplit = z ? a.out_split[1] : a.out_split[0];
+  uint8_t* __restrict__ maskz = z ? a.mask[1] : a.mask[0];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int mb = wmi * TM * 32 + 32 * i;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = wni * TN * 32 + 32 * j + l31;
+      if (!DGRAD) {
+        const int Hp = a.H >> 1, Wp = a.W >> 1;
+        const float bvv = biasz[n];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int win = (mb + 8 * g + 4 * h) >> 2;
+          const int pyy = y0 / 2 + win / (TX / 2), pxx = x0 / 2 + win % (TX / 2);
+          if (pyy >= Hp || pxx >= Wp) continue;
+          const float v0 = acc[i][j][4 * g + 0] + bvv, v1 = acc[i][j][4 * g + 1] + bvv;
+          const float v2 = acc[i][j][4 * g + 2] + bvv, v3 = acc[i][j][4 * g + 3] + bvv;
+          float mx = v0; int arg = 0;
+          if (v1 > mx) { mx = v1; arg = 1; }
+          if (v2 > mx) { mx = v2; arg = 2; }
+          if (v3 > mx) { mx = v3; arg = 3; }
+          const bool pos = mx > 0.f;
+          const float o = pos ? mx : 0.f;
+          const size_t onhwc = (((size_t)b * Hp + pyy) * Wp + pxx) * N + n;
+          if (outz) outz[a.nchw ? (((size_t)b * N + n) * Hp + pyy) * Wp + pxx : onhwc] = o;
+          if (osplit) store_split(osplit, a.out_elems, onhwc, o);
+          if (maskz) maskz[onhwc] = (uint8_t)(pos ? arg : 4);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = mb + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const int win = m >> 2;
+          const int y = y0 + 2 * (win / (TX / 2)) + ((m >> 1) & 1);
+          const int x = x0 + 2 * (win % (TX / 2)) + (m & 1);
+          if (y >= a.H || x >= a.W) continue;
+          const size_t e = (((size_t)b * a.H + y) * a.W + x) * N + n;
+          if (a.pd) a.pd[e] = acc[i][j][r];
+          if (a.pd_split) store_split(a.pd_split, a.pd_elems, e, acc[i][j][r]);
+        }
+      }
+    }
+  }
+}
+
+template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, bool DGRAD>
+__device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, int bx, int by,
+                                                int bz) {
+  using C = SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN>;
+  constexpr int TM = C::TM, TN = C::TN, T = C::T, NCH = C::NCH;
+  __bf16* patch = reinterpret_cast<__bf16*>(smem);
+  __bf16* wbuf = reinterpret_cast<__bf16*>(smem + C::kPatchB);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int z = bz, b = by;
+  const int ty = bx / a.tiles_x, tx = bx % a.tiles_x;
+  const int y0 = ty * TY, x0 = tx * TX;
+  const __bf16* __restrict__ in = z ? a.in[1] : a.in[0];
+  const __bf16* __restrict__ wk = z ? a.wk[1] : a.wk[0];
+
+  // ---- stage the halo patch of channel chunk ch (3 planes, zero outside) ----
+  // Batches of 8 vectors per thread: every load of a batch is issued before
+  // its LDS stores (a load -> store loop pays one memory latency per vector).
+  auto stage_patch = [&](int ch) {
+    constexpr int NV = C::PH * C::PW * (CP / 8);           // 16-byte vectors per plane
+    constexpr int NIT = (3 * NV + C::kThreads - 1) / C::kThreads;
+    constexpr int BAT = 8;
+#pragma unroll
+    for (int i0 = 0; i0 < NIT; i0 += BAT) {
+      u32x4 v[BAT];
+      int dst[BAT];
+#pragma unroll
+      for (int u = 0; u < BAT; ++u) {
+        const int f0 = tid + (i0 + u) * C::kThreads;
+        const bool live = i0 + u < NIT && f0 < 3 * NV;
+        const int f = live ? f0 : 0;
+        const int p = f / NV, r = f - p * NV;
+        const int pix = r / (CP / 8), c8 = r % (CP / 8);
+        const int py = pix / C::PW, px = pix % C::PW;
+        const int gy = y0 - a.pad + py, gx = x0 - a.pad + px;
+        const bool in_img = live && (unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W;
+        dst[u] = live ? p * C::kPlane + py * C::RS + px * C::CS + 8 * c8 : -1;
+        v[u] = u32x4{0u, 0u, 0u, 0u};
+        if (in_img) {
+          if (DGRAD) {   // pooled source: expand through the routing bytes
+            const size_t o = (((size_t)b * (a.H >> 1) + (gy >> 1)) * (a.W >> 1) + (gx >> 1)) * CPT +
+                             ch * CP + 8 * c8;
+            const u32x4 uw = *reinterpret_cast<const u32x4*>(in + p * a.in_elems + o);
+            const uint2 m = *reinterpret_cast<const uint2*>(a.in_route + o);
+            const uint32_t q = ((gy & 1) << 1) | (gx & 1);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {   // bf16 pair e = channels 2e, 2e+1
+              const uint32_t mw = e < 2 ? m.x : m.y;
+              const uint32_t r0 = (mw >> (16 * (e & 1))) & 0xff;
+              const uint32_t r1 = (mw >> (16 * (e & 1) + 8)) & 0xff;
+              v[u][e] = (r0 == q ? (uw[e] & 0xffffu) : 0u) | (r1 == q ? (uw[e] & 0xffff0000u) : 0u);
+            }
+          } else {
+            v[u] = *reinterpret_cast<const u32x4*>(
+                in + p * a.in_elems + (((size_t)b * a.H + gy) * a.W + gx) * CPT + ch * CP + 8 * c8);
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < BAT; ++u)
+        if (dst[u] >= 0) *reinterpret_cast<u32x4*>(patch + dst[u]) = v[u];
+    }
+  };
+
+  // ---- weights: step s = (chunk s / T, tap s % T) -> ring slot s & 1 ----
+  // Two register sets: the loads of step s+2 are issued at the start of step
+  // s and stored at the end of step s+1 (two steps of MFMAs to land in).
+  constexpr int NSTEP = NCH * T;
+  SplitWStage<C, CPT, CP, N> ws0, ws1;
+  auto wload = [&](SplitWStage<C, CPT, CP, N>& w, int st) {
+    const int sc = st < NSTEP ? st : NSTEP - 1;
+    w.load(wk, a.wk_elems, sc / T, sc % T, tid);
+  };
+  stage_patch(0);
+  wload(ws0, 0);
+  ws0.store(wbuf, tid);
+  if (NSTEP > 1) wload(ws1, 1);
+  __syncthreads();
+
+  // ---- per-lane operand offsets (bf16 units) ----
+  const int l31 = lane & 31, h = lane >> 5;
+  const int wmi = wid / WN, wni = wid % WN;
+  int abase[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = wmi * TM * 32 + 32 * i + l31;
+    const int win = m >> 2, dy = (m >> 1) & 1, dx = m & 1;
+    const int wy = win / (TX / 2), wx = win % (TX / 2);
+    abase[i] = (2 * wy + dy) * C::RS + (2 * wx + dx) * C::CS + h * 8;
+  }
+  int bbase[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) bbase[j] = (wni * TN * 32 + 32 * j + l31) * C::CW + h * 8;
+
+  f32x16 acc[TM][TN], cor[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; cor[i][j][r] = 0.f; }
+
+  // one step: the MFMAs of tap t of the resident chunk on ring slot `slot`
+  auto tap_step = [&](int t, int slot) {
+    const __bf16* wb = wbuf + slot * 3 * C::kWSlot;
+    const int ky = t / KS, kx = t % KS;
+    const __bf16* pa = patch + ky * C::RS + kx * C::CS;
+#pragma unroll
+    for (int g = 0; g < C::KSTEP; ++g) {
+      bf16x8 av[3][TM], bv[3][TN];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          av[p][i] = *reinterpret_cast<const bf16x8*>(pa + p * C::kPlane + abase[i] + 16 * g);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          bv[p][j] = *reinterpret_cast<const bf16x8*>(wb + p * C::kWSlot + bbase[j] + 16 * g);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2][i], bv[0][j], cor[i][j], 0, 0, 0);
+          cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[1][j], cor[i][j], 0, 0, 0);
+          cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[2][j], cor[i][j], 0, 0, 0);
+          cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[0][j], cor[i][j], 0, 0, 0);
+          cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[1][j], cor[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[0][j], acc[i][j], 0, 0, 0);
+        }
+    }
+  };
+  // end of step s: store step s+1's weights, restage the patch at a chunk
+  // boundary (the barrier before fences every wave's reads of the old chunk)
+  auto step_end = [&](SplitWStage<C, CPT, CP, N>& w, int s) {
+    // keep the slot store + barrier AFTER the step's MFMAs (hipcc otherwise
+    // hoists them above: every wave then waited for all its LDS reads and the
+    // barrier before its first MFMA of the step)
+    __builtin_amdgcn_sched_barrier(0);
+    const bool chunk_edge = NCH > 1 && (s + 1) % T == 0;
+    if (chunk_edge) {
+      __syncthreads();
+      stage_patch((s + 1) / T);
+    }
+    w.store(wbuf + ((s + 1) & 1) * 3 * C::kWSlot, tid);
+    __syncthreads();
+  };
+  for (int s = 0; s < NSTEP; s += 2) {
+    if (s + 2 < NSTEP) {
+      wload(ws0, s + 2);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    tap_step(s % T, 0);
+    if (s + 1 >= NSTEP) break;
+    step_end(ws1, s);
+    if (s + 3 < NSTEP) {
+      wload(ws1, s + 3);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    tap_step((s + 1) % T, 1);
+    if (s + 2 >= NSTEP) break;
+    step_end(ws0, s + 1);
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] += cor[i][j];
+  split_epilogue<TM, TN, TX, N, DGRAD>(a, acc, b, z, y0, x0, wmi, wni, l31, h);
+}
+
+template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, bool DGRAD>
+__global__ __launch_bounds__(64 * WM * WN) void split_conv_kernel(const SplitArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char sm_split[];
+  split_conv_body<CPT, CP, N, KS, TY, TX, WM, WN, DGRAD>(a, sm_split, blockIdx.x, blockIdx.y,
+                                                        blockIdx.z);
+}
+
+template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, bool DGRAD>
+inline hipError_t launch_split_conv(SplitArgs a, int nz, hipStream_t st) {
+  using C = SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN>;
+  auto kern = split_conv_kernel<CPT, CP, N, KS, TY, TX, WM, WN, DGRAD>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, C::kSmemB);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  a.tiles_x = (a.W + TX - 1) / TX;
+  const int tiles_y = (a.H + TY - 1) / TY;
+  hipLaunchKernelGGL(kern, dim3(tiles_y * a.tiles_x, a.B, nz), dim3(C::kThreads), C::kSmemB, st,
+                     a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// conv1 (4 -> 32 channels, 7x7, pad 3) on the bf16 matrix cores.  Its input
+// is the replay frames: integers 0..255, exact in bf16, so A has ONE plane
+// and a product needs only three MFMAs (a.b0, a.b1, a.b2).  K of a kernel row
+// ky = 7 taps x 4 channels, padded to 32 = two 32x32x16 k-steps; lane half h
+// of step g covers taps kx = 4g + 2h, +1: two adjacent pixels x 4 channels,
+// read as two ds_read_b64 from a bf16 NHWC patch (pixel stride 8 B, one zero
+// column past the halo for the padded tap 7).  The 44.5 KB split weight image
+// [plane][n][ky][kx 0..7][ci] (row stride 232 bf16: conflict-free b128 reads)
+// is staged once per workgroup.
+// ---------------------------------------------------------------------------
+struct Conv1Args {
+  int B, H, W, tiles_x;
+  const float* in[2];          // fp32 NHWC (B,H,W,4) frames (exact integers)
+  const __bf16* wk[2];         // split [n][7][8][4] (kx 7 zero)
+  int64_t wk_elems;            // plane stride of the weight split tensor
+  const float* bias[2];
+  float* out[2];               // fp32 pooled NHWC (nullable)
+  __bf16* out_split[2];        // split pooled NHWC (nullable)
+  int64_t out_elems;
+  uint8_t* mask[2];
+};
+
+constexpr int kConv1WPlane = 32 * 7 * 8 * 4;   // 7168 bf16 per weight plane
+
+template <int TY, int TX, int WM>
+struct Conv1Cfg {
+  static constexpr int PH = TY + 6, PW = TX + 8;     // + zero column for tap 7 (+1 pad)
+  static constexpr int RS0 = PW * 4;
+  static constexpr int RS = RS0 + ((64 - (RS0 % 128)) + 128) % 128;   // == 64 (mod 128) bf16
+  static constexpr int CW = 7 * 32 + 8;                               // 232 bf16 per n row
+  static constexpr int kPatchB = PH * RS * 2;
+  static constexpr int kWB = 3 * 32 * CW * 2;
+  static constexpr int kSmemB = kPatchB + kWB;
+  static constexpr int TM = TY * TX / WM / 32;
+  static_assert(TM >= 1 && TY * TX == WM * TM * 32 && TX % 16 == 0, "tile");
+  static_assert(kSmemB <= 160 * 1024, "LDS");
+};
+
+template <int TY, int TX, int WM>
+__global__ __launch_bounds__(64 * WM) void split_conv1_kernel(const Conv1Args a) {
+  using C = Conv1Cfg<TY, TX, WM>;
+  constexpr int TM = C::TM;
+  extern __shared__ __attribute__((aligned(16))) char sm_c1[];
+  __bf16* patch = reinterpret_cast<__bf16*>(sm_c1);
+  __bf16* wbuf = reinterpret_cast<__bf16*>(sm_c1 + C::kPatchB);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int z = blockIdx.z, b = blockIdx.y;
+  const int ty = blockIdx.x / a.tiles_x, tx = blockIdx.x % a.tiles_x;
+  const int y0 = ty * TY, x0 = tx * TX;
+  const float* __restrict__ in = z ? a.in[1] : a.in[0];
+  const __bf16* __restrict__ wk = z ? a.wk[1] : a.wk[0];
+  constexpr int kThreads = 64 * WM;
+  // patch: one pixel (4 channels) per item, fp32 -> bf16 (exact), loads first
+  {
+    constexpr int NP = C::PH * C::PW;
+    constexpr int NIT = (NP + kThreads - 1) / kThreads;
+    float4 v[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int f = tid + it * kThreads;
+      const int py = f / C::PW, px = f % C::PW;
+      const int gy = y0 - 3 + py, gx = x0 - 3 + px;
+      v[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (f < NP && px < TX + 6 && (unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W)
+        v[it] = *reinterpret_cast<const float4*>(in + (((size_t)b * a.H + gy) * a.W + gx) * 4);
+    }
+    // all 3 x 7168 weight bf16 (16-byte vectors), then the stores
+    constexpr int NW = 3 * kConv1WPlane / 8;
+    constexpr int WIT = (NW + kThreads - 1) / kThreads;
+    u32x4 w[WIT];
+#pragma unroll
+    for (int it = 0; it < WIT; ++it) {
+      const int f0 = tid + it * kThreads;
+      const int f = f0 < NW ? f0 : NW - 1;
+      const int p = f / (kConv1WPlane / 8), r = f % (kConv1WPlane / 8);
+      w[it] = *reinterpret_cast<const u32x4*>(wk + p * a.wk_elems + 8 * (size_t)r);
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int f = tid + it * kThreads;
+      if (f < NP) {
+        const int py = f / C::PW, px = f % C::PW;
+        __bf16 q[4] = {(__bf16)v[it].x, (__bf16)v[it].y, (__bf16)v[it].z, (__bf16)v[it].w};
+        *reinterpret_cast<uint2*>(patch + py * C::RS + px * 4) = *reinterpret_cast<uint2*>(q);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < WIT; ++it) {
+      const int f0 = tid + it * kThreads;
+      const int f = f0 < NW ? f0 : NW - 1;
+      const int p = f / (kConv1WPlane / 8), r = f % (kConv1WPlane / 8);
+      const int n = r / 28, q8 = r % 28;        // 28 vectors of 8 per n row (7 x 8 x 4 / 8)
+      *reinterpret_cast<u32x4*>(wbuf + (p * 32 + n) * C::CW + 8 * q8) = w[it];
+    }
+  }
+  __syncthreads();
+  const int l31 = lane & 31, h = lane >> 5;
+  int abase[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = wid * TM * 32 + 32 * i + l31;
+    const int win = m >> 2, dy = (m >> 1) & 1, dx = m & 1;
+    const int wy = win / (TX / 2), wx = win % (TX / 2);
+    abase[i] = (2 * wy + dy) * C::RS + (2 * wx + dx + 2 * h) * 4;
+  }
+  const int bbase = l31 * C::CW + h * 8;
+  f32x16 acc[TM][1], cor[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { acc[i][0][r] = 0.f; cor[i][r] = 0.f; }
+#pragma unroll
+  for (int ky = 0; ky < 7; ++ky) {
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      bf16x8 bv[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        bv[p] = *reinterpret_cast<const bf16x8*>(wbuf + p * 32 * C::CW + bbase + ky * 32 + 16 * g);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const __bf16* pa = patch + abase[i] + ky * C::RS + 16 * g;
+        const uint2 lo = *reinterpret_cast<const uint2*>(pa);
+        const uint2 hi = *reinterpret_cast<const uint2*>(pa + 4);
+        u32x4 av4 = {lo.x, lo.y, hi.x, hi.y};
+        const bf16x8 av = *reinterpret_cast<bf16x8*>(&av4);
+        cor[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv[2], cor[i], 0, 0, 0);
+        cor[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv[1], cor[i], 0, 0, 0);
+        acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv[0], acc[i][0], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i) acc[i][0] += cor[i];
+  SplitArgs e{};
+  e.H = a.H; e.W = a.W;
+  e.bias[0] = a.bias[0]; e.bias[1] = a.bias[1];
+  e.out[0] = a.out[0]; e.out[1] = a.out[1];
+  e.out_split[0] = a.out_split[0]; e.out_split[1] = a.out_split[1];
+  e.out_elems = a.out_elems;
+  e.mask[0] = a.mask[0]; e.mask[1] = a.mask[1];
+  split_epilogue<TM, 1, TX, 32, false>(e, acc, b, z, y0, x0, wid, 0, l31, h);
+}
+
+template <int TY, int TX, int WM>
+inline hipError_t launch_split_conv1(Conv1Args a, int nz, hipStream_t st, int64_t wk_elems) {
+  a.wk_elems = wk_elems;
+  using C = Conv1Cfg<TY, TX, WM>;
+  auto kern = split_conv1_kernel<TY, TX, WM>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, C::kSmemB);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  a.tiles_x = (a.W + TX - 1) / TX;
+  const int tiles_y = (a.H + TY - 1) / TY;
+  hipLaunchKernelGGL(kern, dim3(tiles_y * a.tiles_x, a.B, nz), dim3(64 * WM), C::kSmemB, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace ddq
