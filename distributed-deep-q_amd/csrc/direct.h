@@ -31,6 +31,7 @@
 #include <type_traits>
 
 #include "common.h"
+#include "split.h"
 
 namespace ddq {
 
@@ -87,6 +88,8 @@ struct DirectArgs {
   float* pdconv;             // dgrad: previous layer's pre-pool gradient (B,2H,2W,N)
   int pd_pooled;             // dgrad: 1 = store the pool-output gradient pooled, NHWC
                              // (B,H,W,N); the consumer routes it through pmask
+  __bf16* pd_split;          // dgrad, pooled: also split (split.h), plane stride
+  int64_t pd_split_elems;    // pd_split_elems (nullable)
 };
 
 template <int V>
@@ -519,6 +522,7 @@ __device__ __forceinline__ void direct_conv_body(const DirectArgs& a, float* sme
           const float v = acc[i][j][r];
           if (a.pd_pooled) {   // one store per element: lanes along n, 128-B runs
             a.pdconv[pix * N + n] = v;
+            if (a.pd_split) store_split(a.pd_split, a.pd_split_elems, pix * N + n, v);
             continue;
           }
           const int mk = a.pmask[pix * N + n];

@@ -10,6 +10,7 @@
 // memory-level parallelism); only the small activation tile goes through LDS.
 #pragma once
 #include "common.h"
+#include "split.h"
 
 namespace ddq {
 
@@ -157,6 +158,8 @@ struct Fc4DgradArgs {
   float* dconv3;                   // NHWC (B, 2S4, 2S4, 64), or pooled (B, S4, S4, 64)
   int pooled;                      // 1: write the pool3-output gradient only (NHWC);
                                    // its consumers expand it through pool3's routing
+  __bf16* dsplit;                  // pooled: also split (split.h; conv3's weight
+  int64_t dsplit_elems;            // gradient), plane stride dsplit_elems (nullable)
 };
 
 // Body on block (bx, by) with an 8 x 1024-float LDS image; 512 threads.
@@ -209,7 +212,9 @@ __device__ __forceinline__ void fc4_dgrad_body(const Fc4DgradArgs& a, float (*re
     uint32_t ch, p, py, px;
     a.fS4sq.divmod((uint32_t)kc, ch, p);
     if (a.pooled) {   // one store per element instead of four (three of them zeros)
-      a.dconv3[((size_t)bb * a.fS4sq.d + p) * 64 + ch] = v;
+      const size_t o = ((size_t)bb * a.fS4sq.d + p) * 64 + ch;
+      a.dconv3[o] = v;
+      if (a.dsplit) store_split(a.dsplit, a.dsplit_elems, o, v);
       continue;
     }
     a.fS4.divmod(p, py, px);

@@ -5,6 +5,7 @@
 #include "direct.h"
 #include "wgrad1.h"
 #include "wgradd.h"
+#include "wgrads.h"
 #include "fc.h"
 #include "split.h"
 
@@ -1471,6 +1472,8 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     f.B = B; f.K = 64 * s4 * s4; f.s4 = s4; f.fS4sq = FastDiv(s4 * s4); f.fS4 = FastDiv(s4);
     f.dh4 = nb.dh4; f.w4 = nb.theta[0] + L.w[3]; f.mask3 = nb.mask3; f.dconv3 = nb.dconv3;
     f.pooled = nb.conv_impl == 1;
+    f.dsplit = nb.conv_impl == 1 ? nb.dconv3s : nullptr;
+    f.dsplit_elems = (int64_t)B * s4 * s4 * 64;
     FcWgrad w;
     w.M = kFc4; w.N = 64 * s4 * s4; w.K = B; w.ksplit_len = ((B + 31) / 32) * 32;
     w.dh4 = nb.dh4; w.x = nb.pool3[0]; w.gw4 = nb.grad + L.w[3];
@@ -1493,6 +1496,8 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
       f.B = B; f.K = p.N; f.s4 = s4; f.fS4sq = p.fS4sq; f.fS4 = p.fS4;
       f.dh4 = nb.dh4; f.w4 = p.w4; f.mask3 = nb.mask3; f.dconv3 = nb.dconv3;
       f.pooled = p.pooled;
+      f.dsplit = p.pooled ? nb.dconv3s : nullptr;
+      f.dsplit_elems = (int64_t)B * s4 * s4 * 64;
       CHECK_LAUNCH(launch_fc4_dgrad_direct(f, s));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgFcD>(p, 1, 1, s));
@@ -1548,11 +1553,16 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     p.NP = nb.wnp[2]; p.dconv = nb.dconv3; p.in = nb.pool2[0]; p.part = nb.wpart + nb.wpart_off[2];
     M("conv3_wgrad");
     if (nb.conv_impl == 1) {
-      // dconv3 holds the pooled gradient (fc4 dgrad, pooled mode): expanded
-      // through pool3's routing bytes while the rows are staged
-      WgradDArgs wa = wgradd_args(p, B, nb.wsplits[2]);
-      wa.droute = nb.mask3;
-      CHECK_LAUNCH((launch_wgradd<64, 64, 3, 1, true>(wa, sw)));
+      // split bf16 (wgrads.h): the pooled gradient of fc4's dgrad, expanded
+      // through pool3's routing bytes while the rows are staged, against the
+      // split pool2
+      WgradDArgs wd = wgradd_args(p, B, nb.wsplits[2]);
+      WgradSArgs ws{};
+      ws.B = B; ws.H = H; ws.W = H; ws.G = wd.G; ws.RPG = wd.RPG; ws.NP = wd.NP;
+      ws.in = nb.pool2s[0]; ws.in_elems = (int64_t)B * H * H * 64;
+      ws.dpool = nb.dconv3s; ws.d_elems = (int64_t)B * (H / 2) * (H / 2) * 64;
+      ws.droute = nb.mask3; ws.part = p.part;
+      CHECK_LAUNCH((launch_wgrads<64, 64, 3, 1>(ws, sw)));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgW3>(p, 1, ns, sw));
     }
@@ -1570,8 +1580,11 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
       // 4x8-pixel tiles (256 workgroups instead of 128: -2.5 us) with the B
       // operand straight from L2 (register-B, no weight ring: -2.5 us more)
       // pool2-output gradient stored pooled (2.1 MB instead of 8.4 MB); the
-      // conv2 wgrad / dgrad expand it through mask2 while staging
+      // conv2 wgrad / dgrad expand it through mask2 while staging (the wgrad
+      // from its split copy)
       d.pd_pooled = 1;
+      d.pd_split = nb.dconv2s;
+      d.pd_split_elems = (int64_t)B * H * H * 64;
       CHECK_LAUNCH((launch_direct<64, 64, 3, 4, 8, 1, 2, true, false, 3, true>(d, 1, s)));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgD3>(p, 1, 1, s));
@@ -1589,11 +1602,14 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     p.NP = nb.wnp[1]; p.dconv = nb.dconv2; p.in = nb.pool1[0]; p.part = nb.wpart + nb.wpart_off[1];
     M("conv2_wgrad");
     if (nb.conv_impl == 1) {
-      WgradDArgs wa = wgradd_args(p, B, nb.wsplits[1]);
-      wa.droute = nb.mask2;   // dconv2 pooled (conv3 dgrad)
-      // (3 waves per SIMD, 168 VGPRs: 43.3 us; with 4-row-per-wave balanced
-      // groups, DDQ_WG2_TARGET=640: 41.6 us; against 39.8 us)
-      CHECK_LAUNCH((launch_wgradd<32, 64, 5, 2, true>(wa, sw)));
+      // split bf16 (wgrads.h) on the split pooled dpool2 (conv3 dgrad) and pool1
+      WgradDArgs wd = wgradd_args(p, B, nb.wsplits[1]);
+      WgradSArgs ws{};
+      ws.B = B; ws.H = H; ws.W = H; ws.G = wd.G; ws.RPG = wd.RPG; ws.NP = wd.NP;
+      ws.in = nb.pool1s[0]; ws.in_elems = (int64_t)B * H * H * 32;
+      ws.dpool = nb.dconv2s; ws.d_elems = (int64_t)B * (H / 2) * (H / 2) * 64;
+      ws.droute = nb.mask2; ws.part = p.part;
+      CHECK_LAUNCH((launch_wgrads<32, 64, 5, 2>(ws, sw)));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgW2>(p, 1, ns, sw));
     }
@@ -1611,7 +1627,10 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
       d.in_route = nb.mask2;   // dconv2 pooled (conv3 dgrad), expanded while staged
       // pool1-output gradient stored pooled (4.2 MB instead of the 16.8 MB
       // un-pooled image, 3/4 zeros); conv1 wgrad expands it through mask1
+      // (from the split copy)
       d.pd_pooled = 1;
+      d.pd_split = nb.dconv1s;
+      d.pd_split_elems = (int64_t)B * H * H * 32;
       // (8x8 tiles -- two 74 KB workgroups per CU -- measured 39.3 us, and
       // 8x8 register-B 42.9 us, against 36.8 us for this configuration)
       // (two 32-pixel blocks per wave over 4 tap groups: 40.6 us)
@@ -1639,13 +1658,13 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     p.NP = nb.wnp[0]; p.dconv = nb.dconv1; p.in = nb.state; p.part = nb.wpart + nb.wpart_off[0];
     M("conv1_wgrad");
     if (nb.conv_impl == 1) {
-      Wgrad1Args w;
+      // split bf16 (wgrads.h): the split pooled dpool1 (conv2 dgrad) against
+      // the frames, three MFMAs per (tap row, 16 pixels)
+      Wgrad1SArgs w{};
       w.B = B; w.H = S; w.W = S; w.R = wgrad1_band(S, S); w.NP = nb.wnp[0];
-      w.dconv = nb.dconv1; w.in = nb.state; w.part = p.part;
-      w.droute = nb.mask1;   // dconv1 holds conv2 dgrad's pooled output
-      // (running the conv2/conv3 slab reduces as extra blocks of this launch
-      // measured 1.7 us slower than the separate reduce kernel)
-      CHECK_LAUNCH(launch_wgrad1(w, s));
+      w.dpool = nb.dconv1s; w.d_elems = (int64_t)B * (S / 2) * (S / 2) * 32;
+      w.droute = nb.mask1; w.in = nb.state; w.part = p.part;
+      CHECK_LAUNCH(launch_wgrad1s(w, s));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgW1>(p, 1, ns, s));
     }

@@ -1,0 +1,566 @@
+// conv2 / conv3 weight gradient on the bf16 matrix cores, fp32-exact split
+// operands (split.h), in the row-streaming form of wgradd.h.
+//
+// dW[co][ky][kx][ci] = sum_{b,y,x} dconv[b][y][x][co] * in[b][y+ky-P][x+kx-P][ci]
+// db[co]             = sum_{b,y,x} dconv[b][y][x][co]
+//
+// A workgroup owns one (co block cb, tap row ky) pair -- KS x CIN/32 output
+// tiles of 32 x 32 -- over a group of image rows; each of its 4 waves streams
+// its own rows through a private LDS region: the input row y+ky-P (3 bf16
+// planes, zero halo) and the cb block of the dconv row (3 planes, expanded
+// from the pooled split gradient through the pool's routing bytes).  One
+// 32x32x16 k-step = 16 pixels of the row; both operands are read pixel-major
+// out of their NHWC rows with ds_read_b64_tr_b16 (a 16-lane group reads 4
+// pixels x 16 channels and each lane receives its channel's 4 pixels), so the
+// kx shift of the input operand is just another row address: no im2col, no
+// shifted copies.  6 MFMAs per (tile, k-step), small products first, into one
+// fp32 accumulator.  The waves' tiles are summed in LDS
+// in fixed order and stored as the group's fp32 slab in the wgrad reducer's
+// layout ([group][co][NP], bias at n = KC; deterministic, no atomics).  The
+// bias column is summed on the VALU (fp32, from the staged split values) by
+// the ky == 0 workgroups.
+#pragma once
+#include "split.h"
+#include "wgradd.h"
+
+namespace ddq {
+
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+struct WgradSArgs {
+  int B, H, W;              // layer grid (input and dconv share H x W)
+  int G, RPG;               // row groups (= slabs) and rows per group
+  int NP;                   // slab pitch
+  const __bf16* in;         // split NHWC (B,H,W,CIN), plane stride in_elems
+  int64_t in_elems;
+  const __bf16* dpool;      // split pooled gradient (B,H/2,W/2,COUT), plane stride d_elems
+  int64_t d_elems;
+  const uint8_t* droute;    // its NHWC routing bytes
+  float* part;              // [G][COUT][NP]
+};
+
+// LDS geometry of one wave's region (bf16 units).  Pixel strides keep the
+// transposed reads conflict-free: a 32-lane half reads 4 pixels x 32 channels
+// = 4 x 64 B; pixel stride == 16 banks (mod 64) puts them on 64 distinct banks.
+template <int CIN, int PAD>
+struct WgradSGeom {
+  static constexpr int PSI = CIN == 32 ? 32 : 96;   // input pixel stride (64 B / 192 B)
+  static constexpr int PSD = 32;                    // dconv pixel stride (64 B)
+  // k-steps cover 16 pixels: rows are sized to W rounded up to 16, the dconv
+  // tail pixels stay zero (never written), the input halo / tail likewise
+  static __host__ __device__ int w16(int W) { return (W + 15) & ~15; }
+  static __host__ __device__ int in_plane(int W) { return (w16(W) + 2 * PAD + 8) * PSI; }
+  static __host__ __device__ int d_plane(int W) { return w16(W) * PSD; }
+  static __host__ __device__ int region(int W) { return 3 * (in_plane(W) + d_plane(W)); }
+};
+
+__device__ __forceinline__ bf16x8 tr_pair(const __bf16* p0, const __bf16* p1) {
+  typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+  const i16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(p0));
+  const i16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(p1));
+  typedef short i16x8 __attribute__((ext_vector_type(8)));
+  const i16x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int CIN, int COUT, int KS, int PAD, int WMAX>
+__device__ __forceinline__ void wgrads_body(const WgradSArgs& a, char* smem, int L) {
+  constexpr int NCB = CIN / 32;
+  constexpr int T = KS * NCB;
+  constexpr int KC = KS * KS * CIN;
+  using Geo = WgradSGeom<CIN, PAD>;
+  const int W = a.W, H = a.H;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int l31 = lane & 31, h = lane >> 5;
+  const int ipl = Geo::in_plane(W), dpl = Geo::d_plane(W);
+  __bf16* rin = reinterpret_cast<__bf16*>(smem) + w * Geo::region(W);   // [3][W+2P+8][PSI]
+  __bf16* rd = rin + 3 * ipl;                                            // [3][W][PSD]
+  // XCD-aware decode (as wgradd): every (cb, ky) workgroup of row group g
+  // gets the same L % 8, so the group's rows stay in one XCD's L2
+  constexpr int NTS = (COUT / 32) * KS;
+  const int xcd = L & 7, q = L >> 3;
+  const int ts = q % NTS, g = xcd + 8 * (q / NTS);
+  if (g >= a.G) return;
+  const int cb = ts / KS, ky = ts % KS;
+  const int r0 = g * a.RPG;
+  const int r1 = min(a.B * H, r0 + a.RPG);
+
+  // zero the pixels rows never write: the input halo / tail, the dconv tail
+  {
+    const int wi = Geo::w16(W) + 2 * PAD + 8;
+    for (int i = lane; i < 3 * wi * (Geo::PSI / 8); i += 64) {
+      const int p = i / (wi * (Geo::PSI / 8)), r = i - p * wi * (Geo::PSI / 8);
+      const int x = r / (Geo::PSI / 8);
+      if (x < PAD || x >= W + PAD) reinterpret_cast<u32x4*>(rin + p * ipl)[r] = u32x4{0u, 0u, 0u, 0u};
+    }
+    for (int i = lane; i < 3 * (Geo::w16(W) - W) * (Geo::PSD / 8); i += 64) {
+      const int per = (Geo::w16(W) - W) * (Geo::PSD / 8);
+      const int p = i / per, r = i - p * per;
+      reinterpret_cast<u32x4*>(rd + p * dpl + W * Geo::PSD)[r] = u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+
+  // one fp32 accumulator per tile for all six products (2 waves per SIMD
+  // need <= 256 registers; a separate correction accumulator took 80-96 more).
+  // Six MFMA roundings per 16 K, against sixteen (one per product) on the
+  // f32-input MFMA path this replaces.
+  f32x16 acc[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // channels 8*(lane&3) + j of cb
+
+  // ---- row staging: global -> registers (issued ahead), registers -> LDS ----
+  // Every lane keeps one 8-channel chunk and walks the pixels (no division
+  // in the loops: a runtime-divisor mapping of the vectors cost ~600 VALU per
+  // row, 10x the MFMAs).  Input: CC chunks per pixel, 64 / CC pixels a pass;
+  // pooled dconv: 4 chunks of the 32-channel block, 16 pooled pixels a pass,
+  // one routing load per pixel chunk for the three planes.
+  constexpr int CC = CIN / 8, PPP = 64 / CC;
+  constexpr int NPI = (WMAX + PPP - 1) / PPP;
+  constexpr int NPD = (WMAX / 2 + 15) / 16;
+  const int ic8 = lane % CC, ipx = lane / CC;
+  const int dc8 = lane & 3, dpx = lane >> 2;
+  struct Regs {
+    u32x4 i[3][NPI];
+    u32x4 d[3][NPD];
+    u32x2 m[NPD];
+  };
+  auto load = [&](Regs& R, int row) {
+    const bool live = row < r1;
+    const int b = row / H, y = row - b * H, yi = y + ky - PAD;
+    const bool vin = live && (unsigned)yi < (unsigned)H;
+    const __bf16* src = a.in + (((size_t)b * H + yi) * W + ipx) * CIN + 8 * ic8;
+#pragma unroll
+    for (int u = 0; u < NPI; ++u) {
+      const bool ok = vin && ipx + u * PPP < W;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        R.i[p][u] = u32x4{0u, 0u, 0u, 0u};
+        if (ok) R.i[p][u] = *reinterpret_cast<const u32x4*>(src + p * a.in_elems + u * PPP * CIN);
+      }
+    }
+    const size_t o0 = (((size_t)b * (H >> 1) + (y >> 1)) * (W >> 1) + dpx) * COUT + cb * 32 + 8 * dc8;
+#pragma unroll
+    for (int u = 0; u < NPD; ++u) {
+      const bool ok = live && dpx + 16 * u < (W >> 1);
+      const size_t o = o0 + (size_t)u * 16 * COUT;
+      R.m[u] = u32x2{0x04040404u, 0x04040404u};
+      if (ok) R.m[u] = *reinterpret_cast<const u32x2*>(a.droute + o);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        R.d[p][u] = u32x4{0u, 0u, 0u, 0u};
+        if (ok) R.d[p][u] = *reinterpret_cast<const u32x4*>(a.dpool + p * a.d_elems + o);
+      }
+    }
+  };
+  auto store = [&](const Regs& R, int row) {
+    const int y = row - (row / H) * H;
+    const uint32_t qy = (y & 1) << 1;
+#pragma unroll
+    for (int u = 0; u < NPI; ++u)
+      if (ipx + u * PPP < W)
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          *reinterpret_cast<u32x4*>(rin + p * ipl + (ipx + u * PPP + PAD) * Geo::PSI + 8 * ic8) =
+              R.i[p][u];
+#pragma unroll
+    for (int u = 0; u < NPD; ++u) {
+      const int px = dpx + 16 * u;
+      if (px >= (W >> 1)) continue;
+#pragma unroll
+      for (int dx = 0; dx < 2; ++dx) {
+        const uint32_t qd = qy | dx;
+        // per bf16 pair e (channels 2e, 2e+1): keep-masks from the routing bytes
+        uint32_t keep[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t mw = R.m[u][e >> 1];
+          const uint32_t ra = (mw >> (16 * (e & 1))) & 0xff;
+          const uint32_t rb = (mw >> (16 * (e & 1) + 8)) & 0xff;
+          keep[e] = (ra == qd ? 0xffffu : 0u) | (rb == qd ? 0xffff0000u : 0u);
+        }
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          u32x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = R.d[p][u][e] & keep[e];
+          *reinterpret_cast<u32x4*>(rd + p * dpl + (2 * px + dx) * Geo::PSD + 8 * dc8) = o;
+          if (ky == 0) {   // bias: fp32 value = sum of the three planes
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              bsum[2 * e] += __builtin_bit_cast(float, o[e] << 16);
+              bsum[2 * e + 1] += __builtin_bit_cast(float, o[e] & 0xffff0000u);
+            }
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  // per-lane transposed-read offsets: group gq = lane >> 4 reads pixel rows
+  // 8*(gq>>1) + {0..3} / {4..7}, channels 16*(gq&1) + 4*(lane&3) of a 32 block
+  const int gq = lane >> 4, iq = (lane & 15) >> 2, ip = lane & 3;
+  const int pix0 = 8 * (gq >> 1) + iq;
+  const int chn = 16 * (gq & 1) + 4 * ip;
+  auto compute = [&]() {
+#pragma unroll
+    for (int s = 0; s < WMAX / 16; ++s) {
+      if (16 * s >= W) break;
+      // every fragment of the k-step first (one LDS round trip per k-step,
+      // not one per tile: the reads were issued right before their MFMAs
+      // and waited on at once), then the MFMAs
+      bf16x8 av[3], bv[KS][NCB][3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const __bf16* pa = rd + p * dpl + (16 * s + pix0) * Geo::PSD + chn;
+        av[p] = tr_pair(pa, pa + 4 * Geo::PSD);
+      }
+#pragma unroll
+      for (int kx = 0; kx < KS; ++kx)
+#pragma unroll
+        for (int c = 0; c < NCB; ++c)
+#pragma unroll
+          for (int p = 0; p < 3; ++p) {
+            const __bf16* pb = rin + p * ipl + (16 * s + pix0 + kx) * Geo::PSI + 32 * c + chn;
+            bv[kx][c][p] = tr_pair(pb, pb + 4 * Geo::PSI);
+          }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int kx = 0; kx < KS; ++kx)
+#pragma unroll
+        for (int c = 0; c < NCB; ++c) {
+          const int t = kx * NCB + c;
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2], bv[kx][c][0], acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], bv[kx][c][1], acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[kx][c][2], acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], bv[kx][c][0], acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[kx][c][1], acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[kx][c][0], acc[t], 0, 0, 0);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+  };
+
+  {   // one register set: the next row's loads are issued right after this
+      // row's LDS stores (which consumed the registers) and land under its MFMAs
+    Regs g;
+    int row = r0 + w;
+    if (row < r1) load(g, row);
+    for (; row < r1; row += 4) {
+      store(g, row);
+      load(g, row + 4);             // rows past r1 read nothing (live = false)
+      __builtin_amdgcn_sched_barrier(0);
+      compute();
+    }
+  }
+
+  // ---- sum the four waves' tiles in fixed order, store the group slab ----
+  float* red = reinterpret_cast<float*>(smem);        // [4 waves][16 r][64 lanes]
+  float* slab = a.part + (size_t)g * COUT * a.NP + (size_t)cb * 32 * a.NP;
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[(w * 16 + r) * 64 + lane] = acc[t][r];
+    __syncthreads();
+    const int nbase = (ky * KS + t / NCB) * CIN + (t % NCB) * 32;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = w + 4 * j;                       // element (r, lane) of the tile
+      const int e = r * 64 + lane;
+      const float v = (red[e] + red[1024 + e]) + (red[2048 + e] + red[3072 + e]);
+      const int co = (r & 3) + 8 * (r >> 2) + 4 * h;
+      slab[(size_t)co * a.NP + nbase + l31] = v;
+    }
+  }
+  if (ky == 0) {   // bias column n = KC: lanes with equal lane & 3 share 8 channels
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[(w * 64 + lane) * 8 + j] = bsum[j];
+    __syncthreads();
+    if (threadIdx.x < 32) {
+      const int co = threadIdx.x, c8 = co >> 3, j = co & 7;
+      float v = 0.f;
+      for (int ww = 0; ww < 4; ++ww)
+        for (int l = c8; l < 64; l += 4) v += red[(ww * 64 + l) * 8 + j];
+      slab[(size_t)co * a.NP + KC] = v;
+    }
+  }
+}
+
+// two waves per SIMD (<= 256 registers): the other wave's MFMAs cover each
+// wave's row staging and LDS round trips
+template <int CIN, int COUT, int KS, int PAD, int WMAX>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void wgrads_kernel(
+    const WgradSArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char sm_wgs[];
+  wgrads_body<CIN, COUT, KS, PAD, WMAX>(a, sm_wgs, blockIdx.x);
+}
+
+template <int CIN, int PAD>
+inline size_t wgrads_smem_bytes(int W) {
+  const size_t f = (size_t)4 * WgradSGeom<CIN, PAD>::region(W) * 2;
+  return f > 4 * 16 * 64 * 4 + 0 ? f : 4 * 16 * 64 * 4;   // >= the 4-wave reduction image
+}
+
+template <int CIN, int COUT, int KS, int PAD, int WMAX>
+inline hipError_t launch_wgrads_w(const WgradSArgs& a, hipStream_t st) {
+  const size_t shm = wgrads_smem_bytes<CIN, PAD>(a.W);
+  if (shm > 160 * 1024) return hipErrorInvalidValue;
+  auto kern = wgrads_kernel<CIN, COUT, KS, PAD, WMAX>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int g8 = (a.G + 7) / 8 * 8;
+  hipLaunchKernelGGL(kern, dim3(g8 * (COUT / 32) * KS), dim3(256), shm, st, a);
+  return hipGetLastError();
+}
+
+// the staging registers are sized for the widest row the instance takes
+template <int CIN, int COUT, int KS, int PAD>
+inline hipError_t launch_wgrads(const WgradSArgs& a, hipStream_t st) {
+  if (a.W <= 16) return launch_wgrads_w<CIN, COUT, KS, PAD, 16>(a, st);
+  if (a.W <= 32) return launch_wgrads_w<CIN, COUT, KS, PAD, 32>(a, st);
+  if (a.W <= 64) return launch_wgrads_w<CIN, COUT, KS, PAD, 64>(a, st);
+  return hipErrorInvalidValue;   // frames > 128 (conv2) / 256 (conv3): not supported
+}
+
+}  // namespace ddq
+
+namespace ddq {
+
+// ---------------------------------------------------------------------------
+// conv1 weight gradient on the bf16 matrix cores.  The input is the replay
+// frames (exact in bf16: ONE plane), so a (tile, k-step) needs three MFMAs
+// (dconv planes x frame).  One workgroup = one image band of R rows, 4 waves;
+// the band's input halo (R+6 rows, single bf16 plane, pixel stride 4: a row
+// read at offset 4x + n is input pixel x + kx - 3, channel ci for
+// n = 4 kx + ci, so the B operand of tap row ky is a plain transposed read
+// of the halo row y + ky, columns n = 0..31) is staged once; every wave
+// streams its own dconv rows (3 planes, expanded from the pooled split
+// gradient through pool1's routing bytes) and accumulates all 7 tap rows.
+// Output: one fp32 slab per band, [band][co][NP], n = ky*28 + kx*4 + ci
+// (columns 28..31 of a tap row are dropped), bias at n = 196.
+// ---------------------------------------------------------------------------
+struct Wgrad1SArgs {
+  int B, H, W, R;              // conv1 grid (H = W = S), band height
+  int NP;                      // slab pitch (>= 197)
+  const __bf16* dpool;         // split pooled gradient (B,H/2,W/2,32), plane stride d_elems
+  int64_t d_elems;
+  const uint8_t* droute;       // pool1's NHWC routing bytes
+  const float* in;             // fp32 NHWC (B,H,W,4) frames (exact in bf16)
+  float* part;                 // [B * H / R][32][NP]
+};
+
+template <int WMAX>
+struct Wgrad1SGeom {
+  static constexpr int PSD = 32;                           // dconv pixel stride (64 B)
+  static __host__ __device__ int in_row(int W) { return 4 * (W + 6) + 64; }   // + read tail
+  static __host__ __device__ int d_plane(int W) { return ((W + 15) & ~15) * PSD; }
+  // the halo patch + four waves' dconv rows; at least the 16 KB image of the
+  // final cross-wave sums
+  static __host__ __device__ size_t bytes(int W, int R) {
+    const size_t a = ((size_t)(R + 6) * in_row(W) + 4 * 3 * d_plane(W)) * 2;
+    return a > (size_t)4 * 16 * 64 * 4 ? a : (size_t)4 * 16 * 64 * 4;
+  }
+};
+
+template <int WMAX>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void wgrad1s_kernel(
+    const Wgrad1SArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char sm_w1[];
+  using Geo = Wgrad1SGeom<WMAX>;
+  const int W = a.W, H = a.H, R = a.R;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int l31 = lane & 31, h = lane >> 5;
+  const int irow = Geo::in_row(W), dpl = Geo::d_plane(W);
+  __bf16* patch = reinterpret_cast<__bf16*>(sm_w1);                 // [R+6][irow]
+  __bf16* rd = patch + (R + 6) * irow + w * 3 * dpl;                // this wave's [3][W16][32]
+  const int bands = H / R;
+  const int band = blockIdx.x;
+  const int b = band / bands, y0 = (band % bands) * R;
+
+  // ---- input halo: fp32 -> bf16 (exact), zero outside the image ----
+  for (int f = threadIdx.x; f < (R + 6) * (irow / 4); f += 256) {
+    const int py = f / (irow / 4), px = f % (irow / 4);
+    const int gy = y0 - 3 + py, gx = px - 3;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if ((unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
+      v = *reinterpret_cast<const float4*>(a.in + (((size_t)b * H + gy) * W + gx) * 4);
+    __bf16 q[4] = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+    *reinterpret_cast<uint2*>(patch + py * irow + 4 * px) = *reinterpret_cast<uint2*>(q);
+  }
+  // dconv tail pixels (W..W16) stay zero
+  for (int i = lane; i < 3 * (((W + 15) & ~15) - W) * 4; i += 64) {
+    const int per = (((W + 15) & ~15) - W) * 4;
+    const int p = i / per, r = i - p * per;
+    reinterpret_cast<u32x4*>(rd + p * dpl + W * Geo::PSD)[r] = u32x4{0u, 0u, 0u, 0u};
+  }
+
+  f32x16 acc[7];
+#pragma unroll
+  for (int t = 0; t < 7; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+
+  // pooled dconv row chunks: lane keeps chunk dc8 (8 of the 32 channels) and
+  // walks pooled pixels dpx, dpx + 16, ...
+  constexpr int NPD = (WMAX / 2 + 15) / 16;
+  const int dc8 = lane & 3, dpx = lane >> 2;
+  struct Regs {
+    u32x4 d[3][NPD];
+    u32x2 m[NPD];
+  };
+  auto load = [&](Regs& G, int r) {
+    const bool live = r < R;
+    const int y = y0 + r;
+    const size_t o0 = (((size_t)b * (H >> 1) + (y >> 1)) * (W >> 1) + dpx) * 32 + 8 * dc8;
+#pragma unroll
+    for (int u = 0; u < NPD; ++u) {
+      const bool ok = live && dpx + 16 * u < (W >> 1);
+      const size_t o = o0 + (size_t)u * 16 * 32;
+      G.m[u] = u32x2{0x04040404u, 0x04040404u};
+      if (ok) G.m[u] = *reinterpret_cast<const u32x2*>(a.droute + o);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        G.d[p][u] = u32x4{0u, 0u, 0u, 0u};
+        if (ok) G.d[p][u] = *reinterpret_cast<const u32x4*>(a.dpool + p * a.d_elems + o);
+      }
+    }
+  };
+  auto store = [&](const Regs& G, int r) {
+    const uint32_t qy = ((y0 + r) & 1) << 1;
+#pragma unroll
+    for (int u = 0; u < NPD; ++u) {
+      const int px = dpx + 16 * u;
+      if (px >= (W >> 1)) continue;
+#pragma unroll
+      for (int dx = 0; dx < 2; ++dx) {
+        const uint32_t qd = qy | dx;
+        uint32_t keep[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t mw = G.m[u][e >> 1];
+          const uint32_t ra = (mw >> (16 * (e & 1))) & 0xff;
+          const uint32_t rb = (mw >> (16 * (e & 1) + 8)) & 0xff;
+          keep[e] = (ra == qd ? 0xffffu : 0u) | (rb == qd ? 0xffff0000u : 0u);
+        }
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          u32x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = G.d[p][u][e] & keep[e];
+          *reinterpret_cast<u32x4*>(rd + p * dpl + (2 * px + dx) * Geo::PSD + 8 * dc8) = o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            bsum[2 * e] += __builtin_bit_cast(float, o[e] << 16);
+            bsum[2 * e + 1] += __builtin_bit_cast(float, o[e] & 0xffff0000u);
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  // transposed-read lane offsets (as wgrads_body)
+  const int gq = lane >> 4, iq = (lane & 15) >> 2, ip = lane & 3;
+  const int pix0 = 8 * (gq >> 1) + iq;
+  const int chn = 16 * (gq & 1) + 4 * ip;
+  __syncthreads();   // the halo patch
+  Regs g;
+  if (w < R) load(g, w);
+  for (int r = w; r < R; r += 4) {
+    store(g, r);
+    load(g, r + 4);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < WMAX / 16; ++s) {
+      if (16 * s >= W) break;
+      // B fragments one tap row ahead of their three MFMAs (all seven live
+      // at once would spill at W = 84)
+      bf16x8 av[3], bv[2];
+      const __bf16* pb = patch + r * irow + 4 * (16 * s + pix0) + chn;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const __bf16* pa = rd + p * dpl + (16 * s + pix0) * Geo::PSD + chn;
+        av[p] = tr_pair(pa, pa + 4 * Geo::PSD);
+      }
+      bv[0] = tr_pair(pb, pb + 16);
+#pragma unroll
+      for (int ky = 0; ky < 7; ++ky) {
+        if (ky < 6) bv[(ky + 1) & 1] = tr_pair(pb + (ky + 1) * irow, pb + (ky + 1) * irow + 16);
+        acc[ky] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2], bv[ky & 1], acc[ky], 0, 0, 0);
+        acc[ky] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], bv[ky & 1], acc[ky], 0, 0, 0);
+        acc[ky] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[ky & 1], acc[ky], 0, 0, 0);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  // ---- the four waves' tiles in fixed order -> the band's slab ----
+  float* red = reinterpret_cast<float*>(sm_w1);
+  float* slab = a.part + (size_t)band * 32 * a.NP;
+#pragma unroll
+  for (int t = 0; t < 7; ++t) {
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[(w * 16 + r) * 64 + lane] = acc[t][r];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = w + 4 * j;
+      const int e = r * 64 + lane;
+      const float v = (red[e] + red[1024 + e]) + (red[2048 + e] + red[3072 + e]);
+      const int co = (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (l31 < 28) slab[(size_t)co * a.NP + t * 28 + l31] = v;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[(w * 64 + lane) * 8 + j] = bsum[j];
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    const int co = threadIdx.x, c8 = co >> 3, j = co & 7;
+    float v = 0.f;
+    for (int ww = 0; ww < 4; ++ww)
+      for (int l = c8; l < 64; l += 4) v += red[(ww * 64 + l) * 8 + j];
+    slab[(size_t)co * a.NP + 196] = v;
+  }
+}
+
+template <int WMAX>
+inline hipError_t launch_wgrad1s_w(const Wgrad1SArgs& a, hipStream_t st) {
+  using Geo = Wgrad1SGeom<WMAX>;
+  const size_t shm = Geo::bytes(a.W, a.R);
+  if (shm > 160 * 1024) return hipErrorInvalidValue;
+  auto kern = wgrad1s_kernel<WMAX>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(a.B * (a.H / a.R)), dim3(256), shm, st, a);
+  return hipGetLastError();
+}
+
+inline hipError_t launch_wgrad1s(const Wgrad1SArgs& a, hipStream_t st) {
+  if (a.W <= 32) return launch_wgrad1s_w<32>(a, st);
+  if (a.W <= 64) return launch_wgrad1s_w<64>(a, st);
+  if (a.W <= 96) return launch_wgrad1s_w<96>(a, st);
+  if (a.W <= 128) return launch_wgrad1s_w<128>(a, st);
+  return hipErrorInvalidValue;
+}
+
+}  // namespace ddq

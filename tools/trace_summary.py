@@ -11,7 +11,12 @@ import re
 import statistics
 import sys
 
-SHORT = [("sample_gather_kernel", "sample"), ("direct_conv_kernel<4, 32, 7", "c1f"),
+SHORT = [("sample_gather_kernel", "sample"), ("split_conv1_kernel", "c1f"),
+         ("split_conv_kernel<32, 32, 64, 5", "c2f"), ("split_conv_kernel<64, 64, 64, 3", "c3f"),
+         ("wgrads_kernel<64, 64, 3", "c3w"), ("wgrads_kernel<32, 64, 5", "c2w"),
+         ("wgrad1s_kernel", "c1w"),
+         ("split_conv_kernel<64, 32, 32, 5", "c2d"), ("split_conv_kernel<64, 64, 64, 3", "c3d"),
+         ("direct_conv_kernel<4, 32, 7", "c1f"),
          ("direct_conv_kernel<32, 64, 5", "c2f"), ("direct_conv_kernel<64, 64, 3, 8, 8, 2, 2, false", "c3f"),
          ("fc4_fwd_direct", "fc4f"), ("fc4_head", "head"), ("fc4_dgrad_direct", "fc4d"),
          ("fc4_bwd_kernel", "fc4bwd"), ("FcWgrad", "fc4w"), ("wgradd_kernel<64, 64, 3", "c3w"),
