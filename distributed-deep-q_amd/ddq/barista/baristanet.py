@@ -28,7 +28,7 @@ import numpy as np
 
 from ..net import DeepQNet, GAMMA
 from .. import params as P
-from . import messaging, netutils
+from . import messaging
 
 
 def parse_architecture(architecture):
@@ -78,9 +78,9 @@ class BaristaNet:
         self.dqn.sync_target()
         self.dataset = None
         self.driver = driver
-        if logpath is None and model is not None:
-            logpath = os.path.join("logs", str(model).split("/")[-1].split(".")[0])
-        self.logger = netutils.NetLogger(self, logpath, reset=reset_log) if logpath else None
+        # logpath / reset_log: accepted for signature compatibility; the
+        # reference's per-step norm logging (netutils.NetLogger) is monitoring,
+        # out of scope here
         B, S = batch, frame
         self.state = np.zeros((B, 4, S, S), np.float32)
         self.action = np.zeros((B, 4, 1, 1), np.float32)
@@ -199,5 +199,4 @@ class BaristaNet:
         return int(a[0]) if (batch_size == 1 and n == 1) else a[:max(batch_size, n)]
 
     def log(self):
-        if self.logger is not None:
-            self.logger.write()
+        """Monitoring hook of the reference (NetLogger); a no-op here."""
