@@ -140,7 +140,7 @@ def _cpu_updates(lib, B, S, seed, threads, budget_s, max_steps):
     return steps, time.perf_counter() - t0
 
 
-def cpu_baseline(B, S, seed, budget_s=12.0, max_steps=64):
+def cpu_baseline(B, S, seed, budget_s=12.0, max_steps=2000):
     """Oracle C restatement (Caffe CPU algorithm: im2col + SGEMM, fp32, OpenMP)
     of the same update step, on all host cores and on one core (BASELINE.md
     section 2), with the reference's own published 2015 Caffe CPU time for
@@ -153,15 +153,23 @@ def cpu_baseline(B, S, seed, budget_s=12.0, max_steps=64):
     except AttributeError:
         cores = os.cpu_count()
     cores = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores))))
+    lib.ddq_cpu_step_flops.restype = ctypes.c_double
+    lib.ddq_cpu_set_isa.restype = ctypes.c_int
+    isa = lib.ddq_cpu_set_isa(512)
+    flops = lib.ddq_cpu_step_flops(B, S)
     steps, dt = _cpu_updates(lib, B, S, seed, cores, budget_s, max_steps)
     s1, d1 = _cpu_updates(lib, B, S, seed, 1, budget_s / 2, max(2, max_steps // 8))
     published = {16: 81.7, 32: 252.8, 64: 981.5, 128: 4044.0}.get(S)
     out = {"value": round(steps / dt, 4), "unit": "updates/s", "cores": cores, "kind": "port",
+           "gflops": round(flops * steps / dt / 1e9, 1),
            "sample": "%d updates (sample->gather->P/Q fwd->target->Q bwd->rmsprop apply) "
-                     "at B=%d, %dx%d, oracle/ddq_cpu.c im2col+SGEMM fp32, %d OpenMP threads, "
-                     "%.1f s" % (steps, B, S, S, cores, dt),
+                     "at B=%d, %dx%d, oracle/ddq_cpu.c: im2col + packed blocked SGEMM "
+                     "(AVX%d micro-kernel) per image for the convs, batch GEMMs for fc4, "
+                     "every layer once, fp32, %d OpenMP threads, %.1f s; %.2f GFLOP per update"
+                     % (steps, B, S, S, isa if isa == 512 else 2, cores, dt, flops / 1e9),
            "cpu_model": cpu_model(),
            "single_core": {"value": round(s1 / d1, 4), "cores": 1,
+                           "gflops": round(flops * s1 / d1 / 1e9, 1),
                            "sample": "%d updates, %.1f s" % (s1, d1)}}
     if published:
         out["reference_published"] = {

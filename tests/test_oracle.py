@@ -183,6 +183,37 @@ def test_c_oracle_matches_numpy_oracle(cpu_lib):
     assert np.max(np.abs(g - gref)) <= 1e-4 * scale
 
 
+@pytest.mark.parametrize("isa", [512, 256])
+@pytest.mark.parametrize("S,B,threads", [(24, 3, 3), (40, 5, 4)])
+def test_c_oracle_blocked_gemm_edges(cpu_lib, isa, S, B, threads):
+    """The packed SGEMM's ragged edges (HW, K and the batch not multiples of
+    the micro-tile) on both micro-kernels, against the numpy oracle."""
+    got = cpu_lib.ddq_cpu_set_isa(isa)
+    if got != isa:
+        pytest.skip("no AVX-512 on this host")
+    try:
+        pQ, pP, st, act, rw, ns, nt = random_case(S, B, seed=S)
+        blobs, grads = ref.full_pass(pQ, pP, st, act, rw, ns, nt)
+        fp = ctypes.POINTER(ctypes.c_float)
+        n = cpu_lib.ddq_cpu_num_params(S)
+        g = np.zeros(n, np.float32)
+        out = np.zeros(2 * B * 4 + 3 * B + 1, np.float32)
+        keep = [np.ascontiguousarray(a, np.float32)
+                for a in (ref.flatten(pQ), ref.flatten(pP), st, act, rw, ns, nt)]
+        rc = cpu_lib.ddq_cpu_full_pass(B, S, *[k.ctypes.data_as(fp) for k in keep],
+                                       ctypes.c_float(0.85), g.ctypes.data_as(fp),
+                                       out.ctypes.data_as(fp), threads)
+        assert rc == 0
+        for lo, key in ((0, "Q_out"), (B * 4, "P_out")):   # fp32 sums of ~4.6e3 terms
+            r = blobs[key].ravel()
+            np.testing.assert_allclose(out[lo:lo + B * 4], r, rtol=1e-5,
+                                       atol=5e-6 * np.abs(r).max())
+        gref = ref.flatten(grads)
+        assert np.max(np.abs(g - gref)) <= 1e-4 * np.abs(gref).max()
+    finally:
+        cpu_lib.ddq_cpu_set_isa(512)
+
+
 def test_c_oracle_apply_matches_restatement(cpu_lib):
     rng = np.random.default_rng(0)
     n = 1000
