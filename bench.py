@@ -17,7 +17,8 @@ replay filled with synthetic Snake frames.
 Prints ONE JSON line (rank 0).  ``value`` = minibatch updates/s summed over
 all ranks (each rank consumes its own minibatch per step: weak scaling).
 ``roofline``: dominant kernel measured with HIP events on the ctx stream
-(ddq_profile_step) vs the f32 MFMA peak.  ``cpu_baseline``: the oracle's C
+(ddq_profile_step) vs the peak of the arithmetic it runs (split-bf16 kernels:
+the bf16 dense peak over their products per f32 product).  ``cpu_baseline``: the oracle's C
 restatement of the Caffe CPU step (oracle/libddq_cpu.so) timed on the host
 cores on a bounded sample of the same workload.
 """
@@ -54,21 +55,39 @@ def kernel_flops(B, S):
 # rocprof kernel symbol (prefix) of each profiled step kernel
 KERNEL_SYMBOL = {
     "sample_gather": "ddq::sample_gather_kernel",
-    "conv1_fwd": "void ddq::direct_conv_kernel<4, 32, 7,",
-    "conv2_fwd": "void ddq::direct_conv_kernel<32, 64, 5,",
-    "conv3_fwd": "void ddq::direct_conv_kernel<64, 64, 3, 8, 8, 2, 2, false",
+    "conv1_fwd": "void ddq::split_conv1_kernel",
+    "conv2_fwd": "void ddq::split_conv_kernel<32, 32, 64, 5,",
+    "conv3_fwd": "void ddq::split_conv_kernel<64, 64, 64, 3, 8, 8, 2, 2, false",
     "fc4_fwd": "void ddq::fc4_fwd_direct_kernel",
     "head": "ddq::fc4_head_kernel",
     "fc4_dgrad": "ddq::fc4_dgrad_direct_kernel",
-    "fc4_wgrad": "void ddq::gemm_f32_kernel<ddq::GemmCfg<64, 64, 32, 2, 2, 1>, ddq::FcWgrad>",
-    "conv3_wgrad": "void ddq::wgradd_kernel<64, 64, 3, 1",
+    "fc4_wgrad": "ddq::fc4_wgrad_kernel",
+    "conv3_wgrad": "void ddq::wgrads_kernel<64, 64, 3, 1",
     "conv3_dgrad": "void ddq::direct_conv_kernel<64, 64, 3, 4, 8, 1, 2, true",
-    "conv2_wgrad": "void ddq::wgradd_kernel<32, 64, 5, 2",
-    "conv2_dgrad": "void ddq::direct_conv_kernel<64, 32, 5,",
-    "conv1_wgrad": "ddq::wgrad1_kernel",
+    "conv2_wgrad": "void ddq::wgrads_kernel<32, 64, 5, 2",
+    "conv2_dgrad": "void ddq::split_conv_kernel<64, 64, 32, 5,",
+    "conv1_wgrad": "void ddq::wgrad1s_kernel",
     "wgrad_reduce": "ddq::wgrad_reduce_kernel",
     "apply": "ddq::apply_kernel",
 }
+
+# How each MFMA kernel computes its f32-exact result (csrc/split.h, wgrads.h):
+# "split" = operands split into three bf16 planes, 6 bf16 products per f32
+# product; "split3" = one operand exact in bf16 (the frames), 3 products;
+# "f32" = v_mfma_f32_32x32x2_f32 / f32 VALU.  Its roofline peak is the bf16
+# dense peak over the products per f32 product (the f32 MFMA peak for "f32").
+KERNEL_ARITH = {
+    "conv1_fwd": "split3", "conv2_fwd": "split", "conv3_fwd": "split",
+    "conv1_wgrad": "split3", "conv2_wgrad": "split", "conv3_wgrad": "split",
+    "conv2_dgrad": "split", "conv3_dgrad": "f32", "fc4_fwd": "f32", "fc4_dgrad": "f32",
+    "fc4_wgrad": "f32",
+}
+BF16_MFMA_PEAK = 2.5e15       # MI355X_MICROARCH.md: dense bf16
+
+
+def arith_peak(kernel):
+    kind = KERNEL_ARITH.get(kernel, "f32")
+    return {"split": BF16_MFMA_PEAK / 6, "split3": BF16_MFMA_PEAK / 3}.get(kind, F32_MFMA_PEAK)
 
 
 def pmc_traffic(label, B, S):
@@ -191,7 +210,9 @@ def kernel_roofline(avg_us, B, S, P):
             continue
         if k in fl:
             tf = fl[k] / (us * 1e-6) / 1e12
-            out[k] = {"TFLOPs": round(tf, 2), "frac": round(tf * 1e12 / F32_MFMA_PEAK, 3)}
+            out[k] = {"TFLOPs": round(tf, 2), "arith": KERNEL_ARITH.get(k, "f32"),
+                      "peak": round(arith_peak(k) / 1e12, 1),
+                      "frac": round(tf * 1e12 / arith_peak(k), 3)}
         elif k == "sample_gather":
             by = 2 * B * 4 * S * S * 5 + B * 24
             out[k] = {"GBps": round(by / (us * 1e-6) / 1e9, 1),
@@ -463,8 +484,13 @@ def main():
                                                      else "+overlap")) if world > 1 else "none",
                        "pipelined": bool(args.pipeline and not args.eager)},
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3),
-                         "peak": F32_MFMA_PEAK / 1e12, "unit": "TFLOP/s",
-                         "frac": round(achieved * 1e12 / F32_MFMA_PEAK, 4),
+                         "peak": round(arith_peak(dom) / 1e12, 1), "unit": "TFLOP/s",
+                         "frac": round(achieved * 1e12 / arith_peak(dom), 4),
+                         "arith": KERNEL_ARITH.get(dom, "f32"),
+                         "peak_basis": "algorithmic f32 FLOPs; peak = bf16 dense 2.5 PF/s over "
+                                       "the bf16 products per f32 product (split: 6, split3: "
+                                       "3; f32 MFMA: 157.3)",
+                         "vs_f32_mfma_peak": round(achieved * 1e12 / F32_MFMA_PEAK, 4),
                          "traffic": pmc_traffic(dom, B, S), "traffic_unit": "bytes/launch",
                          "kernel_us": round(dom_us, 3),
                          "kernel_us_timing": "100 back-to-back launches between HIP events "

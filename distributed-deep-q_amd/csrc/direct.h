@@ -521,7 +521,7 @@ __device__ __forceinline__ void direct_conv_body(const DirectArgs& a, float* sme
           const size_t pix = ((size_t)b * a.H + y) * a.W + x;
           const float v = acc[i][j][r];
           if (a.pd_pooled) {   // one store per element: lanes along n, 128-B runs
-            a.pdconv[pix * N + n] = v;
+            if (a.pdconv) a.pdconv[pix * N + n] = v;   // null: split copy only
             if (a.pd_split) store_split(a.pd_split, a.pd_split_elems, pix * N + n, v);
             continue;
           }

@@ -47,7 +47,11 @@ ParamLayout make_layout(int S) {
   L.wks_off[0] = 0;
   L.wks_off[1] = kConv1WPlane;
   L.wks_off[2] = L.wks_off[1] + wn[1];
-  L.wks_total = L.wks_off[2] + wn[2];
+  // split data-gradient weights of conv2/3: transposed + flipped [ci][tap'][co]
+  L.wkst_off[0] = -1;
+  L.wkst_off[1] = L.wks_off[2] + wn[2];
+  L.wkst_off[2] = -1;
+  L.wks_total = L.wkst_off[1] + wn[1];
   return L;
 }
 
@@ -498,7 +502,7 @@ hipError_t launch_u8_to_nhwc(const uint8_t* src, int n, int S, float* dst, hipSt
 // ---------------------------------------------------------------------------
 // Caffe (co,ci,ky,kx) -> kernel layout (co,ky,kx,ci) for the three convs
 // ---------------------------------------------------------------------------
-struct ConvDims { int64_t w_off, wk_off, wks_off; int cout, cin, ks; };
+struct ConvDims { int64_t w_off, wk_off, wks_off, wkst_off; int cout, cin, ks; };
 
 // e: Caffe-order element (co, ci, ky, kx) of the layer's weight (< 2^31);
 // returns its offset in the kernel layout Wk[co][tap][ci].
@@ -522,12 +526,23 @@ __device__ __forceinline__ int wks_local(const ConvDims& d, int e) {
   return (co * kk + tap) * d.cin + ci;
 }
 
+// e as in wk_local; its offset in the split data-gradient layout of conv2/3:
+// the dgrad is a conv over the output gradient with Wt[ci][tap'][co] =
+// W[co][ci][KS-1-ky][KS-1-kx], tap' = ky' KS + kx' (same padding)
+__device__ __forceinline__ int wkst_local(const ConvDims& d, int e) {
+  const int kk = d.ks * d.ks, per = d.cin * kk;
+  const int co = e / per, rem = e - co * per;
+  const int ci = rem / kk, tap = rem - ci * kk;
+  return (ci * kk + (kk - 1 - tap)) * d.cout + co;
+}
+
 // conv weight element k (of layer d) now holds v: refresh the fp32 kernel
-// layout and the split forward layout
+// layout and the split forward (and data-gradient) layouts
 __device__ __forceinline__ void put_conv_weight(const ConvDims& d, int e, float v, float* wk,
                                                 __bf16* wks, int64_t wks_plane) {
   wk[d.wk_off + wk_local(d, e)] = v;
   store_split(wks, wks_plane, d.wks_off + wks_local(d, e), v);
+  if (d.wkst_off >= 0) store_split(wks, wks_plane, d.wkst_off + wkst_local(d, e), v);
 }
 
 __global__ void relayout_kernel(const float* __restrict__ theta, float* __restrict__ wk,
@@ -542,7 +557,8 @@ __global__ void relayout_kernel(const float* __restrict__ theta, float* __restri
 
 static void conv_dims(const ParamLayout& L, ConvDims* d) {
   const int cout[3] = {32, 64, 64}, cin[3] = {4, 32, 64}, ks[3] = {7, 5, 3};
-  for (int i = 0; i < 3; ++i) d[i] = {L.w[i], L.wk_off[i], L.wks_off[i], cout[i], cin[i], ks[i]};
+  for (int i = 0; i < 3; ++i)
+    d[i] = {L.w[i], L.wk_off[i], L.wks_off[i], L.wkst_off[i], cout[i], cin[i], ks[i]};
 }
 
 hipError_t launch_relayout(const NetBuffers& nb, int z, hipStream_t s) {
@@ -834,6 +850,9 @@ struct ApplyArgs {
 
 __device__ __forceinline__ float apply_one(const ApplyArgs& a, bool first, int64_t i, float th,
                                            float g, float& st) {
+  // no FMA contraction: every call site (the apply launch, the fused fc4
+  // apply, the shard apply) rounds the rules identically
+#pragma clang fp contract(off)
   switch (a.rule) {
     case 0:   // sgd: theta - lr*g  (server.py:81-83, apply_descent :66-68)
       return th - a.lr * g;
@@ -912,6 +931,89 @@ __device__ __forceinline__ void apply_elems(const ApplyTail& t, const ApplyArgs&
   }
 }
 
+// fc4 weight gradient, one (4 R) x 256 tile of dW4[o][k] = sum_n dh4[n][o] x[n][k]
+// per 256-thread block: wave w owns rows o0 = 4 R ot + R w .. +R (wave-uniform,
+// so dh4 is read through scalar loads), lane owns columns k .. k+3.  Every
+// element's sum runs n = 0 .. B-1 in order with fmaf, whatever R, so every
+// caller (the gradient launches and the fused apply) produces the same bits.
+constexpr int kFc4WTileK = 256;
+template <int R>
+__host__ __device__ inline int fc4_wgrad_blocks(int K) {
+  return (512 / (4 * R)) * ((K + kFc4WTileK - 1) / kFc4WTileK);
+}
+
+template <int R>
+__device__ __forceinline__ bool fc4_wgrad_coords(int K, int blk, int& o0, int& k) {
+  const int nkt = (K + kFc4WTileK - 1) / kFc4WTileK;
+  const int ot = blk / nkt, kt = blk - ot * nkt;
+  o0 = ot * 4 * R + R * __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  k = kt * kFc4WTileK + 4 * (threadIdx.x & 63);
+  return k < K;
+}
+
+template <int R>
+__device__ __forceinline__ void fc4_wgrad_sum(int B, int K, const float* __restrict__ dh4,
+                                              const float* __restrict__ x, int o0, int k,
+                                              float (&g)[R][4]) {
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) g[r][e] = 0.f;
+  const float* xp = x + k;
+  const float* dp = dh4 + o0;
+#pragma unroll 4
+  for (int n = 0; n < B; ++n) {
+    const float4 xv = *reinterpret_cast<const float4*>(xp + (size_t)n * K);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const float d = dp[n * 512 + r];
+      g[r][0] = fmaf(d, xv.x, g[r][0]);
+      g[r][1] = fmaf(d, xv.y, g[r][1]);
+      g[r][2] = fmaf(d, xv.z, g[r][2]);
+      g[r][3] = fmaf(d, xv.w, g[r][3]);
+    }
+  }
+}
+
+// Fused fc4-weight apply block (R = 4 rows per wave: 512 blocks at 64x64): the
+// tile's theta / optimizer-state loads are issued first so they land under
+// the gradient sum; the gradient is written to grad as well (the step's
+// gradient stays observable), then the update rule runs (and the P copy on a
+// sync step).
+constexpr int kFc4ApplyR = 4;
+__device__ __forceinline__ void fc4_apply_tile(const ApplyTail& t, const ApplyArgs& a, int B,
+                                               int K, const float* dh4, const float* x, int blk) {
+  constexpr int R = kFc4ApplyR;
+  int o0, k;
+  if (!fc4_wgrad_coords<R>(K, blk, o0, k)) return;
+  const bool first = t.opt_init[2] != 0;
+  const bool sync = t.opt_init[3] != 0;
+  const int64_t i0 = a.lo + (int64_t)o0 * K + k;
+  float4 t4[R], s4[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    t4[r] = *reinterpret_cast<const float4*>(t.theta + i0 + (int64_t)r * K);
+    s4[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.rule != 0 && !first) s4[r] = *reinterpret_cast<const float4*>(t.opt + i0 + (int64_t)r * K);
+  }
+  float g[R][4];
+  fc4_wgrad_sum<R>(B, K, dh4, x, o0, k, g);
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t i = i0 + (int64_t)r * K;
+    *reinterpret_cast<float4*>(const_cast<float*>(t.grad) + i) =
+        make_float4(g[r][0], g[r][1], g[r][2], g[r][3]);
+    float th[4] = {t4[r].x, t4[r].y, t4[r].z, t4[r].w};
+    float st[4] = {s4[r].x, s4[r].y, s4[r].z, s4[r].w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) th[e] = apply_one(a, first, i + e, th[e], g[r][e], st[e]);
+    const float4 o4 = make_float4(th[0], th[1], th[2], th[3]);
+    *reinterpret_cast<float4*>(t.theta + i) = o4;
+    if (a.rule != 0) *reinterpret_cast<float4*>(t.opt + i) = make_float4(st[0], st[1], st[2], st[3]);
+    if (sync) *reinterpret_cast<float4*>(t.thetaP + i) = o4;
+  }
+}
+
 // Prefetch block g: every block draws the (same) sorted index set of the next
 // step with the already-advanced counter, then gathers its slice.
 __device__ __forceinline__ void prefetch_body(const Prefetch& pf, int g) {
@@ -980,15 +1082,16 @@ __device__ __forceinline__ void wred_unit(const float* __restrict__ part, float*
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(
     const float* __restrict__ part, float* __restrict__ grad, WredDims d0, WredDims d1,
     WredDims d2, int nunits, int nub, int64_t* iter, int32_t* opt_init, int book_period,
-    ReplayMeta* bump, int book_inc, HeadSums hs, ApplyTail fat, ApplyArgs faa, Prefetch pf) {
+    ReplayMeta* bump, int book_inc, HeadSums hs, ApplyTail fat, ApplyArgs faa, Prefetch pf,
+    const float* __restrict__ fc4_x, int fc4_k) {
   __shared__ float red[4][64];
   if ((int)blockIdx.x < pf.ng) {   // fused apply: the next step's draw + gather first
     prefetch_body(pf, blockIdx.x);
     return;
   }
   const int bid = blockIdx.x - pf.ng;
-  if (fat.blk0 > 0 && bid >= fat.blk0) {   // fused fc4-weight apply blocks
-    apply_elems(fat, faa, bid - fat.blk0);
+  if (fat.blk0 > 0 && bid >= fat.blk0) {   // fused fc4-weight gradient + apply blocks
+    fc4_apply_tile(fat, faa, hs.B, fc4_k, hs.dh4, fc4_x, bid - fat.blk0);
     return;
   }
   if (opt_init && bid == 0 && threadIdx.x == 0)
@@ -1273,17 +1376,38 @@ static WgradDArgs wgradd_args(const P& p, int B, int G) {
 // fc4 data gradient (blocks [0, nd): fc4_dgrad_body, 512 threads) beside the
 // fc4 weight gradient (blocks [nd, ...): the GEMM engine's FcWgrad, 256
 // threads; the other 4 waves end at once, which s_barrier does not wait for)
-__global__ __launch_bounds__(512) void fc4_bwd_kernel(const Fc4DgradArgs d, const FcWgrad w, int nd,
-                                                      int ndx) {
-  constexpr int kLds = 8 * 1024 > CfgFcW::kSmem ? 8 * 1024 : CfgFcW::kSmem;
-  __shared__ __attribute__((aligned(16))) float smem[kLds];
+// (threads 256..511 of a gradient block end at once, which s_barrier does
+// not wait for)
+__global__ __launch_bounds__(512) void fc4_bwd_kernel(const Fc4DgradArgs d, const float* x,
+                                                      float* gw4, int nd, int ndx) {
+  __shared__ __attribute__((aligned(16))) float smem[8 * 1024];
   const int bid = blockIdx.x;
   if (bid < nd) {
     fc4_dgrad_body(d, reinterpret_cast<float(*)[1024]>(smem), bid % ndx, bid / ndx);
     return;
   }
-  if (threadIdx.x >= CfgFcW::kThreads) return;
-  gemm_f32_body<CfgFcW, FcWgrad>(w, smem, bid - nd, 0, 0);
+  if (threadIdx.x >= 256) return;
+  float g[8][4];
+  int o0, k;
+  if (!fc4_wgrad_coords<8>(d.K, bid - nd, o0, k)) return;
+  fc4_wgrad_sum<8>(d.B, d.K, d.dh4, x, o0, k, g);
+#pragma unroll
+  for (int r = 0; r < 8; ++r)
+    *reinterpret_cast<float4*>(gw4 + (size_t)(o0 + r) * d.K + k) =
+        make_float4(g[r][0], g[r][1], g[r][2], g[r][3]);
+}
+
+// the fc4 weight gradient alone (profiled / concurrent steps)
+__global__ __launch_bounds__(256) void fc4_wgrad_kernel(int B, int K, const float* dh4,
+                                                        const float* x, float* gw4) {
+  float g[8][4];
+  int o0, k;
+  if (!fc4_wgrad_coords<8>(K, blockIdx.x, o0, k)) return;
+  fc4_wgrad_sum<8>(B, K, dh4, x, o0, k, g);
+#pragma unroll
+  for (int r = 0; r < 8; ++r)
+    *reinterpret_cast<float4*>(gw4 + (size_t)(o0 + r) * K + k) =
+        make_float4(g[r][0], g[r][1], g[r][2], g[r][3]);
 }
 
 hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
@@ -1474,12 +1598,11 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     f.pooled = nb.conv_impl == 1;
     f.dsplit = nb.conv_impl == 1 ? nb.dconv3s : nullptr;
     f.dsplit_elems = (int64_t)B * s4 * s4 * 64;
-    FcWgrad w;
-    w.M = kFc4; w.N = 64 * s4 * s4; w.K = B; w.ksplit_len = ((B + 31) / 32) * 32;
-    w.dh4 = nb.dh4; w.x = nb.pool3[0]; w.gw4 = nb.grad + L.w[3];
     const int ndx = f.K / 32, nd = ndx * ((B + 31) / 32);
-    const int nw = ((kFc4 + CfgFcW::BM - 1) / CfgFcW::BM) * ((w.N + CfgFcW::BN - 1) / CfgFcW::BN);
-    hipLaunchKernelGGL(fc4_bwd_kernel, dim3(nd + nw), dim3(512), 0, s, f, w, nd, ndx);
+    // the fused apply computes the fc4 weight gradient tile by tile itself
+    const int nw = nb.fa.on ? 0 : fc4_wgrad_blocks<8>(f.K);
+    hipLaunchKernelGGL(fc4_bwd_kernel, dim3(nd + nw), dim3(512), 0, s, f, nb.pool3[0],
+                       nb.grad + L.w[3], nd, ndx);
     CHECK_LAUNCH(hipGetLastError());
     if (fc4_done) CHECK_LAUNCH(fc4_done(fc4_done_arg));
   }
@@ -1504,11 +1627,11 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     }
   }
   if (!fc4_fused) {  // fc4 wgrad
-    FcWgrad p;
-    p.M = kFc4; p.N = 64 * s4 * s4; p.K = B; p.ksplit_len = ((B + 31) / 32) * 32;
-    p.dh4 = nb.dh4; p.x = nb.pool3[0]; p.gw4 = nb.grad + L.w[3];
+    const int K4 = 64 * s4 * s4;
     M("fc4_wgrad");
-    CHECK_LAUNCH(launch_gemm<CfgFcW>(p, 1, 1, sw));
+    hipLaunchKernelGGL(fc4_wgrad_kernel, dim3(fc4_wgrad_blocks<8>(K4)), dim3(256), 0, sw, B, K4,
+                       nb.dh4, nb.pool3[0], nb.grad + L.w[3]);
+    CHECK_LAUNCH(hipGetLastError());
     // the fc4 weight gradient (the bulk of the flat gradient) is final here:
     // the caller may start reducing it under the conv backward
     if (fc4_done) CHECK_LAUNCH(fc4_done(fc4_done_arg));
@@ -1578,10 +1701,12 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
       DirectArgs d = direct_dgrad_args(nb.dconv3, p.wk, nb.mask2, nb.dconv2, B, H, 1);
       d.in_route = nb.mask3;   // pooled dconv3, expanded while the patch is staged
       // 4x8-pixel tiles (256 workgroups instead of 128: -2.5 us) with the B
-      // operand straight from L2 (register-B, no weight ring: -2.5 us more)
-      // pool2-output gradient stored pooled (2.1 MB instead of 8.4 MB); the
-      // conv2 wgrad / dgrad expand it through mask2 while staging (the wgrad
-      // from its split copy)
+      // operand straight from L2 (register-B, no weight ring: -2.5 us more);
+      // the pool2-output gradient leaves pooled and split only (the conv2
+      // wgrad / dgrad expand it through mask2).  (The split kernel,
+      // split_conv<64,64,64,3,8,8,2,2,DGRAD> on 128 workgroups: 14.3 us
+      // against 12.9 here.)
+      d.pdconv = nullptr;
       d.pd_pooled = 1;
       d.pd_split = nb.dconv2s;
       d.pd_split_elems = (int64_t)B * H * H * 64;
@@ -1622,19 +1747,20 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     p.dconv = nb.dconv2; p.wk = nb.wk[0] + L.wk_off[1]; p.pmask = nb.mask1; p.pdconv = nb.dconv1;
     M("conv2_dgrad");
     if (nb.conv_impl == 1) {
-      // 2 tap groups: two waves per SIMD over the 1024 output blocks
-      DirectArgs d = direct_dgrad_args(nb.dconv2, p.wk, nb.mask1, nb.dconv1, B, H, 2);
-      d.in_route = nb.mask2;   // dconv2 pooled (conv3 dgrad), expanded while staged
-      // pool1-output gradient stored pooled (4.2 MB instead of the 16.8 MB
-      // un-pooled image, 3/4 zeros); conv1 wgrad expands it through mask1
-      // (from the split copy)
-      d.pd_pooled = 1;
-      d.pd_split = nb.dconv1s;
-      d.pd_split_elems = (int64_t)B * H * H * 32;
-      // (8x8 tiles -- two 74 KB workgroups per CU -- measured 39.3 us, and
-      // 8x8 register-B 42.9 us, against 36.8 us for this configuration)
-      // (two 32-pixel blocks per wave over 4 tap groups: 40.6 us)
-      CHECK_LAUNCH((launch_direct<64, 32, 5, 8, 16, 4, 1, true, false, 2>(d, 1, s)));
+      // split bf16 (split.h, DGRAD): the split pooled dpool2 (conv3 dgrad)
+      // expanded through mask2 while staged, one 64-channel chunk (the patch
+      // is staged once: 25 weight steps), 8x16-pixel tiles; the pool1-output
+      // gradient leaves split and pooled (4.2 MB per plane instead of the
+      // 16.8 MB un-pooled image) for the conv1 wgrad, which expands it through
+      // mask1.  (The fp32 direct kernel: 32.5 us; 32-channel chunks: 35.5,
+      // 16x16 tiles (128 workgroups): 31.8, this: 23.2 -- ubench.)
+      SplitArgs a{};
+      a.B = B; a.H = H; a.W = H; a.pad = 2;
+      a.in[0] = nb.dconv2s; a.in_elems = (int64_t)B * (H / 2) * (H / 2) * 64;
+      a.wk[0] = nb.wks[0] + L.wkst_off[1]; a.wk_elems = L.wks_total;
+      a.in_route = nb.mask2;
+      a.pd_split = nb.dconv1s; a.pd_elems = (int64_t)B * H * H * 32;
+      CHECK_LAUNCH((launch_split_conv<64, 64, 32, 5, 8, 16, 4, 1, true>(a, 1, s)));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgD2>(p, 1, 1, s));
     }
@@ -1687,7 +1813,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     if (nb.fa.on) {   // fc4 weights [w4, b4): its gradient is final since fc4_bwd
       faa.lo = L.w[3];
       faa.hi = L.b[3];
-      nfa = (int)(((L.b[3] - L.w[3]) / 4 + 255) / 256);
+      nfa = fc4_wgrad_blocks<kFc4ApplyR>(64 * s4 * s4);
       fat.blk0 = nub + kFc4 / 64;
     }
     Prefetch pf{};
@@ -1695,7 +1821,8 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(pf.ng + nub + kFc4 / 64 + nfa), dim3(256), 0, s,
                        nb.wpart, nb.grad, d[0], d[1], d[2], blk, nub, nb.iter,
                        book ? nb.opt_init : nullptr, book_period,
-                       book && !nb.fa.on ? bump : nullptr, nb.book_inc, hs, fat, faa, pf);
+                       book && !nb.fa.on ? bump : nullptr, nb.book_inc, hs, fat, faa, pf,
+                       nb.pool3[0], 64 * s4 * s4);
     CHECK_LAUNCH(hipGetLastError());
   }
   return hipSuccess;

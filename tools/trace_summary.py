@@ -12,10 +12,12 @@ import statistics
 import sys
 
 SHORT = [("sample_gather_kernel", "sample"), ("split_conv1_kernel", "c1f"),
-         ("split_conv_kernel<32, 32, 64, 5", "c2f"), ("split_conv_kernel<64, 64, 64, 3", "c3f"),
+         ("split_conv_kernel<32, 32, 64, 5", "c2f"),
+         ("split_conv_kernel<64, 64, 64, 3, 8, 8, 2, 2, false", "c3f"),
+         ("split_conv_kernel<64, 64, 64, 3, 8, 8, 2, 2, true", "c3d"),
+         ("split_conv_kernel<64, 64, 32, 5", "c2d"),
          ("wgrads_kernel<64, 64, 3", "c3w"), ("wgrads_kernel<32, 64, 5", "c2w"),
          ("wgrad1s_kernel", "c1w"),
-         ("split_conv_kernel<64, 32, 32, 5", "c2d"), ("split_conv_kernel<64, 64, 64, 3", "c3d"),
          ("direct_conv_kernel<4, 32, 7", "c1f"),
          ("direct_conv_kernel<32, 64, 5", "c2f"), ("direct_conv_kernel<64, 64, 3, 8, 8, 2, 2, false", "c3f"),
          ("fc4_fwd_direct", "fc4f"), ("fc4_head", "head"), ("fc4_dgrad_direct", "fc4d"),

@@ -249,5 +249,16 @@ int main(int argc, char** argv) {
   if (want()) run_conv1<16, 32, 4>("12 conv1 fwd 16x32 4w (TM4)", 50);
   if (want()) run_conv1<16, 16, 4>("13 conv1 fwd 16x16 4w", 50);
   if (want()) run_conv1<32, 32, 16>("14 conv1 fwd 32x32 16w", 50);
+  if (want()) run<64, 32, 32, 5, 16, 8, 4, 1>("15 conv2 dgrad-shape 16x8 4w ch32", d2, 50);
+  if (want()) run<64, 32, 32, 5, 8, 16, 4, 1>("16 conv2 dgrad-shape 8x16 4w ch32", d2, 50);
+  if (want()) run<64, 32, 32, 5, 8, 8, 2, 1>("17 conv2 dgrad-shape 8x8 2w ch32", d2, 50);
+  if (want()) run<64, 64, 32, 5, 8, 16, 4, 1>("18 conv2 dgrad-shape 8x16 4w ch64", d2, 50);
+  if (want()) run<64, 64, 32, 5, 8, 8, 2, 1>("19 conv2 dgrad-shape 8x8 2w ch64", d2, 50);
+  if (want()) run<64, 32, 32, 5, 16, 16, 2, 1>("20 conv2 dgrad-shape 16x16 2w TM4 ch32", d2, 50);
+  if (want()) run<64, 32, 32, 5, 8, 16, 2, 1>("21 conv2 dgrad-shape 8x16 2w TM2 ch32", d2, 50);
+  if (want()) run<64, 64, 32, 5, 16, 8, 4, 1>("22 conv2 dgrad-shape 16x8 4w ch64", d2, 50);
+  if (want()) run<64, 64, 64, 3, 8, 16, 4, 2>("23 conv3 dgrad-shape 8x16 8w ch64", d3, 50);
+  if (want()) run<64, 64, 64, 3, 8, 8, 2, 1>("24 conv3 dgrad-shape 8x8 2w TN2", d3, 50);
+  if (want()) run<64, 64, 64, 3, 4, 16, 2, 2>("25 conv3 dgrad-shape 4x16 4w", d3, 50);
   return 0;
 }
