@@ -363,7 +363,8 @@ def main():
     ap.add_argument("--sweep", action="store_true",
                     help="C3: also run the batch-256 frame-size sweep 16..128 (slow)")
     ap.add_argument("--eager", action="store_true", help="no hipGraph (debug)")
-    ap.add_argument("--exchange", default="allreduce", choices=["allreduce", "sharded", "server"],
+    ap.add_argument("--exchange", default="allreduce",
+                    choices=["allreduce", "sharded", "server", "async"],
                     help="N>1 gradient exchange (include/ddq_hip.h enum ddq_exchange)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="allreduce: do not reduce the fc4 bucket under the conv backward")
@@ -447,8 +448,10 @@ def main():
 
     # per-kernel device times (HIP events on the ctx stream), averaged
     prof = {}
+    pcfg = cfg if args.exchange != "async" or world == 1 else \
+        net.step_cfg(args.rule, lr=1e-4, target_period=10, exchange="none", seed=1234)
     for _ in range(args.profile_steps):
-        for name, us in net.profile_step(cfg):
+        for name, us in net.profile_step(pcfg):
             prof.setdefault(name, []).append(us)
     avg = {k: float(np.median(v)) for k, v in prof.items()}
     flops = kernel_flops(B, S)

@@ -62,6 +62,11 @@ struct ddq_ctx {
   int64_t shard_len = 0;           // parameters owned per rank (multiple of 64)
   float* gsl = nullptr;            // [W][shard_len] received gradient slices
   float* gstage = nullptr;         // [W][P] in-process all-reduce staging
+  // async exchange: the central model's shard this rank owns (Q, and P as of
+  // the last special-update pull), both at full-vector offsets
+  float* own = nullptr;
+  float* pown = nullptr;
+  int64_t async_base = 0;          // iteration at the first async step (everyone pulled)
   std::string comm_err;
   // graph
   hipGraph_t graph = nullptr;
@@ -961,7 +966,13 @@ static bool has_exchange(const ddq_ctx* c, const ddq_step_cfg* cfg) {
 }
 // param-server iterations one step consumes (server.py:200 INCR per gradient)
 static int step_inc(const ddq_ctx* c, const ddq_step_cfg* cfg) {
-  return (has_exchange(c, cfg) && cfg->exchange == DDQ_EXCHANGE_SERVER) ? c->nranks : 1;
+  return (has_exchange(c, cfg) &&
+          (cfg->exchange == DDQ_EXCHANGE_SERVER || cfg->exchange == DDQ_EXCHANGE_ASYNC))
+             ? c->nranks
+             : 1;
+}
+static bool is_async(const ddq_ctx* c, const ddq_step_cfg* cfg) {
+  return has_exchange(c, cfg) && cfg->exchange == DDQ_EXCHANGE_ASYNC;
 }
 
 // Overlapped all-reduce, part 1 (called by launch_backward right after the
@@ -1164,16 +1175,147 @@ static int check_step(ddq_ctx* c, const ddq_step_cfg* cfg) {
   if (c->nb.B >= c->valid)
     return fail(c, DDQ_EINVAL, "Can't draw sample of size %d from replay dataset of size %lld",
                 c->nb.B, (long long)c->valid);
-  if (cfg->exchange < DDQ_EXCHANGE_NONE || cfg->exchange > DDQ_EXCHANGE_SERVER)
+  if (cfg->exchange < DDQ_EXCHANGE_NONE || cfg->exchange > DDQ_EXCHANGE_ASYNC)
     return fail(c, DDQ_EINVAL, "unknown exchange %d", cfg->exchange);
   if (cfg->exchange != DDQ_EXCHANGE_NONE && c->nranks > 1 && !c->comm && !c->local)
     return fail(c, DDQ_ESTATE, "no communicator");
   return DDQ_OK;
 }
 
+// ---------------- asynchronous param server (DDQ_EXCHANGE_ASYNC) ----------------
+// Worker side of a tick: the minibatch draw + gather and the forward/backward
+// on the model this worker last pulled (no apply bookkeeping: the owners keep
+// the iteration), into nb.grad, on the ctx stream.
+static int async_compute(ddq_ctx* c, const ddq_step_cfg* cfg) {
+  const NetBuffers& nb = c->nb;
+  HIP_TRY(c, launch_sample(nb, c->r_meta, cfg->seed, c->stream));
+  HIP_TRY(c, launch_gather(nb, c->r_state, c->r_action, c->r_reward, c->r_nonterm, c->r_meta,
+                           c->stream));
+  return enqueue_fwd_bwd_x(c, nb, nullptr, nullptr, -1, nullptr, false);
+}
+
+// The special update (server.py:186-189) runs when a pull sees iteration %
+// period == 0; with one pull per tick that is every multiple of the period, so
+// a worker's P must be re-pulled iff a multiple lies in (its last pull, now].
+static bool async_pull_p(const ddq_step_cfg* cfg, int64_t last, int64_t now) {
+  return cfg->target_period > 0 && now / cfg->target_period > last / cfg->target_period;
+}
+// the iteration worker (it - 1 - base) % W last pulled at, for its pull at
+// iteration it: one round earlier, or the common start (every rank knows it)
+static int64_t async_last_pull(const ddq_ctx* c, int64_t it) {
+  return it - c->nranks > c->async_base ? it - c->nranks : c->async_base;
+}
+
+// First async step: the owner copies start from this rank's replica (after
+// the pull at iteration 0, which is a special update), and the worker's
+// first gradient is computed on it.
+static int async_begin(ddq_ctx* c, const ddq_step_cfg* cfg, hipStream_t s) {
+  const int64_t P = c->nb.L.total;
+  if (!c->own) TRY(dalloc(c, &c->own, (size_t)P + kShardPad));
+  if (!c->pown) TRY(dalloc(c, &c->pown, (size_t)P + kShardPad));
+  TRY(initial_target_sync(c, cfg));
+  HIP_TRY(c, hipMemcpyAsync(c->own, c->nb.theta[0], P * 4, hipMemcpyDeviceToDevice, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(c->pown, c->nb.theta[1], P * 4, hipMemcpyDeviceToDevice, c->stream));
+  c->async_base = c->applied;
+  TRY(async_compute(c, cfg));
+  (void)s;
+  return DDQ_OK;
+}
+
+// Owner side of a tick, on stream s: the received slice (in gsl) applied to
+// the owned shard on arrival (iteration += 1), and the central P shard
+// updated when this tick's pull is a special update.
+static int async_owner_apply(ddq_ctx* c, const ddq_step_cfg* cfg, int64_t it, hipStream_t s) {
+  const ddq_update_cfg& u = cfg->update;
+  const int64_t L = c->shard_len, off = (int64_t)c->rank * L;
+  HIP_TRY(c, launch_book(c->nb, cfg->target_period > 0 ? cfg->target_period : 0, s));
+  HIP_TRY(c, launch_apply_shard(c->nb, u.rule, u.lr, u.decay, u.eps, u.momentum, u.weight_decay,
+                                c->gsl, off, L, L, 1, s, c->own));
+  if (cfg->target_period > 0 && it % cfg->target_period == 0)
+    HIP_TRY(c, hipMemcpyAsync(c->pown + off, c->own + off, L * 4, hipMemcpyDeviceToDevice, s));
+  return DDQ_OK;
+}
+
+// Worker side after its pull (theta[0], and theta[1] when pull_p, hold the
+// central model): kernel layouts of Q (and P), then the next gradient.
+static int async_after_pull(ddq_ctx* c, const ddq_step_cfg* cfg, bool pull_p) {
+  HIP_TRY(c, launch_refresh(c->nb, c->stream, 0));
+  if (pull_p) {   // P's layouts from the pulled P weights
+    NetBuffers pb = c->nb;
+    pb.theta[0] = c->nb.theta[1]; pb.wk[0] = c->nb.wk[1]; pb.wks[0] = c->nb.wks[1];
+    HIP_TRY(c, launch_refresh(pb, c->stream, 0));
+  }
+  return async_compute(c, cfg);
+}
+
+// One round (W ticks) over RCCL: owner duties and the point-to-point pushes /
+// pulls on the comm stream, this rank's gradient on the ctx stream -- it
+// overlaps the other ranks' ticks.
+static int rccl_async_round(ddq_ctx* c, const ddq_step_cfg* cfg) {
+  const int W = c->nranks, r = c->rank;
+  const int64_t L = c->shard_len;
+  NetBuffers& nb = c->nb;
+  if (!c->cs) TRY(setup_shards(c, W));
+  if (c->steps == 0) TRY(async_begin(c, cfg, c->cs));
+  HIP_TRY(c, hipEventRecord(c->cev[0], c->stream));       // the gradient (and the copies)
+  for (int w = 0; w < W; ++w) {
+    const int64_t it = c->applied + w + 1;    // iteration after tick w's apply
+    const bool pull_p = async_pull_p(cfg, async_last_pull(c, it), it);
+    if (r == w) HIP_TRY(c, hipStreamWaitEvent(c->cs, c->cev[0], 0));
+    // push: worker w's gradient slices to their owners
+    NCCL_TRY(c, ncclGroupStart());
+    if (r == w) {
+      for (int j = 0; j < W; ++j)
+        if (j != r) NCCL_TRY(c, ncclSend(nb.grad + (size_t)j * L, L, ncclFloat, j, c->comm, c->cs));
+    } else {
+      NCCL_TRY(c, ncclRecv(c->gsl, L, ncclFloat, w, c->comm, c->cs));
+    }
+    NCCL_TRY(c, ncclGroupEnd());
+    if (r == w)
+      HIP_TRY(c, hipMemcpyAsync(c->gsl, nb.grad + (size_t)r * L, L * 4, hipMemcpyDeviceToDevice,
+                                c->cs));
+    TRY(async_owner_apply(c, cfg, it, c->cs));
+    // pull: the owners' shards to worker w
+    NCCL_TRY(c, ncclGroupStart());
+    if (r != w) {
+      NCCL_TRY(c, ncclSend(c->own + (size_t)r * L, L, ncclFloat, w, c->comm, c->cs));
+      if (pull_p) NCCL_TRY(c, ncclSend(c->pown + (size_t)r * L, L, ncclFloat, w, c->comm, c->cs));
+    } else {
+      for (int j = 0; j < W; ++j) {
+        if (j == r) continue;
+        NCCL_TRY(c, ncclRecv(nb.theta[0] + (size_t)j * L, L, ncclFloat, j, c->comm, c->cs));
+        if (pull_p)
+          NCCL_TRY(c, ncclRecv(nb.theta[1] + (size_t)j * L, L, ncclFloat, j, c->comm, c->cs));
+      }
+    }
+    NCCL_TRY(c, ncclGroupEnd());
+    if (r == w) {
+      HIP_TRY(c, hipMemcpyAsync(nb.theta[0] + (size_t)r * L, c->own + (size_t)r * L, L * 4,
+                                hipMemcpyDeviceToDevice, c->cs));
+      if (pull_p)
+        HIP_TRY(c, hipMemcpyAsync(nb.theta[1] + (size_t)r * L, c->pown + (size_t)r * L, L * 4,
+                                  hipMemcpyDeviceToDevice, c->cs));
+      HIP_TRY(c, hipEventRecord(c->cev[1], c->cs));
+      HIP_TRY(c, hipStreamWaitEvent(c->stream, c->cev[1], 0));
+      TRY(async_after_pull(c, cfg, pull_p));
+    }
+  }
+  // the step ends when this rank's owner duties are done as well
+  HIP_TRY(c, hipEventRecord(c->cev[1], c->cs));
+  HIP_TRY(c, hipStreamWaitEvent(c->stream, c->cev[1], 0));
+  return DDQ_OK;
+}
+
 int ddq_step_async(ddq_ctx* c, const ddq_step_cfg* cfg) {
   TRY(check_step(c, cfg));
   TRY(set_dev(c));
+  if (is_async(c, cfg)) {
+    if (c->local) return fail(c, DDQ_ESTATE, "in-process group members step with ddq_group_step");
+    TRY(rccl_async_round(c, cfg));
+    c->steps++;
+    c->applied += step_inc(c, cfg);
+    return DDQ_OK;
+  }
   if (c->steps == 0) TRY(initial_target_sync(c, cfg));
   TRY(enqueue_step(c, cfg, nullptr, nullptr));
   c->steps++;
@@ -1205,6 +1347,8 @@ static int capture_steps(ddq_ctx* c, const ddq_step_cfg* cfg, int k, hipGraphExe
 static constexpr int kGraphSteps = 8;
 
 static int ensure_graph(ddq_ctx* c, const ddq_step_cfg* cfg) {
+  if (is_async(c, cfg))
+    return fail(c, DDQ_EINVAL, "the async exchange runs eager steps (ddq_step_async)");
   if (!c->have_graph || memcmp(&c->gcfg, cfg, sizeof(*cfg)) != 0) {
     invalidate_graph(c);
     TRY(capture_steps(c, cfg, 1, &c->gexec));
@@ -1256,6 +1400,8 @@ static int capture_exec(ddq_ctx* c, hipGraphExec_t* out, const std::function<int
 }
 
 static int ensure_pipe(ddq_ctx* c, const ddq_step_cfg* cfg) {
+  if (is_async(c, cfg))
+    return fail(c, DDQ_EINVAL, "the async exchange runs eager steps (ddq_step_async)");
   if (!c->mb2_state) {
     const int B = c->nb.B, S = c->nb.S;
     TRY(dalloc(c, &c->mb2_state, (size_t)B * S * S * 4));
@@ -1377,6 +1523,54 @@ int ddq_group_init(ddq_ctx** ctxs, int32_t W) {
   return DDQ_OK;
 }
 
+// One async round of an in-process group: rccl_async_round's schedule with
+// the point-to-point transfers as device copies, tick by tick (members
+// synchronised between the phases of a tick: a correctness path).
+static int group_async_round(ddq_ctx** ctxs, int W, const ddq_step_cfg* cfg) {
+  auto sync_all = [&]() -> int {
+    for (int r = 0; r < W; ++r) {
+      TRY(set_dev(ctxs[r]));
+      HIP_TRY(ctxs[r], hipStreamSynchronize(ctxs[r]->stream));
+    }
+    return DDQ_OK;
+  };
+  for (int r = 0; r < W; ++r)
+    if (ctxs[r]->steps == 0) {
+      TRY(set_dev(ctxs[r]));
+      TRY(async_begin(ctxs[r], cfg, ctxs[r]->stream));
+    }
+  const int64_t L = ctxs[0]->shard_len;
+  for (int w = 0; w < W; ++w) {
+    const int64_t it = ctxs[0]->applied + w + 1;
+    const bool pull_p = async_pull_p(cfg, async_last_pull(ctxs[0], it), it);
+    TRY(sync_all());
+    for (int r = 0; r < W; ++r) {   // push + owner apply
+      ddq_ctx* c = ctxs[r];
+      TRY(set_dev(c));
+      HIP_TRY(c, hipMemcpyAsync(c->gsl, ctxs[w]->nb.grad + (size_t)r * L, L * 4,
+                                hipMemcpyDeviceToDevice, c->stream));
+      TRY(async_owner_apply(c, cfg, it, c->stream));
+    }
+    TRY(sync_all());
+    ddq_ctx* cw = ctxs[w];           // pull
+    TRY(set_dev(cw));
+    for (int r = 0; r < W; ++r) {
+      HIP_TRY(cw, hipMemcpyAsync(cw->nb.theta[0] + (size_t)r * L, ctxs[r]->own + (size_t)r * L,
+                                 L * 4, hipMemcpyDeviceToDevice, cw->stream));
+      if (pull_p)
+        HIP_TRY(cw, hipMemcpyAsync(cw->nb.theta[1] + (size_t)r * L, ctxs[r]->pown + (size_t)r * L,
+                                   L * 4, hipMemcpyDeviceToDevice, cw->stream));
+    }
+    TRY(async_after_pull(cw, cfg, pull_p));
+  }
+  TRY(sync_all());
+  for (int r = 0; r < W; ++r) {
+    ctxs[r]->steps++;
+    ctxs[r]->applied += step_inc(ctxs[r], cfg);
+  }
+  return DDQ_OK;
+}
+
 // One synchronous data-parallel step of an in-process group: the same
 // kernels and exchange semantics as RCCL ranks, with the collectives done as
 // device copies between the members' buffers, phase by phase.
@@ -1389,6 +1583,7 @@ int ddq_group_step(ddq_ctx** ctxs, int32_t W, const ddq_step_cfg* cfg) {
     TRY(check_step(c, cfg));
   }
   const int ex = cfg->exchange;
+  if (ex == DDQ_EXCHANGE_ASYNC) return group_async_round(ctxs, W, cfg);
   const ddq_update_cfg& u = cfg->update;
   const int64_t P = ctxs[0]->nb.L.total;
   std::vector<hipEvent_t> ev(W);
@@ -1516,6 +1711,7 @@ int ddq_profile_step(ddq_ctx* c, const ddq_step_cfg* cfg, char* names, float* us
                      int32_t* n) {
   TRY(check_step(c, cfg));
   if (!n) return fail(c, DDQ_EINVAL, "null n");
+  if (is_async(c, cfg)) return fail(c, DDQ_EINVAL, "profile steps take no async exchange");
   TRY(set_dev(c));
   c->marks.clear();
   c->ev_used = 0;

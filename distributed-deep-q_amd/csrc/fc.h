@@ -74,14 +74,9 @@ __global__ __launch_bounds__(256) void fc4_fwd_direct_kernel(const Fc4FwdArgs a)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
 
-  float4 wv[kFc4KLen / 32][4];
-#pragma unroll
-  for (int kb = 0; kb < kFc4KLen / 32; ++kb) {
-    const int k = k0 + kb * 32;
-    const bool kin = k < K;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) wv[kb][i] = fc_ld4(rw, kin ? wrow + (k + 4 * i) * 4 : kFcOOB);
-  }
+  // the x tile's loads first: the LDS barrier below then waits for them only,
+  // and the MFMAs of k block kb for their own W loads (W loads issued first:
+  // 6.3 -> 5.2 us in isolation, tools/ubench/fc4_ubench)
   constexpr int kC4 = kFc4KLen / 4;                  // float4 per x row
   constexpr int NX = BT * 32 * kC4 / 256;
   static_assert(NX * 256 == BT * 32 * kC4, "x tile / workgroup");
@@ -92,6 +87,14 @@ __global__ __launch_bounds__(256) void fc4_fwd_direct_kernel(const Fc4FwdArgs a)
     const int r = f / kC4, c4 = f % kC4;
     const int k = k0 + 4 * c4;                       // rows b >= B / k >= K read 0
     xv[it] = fc_ld4(rx, k < K ? (uint32_t)((bt0 + r) * K + k) * 4 : kFcOOB);
+  }
+  float4 wv[kFc4KLen / 32][4];
+#pragma unroll
+  for (int kb = 0; kb < kFc4KLen / 32; ++kb) {
+    const int k = k0 + kb * 32;
+    const bool kin = k < K;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) wv[kb][i] = fc_ld4(rw, kin ? wrow + (k + 4 * i) * 4 : kFcOOB);
   }
 #pragma unroll
   for (int it = 0; it < NX; ++it) {

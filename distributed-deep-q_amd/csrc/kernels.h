@@ -129,10 +129,16 @@ hipError_t launch_relayout(const NetBuffers& nb, int z, hipStream_t s);
 // owner apply of shard [off, off+len) with W gradient slices (stride `slice`)
 // applied in rank order; then, after the theta all-gather, launch_refresh
 // rebuilds the conv kernel layouts and performs a latched P <- Q sync.
+// theta: the parameters updated (default nb.theta[0]; the async exchange's
+// owner copy otherwise)
 hipError_t launch_apply_shard(const NetBuffers& nb, int rule, float lr, float decay, float eps,
                               float momentum, float wd, const float* gsl, int64_t off,
-                              int64_t len, int64_t slice, int W, hipStream_t s);
-hipError_t launch_refresh(const NetBuffers& nb, hipStream_t s);
+                              int64_t len, int64_t slice, int W, hipStream_t s,
+                              float* theta = nullptr);
+// force_sync >= 0: P <- Q decided by the host instead of the latched flag
+hipError_t launch_refresh(const NetBuffers& nb, hipStream_t s, int force_sync = -1);
+// one apply's bookkeeping (first-call / sync latches, iteration += 1)
+hipError_t launch_book(const NetBuffers& nb, int period, hipStream_t s);
 hipError_t launch_sum_slices(float* out, const float* in, int W, int64_t len, int64_t slice,
                              hipStream_t s);
 // Q-tower forward of n states (NHWC f32 in `in`) into scratch, argmax into out.

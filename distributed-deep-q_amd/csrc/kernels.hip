@@ -1163,14 +1163,15 @@ __global__ __launch_bounds__(256) void apply_shard_kernel(
 
 // After the theta all-gather: conv kernel layouts of Q, and P <- Q (weights
 // and kernel layouts) when the step's bookkeeping latched a target sync.
+// force >= 0: the P <- Q decision given by the host (async exchange pulls)
 __global__ __launch_bounds__(256) void refresh_kernel(const float* __restrict__ theta,
                                                       const int32_t* __restrict__ opt_init,
                                                       float* __restrict__ wk,
                                                       float* __restrict__ thetaP,
                                                       float* __restrict__ wkP, __bf16* wks,
                                                       __bf16* wksP, int64_t wks_plane,
-                                                      ApplyArgs a) {
-  const bool sync = opt_init[3] != 0;
+                                                      ApplyArgs a, int force) {
+  const bool sync = force >= 0 ? force != 0 : opt_init[3] != 0;
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i >= a.n || (!sync && i >= a.conv[2].w_off + (int64_t)a.conv[2].cout * a.conv[2].cin * 9))
     return;
@@ -1229,20 +1230,26 @@ bool fused_apply_ok(const ParamLayout& L) {
 
 hipError_t launch_apply_shard(const NetBuffers& nb, int rule, float lr, float decay, float eps,
                               float momentum, float wd, const float* gsl, int64_t off,
-                              int64_t len, int64_t slice, int W, hipStream_t s) {
+                              int64_t len, int64_t slice, int W, hipStream_t s, float* theta) {
   const ApplyArgs a = apply_args(nb, rule, lr, decay, eps, momentum, wd, 0);
   const int64_t blocks = (len / 4 + 255) / 256;
   if (blocks > 0)
-    hipLaunchKernelGGL(apply_shard_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, nb.theta[0],
-                       gsl, nb.opt, nb.opt_init, off, len, slice, W, a);
+    hipLaunchKernelGGL(apply_shard_kernel, dim3((uint32_t)blocks), dim3(256), 0, s,
+                       theta ? theta : nb.theta[0], gsl, nb.opt, nb.opt_init, off, len, slice, W,
+                       a);
   return hipGetLastError();
 }
 
-hipError_t launch_refresh(const NetBuffers& nb, hipStream_t s) {
+hipError_t launch_refresh(const NetBuffers& nb, hipStream_t s, int force_sync) {
   const ApplyArgs a = apply_args(nb, 0, 0.f, 0.f, 0.f, 0.f, 0.f, 0);
   hipLaunchKernelGGL(refresh_kernel, dim3((uint32_t)((a.n / 4 + 255) / 256)), dim3(256), 0, s,
                      nb.theta[0], nb.opt_init, nb.wk[0], nb.theta[1], nb.wk[1], nb.wks[0],
-                     nb.wks[1], nb.L.wks_total, a);
+                     nb.wks[1], nb.L.wks_total, a, force_sync);
+  return hipGetLastError();
+}
+
+hipError_t launch_book(const NetBuffers& nb, int period, hipStream_t s) {
+  hipLaunchKernelGGL(apply_book_kernel, dim3(1), dim3(1), 0, s, nb.iter, nb.opt_init, period);
   return hipGetLastError();
 }
 
@@ -1341,16 +1348,6 @@ int wgrad_splits_for(int layer, int B, int S, int* np, int impl) {
 }
 
 
-static DirectArgs direct_fwd_args(const float* const in[2], const float* const wk[2],
-                                  const float* const bias[2], float* const out[2],
-                                  uint8_t* const mask[2], int B, int H, int pad) {
-  DirectArgs d{};
-  d.B = B; d.H = H; d.W = H; d.pad = pad;
-  for (int z = 0; z < 2; ++z) {
-    d.in[z] = in[z]; d.wk[z] = wk[z]; d.bias[z] = bias[z]; d.out[z] = out[z]; d.mask[z] = mask[z];
-  }
-  return d;
-}
 
 // dgrad = forward conv of the layer's dconv with the transposed, flipped
 // kernel and padding KS-1-PAD (== PAD for the odd kernels of this net).

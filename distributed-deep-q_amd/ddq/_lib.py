@@ -49,7 +49,7 @@ class StepCfg(ctypes.Structure):
 
 
 ABI_VERSION = 3
-EXCHANGES = {"none": 0, "allreduce": 1, "sharded": 2, "server": 3}
+EXCHANGES = {"none": 0, "allreduce": 1, "sharded": 2, "server": 3, "async": 4}
 
 
 _P = ctypes.c_void_p

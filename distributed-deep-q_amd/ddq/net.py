@@ -332,7 +332,7 @@ class DeepQNet:
     # -------------------------------------------------------------------- step
     def step_cfg(self, rule="rmsprop", lr=1e-4, target_period=10, allreduce=False, seed=0,
                  exchange=None, overlap=False, **kw):
-        """exchange: "none" | "allreduce" | "sharded" | "server" (include/ddq_hip.h
+        """exchange: "none" | "allreduce" | "sharded" | "server" | "async" (include/ddq_hip.h
         enum ddq_exchange); allreduce=True is shorthand for "allreduce"."""
         if exchange is None:
             exchange = "allreduce" if allreduce else "none"

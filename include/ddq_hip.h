@@ -104,7 +104,18 @@ enum ddq_exchange {
    * applies the W gradients one by one in rank (ticket) order, exactly as
    * the server applies gradients on arrival; iteration += W per step; then
    * all-gather of theta.  Staleness within a step: 0..W-1 updates. */
-  DDQ_EXCHANGE_SERVER = 3
+  DDQ_EXCHANGE_SERVER = 3,
+  /* Asynchronous param server (server.py:181-209 with free-running workers)
+   * on a deterministic round-robin arrival schedule: rank r owns shard r of
+   * the central model (and its optimizer state); one step = one round of W
+   * ticks; at tick w worker w pushes the gradient it computed on the model
+   * it last pulled, the owners apply it on arrival (iteration += 1), worker
+   * w pulls the owners' shards (and the central P tower when a
+   * special-update pull happened since its last pull) and immediately
+   * computes its next gradient while the other ranks' ticks proceed.
+   * Staleness: W-1 updates, from the arrival order.  Eager steps only
+   * (ddq_step_async / ddq_group_step). */
+  DDQ_EXCHANGE_ASYNC = 4
 };
 
 /* One fused training step (main.py:61-103 debug_process_connection body,

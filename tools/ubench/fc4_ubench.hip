@@ -158,6 +158,118 @@ __global__ __launch_bounds__(64 * NW) void dgrad_nw(const Fc4DgradArgs a) {
   }
 }
 
+// ---- dgrad variant: VEC consecutive k per lane (float2 / float4 loads: 32*VEC*4-B
+// contiguous runs per W4 row), VEC interleaved 32-column MFMA tiles (tile q:
+// k = k0 + VEC*c + q), NW waves split n; fixed-order LDS reduction per tile ----
+template <int VEC, int NW>
+__global__ __launch_bounds__(64 * NW) void dgrad_vec(const Fc4DgradArgs a) {
+  __shared__ float red[NW][1024];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int l31 = lane & 31, h = lane >> 5;
+  const int k0 = blockIdx.x * 32 * VEC;
+  const int K = a.K;
+  constexpr int NPW = 512 / NW;          // n per wave
+  constexpr int NST = NPW / 2;           // MFMA steps (2 n each)
+  const int nb = w * NPW + h * (NPW / 2);
+  const __amdgpu_buffer_rsrc_t ra = fc_rsrc(a.dh4, (uint32_t)(a.B * 512 * 4));
+  const __amdgpu_buffer_rsrc_t rb = fc_rsrc(a.w4, (uint32_t)(512 * K * 4));
+  // A: dh4[b = l31][nb + j], j < NST (float4 chunks)
+  float4 av[NST / 4];
+#pragma unroll
+  for (int i = 0; i < NST / 4; ++i) av[i] = fc_ld4(ra, (uint32_t)(l31 * 512 + nb + 4 * i) * 4);
+  float bv[NST][VEC];
+#pragma unroll
+  for (int j = 0; j < NST; ++j) {
+    const uint32_t off = (uint32_t)((nb + j) * K + k0 + VEC * l31) * 4;
+    if (VEC == 4) {
+      const float4 q = fc_ld4(rb, off);
+      bv[j][0] = q.x; bv[j][1] = q.y; bv[j][2] = q.z; bv[j][VEC - 1] = q.w;
+    } else {
+      auto v = __builtin_amdgcn_raw_buffer_load_b64(rb, (int)off, 0, 0);
+      bv[j][0] = __builtin_bit_cast(float, (uint32_t)v[0]);
+      bv[j][1] = __builtin_bit_cast(float, (uint32_t)v[1]);
+    }
+  }
+  f32x16 acc[VEC];
+#pragma unroll
+  for (int q = 0; q < VEC; ++q)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[q][r] = 0.f;
+#pragma unroll
+  for (int j = 0; j < NST; ++j)
+#pragma unroll
+    for (int q = 0; q < VEC; ++q)
+      acc[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(av[j >> 2], j & 3), bv[j][q], acc[q], 0, 0, 0);
+#pragma unroll
+  for (int q = 0; q < VEC; ++q) {
+    if (q) __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[w][r * 64 + lane] = acc[q][r];
+    __syncthreads();
+    for (int e = threadIdx.x; e < 1024; e += 64 * NW) {
+      float v = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < NW; ++ww) v += red[ww][e];
+      const int r = e >> 6, ln = e & 63;
+      const int bb = fc_acc_row(r, ln);
+      const int kc = k0 + VEC * (ln & 31) + q;
+      a.dconv3[(size_t)bb * K + kc] = v;
+    }
+  }
+}
+
+// ---- fwd variant: x tile loads issued before the W loads (the LDS barrier then
+// waits for x only; the MFMAs of k block kb wait for its own W loads) ----
+__global__ __launch_bounds__(256) void fwd_xfirst(const Fc4FwdArgs a) {
+  constexpr int KL = kFc4KLen, XS = KL + 4;
+  __shared__ __attribute__((aligned(16))) float xs[32 * XS];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int l31 = lane & 31, h = lane >> 5;
+  const int z = blockIdx.z, split = blockIdx.y;
+  const int n0 = blockIdx.x * 128 + w * 32;
+  const int K = a.K, k0 = split * KL;
+  const __amdgpu_buffer_rsrc_t rw = fc_rsrc(z ? a.w[1] : a.w[0], (uint32_t)(512 * K * 4));
+  const __amdgpu_buffer_rsrc_t rx = fc_rsrc(z ? a.x[1] : a.x[0], (uint32_t)(a.B * K * 4));
+  const uint32_t wrow = (uint32_t)((n0 + l31) * K + h * 16) * 4;
+  constexpr int NX = 32 * KL / 4 / 256;
+  float4 xv[NX];
+#pragma unroll
+  for (int it = 0; it < NX; ++it) {
+    const int f = threadIdx.x + 256 * it;
+    const int b = f / (KL / 4), c4 = f % (KL / 4);
+    xv[it] = fc_ld4(rx, (uint32_t)(b * K + k0 + 4 * c4) * 4);
+  }
+  float4 wv[KL / 32][4];
+#pragma unroll
+  for (int kb = 0; kb < KL / 32; ++kb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) wv[kb][i] = fc_ld4(rw, wrow + (k0 + kb * 32 + 4 * i) * 4);
+#pragma unroll
+  for (int it = 0; it < NX; ++it) {
+    const int f = threadIdx.x + 256 * it;
+    const int b = f / (KL / 4), c4 = f % (KL / 4);
+    *reinterpret_cast<float4*>(xs + b * XS + 4 * c4) = xv[it];
+  }
+  __syncthreads();
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < KL / 32; ++kb) {
+    float4 xa[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      xa[i] = *reinterpret_cast<const float4*>(xs + l31 * XS + kb * 32 + h * 16 + 4 * i);
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(xa[j >> 2], j & 3), f4get(wv[kb][j >> 2], j & 3),
+                                                 acc, 0, 0, 0);
+  }
+  float* dst = a.part + ((size_t)(split * a.nz + z) * a.B) * 512 + n0 + l31;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) dst[(size_t)fc_acc_row(r, lane) * 512] = acc[r];
+}
+
 template <class F>
 float time_it(F f, int iters = 200) {
   hipEvent_t e0, e1;
@@ -231,6 +343,11 @@ int main() {
   r("dgrad 8 waves plain dx", T([&] { hipLaunchKernelGGL(dgrad_nw<8>, dim3(K / 32), dim3(512), 0, 0, db); }), dbytes);
   r("dgrad 16 waves plain dx", T([&] { hipLaunchKernelGGL(dgrad_nw<16>, dim3(K / 32), dim3(1024), 0, 0, db); }), dbytes);
   r("dgrad 4 waves plain dx", T([&] { hipLaunchKernelGGL(dgrad_nw<4>, dim3(K / 32), dim3(256), 0, 0, db); }), dbytes);
+  r("dgrad vec2 8 waves", T([&] { hipLaunchKernelGGL((dgrad_vec<2, 8>), dim3(K / 64), dim3(512), 0, 0, db); }), dbytes);
+  r("dgrad vec2 16 waves", T([&] { hipLaunchKernelGGL((dgrad_vec<2, 16>), dim3(K / 64), dim3(1024), 0, 0, db); }), dbytes);
+  r("dgrad vec4 8 waves", T([&] { hipLaunchKernelGGL((dgrad_vec<4, 8>), dim3(K / 128), dim3(512), 0, 0, db); }), dbytes);
+  r("dgrad vec4 16 waves", T([&] { hipLaunchKernelGGL((dgrad_vec<4, 16>), dim3(K / 128), dim3(1024), 0, 0, db); }), dbytes);
+  r("fwd x loads first", T([&] { hipLaunchKernelGGL(fwd_xfirst, fg, dim3(256), 0, 0, fa); }), fbytes);
   r("empty-ish (memset 4B)", T([&] { CK(hipMemsetAsync(dx, 0, 4)); }), 4);
   CK(hipDeviceSynchronize());
   return 0;
