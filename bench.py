@@ -92,9 +92,9 @@ def arith_peak(kernel):
 
 def pmc_traffic(label, B, S):
     """HBM bytes per launch of `label` from the committed PMC summary
-    (profiles/r01_pmc.json, tools/run_measure.sh: FETCH_SIZE x2 + WRITE_SIZE,
+    (profiles/r02_pmc.json, tools/gpu/run_measure.sh: FETCH_SIZE x2 + WRITE_SIZE,
     MI355X_MICROARCH.md gfx950 correction), valid for the bench default shape."""
-    path = os.path.join(ROOT, "profiles", "r01_pmc.json")
+    path = os.path.join(ROOT, "profiles", "r02_pmc.json")
     if (B, S) != (32, 64) or not os.path.exists(path):
         return None
     sym = KERNEL_SYMBOL.get(label)
@@ -337,9 +337,11 @@ def frame_sweep(B=256, frames=range(16, 129, 8), steps=60, warmup=10, rule="rmsp
         fl = net.step_flops()
         res.append({"frame": S, "updates_per_s": round(1 / dt, 2), "ms_per_step": round(dt * 1e3, 4),
                     "step_tflops": round(fl / dt / 1e12, 2),
-                    "frac": round(fl / dt / F32_MFMA_PEAK, 4)})
+                    "frac_of_f32_mfma_peak": round(fl / dt / F32_MFMA_PEAK, 4)})
         net.close()
-    return {"batch": B, "bound": "mfma", "peak_TFLOPs": F32_MFMA_PEAK / 1e12, "frames": res}
+    return {"batch": B, "config": "C3: deepq, batch 256, frame side S, rmsprop, 8-step graphs",
+            "step_tflops_basis": "algorithmic f32 FLOPs of the whole step (SURVEY 8(d))",
+            "f32_mfma_peak_TFLOPs": F32_MFMA_PEAK / 1e12, "frames": res}
 
 
 def main():
@@ -360,6 +362,7 @@ def main():
     ap.add_argument("--chunk-steps", type=int, default=24)
     ap.add_argument("--acting", action="store_true",
                     help="also time updates including acting (select_action + add_experience)")
+    ap.add_argument("--no-sweep", action="store_true", help="skip the C3 frame sweep")
     ap.add_argument("--sweep", action="store_true",
                     help="C3: also run the batch-256 frame-size sweep 16..128 (slow)")
     ap.add_argument("--eager", action="store_true", help="no hipGraph (debug)")
@@ -509,8 +512,11 @@ def main():
             out["with_acting"] = acting_rate(net, cfg, S)
         if not args.no_gather_stress and world == 1:
             out["gather_stress"] = gather_stress()
-        if args.sweep and world == 1:
-            out["frame_sweep"] = frame_sweep()
+        if not args.no_sweep and world == 1:
+            # C3 (BASELINE.json configs[2]): B = 256; the default line carries
+            # the reduced sweep 16 / 64 / 128, --sweep the reference's 16..128/8
+            out["frame_sweep"] = frame_sweep(frames=range(16, 129, 8) if args.sweep
+                                             else (16, 64, 128))
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(B, S, seed=7)
         print(json.dumps(out), flush=True)

@@ -1,13 +1,18 @@
-# rocprofv3 kernel-trace stats + PMC passes of the default bench (round profiles)
+# Round profiles of the shipped step (profiles/r02_*): rocprofv3 kernel-trace
+# stats of the graph bench, then one PMC pass per counter group (FETCH_SIZE and
+# WRITE_SIZE in passes of their own, tools/pmc_passes.txt), then the summaries.
 set -e
 mkdir -p gpurun_out
 R=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -o run -- python3 $R/bench.py --steps 200 --warmup 20 --profile-steps 5 --no-cpu-baseline > $R/gpurun_out/prof_bench.json 2> $R/gpurun_out/prof.err
-timeout -k 10 900 rocprofv3 -i $R/tools/pmc_passes.txt --output-format csv -d $R/gpurun_out/pmc -o pmc -- python3 $R/bench.py --steps 10 --warmup 2 --profile-steps 1 --no-cpu-baseline --eager > $R/gpurun_out/pmc_bench.json 2> $R/gpurun_out/pmc.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -o run -- python3 $R/bench.py --steps 200 --warmup 20 --profile-steps 5 --no-cpu-baseline --no-gather-stress --no-sweep > $R/gpurun_out/prof_bench.json 2> $R/gpurun_out/prof.err
+i=0
+while read -r line; do
+  i=$((i + 1))
+  timeout -s KILL 120 rocprofv3 --pmc ${line#pmc: } --output-format csv -d $R/gpurun_out/pmc/p$i -o pmc -- python3 $R/bench.py --steps 10 --warmup 2 --profile-steps 1 --chunks 0 --no-cpu-baseline --no-gather-stress --no-sweep > $R/gpurun_out/pmc_bench$i.json 2> $R/gpurun_out/pmc$i.err
+done < $R/tools/pmc_passes.txt
 cd $R
 python3 tools/pmc_summary.py gpurun_out/pmc > gpurun_out/pmc_summary.txt
 python3 tools/pmc_json.py gpurun_out/pmc gpurun_out/pmc.json
-t=$(find gpurun_out/prof -name '*kernel_trace.csv' | head -1)
-python3 tools/timeline.py "$t" --nsteps 1 > gpurun_out/timeline.txt
-cat gpurun_out/timeline.txt
+python3 tools/trace_summary.py gpurun_out/prof 0 > gpurun_out/trace_summary.txt
+cat gpurun_out/trace_summary.txt
