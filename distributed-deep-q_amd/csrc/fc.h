@@ -216,7 +216,7 @@ __device__ __forceinline__ void fc4_dgrad_body(const Fc4DgradArgs& a, float (*re
     a.fS4sq.divmod((uint32_t)kc, ch, p);
     if (a.pooled) {   // one store per element instead of four (three of them zeros)
       const size_t o = ((size_t)bb * a.fS4sq.d + p) * 64 + ch;
-      a.dconv3[o] = v;
+      if (a.dconv3) a.dconv3[o] = v;
       if (a.dsplit) store_split(a.dsplit, a.dsplit_elems, o, v);
       continue;
     }

@@ -47,11 +47,11 @@ ParamLayout make_layout(int S) {
   L.wks_off[0] = 0;
   L.wks_off[1] = kConv1WPlane;
   L.wks_off[2] = L.wks_off[1] + wn[1];
-  // split data-gradient weights of conv2/3: transposed + flipped [ci][tap'][co]
-  L.wkst_off[0] = -1;
-  L.wkst_off[1] = L.wks_off[2] + wn[2];
-  L.wkst_off[2] = -1;
-  L.wks_total = L.wkst_off[1] + wn[1];
+  // the conv2 data gradient's weights: Q's split conv2 weights transposed and
+  // flipped, Wt[ci][tap'][co] = W[co][ci][4-ky][4-kx] (rebuilt by the head
+  // kernel of every step from the forward layout)
+  L.wkst_off = L.wks_off[2] + wn[2];
+  L.wks_total = L.wkst_off + wn[1];
   return L;
 }
 
@@ -502,7 +502,7 @@ hipError_t launch_u8_to_nhwc(const uint8_t* src, int n, int S, float* dst, hipSt
 // ---------------------------------------------------------------------------
 // Caffe (co,ci,ky,kx) -> kernel layout (co,ky,kx,ci) for the three convs
 // ---------------------------------------------------------------------------
-struct ConvDims { int64_t w_off, wk_off, wks_off, wkst_off; int cout, cin, ks; };
+struct ConvDims { int64_t w_off, wk_off, wks_off; int cout, cin, ks; };
 
 // e: Caffe-order element (co, ci, ky, kx) of the layer's weight (< 2^31);
 // returns its offset in the kernel layout Wk[co][tap][ci].
@@ -526,23 +526,13 @@ __device__ __forceinline__ int wks_local(const ConvDims& d, int e) {
   return (co * kk + tap) * d.cin + ci;
 }
 
-// e as in wk_local; its offset in the split data-gradient layout of conv2/3:
-// the dgrad is a conv over the output gradient with Wt[ci][tap'][co] =
-// W[co][ci][KS-1-ky][KS-1-kx], tap' = ky' KS + kx' (same padding)
-__device__ __forceinline__ int wkst_local(const ConvDims& d, int e) {
-  const int kk = d.ks * d.ks, per = d.cin * kk;
-  const int co = e / per, rem = e - co * per;
-  const int ci = rem / kk, tap = rem - ci * kk;
-  return (ci * kk + (kk - 1 - tap)) * d.cout + co;
-}
-
 // conv weight element k (of layer d) now holds v: refresh the fp32 kernel
-// layout and the split forward (and data-gradient) layouts
+// layout and the split forward layout (the split data gradient reads the
+// latter transposed)
 __device__ __forceinline__ void put_conv_weight(const ConvDims& d, int e, float v, float* wk,
                                                 __bf16* wks, int64_t wks_plane) {
   wk[d.wk_off + wk_local(d, e)] = v;
   store_split(wks, wks_plane, d.wks_off + wks_local(d, e), v);
-  if (d.wkst_off >= 0) store_split(wks, wks_plane, d.wkst_off + wkst_local(d, e), v);
 }
 
 __global__ void relayout_kernel(const float* __restrict__ theta, float* __restrict__ wk,
@@ -558,7 +548,7 @@ __global__ void relayout_kernel(const float* __restrict__ theta, float* __restri
 static void conv_dims(const ParamLayout& L, ConvDims* d) {
   const int cout[3] = {32, 64, 64}, cin[3] = {4, 32, 64}, ks[3] = {7, 5, 3};
   for (int i = 0; i < 3; ++i)
-    d[i] = {L.w[i], L.wk_off[i], L.wks_off[i], L.wkst_off[i], cout[i], cin[i], ks[i]};
+    d[i] = {L.w[i], L.wk_off[i], L.wks_off[i], cout[i], cin[i], ks[i]};
 }
 
 hipError_t launch_relayout(const NetBuffers& nb, int z, hipStream_t s) {
@@ -626,6 +616,28 @@ __global__ __launch_bounds__(512) void fc4_reduce_out_kernel(
 // of the wgrad slab reduce (per-sample dQ and squared error kept in dqbuf /
 // lpart), so the head costs no launch of its own.
 // ---------------------------------------------------------------------------
+// Blocks [B, B + 25) of the head launch: conv2's split forward weights of Q
+// (wks [co][tap][ci]) transposed + flipped for the conv2 data gradient
+// (Wt[ci][24 - tap][co]), one tap per block through LDS, coalesced both ways.
+// The head is a latency-bound 32-block launch, so these blocks ride for free;
+// every step runs its head after the previous apply changed the weights and
+// before its conv2 data gradient.
+__device__ __forceinline__ void wkst_tap(const __bf16* __restrict__ wks, int64_t plane,
+                                         int64_t src_off, int64_t dst_off, int t) {
+  __shared__ uint16_t tile[3][64][34];
+  const uint16_t* src = reinterpret_cast<const uint16_t*>(wks) + src_off;
+  uint16_t* dst = reinterpret_cast<uint16_t*>(const_cast<__bf16*>(wks)) + dst_off;
+  for (int e = threadIdx.x; e < 3 * 64 * 32; e += blockDim.x) {
+    const int p = e >> 11, r = e & 2047, co = r >> 5, ci = r & 31;
+    tile[p][co][ci] = src[p * plane + (co * 25 + t) * 32 + ci];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 3 * 32 * 64; e += blockDim.x) {
+    const int p = e >> 11, r = e & 2047, ci = r >> 6, co = r & 63;
+    dst[p * plane + (ci * 25 + 24 - t) * 64 + co] = tile[p][co][ci];
+  }
+}
+
 __global__ __launch_bounds__(512) void fc4_head_kernel(
     const float* __restrict__ part, int splits, int B, float gamma,
     const float* __restrict__ thq, const float* __restrict__ thp, int64_t b4_off, int64_t w5_off,
@@ -634,10 +646,14 @@ __global__ __launch_bounds__(512) void fc4_head_kernel(
     float* __restrict__ outq, float* __restrict__ outp, float* q_sa_o, float* p_sa_o,
     float* target_o, float* __restrict__ dqbuf, float* __restrict__ lpart,
     float* __restrict__ dh4, int32_t* latch, const int64_t* iter, int period, int inc,
-    ReplayMeta* bump) {
+    ReplayMeta* bump, const __bf16* wks, int64_t wks_plane, int64_t wks2_off, int64_t wkst_off) {
   __shared__ float red[8][8];
   __shared__ float qp[8];
   const int b = blockIdx.x, n = threadIdx.x, w = n >> 6;
+  if (b >= B) {
+    wkst_tap(wks, wks_plane, wks2_off, wkst_off, b - B);
+    return;
+  }
   // fused apply: latch the step's apply flags now (the values apply_book
   // latches again in the slab reduce), so the fc4 apply blocks of that launch
   // never read them while its block 0 advances the counters
@@ -649,21 +665,36 @@ __global__ __launch_bounds__(512) void fc4_head_kernel(
   const size_t stride = (size_t)2 * B * kFc4;
   float h[2];
   float q[8];
-  // split-K partial sums of both towers: 16 independent loads per round
+  // every operand that does not depend on the partial sums is loaded first,
+  // and the partials 32 splits x 2 towers per round (one round at 64x64):
+  // the kernel is a chain of memory latencies, not of work
+  float bias4[2], w5v[2][4];
+#pragma unroll
+  for (int z = 0; z < 2; ++z) {
+    const float* th = z ? thp : thq;
+    bias4[z] = th[b4_off + n];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) w5v[z][a] = th[w5_off + a * kFc4 + n];
+  }
+  float acv[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) acv[a] = action[b * 4 + a];
+  const float ntb = nonterm[b], rwb = reward[b];
+  // split-K partial sums of both towers, summed in split order
   float acc2[2] = {0.f, 0.f};
   {
     const float* p0 = part + (size_t)b * kFc4 + n;
     const float* p1 = part + ((size_t)B + b) * kFc4 + n;
-    for (int s = 0; s < splits; s += 8) {
-      float v[2][8];
+    for (int s = 0; s < splits; s += 32) {
+      float v[2][32];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {            // clamped, unconditional loads
+      for (int u = 0; u < 32; ++u) {           // clamped, unconditional loads
         const int su = min(s + u, splits - 1);
         v[0][u] = p0[su * stride];
         v[1][u] = p1[su * stride];
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < 32; ++u) {
         const bool in = s + u < splits;
         acc2[0] += in ? v[0][u] : 0.f;
         acc2[1] += in ? v[1][u] : 0.f;
@@ -672,13 +703,11 @@ __global__ __launch_bounds__(512) void fc4_head_kernel(
   }
 #pragma unroll
   for (int z = 0; z < 2; ++z) {
-    const float acc = acc2[z];
-    const float* th = z ? thp : thq;
-    const float v = acc + th[b4_off + n];
+    const float v = acc2[z] + bias4[z];
     h[z] = v > 0.f ? v : 0.f;
     (z ? h4p : h4q)[(size_t)b * kFc4 + n] = h[z];
 #pragma unroll
-    for (int a = 0; a < 4; ++a) q[z * 4 + a] = h[z] * th[w5_off + a * kFc4 + n];
+    for (int a = 0; a < 4; ++a) q[z * 4 + a] = h[z] * w5v[z][a];
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1)
@@ -698,15 +727,15 @@ __global__ __launch_bounds__(512) void fc4_head_kernel(
     (n < 4 ? outq : outp)[b * 4 + (n & 3)] = t;
   }
   __syncthreads();
-  const float* ac = action + b * 4;
+  const float* ac = acv;
   // ELTWISE PROD, SLICE, SUM in slice order (train_val.prototxt:386-422)
   float qs = qp[0] * ac[0];
   qs += qp[1] * ac[1];
   qs += qp[2] * ac[2];
   qs += qp[3] * ac[3];
   float ps = fmaxf(fmaxf(qp[4], qp[5]), fmaxf(qp[6], qp[7]));   // SLICE + MAX
-  ps = ps * nonterm[b];                                          // P_sa_or_term
-  const float tg = gamma * ps + 1.0f * reward[b];                // SUM coeff {0.85, 1}
+  ps = ps * ntb;                                                 // P_sa_or_term
+  const float tg = gamma * ps + 1.0f * rwb;                      // SUM coeff {0.85, 1}
   const float diff = qs - tg;
   const float gsc = diff / (float)B;                             // EUCLIDEAN_LOSS diff
   float dq[4];
@@ -718,9 +747,7 @@ __global__ __launch_bounds__(512) void fc4_head_kernel(
 #pragma unroll
     for (int a = 0; a < 4; ++a) dqbuf[b * 4 + a] = dq[a];
   }
-  const float* w5 = thq + w5_off;
-  const float v = dq[0] * w5[n] + dq[1] * w5[kFc4 + n] + dq[2] * w5[2 * kFc4 + n] +
-                  dq[3] * w5[3 * kFc4 + n];
+  const float v = dq[0] * w5v[0][0] + dq[1] * w5v[0][1] + dq[2] * w5v[0][2] + dq[3] * w5v[0][3];
   dh4[(size_t)b * kFc4 + n] = h[0] > 0.f ? v : 0.f;              // ReLU backward
 }
 
@@ -795,12 +822,12 @@ __device__ void head_sums(int hb, int B, const float* __restrict__ dqbuf,
 
 hipError_t launch_head(const NetBuffers& nb, hipStream_t s, ReplayMeta* bump) {
   const ParamLayout& L = nb.L;
-  hipLaunchKernelGGL(fc4_head_kernel, dim3(nb.B), dim3(kFc4), 0, s, nb.fc4_part, nb.fc4_splits,
+  hipLaunchKernelGGL(fc4_head_kernel, dim3(nb.B + 25), dim3(kFc4), 0, s, nb.fc4_part, nb.fc4_splits,
                      nb.B, nb.gamma, nb.theta[0], nb.theta[1], L.b[3], L.w[4], L.b[4], nb.action,
                      nb.reward, nb.nonterm, nb.h4[0], nb.h4[1], nb.q_out, nb.p_out, nb.q_sa,
                      nb.p_sa, nb.target, nb.dqbuf, nb.lpart, nb.dh4,
                      nb.fa.on ? nb.opt_init : nullptr, nb.iter, nb.fa.period, nb.book_inc,
-                     nb.fa.on ? bump : nullptr);
+                     nb.fa.on ? bump : nullptr, nb.wks[0], L.wks_total, L.wks_off[1], L.wkst_off);
   return hipGetLastError();
 }
 
@@ -1745,7 +1772,8 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     M("conv2_dgrad");
     if (nb.conv_impl == 1) {
       // split bf16 (split.h, DGRAD): the split pooled dpool2 (conv3 dgrad)
-      // expanded through mask2 while staged, one 64-channel chunk (the patch
+      // expanded through mask2 while staged, the transposed split weights the
+      // head kernel rebuilt, one 64-channel chunk (the patch
       // is staged once: 25 weight steps), 8x16-pixel tiles; the pool1-output
       // gradient leaves split and pooled (4.2 MB per plane instead of the
       // 16.8 MB un-pooled image) for the conv1 wgrad, which expands it through
@@ -1754,7 +1782,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
       SplitArgs a{};
       a.B = B; a.H = H; a.W = H; a.pad = 2;
       a.in[0] = nb.dconv2s; a.in_elems = (int64_t)B * (H / 2) * (H / 2) * 64;
-      a.wk[0] = nb.wks[0] + L.wkst_off[1]; a.wk_elems = L.wks_total;
+      a.wk[0] = nb.wks[0] + L.wkst_off; a.wk_elems = L.wks_total;
       a.in_route = nb.mask2;
       a.pd_split = nb.dconv1s; a.pd_elems = (int64_t)B * H * H * 32;
       CHECK_LAUNCH((launch_split_conv<64, 64, 32, 5, 8, 16, 4, 1, true>(a, 1, s)));

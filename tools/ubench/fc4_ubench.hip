@@ -336,7 +336,18 @@ int main() {
   da.B = B; da.K = K; da.s4 = S4; da.fS4sq = FastDiv(S4 * S4); da.fS4 = FastDiv(S4);
   da.dh4 = dh4; da.w4 = w[0]; da.mask3 = mask3; da.dconv3 = dconv3;
   const double dbytes = 512.0 * K * 4 + B * K * 4 * 4;
-  r("dgrad current", T([&] { launch_fc4_dgrad_direct(da, 0); }), dbytes);
+  da.pooled = 0; da.dsplit = nullptr; da.dsplit_elems = 0;
+  r("dgrad unpooled (round 1)", T([&] { launch_fc4_dgrad_direct(da, 0); }), dbytes);
+  {
+    Fc4DgradArgs dp = da;
+    dp.pooled = 1;
+    r("dgrad pooled fp32 only", T([&] { launch_fc4_dgrad_direct(dp, 0); }), dbytes);
+    __bf16* ds;
+    CK(hipMalloc(&ds, 3 * B * K * 2));
+    dp.dsplit = ds; dp.dsplit_elems = (int64_t)B * K;
+    r("dgrad pooled fp32 + split (ship)", T([&] { launch_fc4_dgrad_direct(dp, 0); }), dbytes);
+    dp.dconv3 = nullptr;
+  }
   r("dgrad loads only", T([&] { hipLaunchKernelGGL(dgrad_loadonly, dim3(K / 32), dim3(512), 0, 0, da); }), dbytes);
   Fc4DgradArgs db = da;
   db.dconv3 = dx;
