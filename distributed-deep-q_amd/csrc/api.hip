@@ -261,7 +261,6 @@ int ddq_create(ddq_ctx** out, int device, const ddq_net_desc* desc) {
     TRY(dalloc(c, &nb.dconv3, (size_t)B * S3 * S3 * 64));
     TRY(dalloc(c, &nb.dconv2, (size_t)B * S2 * S2 * 64));
     TRY(dalloc(c, &nb.dconv1, (size_t)B * S * S * 32));
-    TRY(dalloc(c, &nb.dconv3s, (size_t)3 * B * S4 * S4 * 64));
     TRY(dalloc(c, &nb.dconv2s, (size_t)3 * B * S3 * S3 * 64));
     TRY(dalloc(c, &nb.dconv1s, (size_t)3 * B * S2 * S2 * 32));
     int64_t off = 0;

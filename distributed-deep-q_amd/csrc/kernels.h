@@ -57,7 +57,7 @@ struct NetBuffers {
   float *q_out, *p_out, *q_sa, *p_sa, *target, *loss;
   // backward scratch
   float *dh4, *dconv3, *dconv2, *dconv1;
-  __bf16 *dconv3s, *dconv2s, *dconv1s;   // split pooled dpool3 / 2 / 1 (the weight gradients)
+  __bf16 *dconv2s, *dconv1s;        // split pooled dpool2 / dpool1 (conv3 / conv2 data gradients)
   float* wpart;                     // conv wgrad slabs (3 layers, disjoint)
   int64_t wpart_off[3];
   int wsplits[3];

@@ -1620,8 +1620,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     f.B = B; f.K = 64 * s4 * s4; f.s4 = s4; f.fS4sq = FastDiv(s4 * s4); f.fS4 = FastDiv(s4);
     f.dh4 = nb.dh4; f.w4 = nb.theta[0] + L.w[3]; f.mask3 = nb.mask3; f.dconv3 = nb.dconv3;
     f.pooled = nb.conv_impl == 1;
-    f.dsplit = nb.conv_impl == 1 ? nb.dconv3s : nullptr;
-    f.dsplit_elems = (int64_t)B * s4 * s4 * 64;
+    f.dsplit = nullptr;   // conv3's weight gradient splits the fp32 dpool3 itself
     const int ndx = f.K / 32, nd = ndx * ((B + 31) / 32);
     // the fused apply computes the fc4 weight gradient tile by tile itself
     const int nw = nb.fa.on ? 0 : fc4_wgrad_blocks<8>(f.K);
@@ -1643,8 +1642,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
       f.B = B; f.K = p.N; f.s4 = s4; f.fS4sq = p.fS4sq; f.fS4 = p.fS4;
       f.dh4 = nb.dh4; f.w4 = p.w4; f.mask3 = nb.mask3; f.dconv3 = nb.dconv3;
       f.pooled = p.pooled;
-      f.dsplit = p.pooled ? nb.dconv3s : nullptr;
-      f.dsplit_elems = (int64_t)B * s4 * s4 * 64;
+      f.dsplit = nullptr;
       CHECK_LAUNCH(launch_fc4_dgrad_direct(f, s));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgFcD>(p, 1, 1, s));
@@ -1707,9 +1705,10 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
       WgradSArgs ws{};
       ws.B = B; ws.H = H; ws.W = H; ws.G = wd.G; ws.RPG = wd.RPG; ws.NP = wd.NP;
       ws.in = nb.pool2s[0]; ws.in_elems = (int64_t)B * H * H * 64;
-      ws.dpool = nb.dconv3s; ws.d_elems = (int64_t)B * (H / 2) * (H / 2) * 64;
+      // the fp32 pooled dpool3 of the fc4 data gradient, split while staged
+      ws.dpool_f32 = nb.dconv3;
       ws.droute = nb.mask3; ws.part = p.part;
-      CHECK_LAUNCH((launch_wgrads<64, 64, 3, 1>(ws, sw)));
+      CHECK_LAUNCH((launch_wgrads<64, 64, 3, 1, true>(ws, sw)));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgW3>(p, 1, ns, sw));
     }

@@ -38,6 +38,9 @@ struct WgradSArgs {
   int64_t d_elems;
   const uint8_t* droute;    // its NHWC routing bytes
   float* part;              // [G][COUT][NP]
+  const float* dpool_f32;   // DF32 instances: the pooled gradient in fp32 instead
+                            // (split while staged; conv3's, from the fc4 data
+                            // gradient, whose split stores cost 2.7 us there)
 };
 
 // LDS geometry of one wave's region (bf16 units).  Pixel strides keep the
@@ -65,7 +68,7 @@ __device__ __forceinline__ bf16x8 tr_pair(const __bf16* p0, const __bf16* p1) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int CIN, int COUT, int KS, int PAD, int WMAX>
+template <int CIN, int COUT, int KS, int PAD, int WMAX, bool DF32>
 __device__ __forceinline__ void wgrads_body(const WgradSArgs& a, char* smem, int L) {
   constexpr int NCB = CIN / 32;
   constexpr int T = KS * NCB;
@@ -127,6 +130,7 @@ __device__ __forceinline__ void wgrads_body(const WgradSArgs& a, char* smem, int
   struct Regs {
     u32x4 i[3][NPI];
     u32x4 d[3][NPD];
+    float4 f[2][NPD];    // DF32: the 8 fp32 values of the chunk
     u32x2 m[NPD];
   };
   auto load = [&](Regs& R, int row) {
@@ -150,16 +154,44 @@ __device__ __forceinline__ void wgrads_body(const WgradSArgs& a, char* smem, int
       const size_t o = o0 + (size_t)u * 16 * COUT;
       R.m[u] = u32x2{0x04040404u, 0x04040404u};
       if (ok) R.m[u] = *reinterpret_cast<const u32x2*>(a.droute + o);
+      if (DF32) {
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        R.d[p][u] = u32x4{0u, 0u, 0u, 0u};
-        if (ok) R.d[p][u] = *reinterpret_cast<const u32x4*>(a.dpool + p * a.d_elems + o);
+        for (int hh = 0; hh < 2; ++hh) {
+          R.f[hh][u] = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (ok) R.f[hh][u] = *reinterpret_cast<const float4*>(a.dpool_f32 + o + 4 * hh);
+        }
+      } else {
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          R.d[p][u] = u32x4{0u, 0u, 0u, 0u};
+          if (ok) R.d[p][u] = *reinterpret_cast<const u32x4*>(a.dpool + p * a.d_elems + o);
+        }
       }
     }
   };
-  auto store = [&](const Regs& R, int row) {
+  auto store = [&](Regs& R, int row) {
     const int y = row - (row / H) * H;
     const uint32_t qy = (y & 1) << 1;
+    if (DF32) {   // split the fp32 chunk into the three planes (split.h split3)
+#pragma unroll
+      for (int u = 0; u < NPD; ++u)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float x0 = e < 2 ? (e == 0 ? R.f[0][u].x : R.f[0][u].z)
+                                 : (e == 2 ? R.f[1][u].x : R.f[1][u].z);
+          const float x1 = e < 2 ? (e == 0 ? R.f[0][u].y : R.f[0][u].w)
+                                 : (e == 2 ? R.f[1][u].y : R.f[1][u].w);
+          __bf16 h0, m0, l0, h1, m1, l1;
+          split3(x0, h0, m0, l0);
+          split3(x1, h1, m1, l1);
+          R.d[0][u][e] = (uint32_t)__builtin_bit_cast(uint16_t, h0) |
+                         ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+          R.d[1][u][e] = (uint32_t)__builtin_bit_cast(uint16_t, m0) |
+                         ((uint32_t)__builtin_bit_cast(uint16_t, m1) << 16);
+          R.d[2][u][e] = (uint32_t)__builtin_bit_cast(uint16_t, l0) |
+                         ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+        }
+    }
 #pragma unroll
     for (int u = 0; u < NPI; ++u)
       if (ipx + u * PPP < W)
@@ -296,11 +328,11 @@ __device__ __forceinline__ void wgrads_body(const WgradSArgs& a, char* smem, int
 
 // two waves per SIMD (<= 256 registers): the other wave's MFMAs cover each
 // wave's row staging and LDS round trips
-template <int CIN, int COUT, int KS, int PAD, int WMAX>
+template <int CIN, int COUT, int KS, int PAD, int WMAX, bool DF32>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void wgrads_kernel(
     const WgradSArgs a) {
   extern __shared__ __attribute__((aligned(16))) char sm_wgs[];
-  wgrads_body<CIN, COUT, KS, PAD, WMAX>(a, sm_wgs, blockIdx.x);
+  wgrads_body<CIN, COUT, KS, PAD, WMAX, DF32>(a, sm_wgs, blockIdx.x);
 }
 
 template <int CIN, int PAD>
@@ -309,11 +341,11 @@ inline size_t wgrads_smem_bytes(int W) {
   return f > 4 * 16 * 64 * 4 + 0 ? f : 4 * 16 * 64 * 4;   // >= the 4-wave reduction image
 }
 
-template <int CIN, int COUT, int KS, int PAD, int WMAX>
+template <int CIN, int COUT, int KS, int PAD, int WMAX, bool DF32>
 inline hipError_t launch_wgrads_w(const WgradSArgs& a, hipStream_t st) {
   const size_t shm = wgrads_smem_bytes<CIN, PAD>(a.W);
   if (shm > 160 * 1024) return hipErrorInvalidValue;
-  auto kern = wgrads_kernel<CIN, COUT, KS, PAD, WMAX>;
+  auto kern = wgrads_kernel<CIN, COUT, KS, PAD, WMAX, DF32>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -327,11 +359,11 @@ inline hipError_t launch_wgrads_w(const WgradSArgs& a, hipStream_t st) {
 }
 
 // the staging registers are sized for the widest row the instance takes
-template <int CIN, int COUT, int KS, int PAD>
+template <int CIN, int COUT, int KS, int PAD, bool DF32 = false>
 inline hipError_t launch_wgrads(const WgradSArgs& a, hipStream_t st) {
-  if (a.W <= 16) return launch_wgrads_w<CIN, COUT, KS, PAD, 16>(a, st);
-  if (a.W <= 32) return launch_wgrads_w<CIN, COUT, KS, PAD, 32>(a, st);
-  if (a.W <= 64) return launch_wgrads_w<CIN, COUT, KS, PAD, 64>(a, st);
+  if (a.W <= 16) return launch_wgrads_w<CIN, COUT, KS, PAD, 16, DF32>(a, st);
+  if (a.W <= 32) return launch_wgrads_w<CIN, COUT, KS, PAD, 32, DF32>(a, st);
+  if (a.W <= 64) return launch_wgrads_w<CIN, COUT, KS, PAD, 64, DF32>(a, st);
   return hipErrorInvalidValue;   // frames > 128 (conv2) / 256 (conv3): not supported
 }
 
