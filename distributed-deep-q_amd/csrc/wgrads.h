@@ -399,10 +399,10 @@ struct Wgrad1SGeom {
   static constexpr int PSD = 32;                           // dconv pixel stride (64 B)
   static __host__ __device__ int in_row(int W) { return 4 * (W + 6) + 64; }   // + read tail
   static __host__ __device__ int d_plane(int W) { return ((W + 15) & ~15) * PSD; }
-  // the halo patch + the NW waves' dconv rows; at least the image of the
+  // the halo patch + the NW waves' dconv row pairs; at least the image of the
   // final cross-wave sums (NW x 16 x 64 floats)
   static __host__ __device__ size_t bytes(int W, int R) {
-    const size_t a = ((size_t)(R + 6) * in_row(W) + NW * 3 * d_plane(W)) * 2;
+    const size_t a = ((size_t)(R + 6) * in_row(W) + NW * 6 * d_plane(W)) * 2;
     return a > (size_t)NW * 16 * 64 * 4 ? a : (size_t)NW * 16 * 64 * 4;
   }
 };
@@ -417,7 +417,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
   const int l31 = lane & 31, h = lane >> 5;
   const int irow = Geo::in_row(W), dpl = Geo::d_plane(W);
   __bf16* patch = reinterpret_cast<__bf16*>(sm_w1);                 // [R+6][irow]
-  __bf16* rd = patch + (R + 6) * irow + w * 3 * dpl;                // this wave's [3][W16][32]
+  __bf16* rd = patch + (R + 6) * irow + w * 6 * dpl;                // this wave's [2][3][W16][32]
   const int bands = H / R;
   const int band = blockIdx.x;
   const int b = band / bands, y0 = (band % bands) * R;
@@ -433,7 +433,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     *reinterpret_cast<uint2*>(patch + py * irow + 4 * px) = *reinterpret_cast<uint2*>(q);
   }
   // dconv tail pixels (W..W16) stay zero
-  for (int i = lane; i < 3 * (((W + 15) & ~15) - W) * 4; i += 64) {
+  for (int i = lane; i < 6 * (((W + 15) & ~15) - W) * 4; i += 64) {
     const int per = (((W + 15) & ~15) - W) * 4;
     const int p = i / per, r = i - p * per;
     reinterpret_cast<u32x4*>(rd + p * dpl + W * Geo::PSD)[r] = u32x4{0u, 0u, 0u, 0u};
@@ -446,18 +446,21 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
   float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 
-  // pooled dconv row chunks: lane keeps chunk dc8 (8 of the 32 channels) and
-  // walks pooled pixels dpx, dpx + 16, ...
+  // A wave owns pooled dconv rows k (conv rows 2k and 2k+1 of the band): the
+  // pooled row is loaded once and expanded into both conv rows (the four
+  // quadrants of every pooling window) with one routing-byte extraction; the
+  // bias sums every routed value once (route != 4).  Lane keeps chunk dc8
+  // (8 of the 32 channels) and walks pooled pixels dpx, dpx + 16, ...
   constexpr int NPD = (WMAX / 2 + 15) / 16;
   const int dc8 = lane & 3, dpx = lane >> 2;
   struct Regs {
     u32x4 d[3][NPD];
     u32x2 m[NPD];
   };
-  auto load = [&](Regs& G, int r) {
-    const bool live = r < R;
-    const int y = y0 + r;
-    const size_t o0 = (((size_t)b * (H >> 1) + (y >> 1)) * (W >> 1) + dpx) * 32 + 8 * dc8;
+  auto load = [&](Regs& G, int k) {
+    const bool live = 2 * k < R;
+    const int yp = (y0 >> 1) + k;
+    const size_t o0 = (((size_t)b * (H >> 1) + yp) * (W >> 1) + dpx) * 32 + 8 * dc8;
 #pragma unroll
     for (int u = 0; u < NPD; ++u) {
       const bool ok = live && dpx + 16 * u < (W >> 1);
@@ -471,34 +474,41 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
       }
     }
   };
-  auto store = [&](const Regs& G, int r) {
-    const uint32_t qy = ((y0 + r) & 1) << 1;
+  auto store = [&](const Regs& G) {
 #pragma unroll
     for (int u = 0; u < NPD; ++u) {
       const int px = dpx + 16 * u;
       if (px >= (W >> 1)) continue;
+      uint32_t ra[4], rb[4];
 #pragma unroll
-      for (int dx = 0; dx < 2; ++dx) {
-        const uint32_t qd = qy | dx;
+      for (int e = 0; e < 4; ++e) {   // routing bytes of channels 2e, 2e+1
+        const uint32_t mw = G.m[u][e >> 1];
+        ra[e] = (mw >> (16 * (e & 1))) & 0xff;
+        rb[e] = (mw >> (16 * (e & 1) + 8)) & 0xff;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {   // quadrant q = 2 dy + dx
         uint32_t keep[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const uint32_t mw = G.m[u][e >> 1];
-          const uint32_t ra = (mw >> (16 * (e & 1))) & 0xff;
-          const uint32_t rb = (mw >> (16 * (e & 1) + 8)) & 0xff;
-          keep[e] = (ra == qd ? 0xffffu : 0u) | (rb == qd ? 0xffff0000u : 0u);
-        }
+        for (int e = 0; e < 4; ++e)
+          keep[e] = (ra[e] == (uint32_t)q ? 0xffffu : 0u) | (rb[e] == (uint32_t)q ? 0xffff0000u : 0u);
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
           u32x4 o;
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[e] = G.d[p][u][e] & keep[e];
-          *reinterpret_cast<u32x4*>(rd + p * dpl + (2 * px + dx) * Geo::PSD + 8 * dc8) = o;
+          *reinterpret_cast<u32x4*>(rd + ((q >> 1) * 3 + p) * dpl + (2 * px + (q & 1)) * Geo::PSD +
+                                    8 * dc8) = o;
+        }
+      }
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            bsum[2 * e] += __builtin_bit_cast(float, o[e] << 16);
-            bsum[2 * e + 1] += __builtin_bit_cast(float, o[e] & 0xffff0000u);
-          }
+      for (int e = 0; e < 4; ++e) {   // bias: every routed value once
+        const uint32_t any = (ra[e] != 4u ? 0xffffu : 0u) | (rb[e] != 4u ? 0xffff0000u : 0u);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          const uint32_t o = G.d[p][u][e] & any;
+          bsum[2 * e] += __builtin_bit_cast(float, o << 16);
+          bsum[2 * e + 1] += __builtin_bit_cast(float, o & 0xffff0000u);
         }
       }
     }
@@ -512,30 +522,35 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
   const int chn = 16 * (gq & 1) + 4 * ip;
   __syncthreads();   // the halo patch
   Regs g;
-  if (w < R) load(g, w);
-  for (int r = w; r < R; r += NW) {
-    store(g, r);
-    load(g, r + NW);
+  if (2 * w < R) load(g, w);
+  for (int k = w; 2 * k < R; k += NW) {
+    store(g);
+    load(g, k + NW);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int s = 0; s < WMAX / 16; ++s) {
-      if (16 * s >= W) break;
-      // B fragments one tap row ahead of their three MFMAs (all seven live
-      // at once would spill at W = 84)
-      bf16x8 av[3], bv[2];
-      const __bf16* pb = patch + r * irow + 4 * (16 * s + pix0) + chn;
+    for (int dy = 0; dy < 2; ++dy) {
+      const int r = 2 * k + dy;
+      const __bf16* rdr = rd + dy * 3 * dpl;
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        const __bf16* pa = rd + p * dpl + (16 * s + pix0) * Geo::PSD + chn;
-        av[p] = tr_pair(pa, pa + 4 * Geo::PSD);
-      }
-      bv[0] = tr_pair(pb, pb + 16);
+      for (int s = 0; s < WMAX / 16; ++s) {
+        if (16 * s >= W) break;
+        // B fragments one tap row ahead of their three MFMAs (all seven live
+        // at once would spill at W = 84)
+        bf16x8 av[3], bv[2];
+        const __bf16* pb = patch + r * irow + 4 * (16 * s + pix0) + chn;
 #pragma unroll
-      for (int ky = 0; ky < 7; ++ky) {
-        if (ky < 6) bv[(ky + 1) & 1] = tr_pair(pb + (ky + 1) * irow, pb + (ky + 1) * irow + 16);
-        acc[ky] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2], bv[ky & 1], acc[ky], 0, 0, 0);
-        acc[ky] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], bv[ky & 1], acc[ky], 0, 0, 0);
-        acc[ky] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[ky & 1], acc[ky], 0, 0, 0);
+        for (int p = 0; p < 3; ++p) {
+          const __bf16* pa = rdr + p * dpl + (16 * s + pix0) * Geo::PSD + chn;
+          av[p] = tr_pair(pa, pa + 4 * Geo::PSD);
+        }
+        bv[0] = tr_pair(pb, pb + 16);
+#pragma unroll
+        for (int ky = 0; ky < 7; ++ky) {
+          if (ky < 6) bv[(ky + 1) & 1] = tr_pair(pb + (ky + 1) * irow, pb + (ky + 1) * irow + 16);
+          acc[ky] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2], bv[ky & 1], acc[ky], 0, 0, 0);
+          acc[ky] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], bv[ky & 1], acc[ky], 0, 0, 0);
+          acc[ky] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[ky & 1], acc[ky], 0, 0, 0);
+        }
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -577,7 +592,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
 // the kernel is VALU-bound on the routing expansion, not latency-bound)
 template <int WMAX>
 inline hipError_t launch_wgrad1s_w(const Wgrad1SArgs& a, hipStream_t st) {
-  constexpr int NW = 4;
+  constexpr int NW = WMAX <= 64 ? 4 : 2;   // two staged rows per wave: LDS
   using Geo = Wgrad1SGeom<WMAX, NW>;
   const size_t shm = Geo::bytes(a.W, a.R);
   if (shm > 160 * 1024) return hipErrorInvalidValue;

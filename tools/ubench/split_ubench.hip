@@ -260,5 +260,15 @@ int main(int argc, char** argv) {
   if (want()) run<64, 64, 64, 3, 8, 16, 4, 2>("23 conv3 dgrad-shape 8x16 8w ch64", d3, 50);
   if (want()) run<64, 64, 64, 3, 8, 8, 2, 1>("24 conv3 dgrad-shape 8x8 2w TN2", d3, 50);
   if (want()) run<64, 64, 64, 3, 4, 16, 2, 2>("25 conv3 dgrad-shape 4x16 4w", d3, 50);
+  if (want()) run<32, 32, 64, 5, 16, 16, 4, 2>("26 conv2 fwd 16x16 8w TM2", c2, 50);
+  if (want()) run<32, 32, 64, 5, 16, 16, 4, 1>("27 conv2 fwd 16x16 4w TM2 TN2", c2, 50);
+  if (want()) run<32, 32, 64, 5, 16, 16, 2, 2>("28 conv2 fwd 16x16 4w TM4", c2, 50);
+  if (want()) run<64, 64, 64, 3, 16, 8, 4, 1>("29 conv3 fwd 16x8 4w TN2", c3, 50);
+  if (want()) run<64, 32, 64, 3, 16, 16, 8, 1>("30 conv3 fwd 16x16 8w TN2 ch32", c3, 50);
+  if (want()) run<64, 64, 64, 3, 8, 16, 4, 1>("31 conv3 fwd 8x16 4w TN2", c3, 50);
+  if (want()) run<64, 32, 64, 3, 4, 8, 1, 2>("32 conv3 fwd 4x8 2w ch32", c3, 50);
+  if (want()) run<64, 64, 64, 3, 4, 8, 1, 2>("33 conv3 fwd 4x8 2w", c3, 50);
+  if (want()) run<64, 32, 64, 3, 8, 8, 2, 2>("34 conv3 fwd 8x8 4w ch32", c3, 50);
+  if (want()) run<64, 64, 64, 3, 4, 16, 2, 2>("35 conv3 fwd 4x16 4w", c3, 50);
   return 0;
 }
