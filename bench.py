@@ -198,9 +198,19 @@ def cpu_baseline(B, S, seed, budget_s=12.0, max_steps=2000):
     return out
 
 
+# algorithmic HBM bytes per launch of the fc4 kernels: W4 (512 x K fp32 per
+# tower) plus activations in and out (K = 64 (S/8)^2)
+FC4_BYTES = {
+    "fc4_fwd": lambda B, S: 2 * (512 * 64 * (S // 8) ** 2 * 4 + B * 64 * (S // 8) ** 2 * 4),
+    "fc4_dgrad": lambda B, S: 512 * 64 * (S // 8) ** 2 * 4 + B * 512 * 4 + B * 64 * (S // 8) ** 2 * 4,
+    "fc4_wgrad": lambda B, S: 512 * 64 * (S // 8) ** 2 * 4 + B * 512 * 4 + B * 64 * (S // 8) ** 2 * 4,
+}
+
+
 def kernel_roofline(avg_us, B, S, P):
-    """Per-kernel fraction of its roofline: MFMA kernels vs the
-    f32 MFMA peak; the replay gather and the apply vs HBM (algorithmic bytes:
+    """Per-kernel fraction of its roofline: conv kernels vs the
+    peak of their arithmetic (arith_peak); fc4, the replay gather and the apply
+    vs HBM (algorithmic bytes:
     gather 2*B*4*S^2 u8 read + f32 write; rmsprop apply 20*P, +8P on sync
     steps not counted).  Device times are the eager HIP-event times."""
     fl = kernel_flops(B, S)
@@ -208,7 +218,11 @@ def kernel_roofline(avg_us, B, S, P):
     for k, us in avg_us.items():
         if us <= 0:
             continue
-        if k in fl:
+        if k in FC4_BYTES:                 # streaming W4: HBM-bound
+            by = FC4_BYTES[k](B, S)
+            out[k] = {"GBps": round(by / (us * 1e-6) / 1e9, 1), "bound": "hbm",
+                      "frac": round(by / (us * 1e-6) / HBM_PEAK, 3)}
+        elif k in fl:
             tf = fl[k] / (us * 1e-6) / 1e12
             out[k] = {"TFLOPs": round(tf, 2), "arith": KERNEL_ARITH.get(k, "f32"),
                       "peak": round(arith_peak(k) / 1e12, 1),
