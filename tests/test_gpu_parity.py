@@ -165,7 +165,7 @@ def make_params(ref, rng, S, init):
 FULL_PASS_CASES = [
     (16, 32, "uniform", "x3"), (16, 32, "snake", "x3"), (24, 8, "uniform", "x3"),
     (40, 4, "snake", "x3"), (64, 32, "uniform", "x3"), (16, 256, "snake", "x3"),
-    (128, 2, "uniform", "x3"),
+    (128, 2, "uniform", "x3"), (72, 4, "snake", "x3"), (96, 4, "uniform", "x3"),
     # the bench's initial state on its own frames (C1 / C2 shapes)
     (16, 32, "bench", "bench"), (64, 32, "bench", "bench"),
     # C3: batch 256 across the frame sweep (results/cost-vs-image-size-trials.txt)
