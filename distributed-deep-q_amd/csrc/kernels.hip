@@ -1016,6 +1016,11 @@ __device__ __forceinline__ void fc4_apply_tile(const ApplyTail& t, const ApplyAr
   const bool first = t.opt_init[2] != 0;
   const bool sync = t.opt_init[3] != 0;
   const int64_t i0 = a.lo + (int64_t)o0 * K + k;
+  // write-through stores (split.h wt_store4): 25 MB per step that would
+  // otherwise be written back as dirty L2 lines at the launch's end
+  const uint32_t nb = (uint32_t)(a.n * 4);
+  const __amdgpu_buffer_rsrc_t rg = wt_rsrc(t.grad, nb), rt = wt_rsrc(t.theta, nb);
+  const __amdgpu_buffer_rsrc_t ro = wt_rsrc(t.opt, nb), rp = wt_rsrc(t.thetaP, nb);
   float4 t4[R], s4[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
@@ -1028,16 +1033,16 @@ __device__ __forceinline__ void fc4_apply_tile(const ApplyTail& t, const ApplyAr
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int64_t i = i0 + (int64_t)r * K;
-    *reinterpret_cast<float4*>(const_cast<float*>(t.grad) + i) =
-        make_float4(g[r][0], g[r][1], g[r][2], g[r][3]);
+    const uint32_t ib = (uint32_t)(i * 4);
+    wt_store4(rg, ib, make_float4(g[r][0], g[r][1], g[r][2], g[r][3]));
     float th[4] = {t4[r].x, t4[r].y, t4[r].z, t4[r].w};
     float st[4] = {s4[r].x, s4[r].y, s4[r].z, s4[r].w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) th[e] = apply_one(a, first, i + e, th[e], g[r][e], st[e]);
     const float4 o4 = make_float4(th[0], th[1], th[2], th[3]);
-    *reinterpret_cast<float4*>(t.theta + i) = o4;
-    if (a.rule != 0) *reinterpret_cast<float4*>(t.opt + i) = make_float4(st[0], st[1], st[2], st[3]);
-    if (sync) *reinterpret_cast<float4*>(t.thetaP + i) = o4;
+    wt_store4(rt, ib, o4);
+    if (a.rule != 0) wt_store4(ro, ib, make_float4(st[0], st[1], st[2], st[3]));
+    if (sync) wt_store4(rp, ib, o4);
   }
 }
 

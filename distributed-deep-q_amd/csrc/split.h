@@ -47,6 +47,36 @@ __device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l)
   l = (__bf16)(r - (float)m);
 }
 
+// Write-through (sc1) vector store of one float at byte offset `off` of a
+// buffer: the line is written to memory by the store itself, so the kernel's
+// end leaves it clean (a kernel boundary otherwise writes back every dirty L2
+// line the kernel left: ~B / 6 TB/s, MI355X_MICROARCH.md "boundary").
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ void wt_store(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)off, 0, 16);
+}
+__device__ __forceinline__ void wt_store4(__amdgpu_buffer_rsrc_t r, uint32_t off, float4 v) {
+  typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), r, (int)off, 0, 16);
+}
+__device__ __forceinline__ void wt_store_b16(__amdgpu_buffer_rsrc_t r, uint32_t off, __bf16 v) {
+  __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, v), r, (int)off, 0, 16);
+}
+__device__ __forceinline__ void wt_store_b8(__amdgpu_buffer_rsrc_t r, uint32_t off, uint8_t v) {
+  __builtin_amdgcn_raw_buffer_store_b8(v, r, (int)off, 0, 16);
+}
+// the split of v at element e of a split tensor of E elements, write-through
+__device__ __forceinline__ void wt_store_split(__amdgpu_buffer_rsrc_t r, uint32_t E, uint32_t e,
+                                               float v) {
+  __bf16 h, m, l;
+  split3(v, h, m, l);
+  wt_store_b16(r, e * 2, h);
+  wt_store_b16(r, (E + e) * 2, m);
+  wt_store_b16(r, (2 * E + e) * 2, l);
+}
+
 // Store the split of v at element e of a split tensor of E elements.
 __device__ __forceinline__ void store_split(__bf16* t, int64_t E, int64_t e, float v) {
   __bf16 h, m, l;
@@ -159,6 +189,16 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, const f32x16 
   float* __restrict__ outz = z ? a.out[1] : a.out[0];
   __bf16* __restrict__ osplit = z ? a.out_split[1] : a.out_split[0];
   uint8_t* __restrict__ maskz = z ? a.mask[1] : a.mask[0];
+  // every output written through (wt_store): consumed by the next launch,
+  // possibly on another XCD, so it goes to memory anyway -- during the
+  // epilogue rather than as dirty lines at the kernel's end
+  const uint32_t OE = (uint32_t)(DGRAD ? (size_t)a.B * a.H * a.W * N
+                                       : (size_t)a.B * (a.H >> 1) * (a.W >> 1) * N);
+  const __amdgpu_buffer_rsrc_t r_out = wt_rsrc(DGRAD ? (const void*)a.pd : outz, OE * 4);
+  const __amdgpu_buffer_rsrc_t r_spl =
+      wt_rsrc(DGRAD ? (const void*)a.pd_split : osplit,
+              (uint32_t)(DGRAD ? a.pd_elems : a.out_elems) * 6);
+  const __amdgpu_buffer_rsrc_t r_msk = wt_rsrc(maskz, OE);
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int mb = wmi * TM * 32 + 32 * i;
@@ -182,9 +222,11 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, const f32x16 
           const bool pos = mx > 0.f;
           const float o = pos ? mx : 0.f;
           const size_t onhwc = (((size_t)b * Hp + pyy) * Wp + pxx) * N + n;
-          if (outz) outz[a.nchw ? (((size_t)b * N + n) * Hp + pyy) * Wp + pxx : onhwc] = o;
-          if (osplit) store_split(osplit, a.out_elems, onhwc, o);
-          if (maskz) maskz[onhwc] = (uint8_t)(pos ? arg : 4);
+          if (outz)
+            wt_store(r_out, (uint32_t)(a.nchw ? (((size_t)b * N + n) * Hp + pyy) * Wp + pxx : onhwc) * 4,
+                     o);
+          if (osplit) wt_store_split(r_spl, (uint32_t)a.out_elems, (uint32_t)onhwc, o);
+          if (maskz) wt_store_b8(r_msk, (uint32_t)onhwc, (uint8_t)(pos ? arg : 4));
         }
       } else {
 #pragma unroll
@@ -195,8 +237,8 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, const f32x16 
           const int x = x0 + 2 * (win % (TX / 2)) + (m & 1);
           if (y >= a.H || x >= a.W) continue;
           const size_t e = (((size_t)b * a.H + y) * a.W + x) * N + n;
-          if (a.pd) a.pd[e] = acc[i][j][r];
-          if (a.pd_split) store_split(a.pd_split, a.pd_elems, e, acc[i][j][r]);
+          if (a.pd) wt_store(r_out, (uint32_t)e * 4, acc[i][j][r]);
+          if (a.pd_split) wt_store_split(r_spl, (uint32_t)a.pd_elems, (uint32_t)e, acc[i][j][r]);
         }
       }
     }
@@ -533,7 +575,7 @@ __global__ __launch_bounds__(64 * WM) void split_conv1_kernel(const Conv1Args a)
 #pragma unroll
   for (int i = 0; i < TM; ++i) acc[i][0] += cor[i];
   SplitArgs e{};
-  e.H = a.H; e.W = a.W;
+  e.B = a.B; e.H = a.H; e.W = a.W;
   e.bias[0] = a.bias[0]; e.bias[1] = a.bias[1];
   e.out[0] = a.out[0]; e.out[1] = a.out[1];
   e.out_split[0] = a.out_split[0]; e.out_split[1] = a.out_split[1];

@@ -133,38 +133,43 @@ __device__ __forceinline__ void wgrads_body(const WgradSArgs& a, char* smem, int
     float4 f[2][NPD];    // DF32: the 8 fp32 values of the chunk
     u32x2 m[NPD];
   };
+  // Every load is issued unconditionally (clamped to element 0 when out of
+  // range, the value then replaced by zero): with no branches around them the
+  // compiler counts a row set's loads exactly and waits for that set only
+  // (branchy loads made it wait for every outstanding load, vmcnt(0)).
   auto load = [&](Regs& R, int row) {
     const bool live = row < r1;
     const int b = row / H, y = row - b * H, yi = y + ky - PAD;
     const bool vin = live && (unsigned)yi < (unsigned)H;
-    const __bf16* src = a.in + (((size_t)b * H + yi) * W + ipx) * CIN + 8 * ic8;
+    const size_t i0 = (((size_t)b * H + yi) * W + ipx) * CIN + 8 * ic8;
 #pragma unroll
     for (int u = 0; u < NPI; ++u) {
       const bool ok = vin && ipx + u * PPP < W;
+      const size_t o = ok ? i0 + (size_t)u * PPP * CIN : 0;
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
-        R.i[p][u] = u32x4{0u, 0u, 0u, 0u};
-        if (ok) R.i[p][u] = *reinterpret_cast<const u32x4*>(src + p * a.in_elems + u * PPP * CIN);
+        const u32x4 v = *reinterpret_cast<const u32x4*>(a.in + p * a.in_elems + o);
+        R.i[p][u] = ok ? v : u32x4{0u, 0u, 0u, 0u};
       }
     }
     const size_t o0 = (((size_t)b * (H >> 1) + (y >> 1)) * (W >> 1) + dpx) * COUT + cb * 32 + 8 * dc8;
 #pragma unroll
     for (int u = 0; u < NPD; ++u) {
       const bool ok = live && dpx + 16 * u < (W >> 1);
-      const size_t o = o0 + (size_t)u * 16 * COUT;
-      R.m[u] = u32x2{0x04040404u, 0x04040404u};
-      if (ok) R.m[u] = *reinterpret_cast<const u32x2*>(a.droute + o);
+      const size_t o = ok ? o0 + (size_t)u * 16 * COUT : 0;
+      const u32x2 mv = *reinterpret_cast<const u32x2*>(a.droute + o);
+      R.m[u] = ok ? mv : u32x2{0x04040404u, 0x04040404u};
       if (DF32) {
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
-          R.f[hh][u] = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (ok) R.f[hh][u] = *reinterpret_cast<const float4*>(a.dpool_f32 + o + 4 * hh);
+          const float4 v = *reinterpret_cast<const float4*>(a.dpool_f32 + o + 4 * hh);
+          R.f[hh][u] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
         }
       } else {
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
-          R.d[p][u] = u32x4{0u, 0u, 0u, 0u};
-          if (ok) R.d[p][u] = *reinterpret_cast<const u32x4*>(a.dpool + p * a.d_elems + o);
+          const u32x4 v = *reinterpret_cast<const u32x4*>(a.dpool + p * a.d_elems + o);
+          R.d[p][u] = ok ? v : u32x4{0u, 0u, 0u, 0u};
         }
       }
     }
@@ -244,43 +249,46 @@ __device__ __forceinline__ void wgrads_body(const WgradSArgs& a, char* smem, int
 #pragma unroll
     for (int s = 0; s < WMAX / 16; ++s) {
       if (16 * s >= W) break;
-      // every fragment of the k-step first (one LDS round trip per k-step,
-      // not one per tile: the reads were issued right before their MFMAs
-      // and waited on at once), then the MFMAs
-      bf16x8 av[3], bv[KS][NCB][3];
+      // the A fragments, then the B fragments one kx ahead of their MFMAs
+      // (all of them live at once took the registers of a second row set)
+      bf16x8 av[3], bv[2][NCB][3];
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
         const __bf16* pa = rd + p * dpl + (16 * s + pix0) * Geo::PSD + chn;
         av[p] = tr_pair(pa, pa + 4 * Geo::PSD);
       }
-#pragma unroll
-      for (int kx = 0; kx < KS; ++kx)
+      auto bload = [&](int kx) {
 #pragma unroll
         for (int c = 0; c < NCB; ++c)
 #pragma unroll
           for (int p = 0; p < 3; ++p) {
             const __bf16* pb = rin + p * ipl + (16 * s + pix0 + kx) * Geo::PSI + 32 * c + chn;
-            bv[kx][c][p] = tr_pair(pb, pb + 4 * Geo::PSI);
+            bv[kx & 1][c][p] = tr_pair(pb, pb + 4 * Geo::PSI);
           }
-      __builtin_amdgcn_sched_barrier(0);
+      };
+      bload(0);
 #pragma unroll
-      for (int kx = 0; kx < KS; ++kx)
+      for (int kx = 0; kx < KS; ++kx) {
+        if (kx + 1 < KS) bload(kx + 1);
 #pragma unroll
         for (int c = 0; c < NCB; ++c) {
           const int t = kx * NCB + c;
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2], bv[kx][c][0], acc[t], 0, 0, 0);
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], bv[kx][c][1], acc[t], 0, 0, 0);
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[kx][c][2], acc[t], 0, 0, 0);
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], bv[kx][c][0], acc[t], 0, 0, 0);
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[kx][c][1], acc[t], 0, 0, 0);
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[kx][c][0], acc[t], 0, 0, 0);
+          const bf16x8* b = bv[kx & 1][c];
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2], b[0], acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], b[1], acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], b[2], acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], b[0], acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], b[1], acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], b[0], acc[t], 0, 0, 0);
         }
+      }
     }
     __builtin_amdgcn_wave_barrier();
   };
 
   {   // one register set: the next row's loads are issued right after this
-      // row's LDS stores (which consumed the registers) and land under its MFMAs
+      // row's LDS stores and land under its MFMAs (a second set, loading two
+      // rows ahead, measured no faster: the kernel is not waiting on them)
     Regs g;
     int row = r0 + w;
     if (row < r1) load(g, row);
@@ -294,7 +302,10 @@ __device__ __forceinline__ void wgrads_body(const WgradSArgs& a, char* smem, int
 
   // ---- sum the four waves' tiles in fixed order, store the group slab ----
   float* red = reinterpret_cast<float*>(smem);        // [4 waves][16 r][64 lanes]
-  float* slab = a.part + (size_t)g * COUT * a.NP + (size_t)cb * 32 * a.NP;
+  // slab stores write-through (wt_store): the reduce reads them from memory
+  // anyway, and the kernel's end then has no dirty slab lines to write back
+  const __amdgpu_buffer_rsrc_t srs = wt_rsrc(a.part, (uint32_t)((size_t)a.G * COUT * a.NP * 4));
+  const uint32_t sbase = (uint32_t)(((size_t)g * COUT + (size_t)cb * 32) * a.NP * 4);
 #pragma unroll
   for (int t = 0; t < T; ++t) {
     __syncthreads();
@@ -308,7 +319,7 @@ __device__ __forceinline__ void wgrads_body(const WgradSArgs& a, char* smem, int
       const int e = r * 64 + lane;
       const float v = (red[e] + red[1024 + e]) + (red[2048 + e] + red[3072 + e]);
       const int co = (r & 3) + 8 * (r >> 2) + 4 * h;
-      slab[(size_t)co * a.NP + nbase + l31] = v;
+      wt_store(srs, sbase + (uint32_t)((co * a.NP + nbase + l31) * 4), v);
     }
   }
   if (ky == 0) {   // bias column n = KC: lanes with equal lane & 3 share 8 channels
@@ -321,7 +332,7 @@ __device__ __forceinline__ void wgrads_body(const WgradSArgs& a, char* smem, int
       float v = 0.f;
       for (int ww = 0; ww < 4; ++ww)
         for (int l = c8; l < 64; l += 4) v += red[(ww * 64 + l) * 8 + j];
-      slab[(size_t)co * a.NP + KC] = v;
+      wt_store(srs, sbase + (uint32_t)((co * a.NP + KC) * 4), v);
     }
   }
 }
@@ -557,7 +568,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
   }
   // ---- the NW waves' tiles in fixed order -> the band's slab ----
   float* red = reinterpret_cast<float*>(sm_w1);
-  float* slab = a.part + (size_t)band * 32 * a.NP;
+  const __amdgpu_buffer_rsrc_t srs =
+      wt_rsrc(a.part, (uint32_t)((size_t)a.B * (a.H / a.R) * 32 * a.NP * 4));
+  const uint32_t sbase = (uint32_t)((size_t)band * 32 * a.NP * 4);
 #pragma unroll
   for (int t = 0; t < 7; ++t) {
     __syncthreads();
@@ -572,7 +585,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
 #pragma unroll
       for (int ww = 1; ww < NW; ++ww) v += red[ww * 1024 + e];
       const int co = (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (l31 < 28) slab[(size_t)co * a.NP + t * 28 + l31] = v;
+      if (l31 < 28) wt_store(srs, sbase + (uint32_t)((co * a.NP + t * 28 + l31) * 4), v);
     }
   }
   __syncthreads();
@@ -584,7 +597,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     float v = 0.f;
     for (int ww = 0; ww < NW; ++ww)
       for (int l = c8; l < 64; l += 4) v += red[(ww * 64 + l) * 8 + j];
-    slab[(size_t)co * a.NP + 196] = v;
+    wt_store(srs, sbase + (uint32_t)((co * a.NP + 196) * 4), v);
   }
 }
 
