@@ -522,7 +522,9 @@ __device__ __forceinline__ void direct_conv_body(const DirectArgs& a, float* sme
           const float v = acc[i][j][r];
           if (a.pd_pooled) {   // one store per element: lanes along n, 128-B runs
             if (a.pdconv) a.pdconv[pix * N + n] = v;   // null: split copy only
-            if (a.pd_split) store_split(a.pd_split, a.pd_split_elems, pix * N + n, v);
+            if (a.pd_split)   // written through (split.h wt_store_split)
+              wt_store_split(wt_rsrc(a.pd_split, (uint32_t)a.pd_split_elems * 6),
+                             (uint32_t)a.pd_split_elems, (uint32_t)(pix * N + n), v);
             continue;
           }
           const int mk = a.pmask[pix * N + n];

@@ -120,13 +120,16 @@ __global__ __launch_bounds__(256) void fc4_fwd_direct_kernel(const Fc4FwdArgs a)
                                                       0, 0);
   }
   // rows = b, columns = n: lanes store consecutive n
-  float* dst = a.part + ((size_t)(split * a.nz + z) * a.B) * 512 + n0 + l31;
+  // partials written through (split.h wt_store): the head reads them next
+  const __amdgpu_buffer_rsrc_t rp =
+      wt_rsrc(a.part, (uint32_t)((size_t)gridDim.y * a.nz * a.B * 512 * 4));
+  const uint32_t dbase = (uint32_t)((((size_t)(split * a.nz + z) * a.B) * 512 + n0 + l31) * 4);
 #pragma unroll
   for (int t = 0; t < BT; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int b = bt0 + t * 32 + fc_acc_row(r, lane);
-      if (b < a.B) dst[(size_t)b * 512] = acc[t][r];
+      if (b < a.B) wt_store(rp, dbase + (uint32_t)b * 2048, acc[t][r]);
     }
 }
 

@@ -189,16 +189,6 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, const f32x16 
   float* __restrict__ outz = z ? a.out[1] : a.out[0];
   __bf16* __restrict__ osplit = z ? a.out_split[1] : a.out_split[0];
   uint8_t* __restrict__ maskz = z ? a.mask[1] : a.mask[0];
-  // every output written through (wt_store): consumed by the next launch,
-  // possibly on another XCD, so it goes to memory anyway -- during the
-  // epilogue rather than as dirty lines at the kernel's end
-  const uint32_t OE = (uint32_t)(DGRAD ? (size_t)a.B * a.H * a.W * N
-                                       : (size_t)a.B * (a.H >> 1) * (a.W >> 1) * N);
-  const __amdgpu_buffer_rsrc_t r_out = wt_rsrc(DGRAD ? (const void*)a.pd : outz, OE * 4);
-  const __amdgpu_buffer_rsrc_t r_spl =
-      wt_rsrc(DGRAD ? (const void*)a.pd_split : osplit,
-              (uint32_t)(DGRAD ? a.pd_elems : a.out_elems) * 6);
-  const __amdgpu_buffer_rsrc_t r_msk = wt_rsrc(maskz, OE);
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int mb = wmi * TM * 32 + 32 * i;
@@ -222,11 +212,11 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, const f32x16 
           const bool pos = mx > 0.f;
           const float o = pos ? mx : 0.f;
           const size_t onhwc = (((size_t)b * Hp + pyy) * Wp + pxx) * N + n;
-          if (outz)
-            wt_store(r_out, (uint32_t)(a.nchw ? (((size_t)b * N + n) * Hp + pyy) * Wp + pxx : onhwc) * 4,
-                     o);
-          if (osplit) wt_store_split(r_spl, (uint32_t)a.out_elems, (uint32_t)onhwc, o);
-          if (maskz) wt_store_b8(r_msk, (uint32_t)onhwc, (uint8_t)(pos ? arg : 4));
+          // (plain stores: write-through measured no faster here, and slower
+          // for the scattered NCHW pool3 and the routing bytes)
+          if (outz) outz[a.nchw ? (((size_t)b * N + n) * Hp + pyy) * Wp + pxx : onhwc] = o;
+          if (osplit) store_split(osplit, a.out_elems, onhwc, o);
+          if (maskz) maskz[onhwc] = (uint8_t)(pos ? arg : 4);
         }
       } else {
 #pragma unroll
@@ -237,8 +227,8 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, const f32x16 
           const int x = x0 + 2 * (win % (TX / 2)) + (m & 1);
           if (y >= a.H || x >= a.W) continue;
           const size_t e = (((size_t)b * a.H + y) * a.W + x) * N + n;
-          if (a.pd) wt_store(r_out, (uint32_t)e * 4, acc[i][j][r]);
-          if (a.pd_split) wt_store_split(r_spl, (uint32_t)a.pd_elems, (uint32_t)e, acc[i][j][r]);
+          if (a.pd) a.pd[e] = acc[i][j][r];
+          if (a.pd_split) store_split(a.pd_split, a.pd_elems, e, acc[i][j][r]);
         }
       }
     }
