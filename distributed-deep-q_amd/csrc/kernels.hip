@@ -753,12 +753,113 @@ __global__ __launch_bounds__(512) void fc4_head_kernel(
 
 // Cross-sample head sums, run by the 8 trailing blocks of the wgrad slab
 // reduce: block hb owns fc4 units j = 64 hb + lane, 4 sample groups.
-__device__ void head_sums(int hb, int B, const float* __restrict__ dqbuf,
+// ---------------------------------------------------------------------------
+// apply: server.py update rules on the flat Q tower, float4 per thread, with
+//  - the conv kernel-layout copy refreshed from the new values,
+//  - the target sync P <- Q fused in when the NEXT pull will see
+//    iteration % period == 0 (server.py:188-189),
+// ---------------------------------------------------------------------------
+struct ApplyArgs {
+  int64_t n;
+  int64_t lo, hi, skip_lo, skip_len;   // elements [lo, hi) minus [skip_lo, skip_lo + skip_len)
+  int rule, period;
+  float lr, decay, one_minus_decay, eps, momentum, wd;
+  int64_t bias_lo[5], bias_hi[5];   // [lo,hi) element ranges of biases (momentum multipliers)
+  ConvDims conv[3];
+};
+
+__device__ __forceinline__ float apply_rule(const ApplyArgs& a, bool first, bool is_bias,
+                                            float th, float g, float& st);
+
+__device__ __forceinline__ float apply_one(const ApplyArgs& a, bool first, int64_t i, float th,
+                                           float g, float& st) {
+  bool is_bias = false;
+  if (a.rule == 3) {
+#pragma unroll
+    for (int l = 0; l < 5; ++l) is_bias |= (i >= a.bias_lo[l] && i < a.bias_hi[l]);
+  }
+  return apply_rule(a, first, is_bias, th, g, st);
+}
+
+// the rules themselves; is_bias only matters to the momentum rule
+__device__ __forceinline__ float apply_rule(const ApplyArgs& a, bool first, bool is_bias,
+                                            float th, float g, float& st) {
+  // no FMA contraction: every call site (the apply launch, the fused fc4
+  // apply, the shard apply) rounds the rules identically
+#pragma clang fp contract(off)
+  switch (a.rule) {
+    case 0:   // sgd: theta - lr*g  (server.py:81-83, apply_descent :66-68)
+      return th - a.lr * g;
+    case 1: { // rmsprop with the one-step-lagged cache (server.py:86-105)
+      const float g2 = g * g;
+      const float c_use = first ? g2 : st;
+      st = first ? g2 : (a.decay * st + a.one_minus_decay * g2);
+      return th - (a.lr * g) / sqrtf(c_use + a.eps);
+    }
+    case 2: { // adagrad with the current accumulator (server.py:108-124)
+      const float acc = first ? g * g : st + g * g;
+      st = acc;
+      return th - (a.lr * g) / sqrtf(acc + a.eps);
+    }
+    default: { // Caffe SGDSolver momentum (blobs_lr {1,2}, weight_decay {1,0})
+      const float lr = a.lr * (is_bias ? 2.f : 1.f);
+      const float wd = is_bias ? 0.f : a.wd;
+      const float v = a.momentum * (first ? 0.f : st) + lr * (g + wd * th);
+      st = v;
+      return th - v;
+    }
+  }
+}
+
+// Update operands of the apply (the apply launch, or the fused fc4-weight
+// apply blocks of the slab-reduce launch).
+struct ApplyTail {
+  float* theta;
+  const float* grad;
+  float* opt;
+  const int32_t* opt_init;   // [2] first call, [3] P<-Q sync due: latched before the launch
+  float* wk;
+  float* thetaP;
+  float* wkP;
+  __bf16* wks;               // split forward weights of Q / P (plane stride wks_plane)
+  __bf16* wksP;
+  int64_t wks_plane;
+  int blk0;                  // first apply block of the launch
+  int rest;                  // slab reduce: also update conv / fc4-bias / fc5 params
+  int64_t w5_off, b5_off, b4_off;
+};
+
+__device__ __forceinline__ void apply_at(const ApplyTail& t, const ApplyArgs& a, bool first,
+                                         bool sync, int64_t i, float g, float th, float st,
+                                         bool is_bias, bool conv = false,
+                                         const ConvDims& cd = ConvDims{}, int e = 0);
+__device__ __forceinline__ void head_sums(int hb, int B, const float* __restrict__ dqbuf,
                           const float* __restrict__ lpart, const float* __restrict__ h4q,
                           const float* __restrict__ dh4, float* loss_o, float* __restrict__ gw5,
-                          float* __restrict__ gb5, float* __restrict__ gb4) {
+                          float* __restrict__ gb5, float* __restrict__ gb4,
+                          bool ap, const ApplyTail& at, const ApplyArgs& aa) {
   __shared__ float red[4 * 64 * 5];
   const int t = threadIdx.x, lane = t & 63, g = t >> 6;
+  // fused steps: these sums are final here, so their elements are updated
+  // here too (theta / state loaded first, under the sums' loads)
+  const int64_t w5_off = at.w5_off, b5_off = at.b5_off, b4_off = at.b4_off;
+  const bool first = ap && at.opt_init[2] != 0, sync = ap && at.opt_init[3] != 0;
+  float th5[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, st5[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  float thb5 = 0.f, stb5 = 0.f;
+  if (ap && g == 0) {
+    const int jj = hb * 64 + lane;
+    th5[0] = at.theta[b4_off + jj];
+    if (aa.rule != 0 && !first) st5[0] = at.opt[b4_off + jj];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      th5[1 + a] = at.theta[w5_off + a * kFc4 + jj];
+      if (aa.rule != 0 && !first) st5[1 + a] = at.opt[w5_off + a * kFc4 + jj];
+    }
+  }
+  if (ap && hb == 0 && t < 4) {
+    thb5 = at.theta[b5_off + t];
+    if (aa.rule != 0 && !first) stb5 = at.opt[b5_off + t];
+  }
   if (hb == 0 && t < 5) {
     // sequential sums over b, loads issued 16 at a time (clamped indices,
     // dropped): the plain loop was a chain of dependent loads that made
@@ -774,8 +875,12 @@ __device__ void head_sums(int hb, int B, const float* __restrict__ dqbuf,
       for (int u = 0; u < 16; ++u)
         if (b0 + u < B) acc += v[u];
     }
-    if (t < 4) gb5[t] = acc;
-    else *loss_o = acc / (float)B / 2.f;
+    if (t < 4) {
+      gb5[t] = acc;
+      if (ap) apply_at(at, aa, first, sync, b5_off + t, acc, thb5, stb5, true);
+    } else {
+      *loss_o = acc / (float)B / 2.f;
+    }
   }
   const int j = hb * 64 + lane;
   float db = 0.f, dw[4] = {0.f, 0.f, 0.f, 0.f};
@@ -817,6 +922,13 @@ __device__ void head_sums(int hb, int B, const float* __restrict__ dqbuf,
     gb4[j] = s[0];
 #pragma unroll
     for (int a = 0; a < 4; ++a) gw5[a * kFc4 + j] = s[1 + a];
+    if (ap) {
+      apply_at(at, aa, first, sync, b4_off + j, s[0], th5[0], st5[0], true);
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+        apply_at(at, aa, first, sync, w5_off + a * kFc4 + j, s[1 + a], th5[1 + a], st5[1 + a],
+                 false);
+    }
   }
 }
 
@@ -840,6 +952,7 @@ hipError_t launch_head(const NetBuffers& nb, hipStream_t s, ReplayMeta* bump) {
 struct WredDims {
   int64_t w_off, b_off, part_off;
   int cout, cin, ks, splits, np, blk0;   // blk0: first workgroup of this layer
+  int64_t wk_off, wks_off;               // the layer's kernel / split layouts (fused apply)
 };
 
 struct HeadSums {
@@ -859,69 +972,6 @@ __device__ __forceinline__ void apply_book(int64_t* iter, int32_t* opt_init, int
   *iter = it + inc;
   opt_init[0] = 1;
 }
-
-// ---------------------------------------------------------------------------
-// apply: server.py update rules on the flat Q tower, float4 per thread, with
-//  - the conv kernel-layout copy refreshed from the new values,
-//  - the target sync P <- Q fused in when the NEXT pull will see
-//    iteration % period == 0 (server.py:188-189),
-// ---------------------------------------------------------------------------
-struct ApplyArgs {
-  int64_t n;
-  int64_t lo, hi, skip_lo, skip_len;   // elements [lo, hi) minus [skip_lo, skip_lo + skip_len)
-  int rule, period;
-  float lr, decay, one_minus_decay, eps, momentum, wd;
-  int64_t bias_lo[5], bias_hi[5];   // [lo,hi) element ranges of biases (momentum multipliers)
-  ConvDims conv[3];
-};
-
-__device__ __forceinline__ float apply_one(const ApplyArgs& a, bool first, int64_t i, float th,
-                                           float g, float& st) {
-  // no FMA contraction: every call site (the apply launch, the fused fc4
-  // apply, the shard apply) rounds the rules identically
-#pragma clang fp contract(off)
-  switch (a.rule) {
-    case 0:   // sgd: theta - lr*g  (server.py:81-83, apply_descent :66-68)
-      return th - a.lr * g;
-    case 1: { // rmsprop with the one-step-lagged cache (server.py:86-105)
-      const float g2 = g * g;
-      const float c_use = first ? g2 : st;
-      st = first ? g2 : (a.decay * st + a.one_minus_decay * g2);
-      return th - (a.lr * g) / sqrtf(c_use + a.eps);
-    }
-    case 2: { // adagrad with the current accumulator (server.py:108-124)
-      const float acc = first ? g * g : st + g * g;
-      st = acc;
-      return th - (a.lr * g) / sqrtf(acc + a.eps);
-    }
-    default: { // Caffe SGDSolver momentum (blobs_lr {1,2}, weight_decay {1,0})
-      bool is_bias = false;
-#pragma unroll
-      for (int l = 0; l < 5; ++l) is_bias |= (i >= a.bias_lo[l] && i < a.bias_hi[l]);
-      const float lr = a.lr * (is_bias ? 2.f : 1.f);
-      const float wd = is_bias ? 0.f : a.wd;
-      const float v = a.momentum * (first ? 0.f : st) + lr * (g + wd * th);
-      st = v;
-      return th - v;
-    }
-  }
-}
-
-// Update operands of the apply (the apply launch, or the fused fc4-weight
-// apply blocks of the slab-reduce launch).
-struct ApplyTail {
-  float* theta;
-  const float* grad;
-  float* opt;
-  const int32_t* opt_init;   // [2] first call, [3] P<-Q sync due: latched before the launch
-  float* wk;
-  float* thetaP;
-  float* wkP;
-  __bf16* wks;               // split forward weights of Q / P (plane stride wks_plane)
-  __bf16* wksP;
-  int64_t wks_plane;
-  int blk0;                  // first apply block of the launch
-};
 
 // One float4 of parameters per thread: block blk covers elements
 // lo + blk*1024 ..., with the skipped range jumped over (float4-aligned).
@@ -955,6 +1005,24 @@ __device__ __forceinline__ void apply_elems(const ApplyTail& t, const ApplyArgs&
         if (sync) put_conv_weight(d, (int)e0 + e, th[e], t.wkP, t.wksP, t.wks_plane);
       }
     }
+  }
+}
+
+// One element's update in the slab reduce (fused steps): theta / optimizer
+// state (loaded by the caller), the P copy on a sync step, and -- for a conv
+// weight of layer cd -- its kernel / split layouts.  The caller knows whether
+// the element is a bias and which layer it is in, so no range tests here
+// (they kept ~20 more scalars live across the reduce and spilled them).
+__device__ __forceinline__ void apply_at(const ApplyTail& t, const ApplyArgs& a, bool first,
+                                         bool sync, int64_t i, float g, float th, float st,
+                                         bool is_bias, bool conv, const ConvDims& cd, int e) {
+  th = apply_rule(a, first, is_bias, th, g, st);
+  t.theta[i] = th;
+  if (a.rule != 0) t.opt[i] = st;
+  if (sync) t.thetaP[i] = th;
+  if (conv) {
+    put_conv_weight(cd, e, th, t.wk, t.wks, t.wks_plane);
+    if (sync) put_conv_weight(cd, e, th, t.wkP, t.wksP, t.wks_plane);
   }
 }
 
@@ -1073,12 +1141,23 @@ __device__ __forceinline__ void prefetch_body(const Prefetch& pf, int g) {
 constexpr int kWredBlocks = 512;
 constexpr int kWredCh = 32;
 
-__device__ __forceinline__ void wred_unit(const float* __restrict__ part, float* __restrict__ grad,
-                                          const WredDims& d, int lu, float (*red)[64]) {
-  const int col = threadIdx.x & 63, g = threadIdx.x >> 6;
+__device__ __forceinline__ int64_t wred_index(const WredDims& d, int lu, int col, int& n,
+                                              int& kc) {
   const int nblk = d.np / 64;
-  const int co = lu / nblk, n = (lu % nblk) * 64 + col;
-  const int kk = d.ks * d.ks, kc = kk * d.cin;
+  const int co = lu / nblk;
+  const int kk = d.ks * d.ks;
+  n = (lu % nblk) * 64 + col;
+  kc = kk * d.cin;
+  return n < kc ? d.w_off + ((int64_t)co * d.cin + n % d.cin) * kk + n / d.cin : d.b_off + co;
+}
+
+__device__ __forceinline__ void wred_unit(const float* __restrict__ part, float* __restrict__ grad,
+                                          const WredDims& d, int lu, float (*red)[64],
+                                          float* __restrict__ val) {
+  const int col = threadIdx.x & 63, g = threadIdx.x >> 6;
+  int n, kc;
+  const int64_t idx = wred_index(d, lu, col, n, kc);
+  const int co = lu / (d.np / 64);
   float acc = 0.f;
   if (n <= kc) {   // slab padding columns (n > kc) are never read
     const float* p = part + d.part_off + (size_t)co * d.np + n;
@@ -1098,12 +1177,8 @@ __device__ __forceinline__ void wred_unit(const float* __restrict__ part, float*
   __syncthreads();
   if (g == 0 && n <= kc) {
     const float v = (red[0][col] + red[1][col]) + (red[2][col] + red[3][col]);
-    if (n < kc) {
-      const int tap = n / d.cin, ci = n % d.cin;
-      grad[d.w_off + ((size_t)co * d.cin + ci) * kk + tap] = v;
-    } else {
-      grad[d.b_off + co] = v;
-    }
+    grad[idx] = v;
+    if (val) val[col] = v;
   }
   __syncthreads();   // red is reused by the block's next unit
 }
@@ -1128,14 +1203,55 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(
   }
   if (opt_init && bid == 0 && threadIdx.x == 0)
     apply_book(iter, opt_init, book_period, bump, book_inc);
+  // fused steps (rest_apply): every remaining parameter is updated here,
+  // where its gradient becomes final -- no separate apply launch
+  const bool rest = fat.rest != 0;
   if (bid >= nub) {
     head_sums(bid - nub, hs.B, hs.dqbuf, hs.lpart, hs.h4q, hs.dh4, hs.loss, hs.gw5, hs.gb5,
-              hs.gb4);
+              hs.gb4, rest, fat, faa);
     return;
   }
-  for (int u = bid; u < nunits; u += nub) {
-    const WredDims d = u >= d1.blk0 ? d1 : (u >= d2.blk0 ? d2 : d0);
-    wred_unit(part, grad, d, u - d.blk0, red);
+  if (!rest) {
+    for (int u = bid; u < nunits; u += nub) {
+      const WredDims d = u >= d1.blk0 ? d1 : (u >= d2.blk0 ? d2 : d0);
+      wred_unit(part, grad, d, u - d.blk0, red, nullptr);
+    }
+    return;
+  }
+  // fused steps: groups of 4 units; thread t updates element (unit t/64,
+  // column t%64) of its group once the 4 sums are in LDS, with its theta /
+  // state loaded before the group's slab loads
+  __shared__ float val[4][64];
+  const bool first = fat.opt_init[2] != 0, sync = fat.opt_init[3] != 0;
+  for (int u0 = bid; u0 < nunits; u0 += 4 * nub) {
+    // k is per wave: readfirstlane keeps the layer selection below scalar
+    const int k = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), col = threadIdx.x & 63;
+    const int u = u0 + k * nub;
+    int n = 0, kc = -1;
+    int64_t idx = 0;
+    float th = 0.f, st = 0.f;
+    if (u < nunits) {
+      const WredDims d = u >= d1.blk0 ? d1 : (u >= d2.blk0 ? d2 : d0);
+      idx = wred_index(d, u - d.blk0, col, n, kc);
+      if (n <= kc) {
+        th = fat.theta[idx];
+        if (faa.rule != 0 && !first) st = fat.opt[idx];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int uj = u0 + j * nub;
+      if (uj < nunits) {
+        const WredDims d = uj >= d1.blk0 ? d1 : (uj >= d2.blk0 ? d2 : d0);
+        wred_unit(part, grad, d, uj - d.blk0, red, val[j]);
+      }
+    }
+    if (u < nunits && n <= kc) {
+      const WredDims d = u >= d1.blk0 ? d1 : (u >= d2.blk0 ? d2 : d0);
+      const ConvDims cd{d.w_off, d.wk_off, d.wks_off, d.cout, d.cin, d.ks};
+      const bool w = n < kc;
+      apply_at(fat, faa, first, sync, idx, val[k][col], th, st, !w, w, cd, (int)(idx - d.w_off));
+    }
   }
 }
 
@@ -1250,7 +1366,8 @@ static ApplyArgs apply_args(const NetBuffers& nb, int rule, float lr, float deca
 
 static ApplyTail apply_tail(const NetBuffers& nb) {
   return ApplyTail{nb.theta[0], nb.grad,  nb.opt,    nb.opt_init,      nb.wk[0],
-                   nb.theta[1], nb.wk[1], nb.wks[0], nb.wks[1], nb.L.wks_total, 0};
+                   nb.theta[1], nb.wk[1], nb.wks[0], nb.wks[1], nb.L.wks_total, 0,
+                   0,           nb.L.w[4], nb.L.b[4], nb.L.b[3]};
 }
 
 // The fused fc4-weight apply (NetBuffers::fa): fc4's weight gradient is final
@@ -1311,12 +1428,10 @@ hipError_t launch_apply(const NetBuffers& nb, int rule, float lr, float decay, f
   Prefetch pf{};
   if (pre) pf = *pre;
   ApplyArgs a = apply_args(nb, rule, lr, decay, eps, momentum, wd, period);
-  if (nb.fa.on) {   // fc4 weights were applied by the slab-reduce launch
-    a.skip_lo = nb.L.w[3];
-    a.skip_len = nb.L.b[3] - nb.L.w[3];
-  }
   if (!booked) hipLaunchKernelGGL(apply_book_kernel, dim3(1), dim3(1), 0, s, nb.iter, nb.opt_init, period);
-  const int blocks = (int)(((a.n - a.skip_len) / 4 + 255) / 256);
+  // fused steps: the slab-reduce launch already updated every parameter
+  const int blocks = nb.fa.on ? 0 : (int)(((a.n - a.skip_len) / 4 + 255) / 256);
+  if (blocks + pf.ng == 0) return hipSuccess;
   hipLaunchKernelGGL(apply_kernel, dim3(blocks + pf.ng), dim3(256), 0, s, apply_tail(nb), a, pf);
   return hipGetLastError();
 }
@@ -1800,7 +1915,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
   int blk = 0;
   for (int l : {0, 2, 1}) {           // unit order: longest slab stacks first
     d[l] = {L.w[l], L.b[l], nb.wpart_off[l], cout[l], cin[l], ks[l], nb.wsplits[l], nb.wnp[l],
-            blk};
+            blk, L.wk_off[l], L.wks_off[l]};
     blk += cout[l] * (nb.wnp[l] / 64);
   }
   {  // conv1 wgrad
@@ -1844,6 +1959,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
       faa.hi = L.b[3];
       nfa = fc4_wgrad_blocks<kFc4ApplyR>(64 * s4 * s4);
       fat.blk0 = nub + kFc4 / 64;
+      fat.rest = 1;   // and everything else where its gradient is reduced
     }
     Prefetch pf{};
     if (pre && nb.fa.on) pf = *pre;
