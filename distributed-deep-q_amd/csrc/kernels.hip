@@ -824,9 +824,10 @@ struct ApplyTail {
   __bf16* wks;               // split forward weights of Q / P (plane stride wks_plane)
   __bf16* wksP;
   int64_t wks_plane;
-  int blk0;                  // first apply block of the launch
+  int nfa;                   // slab reduce: fc4 apply blocks (the first of the launch)
   int rest;                  // slab reduce: also update conv / fc4-bias / fc5 params
   int64_t w5_off, b5_off, b4_off;
+  int skip;                  // experiment builds only: block roles to skip (timing A/B)
 };
 
 __device__ __forceinline__ void apply_at(const ApplyTail& t, const ApplyArgs& a, bool first,
@@ -953,6 +954,7 @@ struct WredDims {
   int64_t w_off, b_off, part_off;
   int cout, cin, ks, splits, np, blk0;   // blk0: first workgroup of this layer
   int64_t wk_off, wks_off;               // the layer's kernel / split layouts (fused apply)
+  int G;                                 // waves per unit (1, 2 or 4)
 };
 
 struct HeadSums {
@@ -1130,16 +1132,17 @@ __device__ __forceinline__ void prefetch_body(const Prefetch& pf, int g) {
               pf.reward, pf.nonterm, bx, b, z);
 }
 
-// Slab reduce: a unit = 64 slab columns n of one (layer, co).  Persistent
-// 256-thread blocks (kWredBlocks, two per CU) walk the units, longest layer
-// first; the 4 waves are split groups g summing slabs s = g, g+4, ... (the
-// order of a plain loop) with up to kWredCh loads in flight per thread, then
-// meet in LDS in fixed order.  Measured: an (almost) empty launch of ~8000
-// waves alone costs ~4.7 us on this chip, and a 4-load-per-round loop left
-// conv1's units (256 slabs) 16 dependent memory rounds deep; one block per
-// unit (1600 blocks) or 1024-thread blocks were both slower.
-constexpr int kWredBlocks = 512;
-constexpr int kWredCh = 32;
+// Slab reduce: a unit = 64 slab columns n of one (layer, co), summed over the
+// layer's slabs s in the order of four interleaved plain loops (group
+// g = s % 4 sums s = g, g+4, ... in turn) combined as (g0 + g1) + (g2 + g3).
+// G waves of a block share one unit (G = 1, 2 or 4 per layer, from its slab
+// count): wave h of the unit loads slabs s = h, h+G, ... -- at most kWredCh
+// in flight per lane, one memory round for this net's slab counts -- into
+// 4/G group accumulators, the groups meet in LDS when G > 1.  Every wave
+// holds one unit, so the launch is one round deep; measured: persistent
+// 4-wave blocks walking 4 units each (one LDS meet per unit) took 5 dependent
+// rounds and ~19 us, an (almost) empty launch of ~8000 waves ~4.7 us.
+constexpr int kWredCh = 64;
 
 __device__ __forceinline__ int64_t wred_index(const WredDims& d, int lu, int col, int& n,
                                               int& kc) {
@@ -1151,108 +1154,104 @@ __device__ __forceinline__ int64_t wred_index(const WredDims& d, int lu, int col
   return n < kc ? d.w_off + ((int64_t)co * d.cin + n % d.cin) * kk + n / d.cin : d.b_off + co;
 }
 
-__device__ __forceinline__ void wred_unit(const float* __restrict__ part, float* __restrict__ grad,
-                                          const WredDims& d, int lu, float (*red)[64],
-                                          float* __restrict__ val) {
-  const int col = threadIdx.x & 63, g = threadIdx.x >> 6;
+template <int G>
+__device__ __forceinline__ void wred_block(const float* __restrict__ part, float* __restrict__ grad,
+                                           const WredDims& d, int lb, float (*red)[4][64],
+                                           bool rest, const ApplyTail& fat,
+                                           const ApplyArgs& faa) {
+  constexpr int NA = 4 / G;   // group accumulators per wave
+  // w is per wave: readfirstlane keeps the unit arithmetic scalar
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), col = threadIdx.x & 63;
+  const int slot = w / G, h = w % G;
+  const int lu = lb * NA + slot;
   int n, kc;
   const int64_t idx = wred_index(d, lu, col, n, kc);
-  const int co = lu / (d.np / 64);
-  float acc = 0.f;
-  if (n <= kc) {   // slab padding columns (n > kc) are never read
+  const bool live = n <= kc;   // slab padding columns (n > kc) are never read
+  // fused steps: the unit's element is updated here once its gradient is
+  // final; theta / state are loaded before the slab loads
+  const bool first = rest && fat.opt_init[2] != 0, sync = rest && fat.opt_init[3] != 0;
+  float th = 0.f, st = 0.f;
+  if (rest && h == 0 && live) {
+    th = fat.theta[idx];
+    if (faa.rule != 0 && !first) st = fat.opt[idx];
+  }
+  float acc[NA];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) acc[j] = 0.f;
+  if (live) {
+    const int co = lu / (d.np / 64);
     const float* p = part + d.part_off + (size_t)co * d.np + n;
     const size_t stride = (size_t)d.cout * d.np;
-    const int cnt = (d.splits - g + 3) >> 2;          // this group's slabs g + 4i
+    const int cnt = (d.splits - h + G - 1) / G;          // this wave's slabs h + G i
     for (int i0 = 0; i0 < cnt; i0 += kWredCh) {
       float v[kWredCh];
 #pragma unroll
-      for (int u = 0; u < kWredCh; ++u)               // clamped, unconditional
-        v[u] = p[(size_t)(g + 4 * min(i0 + u, cnt - 1)) * stride];
+      for (int u = 0; u < kWredCh; ++u)                 // clamped, unconditional
+        v[u] = p[(size_t)(h + G * min(i0 + u, cnt - 1)) * stride];
 #pragma unroll
-      for (int u = 0; u < kWredCh; ++u)
-        if (i0 + u < cnt) acc += v[u];
+      for (int u = 0; u < kWredCh; ++u)                 // slab h + G (i0 + u): group
+        if (i0 + u < cnt) acc[u % NA] += v[u];          // h + G (u % NA)
     }
   }
-  red[g][col] = acc;
-  __syncthreads();
-  if (g == 0 && n <= kc) {
-    const float v = (red[0][col] + red[1][col]) + (red[2][col] + red[3][col]);
-    grad[idx] = v;
-    if (val) val[col] = v;
+  float v;
+  if constexpr (G == 1) {
+    v = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < NA; ++j) red[slot][h + G * j][col] = acc[j];
+    __syncthreads();
+    v = (red[slot][0][col] + red[slot][1][col]) + (red[slot][2][col] + red[slot][3][col]);
   }
-  __syncthreads();   // red is reused by the block's next unit
+  if (h == 0 && live) {
+    grad[idx] = v;
+    if (rest) {
+      const ConvDims cd{d.w_off, d.wk_off, d.wks_off, d.cout, d.cin, d.ks};
+      const bool wt = n < kc;
+      apply_at(fat, faa, first, sync, idx, v, th, st, !wt, wt, cd, (int)(idx - d.w_off));
+    }
+  }
 }
 
-// Units [d.blk0, ...) of each layer (conv1, conv3, conv2 order: d0 < d2 <
-// d1), blocks [0, nub) persistent over the units, blocks [nub, nub + 8) the
-// head sums; block 0 also latches the apply bookkeeping.
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(
+// Reduce blocks [d.blk0, ...) of each layer (conv1, conv3, conv2 order: d0 <
+// d2 < d1; a block holds 4 / G units), blocks [nub, nub + 8) the head sums;
+// block 0 also latches the apply bookkeeping.  Fused steps (fat.rest) update
+// every parameter here, where its gradient becomes final -- no separate apply
+// launch.
+__global__ __launch_bounds__(256, 4) void wgrad_reduce_kernel(
     const float* __restrict__ part, float* __restrict__ grad, WredDims d0, WredDims d1,
-    WredDims d2, int nunits, int nub, int64_t* iter, int32_t* opt_init, int book_period,
+    WredDims d2, int nub, int64_t* iter, int32_t* opt_init, int book_period,
     ReplayMeta* bump, int book_inc, HeadSums hs, ApplyTail fat, ApplyArgs faa, Prefetch pf,
     const float* __restrict__ fc4_x, int fc4_k) {
-  __shared__ float red[4][64];
+  __shared__ float red[4][4][64];
   if ((int)blockIdx.x < pf.ng) {   // fused apply: the next step's draw + gather first
-    prefetch_body(pf, blockIdx.x);
+    if (!(fat.skip & 8)) prefetch_body(pf, blockIdx.x);
     return;
   }
-  const int bid = blockIdx.x - pf.ng;
-  if (fat.blk0 > 0 && bid >= fat.blk0) {   // fused fc4-weight gradient + apply blocks
-    fc4_apply_tile(fat, faa, hs.B, fc4_k, hs.dh4, fc4_x, bid - fat.blk0);
-    return;
+  int bid = blockIdx.x - pf.ng;
+  if (fat.nfa > 0) {   // fused fc4-weight gradient + apply blocks come first: the
+                       // longest HBM streams start before the reduce blocks
+    if (bid < fat.nfa) {
+      if (!(fat.skip & 1)) fc4_apply_tile(fat, faa, hs.B, fc4_k, hs.dh4, fc4_x, bid);
+      return;
+    }
+    bid -= fat.nfa;
   }
   if (opt_init && bid == 0 && threadIdx.x == 0)
     apply_book(iter, opt_init, book_period, bump, book_inc);
-  // fused steps (rest_apply): every remaining parameter is updated here,
-  // where its gradient becomes final -- no separate apply launch
   const bool rest = fat.rest != 0;
+  if (fat.skip & (bid >= nub ? 2 : 4)) return;
   if (bid >= nub) {
     head_sums(bid - nub, hs.B, hs.dqbuf, hs.lpart, hs.h4q, hs.dh4, hs.loss, hs.gw5, hs.gb5,
               hs.gb4, rest, fat, faa);
     return;
   }
-  if (!rest) {
-    for (int u = bid; u < nunits; u += nub) {
-      const WredDims d = u >= d1.blk0 ? d1 : (u >= d2.blk0 ? d2 : d0);
-      wred_unit(part, grad, d, u - d.blk0, red, nullptr);
-    }
-    return;
-  }
-  // fused steps: groups of 4 units; thread t updates element (unit t/64,
-  // column t%64) of its group once the 4 sums are in LDS, with its theta /
-  // state loaded before the group's slab loads
-  __shared__ float val[4][64];
-  const bool first = fat.opt_init[2] != 0, sync = fat.opt_init[3] != 0;
-  for (int u0 = bid; u0 < nunits; u0 += 4 * nub) {
-    // k is per wave: readfirstlane keeps the layer selection below scalar
-    const int k = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), col = threadIdx.x & 63;
-    const int u = u0 + k * nub;
-    int n = 0, kc = -1;
-    int64_t idx = 0;
-    float th = 0.f, st = 0.f;
-    if (u < nunits) {
-      const WredDims d = u >= d1.blk0 ? d1 : (u >= d2.blk0 ? d2 : d0);
-      idx = wred_index(d, u - d.blk0, col, n, kc);
-      if (n <= kc) {
-        th = fat.theta[idx];
-        if (faa.rule != 0 && !first) st = fat.opt[idx];
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int uj = u0 + j * nub;
-      if (uj < nunits) {
-        const WredDims d = uj >= d1.blk0 ? d1 : (uj >= d2.blk0 ? d2 : d0);
-        wred_unit(part, grad, d, uj - d.blk0, red, val[j]);
-      }
-    }
-    if (u < nunits && n <= kc) {
-      const WredDims d = u >= d1.blk0 ? d1 : (u >= d2.blk0 ? d2 : d0);
-      const ConvDims cd{d.w_off, d.wk_off, d.wks_off, d.cout, d.cin, d.ks};
-      const bool w = n < kc;
-      apply_at(fat, faa, first, sync, idx, val[k][col], th, st, !w, w, cd, (int)(idx - d.w_off));
-    }
-  }
+  const WredDims& d = bid >= d1.blk0 ? d1 : (bid >= d2.blk0 ? d2 : d0);
+  if (d.G == 1)
+    wred_block<1>(part, grad, d, bid - d.blk0, red, rest, fat, faa);
+  else if (d.G == 2)
+    wred_block<2>(part, grad, d, bid - d.blk0, red, rest, fat, faa);
+  else
+    wred_block<4>(part, grad, d, bid - d.blk0, red, rest, fat, faa);
 }
 
 // Blocks [0, pf.ng) of the apply launch draw + gather the NEXT step's
@@ -1367,7 +1366,7 @@ static ApplyArgs apply_args(const NetBuffers& nb, int rule, float lr, float deca
 static ApplyTail apply_tail(const NetBuffers& nb) {
   return ApplyTail{nb.theta[0], nb.grad,  nb.opt,    nb.opt_init,      nb.wk[0],
                    nb.theta[1], nb.wk[1], nb.wks[0], nb.wks[1], nb.L.wks_total, 0,
-                   0,           nb.L.w[4], nb.L.b[4], nb.L.b[3]};
+                   0,           nb.L.w[4], nb.L.b[4], nb.L.b[3], 0};
 }
 
 // The fused fc4-weight apply (NetBuffers::fa): fc4's weight gradient is final
@@ -1913,10 +1912,13 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
   WredDims d[3];
   const int cout[3] = {32, 64, 64}, cin[3] = {4, 32, 64}, ks[3] = {7, 5, 3};
   int blk = 0;
-  for (int l : {0, 2, 1}) {           // unit order: longest slab stacks first
-    d[l] = {L.w[l], L.b[l], nb.wpart_off[l], cout[l], cin[l], ks[l], nb.wsplits[l], nb.wnp[l],
-            blk, L.wk_off[l], L.wks_off[l]};
-    blk += cout[l] * (nb.wnp[l] / 64);
+  for (int l : {0, 2, 1}) {
+    // waves per unit: enough that each holds at most kWredCh slabs (4 at most)
+    const int sp = nb.wsplits[l];
+    const int G = sp <= kWredCh ? 1 : (sp <= 2 * kWredCh ? 2 : 4);
+    d[l] = {L.w[l], L.b[l], nb.wpart_off[l], cout[l], cin[l], ks[l], sp, nb.wnp[l],
+            blk, L.wk_off[l], L.wks_off[l], G};
+    blk += cout[l] * (nb.wnp[l] / 64) * G / 4;   // units per layer: a multiple of 32
   }
   {  // conv1 wgrad
     ConvWgrad<4, 32, 7, 3> p;
@@ -1948,23 +1950,26 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     M("wgrad_reduce");
     HeadSums hs{0, B, nb.dqbuf, nb.lpart, nb.h4[0], nb.dh4, nb.loss, nb.grad + L.w[4],
                 nb.grad + L.b[4], nb.grad + L.b[3]};
-    const int nub = blk < kWredBlocks ? blk : kWredBlocks;
+    const int nub = blk;
     ApplyTail fat = apply_tail(nb);
     ApplyArgs faa = apply_args(nb, nb.fa.rule, nb.fa.lr, nb.fa.decay, nb.fa.eps, nb.fa.momentum,
                                nb.fa.wd, nb.fa.period);
     int nfa = 0;
-    fat.blk0 = 0;
+    fat.nfa = 0;
     if (nb.fa.on) {   // fc4 weights [w4, b4): its gradient is final since fc4_bwd
       faa.lo = L.w[3];
       faa.hi = L.b[3];
       nfa = fc4_wgrad_blocks<kFc4ApplyR>(64 * s4 * s4);
-      fat.blk0 = nub + kFc4 / 64;
+      fat.nfa = nfa;
       fat.rest = 1;   // and everything else where its gradient is reduced
     }
+#ifdef DDQ_EXPERIMENTS
+    if (const char* e = getenv("DDQ_WRED_SKIP")) fat.skip = atoi(e);
+#endif
     Prefetch pf{};
     if (pre && nb.fa.on) pf = *pre;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(pf.ng + nub + kFc4 / 64 + nfa), dim3(256), 0, s,
-                       nb.wpart, nb.grad, d[0], d[1], d[2], blk, nub, nb.iter,
+                       nb.wpart, nb.grad, d[0], d[1], d[2], nub, nb.iter,
                        book ? nb.opt_init : nullptr, book_period,
                        book && !nb.fa.on ? bump : nullptr, nb.book_inc, hs, fat, faa, pf,
                        nb.pool3[0], 64 * s4 * s4);
