@@ -17,6 +17,7 @@ struct ParamLayout {
   int64_t wk_total;
   int64_t wks_off[3];      // offsets of the split (3 x bf16) forward weights in a wks plane
   int64_t wkst_off;        // conv2 data-gradient split weights [ci][tap'][co] (Q only)
+  int64_t wkst3_off;       // conv3 data-gradient split weights [ci][tap'][co] (Q only)
   int64_t wks_total;       // elements per wks plane (conv1 padded to kx = 8)
 };
 ParamLayout make_layout(int S);

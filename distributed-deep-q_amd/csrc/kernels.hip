@@ -51,7 +51,8 @@ ParamLayout make_layout(int S) {
   // flipped, Wt[ci][tap'][co] = W[co][ci][4-ky][4-kx] (rebuilt by the head
   // kernel of every step from the forward layout)
   L.wkst_off = L.wks_off[2] + wn[2];
-  L.wks_total = L.wkst_off + wn[1];
+  L.wkst3_off = L.wkst_off + wn[1];   // conv3's likewise (Wt[ci][8-tap][co])
+  L.wks_total = L.wkst3_off + wn[2];
   return L;
 }
 
@@ -616,25 +617,27 @@ __global__ __launch_bounds__(512) void fc4_reduce_out_kernel(
 // of the wgrad slab reduce (per-sample dQ and squared error kept in dqbuf /
 // lpart), so the head costs no launch of its own.
 // ---------------------------------------------------------------------------
-// Blocks [B, B + 25) of the head launch: conv2's split forward weights of Q
-// (wks [co][tap][ci]) transposed + flipped for the conv2 data gradient
-// (Wt[ci][24 - tap][co]), one tap per block through LDS, coalesced both ways.
-// The head is a latency-bound 32-block launch, so these blocks ride for free;
-// every step runs its head after the previous apply changed the weights and
-// before its conv2 data gradient.
+// Blocks [B, B + 25 + 9) of the head launch: conv2's and conv3's split
+// forward weights of Q (wks [co][tap][ci], 64 co) transposed + flipped for
+// their data gradients (Wt[ci][T-1 - tap][co]), one tap per block through
+// LDS, coalesced both ways.  The head is a latency-bound 32-block launch, so
+// these blocks ride for free; every step runs its head after the previous
+// apply changed the weights and before its conv data gradients.
+template <int CI, int T>
 __device__ __forceinline__ void wkst_tap(const __bf16* __restrict__ wks, int64_t plane,
                                          int64_t src_off, int64_t dst_off, int t) {
-  __shared__ uint16_t tile[3][64][34];
+  __shared__ uint16_t tile[3][64][CI + 2];
+  constexpr int E = 64 * CI;
   const uint16_t* src = reinterpret_cast<const uint16_t*>(wks) + src_off;
   uint16_t* dst = reinterpret_cast<uint16_t*>(const_cast<__bf16*>(wks)) + dst_off;
-  for (int e = threadIdx.x; e < 3 * 64 * 32; e += blockDim.x) {
-    const int p = e >> 11, r = e & 2047, co = r >> 5, ci = r & 31;
-    tile[p][co][ci] = src[p * plane + (co * 25 + t) * 32 + ci];
+  for (int e = threadIdx.x; e < 3 * E; e += blockDim.x) {
+    const int p = e / E, r = e % E, co = r / CI, ci = r % CI;
+    tile[p][co][ci] = src[p * plane + (co * T + t) * CI + ci];
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < 3 * 32 * 64; e += blockDim.x) {
-    const int p = e >> 11, r = e & 2047, ci = r >> 6, co = r & 63;
-    dst[p * plane + (ci * 25 + 24 - t) * 64 + co] = tile[p][co][ci];
+  for (int e = threadIdx.x; e < 3 * E; e += blockDim.x) {
+    const int p = e / E, r = e % E, ci = r >> 6, co = r & 63;
+    dst[p * plane + (ci * T + T - 1 - t) * 64 + co] = tile[p][co][ci];
   }
 }
 
@@ -646,12 +649,17 @@ __global__ __launch_bounds__(512) void fc4_head_kernel(
     float* __restrict__ outq, float* __restrict__ outp, float* q_sa_o, float* p_sa_o,
     float* target_o, float* __restrict__ dqbuf, float* __restrict__ lpart,
     float* __restrict__ dh4, int32_t* latch, const int64_t* iter, int period, int inc,
-    ReplayMeta* bump, const __bf16* wks, int64_t wks_plane, int64_t wks2_off, int64_t wkst_off) {
+    ReplayMeta* bump, const __bf16* wks, int64_t wks_plane, int64_t wks2_off, int64_t wkst_off,
+    int64_t wks3_off, int64_t wkst3_off) {
   __shared__ float red[8][8];
   __shared__ float qp[8];
   const int b = blockIdx.x, n = threadIdx.x, w = n >> 6;
+  if (b >= B + 25) {
+    wkst_tap<64, 9>(wks, wks_plane, wks3_off, wkst3_off, b - B - 25);
+    return;
+  }
   if (b >= B) {
-    wkst_tap(wks, wks_plane, wks2_off, wkst_off, b - B);
+    wkst_tap<32, 25>(wks, wks_plane, wks2_off, wkst_off, b - B);
     return;
   }
   // fused apply: latch the step's apply flags now (the values apply_book
@@ -935,12 +943,13 @@ __device__ __forceinline__ void head_sums(int hb, int B, const float* __restrict
 
 hipError_t launch_head(const NetBuffers& nb, hipStream_t s, ReplayMeta* bump) {
   const ParamLayout& L = nb.L;
-  hipLaunchKernelGGL(fc4_head_kernel, dim3(nb.B + 25), dim3(kFc4), 0, s, nb.fc4_part, nb.fc4_splits,
+  hipLaunchKernelGGL(fc4_head_kernel, dim3(nb.B + 25 + 9), dim3(kFc4), 0, s, nb.fc4_part, nb.fc4_splits,
                      nb.B, nb.gamma, nb.theta[0], nb.theta[1], L.b[3], L.w[4], L.b[4], nb.action,
                      nb.reward, nb.nonterm, nb.h4[0], nb.h4[1], nb.q_out, nb.p_out, nb.q_sa,
                      nb.p_sa, nb.target, nb.dqbuf, nb.lpart, nb.dh4,
                      nb.fa.on ? nb.opt_init : nullptr, nb.iter, nb.fa.period, nb.book_inc,
-                     nb.fa.on ? bump : nullptr, nb.wks[0], L.wks_total, L.wks_off[1], L.wkst_off);
+                     nb.fa.on ? bump : nullptr, nb.wks[0], L.wks_total, L.wks_off[1], L.wkst_off,
+                     L.wks_off[2], L.wkst3_off);
   return hipGetLastError();
 }
 
@@ -1623,7 +1632,9 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
       a2.out[1] = nullptr;
       a2.out_elems = (int64_t)B * (H / 2) * (H / 2) * 64;
       a2.mask[0] = nb.mask2; a2.mask[1] = nullptr;
-      CHECK_LAUNCH((launch_split_conv<32, 32, 64, 5, 16, 16, 8, 2, false>(a2, nz, s)));
+      // (k groups here -- 4x2 waves x 2 groups, 2 m tiles a wave -- measured
+      // 32.2 against 31.4 us: the 16 waves already cover the LDS latency)
+      CHECK_LAUNCH((launch_split_conv<32, 32, 64, 5, 16, 16, 8, 2, 1, false>(a2, nz, s)));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgConv2F>(p, nz, 1, s));
     }
@@ -1656,7 +1667,9 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
       a3.wk_elems = L.wks_total;
       a3.nchw = 1;
       a3.mask[0] = nb.mask3; a3.mask[1] = nullptr;
-      CHECK_LAUNCH((launch_split_conv<64, 64, 64, 3, 8, 8, 2, 2, false>(a3, nz, s)));
+      // two k groups of 4 waves (2 waves per SIMD on the LDS-bound single
+      // workgroup per CU): 12.6 -> 11.3 us; four groups measured the same
+      CHECK_LAUNCH((launch_split_conv<64, 64, 64, 3, 8, 8, 2, 2, 2, false>(a3, nz, s)));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgConv3F>(p, nz, 1, s));
     }
@@ -1840,19 +1853,19 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     p.dconv = nb.dconv3; p.wk = nb.wk[0] + L.wk_off[2]; p.pmask = nb.mask2; p.pdconv = nb.dconv2;
     M("conv3_dgrad");
     if (nb.conv_impl == 1) {
-      DirectArgs d = direct_dgrad_args(nb.dconv3, p.wk, nb.mask2, nb.dconv2, B, H, 1);
-      d.in_route = nb.mask3;   // pooled dconv3, expanded while the patch is staged
-      // 4x8-pixel tiles (256 workgroups instead of 128: -2.5 us) with the B
-      // operand straight from L2 (register-B, no weight ring: -2.5 us more);
-      // the pool2-output gradient leaves pooled and split only (the conv2
-      // wgrad / dgrad expand it through mask2).  (The split kernel,
-      // split_conv<64,64,64,3,8,8,2,2,DGRAD> on 128 workgroups: 14.3 us
-      // against 12.9 here.)
-      d.pdconv = nullptr;
-      d.pd_pooled = 1;
-      d.pd_split = nb.dconv2s;
-      d.pd_split_elems = (int64_t)B * H * H * 64;
-      CHECK_LAUNCH((launch_direct<64, 64, 3, 4, 8, 1, 2, true, false, 3, true>(d, 1, s)));
+      // split bf16 on conv3's transposed + flipped split weights (built by the
+      // head), the fp32 pooled dpool3 of the fc4 data gradient expanded
+      // through pool3's routing bytes and split while the patch is staged;
+      // 4x8-pixel tiles (256 workgroups) x four k groups (8 waves): 12.5 ->
+      // 8.5 us against the f32 direct kernel (4 waves, register-B).  The
+      // pool2-output gradient leaves pooled and split only (conv2's weight /
+      // data gradients expand it through mask2).
+      SplitArgs a{};
+      a.B = B; a.H = H; a.W = H; a.pad = 1;
+      a.in_f32 = nb.dconv3; a.in_route = nb.mask3;
+      a.wk[0] = nb.wks[0] + L.wkst3_off; a.wk_elems = L.wks_total;
+      a.pd_split = nb.dconv2s; a.pd_elems = (int64_t)B * H * H * 64;
+      CHECK_LAUNCH((launch_split_conv<64, 64, 64, 3, 4, 8, 1, 2, 4, true>(a, 1, s)));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgD3>(p, 1, 1, s));
     }
@@ -1903,7 +1916,11 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
       a.wk[0] = nb.wks[0] + L.wkst_off; a.wk_elems = L.wks_total;
       a.in_route = nb.mask2;
       a.pd_split = nb.dconv1s; a.pd_elems = (int64_t)B * H * H * 32;
-      CHECK_LAUNCH((launch_split_conv<64, 64, 32, 5, 8, 16, 4, 1, true>(a, 1, s)));
+      // four k groups (one 16-channel k-step of every tap each): 16 waves on
+      // the CU's single workgroup instead of 4 -- 28.8 -> 20.9 us (two groups
+      // 23.3); the groups' sums meet in LDS in fixed order and every group
+      // stores a quarter of the epilogue
+      CHECK_LAUNCH((launch_split_conv<64, 64, 32, 5, 8, 16, 4, 1, 4, true>(a, 1, s)));
     } else {
       CHECK_LAUNCH(launch_gemm<CfgD2>(p, 1, 1, s));
     }

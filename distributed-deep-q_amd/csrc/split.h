@@ -94,7 +94,7 @@ __device__ __forceinline__ void store_split(__bf16* t, int64_t E, int64_t e, flo
 // CPT input channels are processed in NCH = CPT / CP chunks of CP (the patch
 // of one chunk is resident at a time: conv2 dgrad's 64-channel patch of a
 // 16 x 16 tile would not fit LDS with its 3 planes).
-template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN>
+template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK = 1>
 struct SplitCfg {
   static constexpr int NCH = CPT / CP;
   static constexpr int PH = TY + KS - 1, PW = TX + KS - 1;
@@ -104,8 +104,9 @@ struct SplitCfg {
   static constexpr int CW = CP + 8;                                   // bf16 per weight row
   static constexpr int T = KS * KS;
   static constexpr int KSTEP = CP / 16;
-  static constexpr int kGroup = 64 * WM * WN;
+  static constexpr int kGroup = 64 * WM * WN * WK;                     // all waves stage
   static constexpr int kThreads = kGroup;
+  static constexpr int KSW = KSTEP / WK;                              // k-steps per wave
   static constexpr int TM = TY * TX / WM / 32;
   static constexpr int TN = N / WN / 32;
   static constexpr int kPlane = PH * RS;                              // bf16 per patch plane
@@ -116,6 +117,10 @@ struct SplitCfg {
   static_assert(CPT % CP == 0 && CP % 16 == 0 && TY % 2 == 0 && TX % 2 == 0, "shape");
   static_assert(TM >= 1 && TN >= 1 && TY * TX == WM * TM * 32 && N == WN * TN * 32, "wave tile");
   static_assert(kSmemB <= 160 * 1024, "LDS budget");
+  static_assert(KSTEP % WK == 0, "k split");
+  // every k group's accumulators for the fixed-order sums of the epilogue
+  static_assert(WK == 1 || WK * WM * WN * 16 * 64 * 4 <= kSmemB, "k-split reduction");
+  static_assert(4 % WK == 0, "epilogue windows per k group");
 };
 
 // Weight staging of one (chunk, tap) (3 planes of N x CP bf16): a global ->
@@ -169,6 +174,8 @@ struct SplitArgs {
   int nchw;                  // fwd: fp32 output in Caffe (B,N,H/2,W/2) order
   uint8_t* mask[2];          // fwd: NHWC routing bytes (nullable)
   const uint8_t* in_route;   // dgrad: routing bytes of the pooled source (NHWC)
+  const float* in_f32;       // dgrad: the pooled source in fp32 (B,H/2,W/2,CPT), split
+                             // while staged (instead of in; conv3's, from fc4)
   float* pd;                 // dgrad: fp32 gradient of the previous pool output (nullable)
   __bf16* pd_split;          // dgrad: split gradient of the previous pool output (nullable)
   int64_t pd_elems;
@@ -181,10 +188,12 @@ struct SplitArgs {
 //         NHWC output, the routing byte (0..3, 4 = ReLU'd window) to mask.
 //  dgrad: the gradient of the previous layer's pool output, NHWC, fp32 and / or
 //         split (the consumer routes it through that pool's mask).
-template <int TM, int TN, int TX, int N, bool DGRAD>
+// With WK k groups, group wkg finishes the windows gi (rows 4gi..4gi+3) with
+// gi % WK == wkg.
+template <int TM, int TN, int TX, int N, bool DGRAD, int WK = 1>
 __device__ __forceinline__ void split_epilogue(const SplitArgs& a, const f32x16 (&acc)[TM][TN],
                                                int b, int z, int y0, int x0, int wmi, int wni,
-                                               int l31, int h) {
+                                               int l31, int h, int wkg = 0) {
   const float* __restrict__ biasz = z ? a.bias[1] : a.bias[0];
   float* __restrict__ outz = z ? a.out[1] : a.out[0];
   __bf16* __restrict__ osplit = z ? a.out_split[1] : a.out_split[0];
@@ -200,6 +209,7 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, const f32x16 
         const float bvv = biasz[n];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
+          if (g % WK != wkg) continue;
           const int win = (mb + 8 * g + 4 * h) >> 2;
           const int pyy = y0 / 2 + win / (TX / 2), pxx = x0 / 2 + win % (TX / 2);
           if (pyy >= Hp || pxx >= Wp) continue;
@@ -221,6 +231,7 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, const f32x16 
       } else {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
+          if ((r >> 2) % WK != wkg) continue;
           const int m = mb + (r & 3) + 8 * (r >> 2) + 4 * h;
           const int win = m >> 2;
           const int y = y0 + 2 * (win / (TX / 2)) + ((m >> 1) & 1);
@@ -235,10 +246,10 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, const f32x16 
   }
 }
 
-template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, bool DGRAD>
+template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, bool DGRAD>
 __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, int bx, int by,
                                                 int bz) {
-  using C = SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN>;
+  using C = SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK>;
   constexpr int TM = C::TM, TN = C::TN, T = C::T, NCH = C::NCH;
   __bf16* patch = reinterpret_cast<__bf16*>(smem);
   __bf16* wbuf = reinterpret_cast<__bf16*>(smem + C::kPatchB);
@@ -252,7 +263,7 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
   // ---- stage the halo patch of channel chunk ch (3 planes, zero outside) ----
   // Batches of 8 vectors per thread: every load of a batch is issued before
   // its LDS stores (a load -> store loop pays one memory latency per vector).
-  auto stage_patch = [&](int ch) {
+  auto stage_patch_split = [&](int ch) {
     constexpr int NV = C::PH * C::PW * (CP / 8);           // 16-byte vectors per plane
     constexpr int NIT = (3 * NV + C::kThreads - 1) / C::kThreads;
     constexpr int BAT = 8;
@@ -298,6 +309,72 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
     }
   };
 
+  // fp32 pooled source (dgrad): a (pixel, 8-channel) item loads 32 B + its 8
+  // routing bytes, keeps the routed quadrant's values, splits them (split3)
+  // and stores all three planes
+  auto stage_patch_f32 = [&](int ch) {
+    constexpr int NI = C::PH * C::PW * (CP / 8);           // items (one per 16-byte vector)
+    constexpr int NIT = (NI + C::kThreads - 1) / C::kThreads;
+    constexpr int BAT = 4;
+#pragma unroll
+    for (int i0 = 0; i0 < NIT; i0 += BAT) {
+      float4 f[BAT][2];
+      uint2 m[BAT];
+      int dst[BAT];
+      uint32_t q[BAT];
+#pragma unroll
+      for (int u = 0; u < BAT; ++u) {
+        const int f0 = tid + (i0 + u) * C::kThreads;
+        const bool live = i0 + u < NIT && f0 < NI;
+        const int r = live ? f0 : 0;
+        const int pix = r / (CP / 8), c8 = r % (CP / 8);
+        const int py = pix / C::PW, px = pix % C::PW;
+        const int gy = y0 - a.pad + py, gx = x0 - a.pad + px;
+        const bool in_img = live && (unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W;
+        dst[u] = live ? py * C::RS + px * C::CS + 8 * c8 : -1;
+        q[u] = ((gy & 1) << 1) | (gx & 1);
+        f[u][0] = f[u][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+        m[u] = make_uint2(0x04040404u, 0x04040404u);
+        if (in_img) {
+          const size_t o = (((size_t)b * (a.H >> 1) + (gy >> 1)) * (a.W >> 1) + (gx >> 1)) * CPT +
+                           ch * CP + 8 * c8;
+          f[u][0] = *reinterpret_cast<const float4*>(a.in_f32 + o);
+          f[u][1] = *reinterpret_cast<const float4*>(a.in_f32 + o + 4);
+          m[u] = *reinterpret_cast<const uint2*>(a.in_route + o);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < BAT; ++u) {
+        if (dst[u] < 0) continue;
+        u32x4 v[3];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {   // bf16 pair e = channels 2e, 2e+1
+          const uint32_t mw = e < 2 ? m[u].x : m[u].y;
+          const uint32_t r0 = (mw >> (16 * (e & 1))) & 0xff;
+          const uint32_t r1 = (mw >> (16 * (e & 1) + 8)) & 0xff;
+          const float4 fv = f[u][e >> 1];
+          const float x0 = r0 == q[u] ? ((e & 1) ? fv.z : fv.x) : 0.f;
+          const float x1 = r1 == q[u] ? ((e & 1) ? fv.w : fv.y) : 0.f;
+          __bf16 h0, m0, l0, h1, m1, l1;
+          split3(x0, h0, m0, l0);
+          split3(x1, h1, m1, l1);
+          v[0][e] = (uint32_t)__builtin_bit_cast(uint16_t, h0) |
+                    ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+          v[1][e] = (uint32_t)__builtin_bit_cast(uint16_t, m0) |
+                    ((uint32_t)__builtin_bit_cast(uint16_t, m1) << 16);
+          v[2][e] = (uint32_t)__builtin_bit_cast(uint16_t, l0) |
+                    ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+        }
+#pragma unroll
+        for (int p = 0; p < 3; ++p) *reinterpret_cast<u32x4*>(patch + p * C::kPlane + dst[u]) = v[p];
+      }
+    }
+  };
+  auto stage_patch = [&](int ch) {
+    if (DGRAD && a.in_f32) stage_patch_f32(ch);
+    else stage_patch_split(ch);
+  };
+
   // ---- weights: step s = (chunk s / T, tap s % T) -> ring slot s & 1 ----
   // Two register sets: the loads of step s+2 are issued at the start of step
   // s and stored at the end of step s+1 (two steps of MFMAs to land in).
@@ -315,18 +392,22 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
 
   // ---- per-lane operand offsets (bf16 units) ----
   const int l31 = lane & 31, h = lane >> 5;
-  const int wmi = wid / WN, wni = wid % WN;
+  // wave = (k group wkg, m block wmi, n block wni); k group wkg runs k-steps
+  // [wkg * KSW, +KSW) of every tap: WK x the waves on the same LDS images
+  const int wkg = wid / (WM * WN), wmn = wid % (WM * WN);
+  const int wmi = wmn / WN, wni = wmn % WN;
   int abase[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int m = wmi * TM * 32 + 32 * i + l31;
     const int win = m >> 2, dy = (m >> 1) & 1, dx = m & 1;
     const int wy = win / (TX / 2), wx = win % (TX / 2);
-    abase[i] = (2 * wy + dy) * C::RS + (2 * wx + dx) * C::CS + h * 8;
+    abase[i] = (2 * wy + dy) * C::RS + (2 * wx + dx) * C::CS + h * 8 + 16 * C::KSW * wkg;
   }
   int bbase[TN];
 #pragma unroll
-  for (int j = 0; j < TN; ++j) bbase[j] = (wni * TN * 32 + 32 * j + l31) * C::CW + h * 8;
+  for (int j = 0; j < TN; ++j)
+    bbase[j] = (wni * TN * 32 + 32 * j + l31) * C::CW + h * 8 + 16 * C::KSW * wkg;
 
   f32x16 acc[TM][TN], cor[TM][TN];
 #pragma unroll
@@ -342,7 +423,7 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
     const int ky = t / KS, kx = t % KS;
     const __bf16* pa = patch + ky * C::RS + kx * C::CS;
 #pragma unroll
-    for (int g = 0; g < C::KSTEP; ++g) {
+    for (int g = 0; g < C::KSW; ++g) {
       bf16x8 av[3][TM], bv[3][TN];
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
@@ -401,20 +482,44 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] += cor[i][j];
-  split_epilogue<TM, TN, TX, N, DGRAD>(a, acc, b, z, y0, x0, wmi, wni, l31, h);
+  if (WK > 1) {
+    // every k group parks its sums in LDS; group k then finishes the pooling
+    // windows gi (4 accumulator rows each) with gi % WK == k, summing the
+    // groups in fixed order 0..WK-1 (deterministic), so all waves share the
+    // epilogue's stores
+    float* red = reinterpret_cast<float*>(smem);   // one 32x32 tile per wave at a time
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        __syncthreads();                            // patch / previous tile reads done
+#pragma unroll
+        for (int r = 0; r < 16; ++r) red[((wkg * WM * WN + wmn) * 16 + r) * 64 + lane] = acc[i][j][r];
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          if ((r >> 2) % WK != wkg) continue;      // (wave-uniform)
+          float v = 0.f;
+#pragma unroll
+          for (int k = 0; k < WK; ++k) v += red[((k * WM * WN + wmn) * 16 + r) * 64 + lane];
+          acc[i][j][r] = v;
+        }
+      }
+  }
+  split_epilogue<TM, TN, TX, N, DGRAD, WK>(a, acc, b, z, y0, x0, wmi, wni, l31, h, wkg);
 }
 
-template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, bool DGRAD>
-__global__ __launch_bounds__(64 * WM * WN) void split_conv_kernel(const SplitArgs a) {
+template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, bool DGRAD>
+__global__ __launch_bounds__(64 * WM * WN * WK) void split_conv_kernel(const SplitArgs a) {
   extern __shared__ __attribute__((aligned(16))) char sm_split[];
-  split_conv_body<CPT, CP, N, KS, TY, TX, WM, WN, DGRAD>(a, sm_split, blockIdx.x, blockIdx.y,
-                                                        blockIdx.z);
+  split_conv_body<CPT, CP, N, KS, TY, TX, WM, WN, WK, DGRAD>(a, sm_split, blockIdx.x, blockIdx.y,
+                                                            blockIdx.z);
 }
 
-template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, bool DGRAD>
+template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, bool DGRAD>
 inline hipError_t launch_split_conv(SplitArgs a, int nz, hipStream_t st) {
-  using C = SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN>;
-  auto kern = split_conv_kernel<CPT, CP, N, KS, TY, TX, WM, WN, DGRAD>;
+  using C = SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK>;
+  auto kern = split_conv_kernel<CPT, CP, N, KS, TY, TX, WM, WN, WK, DGRAD>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),

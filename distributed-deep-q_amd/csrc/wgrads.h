@@ -92,12 +92,18 @@ __device__ __forceinline__ void wgrads_body(const WgradSArgs& a, char* smem, int
 
   // zero the pixels rows never write: the input halo / tail, the dconv tail
   {
-    const int wi = Geo::w16(W) + 2 * PAD + 8;
-    for (int i = lane; i < 3 * wi * (Geo::PSI / 8); i += 64) {
-      const int p = i / (wi * (Geo::PSI / 8)), r = i - p * wi * (Geo::PSI / 8);
-      const int x = r / (Geo::PSI / 8);
-      if (x < PAD || x >= W + PAD) reinterpret_cast<u32x4*>(rin + p * ipl)[r] = u32x4{0u, 0u, 0u, 0u};
-    }
+    // only the halo / tail pixels (x < PAD, x >= W + PAD), compile-time
+    // divisors: walking every pixel with runtime divisions cost ~1500 VALU a
+    // wave, more than conv3's MFMAs of a wave's rows
+    constexpr int CPV = Geo::PSI / 8;
+    const int nh = Geo::w16(W) + 2 * PAD + 8 - W;   // halo + tail pixels of a row
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      for (int i = lane; i < nh * CPV; i += 64) {
+        const int hx = i / CPV, c = i % CPV;
+        const int x = hx < PAD ? hx : hx + W;
+        reinterpret_cast<u32x4*>(rin + p * ipl + x * Geo::PSI)[c] = u32x4{0u, 0u, 0u, 0u};
+      }
     for (int i = lane; i < 3 * (Geo::w16(W) - W) * (Geo::PSD / 8); i += 64) {
       const int per = (Geo::w16(W) - W) * (Geo::PSD / 8);
       const int p = i / per, r = i - p * per;

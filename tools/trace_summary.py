@@ -13,8 +13,8 @@ import sys
 
 SHORT = [("sample_gather_kernel", "sample"), ("split_conv1_kernel", "c1f"),
          ("split_conv_kernel<32, 32, 64, 5", "c2f"),
-         ("split_conv_kernel<64, 64, 64, 3, 8, 8, 2, 2, false", "c3f"),
-         ("split_conv_kernel<64, 64, 64, 3, 8, 8, 2, 2, true", "c3d"),
+         ("split_conv_kernel<64, 64, 64, 3, 8, 8, 2, 2,", "c3f"),
+         ("split_conv_kernel<64, 64, 64, 3, 4, 8,", "c3d"),
          ("split_conv_kernel<64, 64, 32, 5", "c2d"),
          ("wgrads_kernel<64, 64, 3", "c3w"), ("wgrads_kernel<32, 64, 5", "c2w"),
          ("wgrad1s_kernel", "c1w"),

@@ -81,13 +81,13 @@ static void run(const char* name, const Prob& P, int reps) {
     a.out[z] = dout + z * Eo; a.out_split[z] = dos + z * 3 * Eo; a.mask[z] = dm + z * Eo;
   }
   a.in_elems = x.size(); a.wk_elems = w.size(); a.out_elems = Eo;
-  CK((launch_split_conv<CPT, CP, N, KS, TY, TX, WM, WN, false>(a, P.nz, 0)));
+  CK((launch_split_conv<CPT, CP, N, KS, TY, TX, WM, WN, 1, false>(a, P.nz, 0)));
   CK(hipDeviceSynchronize());
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   CK(hipEventRecord(e0, 0));
-  for (int i = 0; i < reps; ++i) CK((launch_split_conv<CPT, CP, N, KS, TY, TX, WM, WN, false>(a, P.nz, 0)));
+  for (int i = 0; i < reps; ++i) CK((launch_split_conv<CPT, CP, N, KS, TY, TX, WM, WN, 1, false>(a, P.nz, 0)));
   CK(hipEventRecord(e1, 0));
   CK(hipEventSynchronize(e1));
   float ms;
