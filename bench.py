@@ -58,9 +58,9 @@ KERNEL_SYMBOL = {
     "conv1_fwd": "void ddq::split_conv1_kernel",
     "conv2_fwd": "void ddq::split_conv_kernel<32, 32, 64, 5,",
     "conv3_fwd": "void ddq::split_conv_kernel<64, 64, 64, 3, 8, 8, 2, 2,",
-    "fc4_fwd": "void ddq::fc4_fwd_direct_kernel",
+    "fc4_fwd": "void ddq::fc4_fwd_split_kernel",
     "head": "ddq::fc4_head_kernel",
-    "fc4_dgrad": "ddq::fc4_dgrad_direct_kernel",
+    "fc4_dgrad": "void ddq::fc4_dgrad_direct_kernel",
     "fc4_wgrad": "ddq::fc4_wgrad_kernel",
     "conv3_wgrad": "void ddq::wgrads_kernel<64, 64, 3, 1",
     "conv3_dgrad": "void ddq::split_conv_kernel<64, 64, 64, 3, 4, 8,",
@@ -79,7 +79,7 @@ KERNEL_SYMBOL = {
 KERNEL_ARITH = {
     "conv1_fwd": "split3", "conv2_fwd": "split", "conv3_fwd": "split",
     "conv1_wgrad": "split3", "conv2_wgrad": "split", "conv3_wgrad": "split",
-    "conv2_dgrad": "split", "conv3_dgrad": "split", "fc4_fwd": "f32", "fc4_dgrad": "f32",
+    "conv2_dgrad": "split", "conv3_dgrad": "split", "fc4_fwd": "split", "fc4_dgrad": "split",
     "fc4_wgrad": "f32",
 }
 BF16_MFMA_PEAK = 2.5e15       # MI355X_MICROARCH.md: dense bf16

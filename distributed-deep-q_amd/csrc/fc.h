@@ -133,15 +133,132 @@ __global__ __launch_bounds__(256) void fc4_fwd_direct_kernel(const Fc4FwdArgs a)
     }
 }
 
+// The same tile on the bf16 matrix cores with fp32-exact split operands
+// (split.h): the f32 MFMA's 64 cycles per 2 k left the wave's 64 MFMAs
+// (4096 cycles) behind its W4 loads.  Per 32-k block a lane's 16 consecutive
+// k (16h .. 16h+15) are two 8-k halves, one per 32x32x16 step: step s pairs
+// k = 16h + 8s + e of both operands (a permutation of the block's k, the
+// same for A and B), 6 MFMAs a step (192 cycles against 1024 per block).  The
+// x tile is split once while staged (3 bf16 planes in LDS, row stride
+// 136 bf16: conflict-free b128 reads); the W values are split in registers.
+__device__ __forceinline__ void split8(const float4& lo, const float4& hi, bf16x8& s0, bf16x8& s1,
+                                       bf16x8& s2) {
+  const float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    __bf16 h, m, l;
+    split3(v[e], h, m, l);
+    s0[e] = h;
+    s1[e] = m;
+    s2[e] = l;
+  }
+}
+
+template <int BT>
+__global__ __launch_bounds__(256) void fc4_fwd_split_kernel(const Fc4FwdArgs a) {
+  constexpr int XSB = kFc4KLen + 8;     // bf16 per LDS row (272 B)
+  __shared__ __attribute__((aligned(16))) __bf16 xs[3][BT * 32 * XSB];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int l31 = lane & 31, h = lane >> 5;
+  const int z = blockIdx.z % a.nz, split = blockIdx.y;
+  const int bt0 = (blockIdx.z / a.nz) * (BT * 32);
+  const int n0 = blockIdx.x * 128 + w * 32;
+  const int K = a.K;
+  const int k0 = split * kFc4KLen;
+  const __amdgpu_buffer_rsrc_t rw = fc_rsrc(z ? a.w[1] : a.w[0], (uint32_t)(512 * K * 4));
+  const __amdgpu_buffer_rsrc_t rx = fc_rsrc(z ? a.x[1] : a.x[0], (uint32_t)(a.B * K * 4));
+  const uint32_t wrow = (uint32_t)((n0 + l31) * K + h * 16) * 4;
+
+  f32x16 acc[BT], cor[BT];
+#pragma unroll
+  for (int t = 0; t < BT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { acc[t][r] = 0.f; cor[t][r] = 0.f; }
+
+  constexpr int kC4 = kFc4KLen / 4;
+  constexpr int NX = BT * 32 * kC4 / 256;
+  static_assert(NX * 256 == BT * 32 * kC4, "x tile / workgroup");
+  float4 xv[NX];
+#pragma unroll
+  for (int it = 0; it < NX; ++it) {
+    const int f = threadIdx.x + 256 * it;
+    const int r = f / kC4, c4 = f % kC4;
+    const int k = k0 + 4 * c4;
+    xv[it] = fc_ld4(rx, k < K ? (uint32_t)((bt0 + r) * K + k) * 4 : kFcOOB);
+  }
+  float4 wv[kFc4KLen / 32][4];
+#pragma unroll
+  for (int kb = 0; kb < kFc4KLen / 32; ++kb) {
+    const int k = k0 + kb * 32;
+    const bool kin = k < K;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) wv[kb][i] = fc_ld4(rw, kin ? wrow + (k + 4 * i) * 4 : kFcOOB);
+  }
+#pragma unroll
+  for (int it = 0; it < NX; ++it) {
+    const int f = threadIdx.x + 256 * it;
+    const int o = (f / kC4) * XSB + 4 * (f % kC4);
+    const float v[4] = {xv[it].x, xv[it].y, xv[it].z, xv[it].w};
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    bf16x4 p0, p1, p2;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      __bf16 hh, mm, ll;
+      split3(v[e], hh, mm, ll);
+      p0[e] = hh;
+      p1[e] = mm;
+      p2[e] = ll;
+    }
+    *reinterpret_cast<bf16x4*>(&xs[0][o]) = p0;
+    *reinterpret_cast<bf16x4*>(&xs[1][o]) = p1;
+    *reinterpret_cast<bf16x4*>(&xs[2][o]) = p2;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int kb = 0; kb < kFc4KLen / 32; ++kb)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 b0, b1, b2;
+      split8(wv[kb][2 * s], wv[kb][2 * s + 1], b0, b1, b2);
+#pragma unroll
+      for (int t = 0; t < BT; ++t) {
+        const int o = (t * 32 + l31) * XSB + kb * 32 + 16 * h + 8 * s;
+        const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(&xs[0][o]);
+        const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(&xs[1][o]);
+        const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(&xs[2][o]);
+        cor[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, cor[t], 0, 0, 0);
+        cor[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, cor[t], 0, 0, 0);
+        cor[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, cor[t], 0, 0, 0);
+        cor[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, cor[t], 0, 0, 0);
+        cor[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, cor[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[t], 0, 0, 0);
+      }
+    }
+  const __amdgpu_buffer_rsrc_t rp =
+      wt_rsrc(a.part, (uint32_t)((size_t)gridDim.y * a.nz * a.B * 512 * 4));
+  const uint32_t dbase = (uint32_t)((((size_t)(split * a.nz + z) * a.B) * 512 + n0 + l31) * 4);
+#pragma unroll
+  for (int t = 0; t < BT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int b = bt0 + t * 32 + fc_acc_row(r, lane);
+      if (b < a.B) wt_store(rp, dbase + (uint32_t)b * 2048, acc[t][r] + cor[t][r]);
+    }
+}
+
 inline int fc4_fwd_splits(int K) { return (K + kFc4KLen - 1) / kFc4KLen; }
 
 inline hipError_t launch_fc4_fwd_direct(const Fc4FwdArgs& a, hipStream_t st) {
+  bool sp = true;
+#ifdef DDQ_EXPERIMENTS
+  if (const char* e = getenv("DDQ_FC4_SPLIT")) sp = atoi(e) != 0;
+#endif
   if (a.B <= 32) {
-    hipLaunchKernelGGL(fc4_fwd_direct_kernel<1>, dim3(512 / 128, fc4_fwd_splits(a.K), a.nz),
-                       dim3(256), 0, st, a);
+    hipLaunchKernelGGL(sp ? fc4_fwd_split_kernel<1> : fc4_fwd_direct_kernel<1>,
+                       dim3(512 / 128, fc4_fwd_splits(a.K), a.nz), dim3(256), 0, st, a);
   } else {
     const int nbt = (a.B + 63) / 64;
-    hipLaunchKernelGGL(fc4_fwd_direct_kernel<2>,
+    hipLaunchKernelGGL(sp ? fc4_fwd_split_kernel<2> : fc4_fwd_direct_kernel<2>,
                        dim3(512 / 128, fc4_fwd_splits(a.K), a.nz * nbt), dim3(256), 0, st, a);
   }
   return hipGetLastError();
@@ -169,6 +286,10 @@ struct Fc4DgradArgs {
 };
 
 // Body on block (bx, by) with an 8 x 1024-float LDS image; 512 threads.
+// SPLIT: the 32 f32 MFMAs of a wave (64 cycles each) as 24 bf16 ones on
+// fp32-exact split operands (split.h; 32 cycles each): step s of a 32-n block
+// pairs n = 16h + 8s + e of both operands, as fc4_fwd_split_kernel.
+template <bool SPLIT>
 __device__ __forceinline__ void fc4_dgrad_body(const Fc4DgradArgs& a, float (*red)[1024], int bx,
                                                int by) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -194,12 +315,38 @@ __device__ __forceinline__ void fc4_dgrad_body(const Fc4DgradArgs& a, float (*re
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  if (SPLIT) {
+    f32x16 cor;
 #pragma unroll
-  for (int blk = 0; blk < 2; ++blk)
+    for (int r = 0; r < 16; ++r) cor[r] = 0.f;
 #pragma unroll
-    for (int j = 0; j < 16; ++j)
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(av[blk][j >> 2], j & 3), bv[blk][j], acc,
-                                                 0, 0, 0);
+    for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 a0, a1, a2, b0, b1, b2;
+        split8(av[blk][2 * s], av[blk][2 * s + 1], a0, a1, a2);
+        split8(make_float4(bv[blk][8 * s + 0], bv[blk][8 * s + 1], bv[blk][8 * s + 2],
+                           bv[blk][8 * s + 3]),
+               make_float4(bv[blk][8 * s + 4], bv[blk][8 * s + 5], bv[blk][8 * s + 6],
+                           bv[blk][8 * s + 7]),
+               b0, b1, b2);
+        cor = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, cor, 0, 0, 0);
+        cor = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, cor, 0, 0, 0);
+        cor = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, cor, 0, 0, 0);
+        cor = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, cor, 0, 0, 0);
+        cor = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, cor, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc, 0, 0, 0);
+      }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] += cor[r];
+  } else {
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(av[blk][j >> 2], j & 3), bv[blk][j], acc,
+                                                   0, 0, 0);
+  }
 #pragma unroll
   for (int r = 0; r < 16; ++r) red[w][r * 64 + lane] = acc[r];
   __syncthreads();
@@ -233,14 +380,24 @@ __device__ __forceinline__ void fc4_dgrad_body(const Fc4DgradArgs& a, float (*re
   }
 }
 
+template <bool SPLIT>
 __global__ __launch_bounds__(512) void fc4_dgrad_direct_kernel(const Fc4DgradArgs a) {
   __shared__ float red[8][1024];
-  fc4_dgrad_body(a, red, blockIdx.x, blockIdx.y);
+  fc4_dgrad_body<SPLIT>(a, red, blockIdx.x, blockIdx.y);
+}
+
+inline bool fc4_dgrad_split() {
+#ifdef DDQ_EXPERIMENTS
+  if (const char* e = getenv("DDQ_FC4D_SPLIT")) return atoi(e) != 0;
+#endif
+  return true;
 }
 
 inline hipError_t launch_fc4_dgrad_direct(const Fc4DgradArgs& a, hipStream_t st) {
   dim3 grid(a.K / 32, (a.B + 31) / 32);
-  hipLaunchKernelGGL(fc4_dgrad_direct_kernel, grid, dim3(512), 0, st, a);
+  hipLaunchKernelGGL(fc4_dgrad_split() ? fc4_dgrad_direct_kernel<true>
+                                       : fc4_dgrad_direct_kernel<false>,
+                     grid, dim3(512), 0, st, a);
   return hipGetLastError();
 }
 

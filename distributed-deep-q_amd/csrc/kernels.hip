@@ -1530,12 +1530,13 @@ static WgradDArgs wgradd_args(const P& p, int B, int G) {
 // threads; the other 4 waves end at once, which s_barrier does not wait for)
 // (threads 256..511 of a gradient block end at once, which s_barrier does
 // not wait for)
+template <bool SPLIT>
 __global__ __launch_bounds__(512) void fc4_bwd_kernel(const Fc4DgradArgs d, const float* x,
                                                       float* gw4, int nd, int ndx) {
   __shared__ __attribute__((aligned(16))) float smem[8 * 1024];
   const int bid = blockIdx.x;
   if (bid < nd) {
-    fc4_dgrad_body(d, reinterpret_cast<float(*)[1024]>(smem), bid % ndx, bid / ndx);
+    fc4_dgrad_body<SPLIT>(d, reinterpret_cast<float(*)[1024]>(smem), bid % ndx, bid / ndx);
     return;
   }
   if (threadIdx.x >= 256) return;
@@ -1756,7 +1757,8 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     const int ndx = f.K / 32, nd = ndx * ((B + 31) / 32);
     // the fused apply computes the fc4 weight gradient tile by tile itself
     const int nw = nb.fa.on ? 0 : fc4_wgrad_blocks<8>(f.K);
-    hipLaunchKernelGGL(fc4_bwd_kernel, dim3(nd + nw), dim3(512), 0, s, f, nb.pool3[0],
+    hipLaunchKernelGGL(fc4_dgrad_split() ? fc4_bwd_kernel<true> : fc4_bwd_kernel<false>,
+                       dim3(nd + nw), dim3(512), 0, s, f, nb.pool3[0],
                        nb.grad + L.w[3], nd, ndx);
     CHECK_LAUNCH(hipGetLastError());
     if (fc4_done) CHECK_LAUNCH(fc4_done(fc4_done_arg));

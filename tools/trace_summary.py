@@ -20,7 +20,7 @@ SHORT = [("sample_gather_kernel", "sample"), ("split_conv1_kernel", "c1f"),
          ("wgrad1s_kernel", "c1w"),
          ("direct_conv_kernel<4, 32, 7", "c1f"),
          ("direct_conv_kernel<32, 64, 5", "c2f"), ("direct_conv_kernel<64, 64, 3, 8, 8, 2, 2, false", "c3f"),
-         ("fc4_fwd_direct", "fc4f"), ("fc4_head", "head"), ("fc4_dgrad_direct", "fc4d"),
+         ("fc4_fwd_direct", "fc4f"), ("fc4_fwd_split", "fc4f"), ("fc4_head", "head"), ("fc4_dgrad_direct", "fc4d"),
          ("fc4_bwd_kernel", "fc4bwd"), ("FcWgrad", "fc4w"), ("wgradd_kernel<64, 64, 3", "c3w"),
          ("direct_conv_kernel<64, 64, 3, 8, 8, 2, 2, true", "c3d"), ("wgradd_kernel<32, 64, 5", "c2w"),
          ("direct_conv_kernel<64, 32, 5", "c2d"), ("wgrad1_kernel", "c1w"),
