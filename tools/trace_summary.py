@@ -58,7 +58,7 @@ def main():
         except Exception:
             pass
     print("variant %s: %s | sum %.1f us | %s" % (label, val, tot,
-          " ".join("%s=%.1f" % (k, out[k]) for _, k in SHORT if k in out)))
+          " ".join("%s=%.1f" % (k, out[k]) for k in dict.fromkeys(k for _, k in SHORT) if k in out)))
 
 
 if __name__ == "__main__":
