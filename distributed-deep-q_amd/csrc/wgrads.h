@@ -139,50 +139,69 @@ __device__ __forceinline__ void wgrads_body(const WgradSArgs& a, char* smem, int
     float4 f[2][NPD];    // DF32: the 8 fp32 values of the chunk
     u32x2 m[NPD];
   };
-  // Every load is issued unconditionally (clamped to element 0 when out of
-  // range, the value then replaced by zero): with no branches around them the
-  // compiler counts a row set's loads exactly and waits for that set only
-  // (branchy loads made it wait for every outstanding load, vmcnt(0)).
+  // Every load is issued unconditionally as a bounds-checked buffer load: an
+  // out-of-range vector gets the offset kOOB and reads 0, so there is no
+  // select after the load and no 64-bit address math (the loads used to be
+  // clamped to element 0 and zeroed with v_cndmask).  With no branches
+  // around them the compiler counts a row set's loads exactly and waits for
+  // that set only.  The row's (image, y) advance by the wave stride without
+  // a runtime division (H >= 8 > 4).
+  constexpr uint32_t kOOB = 0x80000000u;
+  const uint32_t ib = (uint32_t)(a.in_elems * 2);
+  const __amdgpu_buffer_rsrc_t rin_g[3] = {
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.in, (short)0, (int)ib, 0x00020000),
+      __builtin_amdgcn_make_buffer_rsrc((void*)(a.in + a.in_elems), (short)0, (int)ib, 0x00020000),
+      __builtin_amdgcn_make_buffer_rsrc((void*)(a.in + 2 * a.in_elems), (short)0, (int)ib,
+                                        0x00020000)};
+  const uint32_t db = (uint32_t)(a.B * (H >> 1) * (W >> 1) * COUT);   // elements of a plane
+  const __amdgpu_buffer_rsrc_t rd_g[3] = {
+      __builtin_amdgcn_make_buffer_rsrc((void*)(DF32 ? (const void*)a.dpool_f32 : (const void*)a.dpool),
+                                        (short)0, (int)(DF32 ? db * 4 : db * 2), 0x00020000),
+      __builtin_amdgcn_make_buffer_rsrc((void*)(DF32 ? nullptr : a.dpool + a.d_elems), (short)0,
+                                        (int)(db * 2), 0x00020000),
+      __builtin_amdgcn_make_buffer_rsrc((void*)(DF32 ? nullptr : a.dpool + 2 * a.d_elems), (short)0,
+                                        (int)(db * 2), 0x00020000)};
+  const __amdgpu_buffer_rsrc_t rm_g =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.droute, (short)0, (int)db, 0x00020000);
+  int lb = (r0 + w) / H, ly = (r0 + w) - lb * H;   // (image, y) of the next row to load
   auto load = [&](Regs& R, int row) {
     const bool live = row < r1;
-    const int b = row / H, y = row - b * H, yi = y + ky - PAD;
+    const int yi = ly + ky - PAD;
     const bool vin = live && (unsigned)yi < (unsigned)H;
-    const size_t i0 = (((size_t)b * H + yi) * W + ipx) * CIN + 8 * ic8;
+    const uint32_t i0 = (uint32_t)(((lb * H + yi) * W + ipx) * CIN + 8 * ic8);
 #pragma unroll
     for (int u = 0; u < NPI; ++u) {
       const bool ok = vin && ipx + u * PPP < W;
-      const size_t o = ok ? i0 + (size_t)u * PPP * CIN : 0;
+      const uint32_t o = ok ? (i0 + (uint32_t)(u * PPP * CIN)) * 2 : kOOB;
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        const u32x4 v = *reinterpret_cast<const u32x4*>(a.in + p * a.in_elems + o);
-        R.i[p][u] = ok ? v : u32x4{0u, 0u, 0u, 0u};
-      }
+      for (int p = 0; p < 3; ++p)
+        R.i[p][u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rin_g[p], (int)o, 0, 0));
     }
-    const size_t o0 = (((size_t)b * (H >> 1) + (y >> 1)) * (W >> 1) + dpx) * COUT + cb * 32 + 8 * dc8;
+    const uint32_t o0 =
+        (uint32_t)(((lb * (H >> 1) + (ly >> 1)) * (W >> 1) + dpx) * COUT + cb * 32 + 8 * dc8);
 #pragma unroll
     for (int u = 0; u < NPD; ++u) {
       const bool ok = live && dpx + 16 * u < (W >> 1);
-      const size_t o = ok ? o0 + (size_t)u * 16 * COUT : 0;
-      const u32x2 mv = *reinterpret_cast<const u32x2*>(a.droute + o);
-      R.m[u] = ok ? mv : u32x2{0x04040404u, 0x04040404u};
+      const uint32_t o = ok ? o0 + (uint32_t)(u * 16 * COUT) : 0u;
+      // routing bytes past the range read 0: the values there read 0 as well
+      R.m[u] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rm_g, (int)(ok ? o : kOOB), 0, 0));
       if (DF32) {
 #pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          const float4 v = *reinterpret_cast<const float4*>(a.dpool_f32 + o + 4 * hh);
-          R.f[hh][u] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
+        for (int hh = 0; hh < 2; ++hh)
+          R.f[hh][u] = __builtin_bit_cast(
+              float4, __builtin_amdgcn_raw_buffer_load_b128(rd_g[0], (int)(ok ? (o + 4 * hh) * 4 : kOOB), 0, 0));
       } else {
 #pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          const u32x4 v = *reinterpret_cast<const u32x4*>(a.dpool + p * a.d_elems + o);
-          R.d[p][u] = ok ? v : u32x4{0u, 0u, 0u, 0u};
-        }
+        for (int p = 0; p < 3; ++p)
+          R.d[p][u] = __builtin_bit_cast(
+              u32x4, __builtin_amdgcn_raw_buffer_load_b128(rd_g[p], (int)(ok ? o * 2 : kOOB), 0, 0));
       }
     }
+    ly += 4;
+    if (ly >= H) { ly -= H; ++lb; }
   };
   auto store = [&](Regs& R, int row) {
-    const int y = row - (row / H) * H;
-    const uint32_t qy = (y & 1) << 1;
+    const uint32_t qy = (row & 1) << 1;   // H is even: row and y have one parity
     if (DF32) {   // split the fp32 chunk into the three planes (split.h split3)
 #pragma unroll
       for (int u = 0; u < NPD; ++u)
@@ -474,21 +493,31 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     u32x4 d[3][NPD];
     u32x2 m[NPD];
   };
+  // bounds-checked buffer loads (wgrads_body): out-of-range chunks read 0 --
+  // routing bytes 0 with values 0, which route and sum nothing
+  constexpr uint32_t kOOB = 0x80000000u;
+  const uint32_t db = (uint32_t)(a.B * (H >> 1) * (W >> 1) * 32);
+  const __amdgpu_buffer_rsrc_t rd_g[3] = {
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.dpool, (short)0, (int)(db * 2), 0x00020000),
+      __builtin_amdgcn_make_buffer_rsrc((void*)(a.dpool + a.d_elems), (short)0, (int)(db * 2),
+                                        0x00020000),
+      __builtin_amdgcn_make_buffer_rsrc((void*)(a.dpool + 2 * a.d_elems), (short)0, (int)(db * 2),
+                                        0x00020000)};
+  const __amdgpu_buffer_rsrc_t rm_g =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.droute, (short)0, (int)db, 0x00020000);
   auto load = [&](Regs& G, int k) {
     const bool live = 2 * k < R;
     const int yp = (y0 >> 1) + k;
-    const size_t o0 = (((size_t)b * (H >> 1) + yp) * (W >> 1) + dpx) * 32 + 8 * dc8;
+    const uint32_t o0 = (uint32_t)(((b * (H >> 1) + yp) * (W >> 1) + dpx) * 32 + 8 * dc8);
 #pragma unroll
     for (int u = 0; u < NPD; ++u) {
       const bool ok = live && dpx + 16 * u < (W >> 1);
-      const size_t o = o0 + (size_t)u * 16 * 32;
-      G.m[u] = u32x2{0x04040404u, 0x04040404u};
-      if (ok) G.m[u] = *reinterpret_cast<const u32x2*>(a.droute + o);
+      const uint32_t o = o0 + (uint32_t)(u * 16 * 32);
+      G.m[u] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rm_g, (int)(ok ? o : kOOB), 0, 0));
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        G.d[p][u] = u32x4{0u, 0u, 0u, 0u};
-        if (ok) G.d[p][u] = *reinterpret_cast<const u32x4*>(a.dpool + p * a.d_elems + o);
-      }
+      for (int p = 0; p < 3; ++p)
+        G.d[p][u] = __builtin_bit_cast(
+            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rd_g[p], (int)(ok ? o * 2 : kOOB), 0, 0));
     }
   };
   auto store = [&](const Regs& G) {
