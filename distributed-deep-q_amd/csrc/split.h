@@ -38,6 +38,7 @@ namespace ddq {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));   // native vector: promotable
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 // x -> (x0, x1, x2) bf16, x0 + x1 + x2 == x to 2^-24 |x| (RNE conversions)
 __device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
@@ -263,6 +264,17 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
   // ---- stage the halo patch of channel chunk ch (3 planes, zero outside) ----
   // Batches of 8 vectors per thread: every load of a batch is issued before
   // its LDS stores (a load -> store loop pays one memory latency per vector).
+  constexpr uint32_t kOOB = 0x80000000u;
+  // plane extent of the split source: (B, H, W, CPT), pooled (B, H/2, W/2, CPT) for DGRAD
+  const uint32_t src_elems = DGRAD ? (uint32_t)(a.B * (a.H >> 1) * (a.W >> 1) * CPT)
+                                   : (uint32_t)(a.B * a.H * a.W * CPT);
+  __amdgpu_buffer_rsrc_t rin[3];
+#pragma unroll
+  for (int p = 0; p < 3; ++p)
+    rin[p] = __builtin_amdgcn_make_buffer_rsrc((void*)(in + p * a.in_elems), (short)0,
+                                               (int)(src_elems * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rroute =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.in_route, (short)0, (int)src_elems, 0x00020000);
   auto stage_patch_split = [&](int ch) {
     constexpr int NV = C::PH * C::PW * (CP / 8);           // 16-byte vectors per plane
     constexpr int NIT = (3 * NV + C::kThreads - 1) / C::kThreads;
@@ -282,25 +294,28 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
         const int gy = y0 - a.pad + py, gx = x0 - a.pad + px;
         const bool in_img = live && (unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W;
         dst[u] = live ? p * C::kPlane + py * C::RS + px * C::CS + 8 * c8 : -1;
-        v[u] = u32x4{0u, 0u, 0u, 0u};
-        if (in_img) {
-          if (DGRAD) {   // pooled source: expand through the routing bytes
-            const size_t o = (((size_t)b * (a.H >> 1) + (gy >> 1)) * (a.W >> 1) + (gx >> 1)) * CPT +
-                             ch * CP + 8 * c8;
-            const u32x4 uw = *reinterpret_cast<const u32x4*>(in + p * a.in_elems + o);
-            const uint2 m = *reinterpret_cast<const uint2*>(a.in_route + o);
-            const uint32_t q = ((gy & 1) << 1) | (gx & 1);
+        // bounds-checked buffer loads: outside the image (or past the
+        // items) the offset is out of range and the vector reads 0 -- no
+        // branch, select or 64-bit address per vector
+        if (DGRAD) {   // pooled source: expand through the routing bytes
+          const uint32_t o = (uint32_t)(((b * (a.H >> 1) + (gy >> 1)) * (a.W >> 1) + (gx >> 1)) * CPT +
+                                        ch * CP + 8 * c8);
+          const u32x4 uw = __builtin_bit_cast(
+              u32x4, __builtin_amdgcn_raw_buffer_load_b128(rin[p], (int)(in_img ? o * 2 : kOOB), 0, 0));
+          const u32x2 m = __builtin_bit_cast(
+              u32x2, __builtin_amdgcn_raw_buffer_load_b64(rroute, (int)(in_img ? o : kOOB), 0, 0));
+          const uint32_t q = ((gy & 1) << 1) | (gx & 1);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {   // bf16 pair e = channels 2e, 2e+1
-              const uint32_t mw = e < 2 ? m.x : m.y;
-              const uint32_t r0 = (mw >> (16 * (e & 1))) & 0xff;
-              const uint32_t r1 = (mw >> (16 * (e & 1) + 8)) & 0xff;
-              v[u][e] = (r0 == q ? (uw[e] & 0xffffu) : 0u) | (r1 == q ? (uw[e] & 0xffff0000u) : 0u);
-            }
-          } else {
-            v[u] = *reinterpret_cast<const u32x4*>(
-                in + p * a.in_elems + (((size_t)b * a.H + gy) * a.W + gx) * CPT + ch * CP + 8 * c8);
+          for (int e = 0; e < 4; ++e) {   // bf16 pair e = channels 2e, 2e+1 (zeros route nothing)
+            const uint32_t mw = m[e >> 1];
+            const uint32_t r0 = (mw >> (16 * (e & 1))) & 0xff;
+            const uint32_t r1 = (mw >> (16 * (e & 1) + 8)) & 0xff;
+            v[u][e] = (r0 == q ? (uw[e] & 0xffffu) : 0u) | (r1 == q ? (uw[e] & 0xffff0000u) : 0u);
           }
+        } else {
+          const uint32_t o = (uint32_t)(((b * a.H + gy) * a.W + gx) * CPT + ch * CP + 8 * c8);
+          v[u] = __builtin_bit_cast(
+              u32x4, __builtin_amdgcn_raw_buffer_load_b128(rin[p], (int)(in_img ? o * 2 : kOOB), 0, 0));
         }
       }
 #pragma unroll
