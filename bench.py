@@ -48,7 +48,7 @@ def kernel_flops(B, S):
     c3 = 2.0 * B * s3 * s3 * 64 * 576
     fc = 2.0 * B * 512 * k4
     return {"conv1_fwd": 2 * c1, "conv2_fwd": 2 * c2, "conv3_fwd": 2 * c3, "fc4_fwd": 2 * fc,
-            "fc4_dgrad": fc, "fc4_wgrad": fc, "conv3_wgrad": c3, "conv3_dgrad": c3,
+            "fc4_bwd": fc, "conv3_wgrad": c3, "conv3_dgrad": c3,
             "conv2_wgrad": c2, "conv2_dgrad": c2, "conv1_wgrad": c1}
 
 
@@ -60,8 +60,7 @@ KERNEL_SYMBOL = {
     "conv3_fwd": "void ddq::split_conv_kernel<64, 64, 64, 3, 8, 8, 2, 2,",
     "fc4_fwd": "void ddq::fc4_fwd_split_kernel",
     "head": "ddq::fc4_head_kernel",
-    "fc4_dgrad": "void ddq::fc4_dgrad_direct_kernel",
-    "fc4_wgrad": "ddq::fc4_wgrad_kernel",
+    "fc4_bwd": "void ddq::fc4_bwd_kernel",
     "conv3_wgrad": "void ddq::wgrads_kernel<64, 64, 3, 1",
     "conv3_dgrad": "void ddq::split_conv_kernel<64, 64, 64, 3, 4, 8,",
     "conv2_wgrad": "void ddq::wgrads_kernel<32, 64, 5, 2",
@@ -79,8 +78,7 @@ KERNEL_SYMBOL = {
 KERNEL_ARITH = {
     "conv1_fwd": "split3", "conv2_fwd": "split", "conv3_fwd": "split",
     "conv1_wgrad": "split3", "conv2_wgrad": "split", "conv3_wgrad": "split",
-    "conv2_dgrad": "split", "conv3_dgrad": "split", "fc4_fwd": "split", "fc4_dgrad": "split",
-    "fc4_wgrad": "f32",
+    "conv2_dgrad": "split", "conv3_dgrad": "split", "fc4_fwd": "split", "fc4_bwd": "split",
 }
 BF16_MFMA_PEAK = 2.5e15       # MI355X_MICROARCH.md: dense bf16
 
@@ -91,17 +89,38 @@ def arith_peak(kernel):
 
 
 def pmc_traffic(label, B, S):
-    """HBM bytes per launch of `label` from the committed PMC summary
-    (profiles/r02_pmc.json, tools/gpu/run_measure.sh: FETCH_SIZE x2 + WRITE_SIZE,
-    MI355X_MICROARCH.md gfx950 correction), valid for the bench default shape."""
-    path = os.path.join(ROOT, "profiles", "r02_pmc.json")
-    if (B, S) != (32, 64) or not os.path.exists(path):
-        return None
+    """(HBM bytes per launch of `label`, source file) from the newest committed
+    PMC summary (profiles/rNN_pmc.json, tools/gpu/run_measure.sh: FETCH_SIZE x2
+    + WRITE_SIZE, MI355X_MICROARCH.md gfx950 correction) -- a separate
+    rocprofv3 --pmc run of the same bench command, NOT measured in this run;
+    valid for the bench default shape only."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc.json")))
+    if (B, S) != (32, 64) or not paths:
+        return None, None
     sym = KERNEL_SYMBOL.get(label)
-    for name, e in json.load(open(path))["kernels"].items():
+    for name, e in json.load(open(paths[-1]))["kernels"].items():
         if sym and name.startswith(sym) and "hbm_bytes" in e:
-            return round(e["hbm_bytes"])
-    return None
+            return round(e["hbm_bytes"]), os.path.relpath(paths[-1], ROOT)
+    return None, None
+
+
+def step_roofline(B, S, P):
+    """Ideal time of one update step: every MFMA kernel at the peak of the
+    arithmetic it runs (split: bf16 dense / 6, split3: / 3 -- csrc/split.h)
+    plus the step's algorithmic HBM bytes at 8 TB/s (replay gather u8 read +
+    f32 minibatch write, fc4 weights read by the two forwards and the data
+    gradient, rmsprop apply 20 P).  The fraction measured / ideal is the
+    step's roofline fraction (SURVEY 8(d) composite, split-aware)."""
+    fl = kernel_flops(B, S)
+    mfma_s = sum(v / arith_peak(k) for k, v in fl.items() if k in KERNEL_ARITH)
+    K4 = 64 * (S // 8) ** 2
+    gather = 2 * B * 4 * S * S + 2 * B * 4 * S * S * 4 + B * 24
+    fc4 = 3 * 512 * K4 * 4
+    apply_b = 20 * P
+    hbm_s = (gather + fc4 + apply_b) / HBM_PEAK
+    return {"ideal_us": round((mfma_s + hbm_s) * 1e6, 2), "mfma_us": round(mfma_s * 1e6, 2),
+            "hbm_us": round(hbm_s * 1e6, 2), "hbm_bytes": gather + fc4 + apply_b}
 
 
 def fill_replay(net, N, S, seed):
@@ -159,11 +178,17 @@ def _cpu_updates(lib, B, S, seed, threads, budget_s, max_steps):
     return steps, time.perf_counter() - t0
 
 
-def cpu_baseline(B, S, seed, budget_s=12.0, max_steps=2000):
+PUBLISHED_CPU_MS = {16: 81.7, 32: 252.8, 64: 981.5, 128: 4044.0}   # results/cost-vs-image-size.txt
+
+
+def cpu_baseline(B, S, seed, budget_s=12.0, max_steps=2000,
+                 extra=((32, 16, 5.0), (256, 16, 5.0))):
     """Oracle C restatement (Caffe CPU algorithm: im2col + SGEMM, fp32, OpenMP)
     of the same update step, on all host cores and on one core (BASELINE.md
     section 2), with the reference's own published 2015 Caffe CPU time for
-    context (results/cost-vs-image-size.txt:4, hardware unstated)."""
+    context (results/cost-vs-image-size.txt:2-5, hardware unstated); `extra`
+    (B, S, seconds): the same at deepq16 (the reference's headline, S = 16
+    B = 32) and at a C3 sweep point (B = 256)."""
     lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "libddq_cpu.so"))
     lib.ddq_cpu_full_pass.restype = ctypes.c_int
     lib.ddq_cpu_apply.restype = ctypes.c_int
@@ -178,7 +203,7 @@ def cpu_baseline(B, S, seed, budget_s=12.0, max_steps=2000):
     flops = lib.ddq_cpu_step_flops(B, S)
     steps, dt = _cpu_updates(lib, B, S, seed, cores, budget_s, max_steps)
     s1, d1 = _cpu_updates(lib, B, S, seed, 1, budget_s / 2, max(2, max_steps // 8))
-    published = {16: 81.7, 32: 252.8, 64: 981.5, 128: 4044.0}.get(S)
+    published = PUBLISHED_CPU_MS.get(S)
     out = {"value": round(steps / dt, 4), "unit": "updates/s", "cores": cores, "kind": "port",
            "gflops": round(flops * steps / dt / 1e9, 1),
            "sample": "%d updates (sample->gather->P/Q fwd->target->Q bwd->rmsprop apply) "
@@ -195,15 +220,60 @@ def cpu_baseline(B, S, seed, budget_s=12.0, max_steps=2000):
             "value": round(1000.0 / published, 4), "unit": "updates/s (fwd+bwd only)",
             "source": "results/cost-vs-image-size.txt (Caffe CPU, %.1f ms fwd+bwd at %dx%d "
                       "B=32, hardware unstated)" % (published, S, S)}
+    cfgs = []
+    for eb, es, sec in extra:
+        fl = lib.ddq_cpu_step_flops(eb, es)
+        n, d = _cpu_updates(lib, eb, es, seed, cores, sec, max_steps)
+        n1, d1 = _cpu_updates(lib, eb, es, seed, 1, sec / 2, max(2, max_steps // 8))
+        e = {"batch": eb, "frame": es, "value": round(n / d, 4), "cores": cores,
+             "gflops": round(fl * n / d / 1e9, 1), "sample": "%d updates, %.1f s" % (n, d),
+             "single_core": {"value": round(n1 / d1, 4), "cores": 1,
+                             "gflops": round(fl * n1 / d1 / 1e9, 1),
+                             "sample": "%d updates, %.1f s" % (n1, d1)}}
+        if eb == 32 and es in PUBLISHED_CPU_MS:
+            e["reference_published"] = {"value": round(1000.0 / PUBLISHED_CPU_MS[es], 4),
+                                        "unit": "updates/s (fwd+bwd only, Caffe CPU, "
+                                                "%.1f ms)" % PUBLISHED_CPU_MS[es]}
+        cfgs.append(e)
+    out["configs"] = cfgs
     return out
+
+
+def deepq16_line(steps=2000, warmup=100, rule="rmsprop"):
+    """The reference's own headline shape, deepq16 (S = 16, B = 32,
+    models/deepq/train_val.prototxt:8-11; results/cost-vs-image-size.txt:2):
+    the same pipelined graph step on one GPU, 30 000-slot replay."""
+    import ddq
+    from ddq.params import init_params_flat
+    B, S = 32, 16
+    net = ddq.DeepQNet(batch=B, frame=S)
+    theta = init_params_flat(S, seed=42)
+    net.set_flat(0, theta)
+    net.set_flat(1, theta)
+    net.replay_create(30000)
+    fill_replay(net, 30000, S, seed=1000)
+    cfg = net.step_cfg(rule, lr=1e-4, target_period=10, seed=1234)
+    net.step_prepare(cfg, "pipelined")
+    net.step_pipelined(cfg, warmup)
+    net.synchronize()
+    t0 = time.perf_counter()
+    net.step_pipelined(cfg, steps)
+    net.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    rl = step_roofline(B, S, net.num_params)
+    net.close()
+    return {"batch": B, "frame": S, "updates_per_s": round(1 / dt, 2),
+            "ms_per_step": round(dt * 1e3, 4), "steps": steps,
+            "step_ideal_us": rl["ideal_us"], "step_frac": round(rl["ideal_us"] * 1e-6 / dt, 4),
+            "reference_published_fwd_bwd_ms": PUBLISHED_CPU_MS[16]}
 
 
 # algorithmic HBM bytes per launch of the fc4 kernels: W4 (512 x K fp32 per
 # tower) plus activations in and out (K = 64 (S/8)^2)
 FC4_BYTES = {
     "fc4_fwd": lambda B, S: 2 * (512 * 64 * (S // 8) ** 2 * 4 + B * 64 * (S // 8) ** 2 * 4),
-    "fc4_dgrad": lambda B, S: 512 * 64 * (S // 8) ** 2 * 4 + B * 512 * 4 + B * 64 * (S // 8) ** 2 * 4,
-    "fc4_wgrad": lambda B, S: 512 * 64 * (S // 8) ** 2 * 4 + B * 512 * 4 + B * 64 * (S // 8) ** 2 * 4,
+    # the data gradient (the fused apply computes the weight gradient)
+    "fc4_bwd": lambda B, S: 512 * 64 * (S // 8) ** 2 * 4 + B * 512 * 4 + B * 64 * (S // 8) ** 2 * 4,
 }
 
 
@@ -326,6 +396,77 @@ def gather_stress(S=64, N=1_000_000, sizes=(256, 4096, 32768), seed=3):
             "launches": out}
 
 
+EXCHANGE_PATHS = (   # (label, exchange, overlap, step mode)
+    ("allreduce+overlap", "allreduce", True, "pipelined"),
+    ("allreduce", "allreduce", False, "pipelined"),
+    ("sharded", "sharded", False, "graph"),
+    ("server", "server", False, "graph"),
+    ("async", "async", False, "eager"),            # round-robin rounds, eager
+    ("async-graph", "async", False, "graph"),      # round-robin rounds as hipGraphs
+    ("async-ticket", "async", False, "ticket"))    # arrival order (AsyncTicketLoop)
+
+
+def exchange_paths(net, rule, ref_value, steps=240, warmup=24, profile=5):
+    """The per-GPU path of BASELINE configs 4 / 5 measured on one GPU: every
+    gradient exchange through a 1-rank RCCL communicator (the same kernels,
+    RCCL calls, comm-stream overlap and graph capture as N > 1, without the
+    wire time), against the exchange-free step of the same run."""
+    import ddq
+    from ddq import dist as ddist
+    from ddq.params import init_params_flat
+    out = {}
+    for label, ex, ov, mode in EXCHANGE_PATHS:
+        if ex == "async":     # a fresh worker: once begun, a ctx runs async steps only
+            net = ddq.DeepQNet(batch=net.batch, frame=net.frame, device=net.device)
+            theta = init_params_flat(net.frame, seed=42)
+            net.set_flat(0, theta)
+            net.set_flat(1, theta)
+            net.replay_create(30000)
+            fill_replay(net, 30000, net.frame, seed=1000)
+            ddist.setup_comm(net, 0, 1)
+        elif "comm" not in out:
+            ddist.setup_comm(net, 0, 1)
+            out["comm"] = True
+        cfg = net.step_cfg(rule, lr=1e-4, target_period=10, exchange=ex, overlap=ov, seed=1234)
+        if mode != "ticket":
+            net.step_prepare(cfg, mode)
+        loop = ddist.AsyncTicketLoop(net, cfg, ddist.ticket_store(1), 0, 1) \
+            if mode == "ticket" else None
+
+        def run(k):
+            if mode == "pipelined":
+                net.step_pipelined(cfg, k)
+            elif mode == "graph":
+                net.step_graph(cfg, k)
+            elif mode == "ticket":
+                loop.run(k)
+                net.synchronize()
+            else:
+                for _ in range(k):
+                    net.step(cfg)
+        run(warmup)
+        net.synchronize()
+        t0 = time.perf_counter()
+        run(steps)
+        net.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        e = {"updates_per_s": round(1 / dt, 2), "ms_per_step": round(dt * 1e3, 4), "mode": mode,
+             "vs_exchange_free": round((1 / dt) / ref_value, 4)}
+        if ex != "async":
+            prof = {}
+            for _ in range(profile):
+                for name, us in net.profile_step(cfg):
+                    prof.setdefault(name, []).append(us)
+            e["kernels_us"] = {k: round(float(np.median(v)), 2) for k, v in prof.items()}
+        else:
+            net.close()
+        out[label] = e
+    out.pop("comm", None)
+    return {"note": "world-1 RCCL communicator: the N>1 per-GPU step (kernels, RCCL calls, "
+                    "comm-stream overlap, graphs) without wire time; vs_exchange_free = "
+                    "this path's updates/s over the main line's", "paths": out}
+
+
 def frame_sweep(B=256, frames=range(16, 129, 8), steps=60, warmup=10, rule="rmsprop"):
     """batch 256, frame side 16..128 (results/cost-vs-image-size)."""
     import ddq
@@ -349,16 +490,25 @@ def frame_sweep(B=256, frames=range(16, 129, 8), steps=60, warmup=10, rule="rmsp
         net.synchronize()
         dt = (time.perf_counter() - t0) / steps
         fl = net.step_flops()
+        rl = step_roofline(B, S, net.num_params)
         res.append({"frame": S, "updates_per_s": round(1 / dt, 2), "ms_per_step": round(dt * 1e3, 4),
                     "step_tflops": round(fl / dt / 1e12, 2),
-                    "frac_of_f32_mfma_peak": round(fl / dt / F32_MFMA_PEAK, 4)})
+                    "frac_of_step_roofline": round(rl["ideal_us"] * 1e-6 / dt, 4),
+                    "ideal_us": rl["ideal_us"],
+                    "vs_f32_mfma_peak": round(fl / dt / F32_MFMA_PEAK, 4)})
         net.close()
     return {"batch": B, "config": "C3: deepq, batch 256, frame side S, rmsprop, 8-step graphs",
             "step_tflops_basis": "algorithmic f32 FLOPs of the whole step (SURVEY 8(d))",
+            "frac_basis": "step_roofline(): each MFMA kernel at the peak of its arithmetic "
+                          "(split / split3) + algorithmic HBM bytes at 8 TB/s",
             "f32_mfma_peak_TFLOPs": F32_MFMA_PEAK / 1e12, "frames": res}
 
 
 def main():
+    # the JSON line is the only thing on stdout: C-level writes to fd 1 (e.g.
+    # RCCL's version banner at communicator init) go to stderr
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=500)
@@ -383,6 +533,15 @@ def main():
     ap.add_argument("--exchange", default="allreduce",
                     choices=["allreduce", "sharded", "server", "async"],
                     help="N>1 gradient exchange (include/ddq_hip.h enum ddq_exchange)")
+    ap.add_argument("--force-exchange", default=None,
+                    choices=["allreduce", "sharded", "server", "async"],
+                    help="N=1: run this exchange through a 1-rank RCCL communicator (the N>1 "
+                         "per-GPU path) for the main line")
+    ap.add_argument("--no-exchange-paths", action="store_true",
+                    help="skip the world-1 timing of every exchange path (N=1 only)")
+    ap.add_argument("--async-order", default="rr", choices=["rr", "ticket"],
+                    help="async exchange: round-robin rounds (deterministic) or arrival-order "
+                         "tickets (ddq.dist.AsyncTicketLoop); a step = W pushes either way")
     ap.add_argument("--no-overlap", action="store_true",
                     help="allreduce: do not reduce the fc4 bucket under the conv backward")
     ap.add_argument("--no-pipeline", action="store_true",
@@ -409,12 +568,22 @@ def main():
     fill_replay(net, args.replay, S, seed=1000 + rank)
     if world > 1:
         ddist.setup_comm(net, rank, world)
+    elif args.force_exchange:
+        ddist.setup_comm(net, 0, 1)
+        args.exchange = args.force_exchange
+    exchanged = world > 1 or bool(args.force_exchange)
     cfg = net.step_cfg(args.rule, lr=1e-4, target_period=10,
-                       exchange=args.exchange if world > 1 else "none",
+                       exchange=args.exchange if exchanged else "none",
                        overlap=not args.no_overlap, seed=ddist.index_seed(1234, rank))
 
+    ticket = None
+    if exchanged and args.exchange == "async" and args.async_order == "ticket":
+        ticket = ddist.AsyncTicketLoop(net, cfg, ddist.ticket_store(world, rank), rank, world)
+
     def run(k):
-        if args.eager:
+        if ticket is not None:
+            ticket.run(k * world)
+        elif args.eager:
             for _ in range(k):
                 net.step(cfg)
         elif args.pipeline:
@@ -426,8 +595,10 @@ def main():
     # the first mode every rank prepared (gloo MIN): a rank whose capture of the
     # comm-stream exchange is refused falls back TOGETHER with the others, so
     # no rank waits in an RCCL collective the rest abandoned.
-    if args.eager:
+    if args.eager or ticket is not None:
         modes = [("eager", False)]
+    elif exchanged and args.exchange == "async":
+        modes = [("graph", False), ("eager", False)]
     elif args.pipeline:
         modes = [("pipelined", not args.no_overlap), ("graph", False), ("eager", False)]
     else:
@@ -465,7 +636,7 @@ def main():
 
     # per-kernel device times (HIP events on the ctx stream), averaged
     prof = {}
-    pcfg = cfg if args.exchange != "async" or world == 1 else \
+    pcfg = cfg if not (exchanged and args.exchange == "async") else \
         net.step_cfg(args.rule, lr=1e-4, target_period=10, exchange="none", seed=1234)
     for _ in range(args.profile_steps):
         for name, us in net.profile_step(pcfg):
@@ -479,6 +650,8 @@ def main():
         else avg[dom]
     achieved = flops[dom] / (dom_us * 1e-6) / 1e12
     step_flops = net.step_flops()
+    step_rl = step_roofline(B, S, net.num_params)
+    traffic, traffic_src = pmc_traffic(dom, B, S)
 
     if rank == 0:
         out = {
@@ -501,7 +674,7 @@ def main():
                        "parallelism": "dp%d" % world, "graph": not args.eager,
                        "exchange": (args.exchange + ("" if args.no_overlap or
                                                      args.exchange != "allreduce"
-                                                     else "+overlap")) if world > 1 else "none",
+                                                     else "+overlap")) if exchanged else "none",
                        "pipelined": bool(args.pipeline and not args.eager)},
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3),
                          "peak": round(arith_peak(dom) / 1e12, 1), "unit": "TFLOP/s",
@@ -511,12 +684,16 @@ def main():
                                        "the bf16 products per f32 product (split: 6, split3: "
                                        "3; f32 MFMA: 157.3)",
                          "vs_f32_mfma_peak": round(achieved * 1e12 / F32_MFMA_PEAK, 4),
-                         "traffic": pmc_traffic(dom, B, S), "traffic_unit": "bytes/launch",
+                         "traffic": traffic, "traffic_unit": "bytes/launch",
+                         "traffic_source": traffic_src,
                          "kernel_us": round(dom_us, 3),
                          "kernel_us_timing": "100 back-to-back launches between HIP events "
                                              "on the ctx stream",
                          "step_tflops": round(step_flops / (dt / args.steps) / 1e12, 3),
-                         "step_frac": round(step_flops / (dt / args.steps) / F32_MFMA_PEAK, 4)},
+                         "step_ideal_us": step_rl["ideal_us"],
+                         "step_frac": round(step_rl["ideal_us"] * 1e-3 / (dt / args.steps * 1e3), 4),
+                         "step_frac_basis": "step_roofline(): MFMA kernels at their "
+                                            "arithmetic's peak + algorithmic HBM bytes"},
             "kernels_us": {k: round(v, 2) for k, v in avg.items()},
             "kernel_roofline": kernel_roofline(avg, B, S, net.num_params),
             "step_ms_distribution": dist_ms,
@@ -527,13 +704,16 @@ def main():
         if not args.no_gather_stress and world == 1:
             out["gather_stress"] = gather_stress()
         if not args.no_sweep and world == 1:
+            out["deepq16"] = deepq16_line()
             # C3 (BASELINE.json configs[2]): B = 256; the default line carries
             # the reduced sweep 16 / 64 / 128, --sweep the reference's 16..128/8
             out["frame_sweep"] = frame_sweep(frames=range(16, 129, 8) if args.sweep
                                              else (16, 64, 128))
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(B, S, seed=7)
-        print(json.dumps(out), flush=True)
+        if not args.no_exchange_paths and world == 1 and not args.force_exchange:
+            out["exchange_paths"] = exchange_paths(net, args.rule, out["value"])
+        print(json.dumps(out), file=json_out, flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -7,8 +7,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <string>
+#include <chrono>
 #include <functional>
+#include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/ddq_hip.h"
@@ -16,7 +18,7 @@
 
 namespace ddq {
 int fc4_splits_for(int S);
-int wgrad_splits_for(int layer, int B, int S, int* np, int impl);
+int wgrad_splits_for(int layer, int B, int S, int* np);
 }  // namespace ddq
 
 using namespace ddq;
@@ -46,19 +48,20 @@ struct ddq_ctx {
   int64_t head = 0, valid = 0, capacity = 0;
   // acting scratch
   uint8_t* act_u8 = nullptr;
-  float *act_in = nullptr, *act_p1 = nullptr, *act_p2 = nullptr, *act_p3 = nullptr;
+  float *act_in = nullptr, *act_p3 = nullptr;
   float *act_h4 = nullptr, *act_part = nullptr, *act_q = nullptr;
   __bf16 *act_p1s = nullptr, *act_p2s = nullptr;
   int32_t* act_out = nullptr;
   // index log (ddq_index_log_enable)
   int32_t* log_buf = nullptr;
   int64_t log_buf_cap = 0;
+  int64_t log_first = 0;           // first draw the log holds (the counter at enable)
   // comm (RCCL ranks, or an in-process group of ctxs exchanging by device copies)
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
   bool local = false;              // member of an in-process group (ddq_group_init)
   hipStream_t cs = nullptr;        // comm stream of the overlapped all-reduce
-  hipEvent_t cev[2] = {};
+  hipEvent_t cev[3] = {};
   int64_t shard_len = 0;           // parameters owned per rank (multiple of 64)
   float* gsl = nullptr;            // [W][shard_len] received gradient slices
   float* gstage = nullptr;         // [W][P] in-process all-reduce staging
@@ -66,7 +69,22 @@ struct ddq_ctx {
   // the last special-update pull), both at full-vector offsets
   float* own = nullptr;
   float* pown = nullptr;
-  int64_t async_base = 0;          // iteration at the first async step (everyone pulled)
+  bool async_on = false;           // the async exchange began (async_begin)
+  std::vector<int64_t> last_pull;  // iteration of every worker's last pull
+  int64_t async_ticks = 0;         // pushes applied since async_begin
+  hipEvent_t grad_ev = nullptr;    // this worker's gradient is ready (pushable)
+  hipEvent_t tick_ev = nullptr;    // owner duties of the last tick done (comm stream)
+  int64_t straggle_us = 0;         // ddq_set_straggle: host-side delay per gradient
+  bool ready_seen = false;         // grad_ev observed complete at ready_at
+  std::chrono::steady_clock::time_point ready_at{};
+  int64_t rr_rounds = 0;           // round-robin rounds since the last ticket-order tick
+  bool acapture = false;           // capturing async rounds: grad_ev recorded before the
+  bool grad_ev_captured = false;   // capture began is not waited on (the graph launch
+                                   // follows that work on the stream anyway)
+  hipGraphExec_t agexec = nullptr; // kAsync round-robin rounds as one graph
+  int agraph_rounds = 0;
+  int64_t agraph_phase = -1;       // iteration % period the graph was captured at
+  ddq_step_cfg acfg{};
   std::string comm_err;
   // graph
   hipGraph_t graph = nullptr;
@@ -197,6 +215,14 @@ int ddq_create(ddq_ctx** out, int device, const ddq_net_desc* desc) {
                 desc->frame);
   if (desc->batch < 1 || desc->batch > 1024)
     return fail(nullptr, DDQ_EINVAL, "batch must be in [1,1024] (got %d)", desc->batch);
+  // the kernels address every tensor through 32-bit buffer descriptors /
+  // offsets (kOOB = 2^31 marks an out-of-range vector): the largest ones are
+  // a split activation plane (16 B S^2 bytes) and fc4's weights (2^11 S^2)
+  if ((int64_t)16 * desc->batch * desc->frame * desc->frame >= (1ll << 31) ||
+      (int64_t)2048 * desc->frame * desc->frame >= (1ll << 31))
+    return fail(nullptr, DDQ_EINVAL,
+                "batch * frame^2 too large for 32-bit tensor offsets (need 16*B*S^2 < 2^31 "
+                "and S < 1024; got B=%d, S=%d)", desc->batch, desc->frame);
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
   if (e != hipSuccess || ndev == 0)
@@ -214,16 +240,6 @@ int ddq_create(ddq_ctx** out, int device, const ddq_net_desc* desc) {
     for (auto& e : nb.ev) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     const int B = desc->batch, S = desc->frame;
     nb.B = B; nb.S = S; nb.gamma = desc->gamma;
-    nb.conv_impl = 1;   // direct (patch-in-LDS) conv kernels
-    nb.variant = 0;
-#ifdef DDQ_EXPERIMENTS
-    {   // A/B tuning knobs: experiment builds only (make EXPERIMENTS=1)
-      const char* impl = getenv("DDQ_CONV_IMPL");
-      if (impl && strcmp(impl, "gemm") == 0) nb.conv_impl = 0;
-      const char* var = getenv("DDQ_VARIANT");
-      nb.variant = var ? atoi(var) : 0;
-    }
-#endif
     nb.L = make_layout(S);
     const int64_t P = nb.L.total;
     const int S2 = S / 2, S3 = S / 4, S4 = S / 8;
@@ -234,12 +250,9 @@ int ddq_create(ddq_ctx** out, int device, const ddq_net_desc* desc) {
     TRY(dalloc(c, &nb.nonterm, (size_t)B));
     TRY(dalloc(c, &nb.idx, (size_t)B));
     for (int z = 0; z < 2; ++z) {
-      TRY(dalloc(c, &nb.pool1[z], (size_t)B * S2 * S2 * 32));
-      TRY(dalloc(c, &nb.pool2[z], (size_t)B * S3 * S3 * 64));
       TRY(dalloc(c, &nb.pool3[z], (size_t)B * S4 * S4 * 64));
       TRY(dalloc(c, &nb.h4[z], (size_t)B * 512));
       TRY(dalloc(c, &nb.theta[z], (size_t)P + kShardPad));
-      TRY(dalloc(c, &nb.wk[z], (size_t)nb.L.wk_total));
       TRY(dalloc(c, &nb.wks[z], (size_t)3 * nb.L.wks_total));   // zero: conv1's kx 7 stays 0
       TRY(dalloc(c, &nb.pool1s[z], (size_t)3 * B * S2 * S2 * 32));
       TRY(dalloc(c, &nb.pool2s[z], (size_t)3 * B * S3 * S3 * 64));
@@ -259,14 +272,12 @@ int ddq_create(ddq_ctx** out, int device, const ddq_net_desc* desc) {
     TRY(dalloc(c, &nb.dqbuf, (size_t)B * 4));
     TRY(dalloc(c, &nb.lpart, (size_t)B));
     TRY(dalloc(c, &nb.dconv3, (size_t)B * S3 * S3 * 64));
-    TRY(dalloc(c, &nb.dconv2, (size_t)B * S2 * S2 * 64));
-    TRY(dalloc(c, &nb.dconv1, (size_t)B * S * S * 32));
     TRY(dalloc(c, &nb.dconv2s, (size_t)3 * B * S3 * S3 * 64));
     TRY(dalloc(c, &nb.dconv1s, (size_t)3 * B * S2 * S2 * 32));
     int64_t off = 0;
     const int cout[3] = {32, 64, 64};
     for (int l = 0; l < 3; ++l) {
-      nb.wsplits[l] = wgrad_splits_for(l, B, S, &nb.wnp[l], nb.conv_impl);
+      nb.wsplits[l] = wgrad_splits_for(l, B, S, &nb.wnp[l]);
       nb.wpart_off[l] = off;
       off += (int64_t)nb.wsplits[l] * cout[l] * nb.wnp[l];
     }
@@ -281,8 +292,6 @@ int ddq_create(ddq_ctx** out, int device, const ddq_net_desc* desc) {
     // acting scratch (n <= B)
     TRY(dalloc(c, &c->act_u8, (size_t)B * 4 * S * S));
     TRY(dalloc(c, &c->act_in, (size_t)B * S * S * 4));
-    TRY(dalloc(c, &c->act_p1, (size_t)B * S2 * S2 * 32));
-    TRY(dalloc(c, &c->act_p2, (size_t)B * S3 * S3 * 64));
     TRY(dalloc(c, &c->act_p1s, (size_t)3 * B * S2 * S2 * 32));
     TRY(dalloc(c, &c->act_p2s, (size_t)3 * B * S3 * S3 * 64));
     TRY(dalloc(c, &c->act_p3, (size_t)B * S4 * S4 * 64));
@@ -305,8 +314,10 @@ int ddq_create(ddq_ctx** out, int device, const ddq_net_desc* desc) {
 int ddq_destroy(ddq_ctx* c) {
   if (!c) return DDQ_OK;
   hipSetDevice(c->device);
+  if (c->cs) hipStreamSynchronize(c->cs);
   if (c->stream) hipStreamSynchronize(c->stream);
   invalidate_graph(c);
+  if (c->agexec) hipGraphExecDestroy(c->agexec);
   for (auto& e : c->ev_pool) hipEventDestroy(e);
   if (c->comm) ncclCommDestroy(c->comm);
   for (void* p : c->allocs) hipFree(p);
@@ -315,6 +326,8 @@ int ddq_destroy(ddq_ctx* c) {
     if (e) hipEventDestroy(e);
   if (c->nb.side) hipStreamDestroy(c->nb.side);
   if (c->cs) hipStreamDestroy(c->cs);
+  if (c->grad_ev) hipEventDestroy(c->grad_ev);
+  if (c->tick_ev) hipEventDestroy(c->tick_ev);
   for (auto& e : c->cev)
     if (e) hipEventDestroy(e);
   delete c;
@@ -346,6 +359,7 @@ int ddq_get_stream(const ddq_ctx* c, void** s) {
 int ddq_synchronize(ddq_ctx* c) {
   if (!c) return fail(nullptr, DDQ_EINVAL, "null ctx");
   TRY(set_dev(c));
+  if (c->cs) HIP_TRY(c, hipStreamSynchronize(c->cs));   // owner duties of async ticks
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return DDQ_OK;
 }
@@ -433,8 +447,6 @@ int ddq_sync_target(ddq_ctx* c) {
   if (!c) return fail(nullptr, DDQ_EINVAL, "null ctx");
   TRY(set_dev(c));
   HIP_TRY(c, hipMemcpyAsync(c->nb.theta[1], c->nb.theta[0], c->nb.L.total * 4,
-                            hipMemcpyDeviceToDevice, c->stream));
-  HIP_TRY(c, hipMemcpyAsync(c->nb.wk[1], c->nb.wk[0], c->nb.L.wk_total * 4,
                             hipMemcpyDeviceToDevice, c->stream));
   HIP_TRY(c, hipMemcpyAsync(c->nb.wks[1], c->nb.wks[0], c->nb.L.wks_total * 3 * 2,
                             hipMemcpyDeviceToDevice, c->stream));
@@ -660,6 +672,11 @@ int ddq_index_log_enable(ddq_ctx* c, int64_t draws) {
   if (draws < 0 || draws > (1ll << 24)) return fail(c, DDQ_EINVAL, "draws must be in [0, 2^24]");
   TRY(set_dev(c));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  // the ring restarts at the current draw: earlier draws (or entries of a
+  // ring of another capacity) are never reported as logged
+  ReplayMeta m;
+  HIP_TRY(c, scopy(c, &m, c->r_meta, sizeof(m), hipMemcpyDeviceToHost));
+  c->log_first = (int64_t)m.counter;
   if (draws == 0) {
     c->nb.idx_log = nullptr;
     c->nb.log_cap = 0;
@@ -692,10 +709,11 @@ int ddq_index_log_read(ddq_ctx* c, int64_t first, int64_t n, int32_t* out) {
   if (!c->nb.idx_log) return fail(c, DDQ_ESTATE, "index log not enabled");
   int64_t drawn = 0;
   TRY(ddq_replay_draws(c, &drawn));
-  if (first < 0 || n < 0 || first + n > drawn || drawn - first > c->nb.log_cap)
-    return fail(c, DDQ_EINVAL, "draws [%lld, %lld) not in the log (drawn %lld, cap %lld)",
-                (long long)first, (long long)(first + n), (long long)drawn,
-                (long long)c->nb.log_cap);
+  if (first < c->log_first || n < 0 || first + n > drawn || drawn - first > c->nb.log_cap)
+    return fail(c, DDQ_EINVAL,
+                "draws [%lld, %lld) not in the log (logged from draw %lld, drawn %lld, cap %lld)",
+                (long long)first, (long long)(first + n), (long long)c->log_first,
+                (long long)drawn, (long long)c->nb.log_cap);
   const int B = c->nb.B;
   for (int64_t d = first; d < first + n; ++d)
     HIP_TRY(c, hipMemcpyAsync(out + (d - first) * B, c->nb.idx_log + (d % c->nb.log_cap) * B,
@@ -773,12 +791,10 @@ static int enqueue_fwd_bwd(ddq_ctx* c, const NetBuffers& nb, void (*mark)(void*,
   HIP_TRY(c, launch_forward(nb, 2, c->stream, mark, marg, false));
   if (mark) mark(marg, "head");
   HIP_TRY(c, launch_head(nb, c->stream));
-  // Serial by default: forking the weight-gradient kernels onto a side stream
-  // costs more in cross-stream graph edges (6-14 us idle each, measured) than
-  // the overlap returns, as every kernel here fills the GPU on its own
-  // (DDQ_VARIANT bit 16 re-enables the concurrent branch for A/B runs).
-  HIP_TRY(c, launch_backward(nb, c->stream, mark, marg, mark == nullptr && (nb.variant & 16),
-                             book >= 0, book, bump));
+  // one stream: forking the weight-gradient kernels onto a side stream cost
+  // more in cross-stream graph edges (6-14 us idle each, measured) than the
+  // overlap returned, as every kernel here fills the GPU on its own
+  HIP_TRY(c, launch_backward(nb, c->stream, mark, marg, book >= 0, book, bump));
   return DDQ_OK;
 }
 static int enqueue_fwd_bwd(ddq_ctx* c, void (*mark)(void*, const char*), void* marg) {
@@ -801,8 +817,8 @@ int ddq_forward_backward(ddq_ctx* c, float* loss) {
 int ddq_forward_q(ddq_ctx* c) {
   if (!c) return fail(nullptr, DDQ_EINVAL, "null ctx");
   TRY(set_dev(c));
-  HIP_TRY(c, launch_act(c->nb, c->nb.state, c->nb.B, c->act_p1, c->act_p2, c->act_p3, c->act_h4,
-                        c->act_part, c->nb.q_out, nullptr, c->act_p1s, c->act_p2s, c->stream));
+  HIP_TRY(c, launch_act(c->nb, c->nb.state, c->nb.B, c->act_p3, c->act_h4, c->act_part,
+                        c->nb.q_out, nullptr, c->act_p1s, c->act_p2s, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return DDQ_OK;
 }
@@ -835,10 +851,6 @@ int ddq_read_pool_mask(ddq_ctx* c, int32_t layer, uint8_t* dst, int64_t n) {
   const uint8_t* src = layer == 1 ? c->nb.mask1 : (layer == 2 ? c->nb.mask2 : c->nb.mask3);
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   HIP_TRY(c, scopy(c, tmp.data(), src, cnt, hipMemcpyDeviceToHost));
-  if (layer == 3 && c->nb.conv_impl != 1) {   // GEMM engine: pool3 routing in Caffe order
-    memcpy(dst, tmp.data(), cnt);
-    return DDQ_OK;
-  }
   for (int b = 0; b < B; ++b)
     for (int ch = 0; ch < C; ++ch)
       for (int p = 0; p < Hp * Hp; ++p)
@@ -853,8 +865,8 @@ int ddq_select_action(ddq_ctx* c, const uint8_t* states, int32_t n, int32_t* act
   const size_t bytes = (size_t)n * 4 * c->nb.S * c->nb.S;
   HIP_TRY(c, hipMemcpyAsync(c->act_u8, states, bytes, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(c, launch_u8_to_nhwc(c->act_u8, n, c->nb.S, c->act_in, c->stream));
-  HIP_TRY(c, launch_act(c->nb, c->act_in, n, c->act_p1, c->act_p2, c->act_p3, c->act_h4,
-                        c->act_part, c->act_q, c->act_out, c->act_p1s, c->act_p2s, c->stream));
+  HIP_TRY(c, launch_act(c->nb, c->act_in, n, c->act_p3, c->act_h4, c->act_part, c->act_q,
+                        c->act_out, c->act_p1s, c->act_p2s, c->stream));
   HIP_TRY(c, hipMemcpyAsync(actions, c->act_out, n * 4, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return DDQ_OK;
@@ -973,10 +985,19 @@ static int step_inc(const ddq_ctx* c, const ddq_step_cfg* cfg) {
 static bool is_async(const ddq_ctx* c, const ddq_step_cfg* cfg) {
   return has_exchange(c, cfg) && cfg->exchange == DDQ_EXCHANGE_ASYNC;
 }
+// Once the async exchange began, the central model lives in the owners'
+// shards: other step kinds would train a replica the owners never see.
+static int check_not_async(ddq_ctx* c) {
+  if (c->async_on)
+    return fail(c, DDQ_ESTATE, "the async exchange is in progress on this ctx (its central "
+                               "model lives in the owners' shards): async steps only");
+  return DDQ_OK;
+}
 
 // Overlapped all-reduce, part 1 (called by launch_backward right after the
 // fc4 weight-gradient kernel): the comm stream sums the fc4 weight bucket
-// (2.1 M of the 2.2 M parameters at 64x64) while the conv backward runs.
+// (2.1 M of the 2.2 M parameters at 64x64) while the conv backward runs;
+// cev[2] marks it done (the fused apply's slab-reduce launch waits for it).
 static hipError_t fc4_bucket_start(void* arg) {
   ddq_ctx* c = reinterpret_cast<ddq_ctx*>(arg);
   const ParamLayout& L = c->nb.L;
@@ -989,7 +1010,7 @@ static hipError_t fc4_bucket_start(void* arg) {
     c->comm_err = ncclGetErrorString(r);
     return hipErrorUnknown;
   }
-  return hipSuccess;
+  return hipEventRecord(c->cev[2], c->cs);
 }
 
 static int enqueue_fwd_bwd_x(ddq_ctx* c, const NetBuffers& nb, void (*mark)(void*, const char*),
@@ -998,9 +1019,8 @@ static int enqueue_fwd_bwd_x(ddq_ctx* c, const NetBuffers& nb, void (*mark)(void
   HIP_TRY(c, launch_forward(nb, 2, c->stream, mark, marg, false));
   if (mark) mark(marg, "head");
   HIP_TRY(c, launch_head(nb, c->stream, bump));   // fused apply: the draw counter advances here
-  hipError_t e = launch_backward(nb, c->stream, mark, marg, mark == nullptr && (nb.variant & 16),
-                                 book >= 0, book, bump, overlap ? fc4_bucket_start : nullptr, c,
-                                 pf);
+  hipError_t e = launch_backward(nb, c->stream, mark, marg, book >= 0, book, bump,
+                                 overlap ? fc4_bucket_start : nullptr, c, pf);
   if (e != hipSuccess && !c->comm_err.empty()) {
     std::string m = c->comm_err;
     c->comm_err.clear();
@@ -1012,8 +1032,9 @@ static int enqueue_fwd_bwd_x(ddq_ctx* c, const NetBuffers& nb, void (*mark)(void
 
 // Gradient exchange + apply of one step over RCCL (graph-capturable):
 //  ALLREDUCE  sum all-reduce, replicated apply (overlap: fc4 bucket on the
-//             comm stream under the conv backward, the rest -- conv layers,
-//             fc4 bias, Q_out -- as one grouped call after the slab reduce);
+//             comm stream under the conv backward, applied by the slab-reduce
+//             launch (nb.fa.ext); the rest -- conv layers, fc4 bias, Q_out --
+//             as one grouped call after the slab reduce, then their apply);
 //  SHARDED    reduce-scatter(sum) -> owner apply of its 1/W shard ->
 //             in-place all-gather of theta -> conv layouts / P <- Q refresh;
 //  SERVER     all-to-all of gradient slices -> owner applies the W gradients
@@ -1028,7 +1049,20 @@ static int enqueue_exchange_apply(ddq_ctx* c, const ddq_step_cfg* cfg, const Net
   if (ex == DDQ_EXCHANGE_NONE || ex == DDQ_EXCHANGE_ALLREDUCE) {
     if (ex == DDQ_EXCHANGE_ALLREDUCE) {
       if (mark) mark(marg, "allreduce");
-      if (overlap) {
+      if (overlap && nb.fa.on) {
+        // fc4's weights were summed under the conv backward and applied by
+        // the slab-reduce launch (nb.fa.ext), whose stream waited for that
+        // all-reduce: the rest (4 % of the parameters) right here on the ctx
+        // stream -- nothing is left to overlap it with, and a comm-stream
+        // round trip costs a graph fork / join (measured 0.968 against 0.995
+        // of the exchange-free step at world 1 with it)
+        NCCL_TRY(c, ncclGroupStart());
+        NCCL_TRY(c, ncclAllReduce(nb.grad, nb.grad, (size_t)L.w[3], ncclFloat, ncclSum, c->comm,
+                                  c->stream));
+        NCCL_TRY(c, ncclAllReduce(nb.grad + L.b[3], nb.grad + L.b[3], (size_t)(L.total - L.b[3]),
+                                  ncclFloat, ncclSum, c->comm, c->stream));
+        NCCL_TRY(c, ncclGroupEnd());
+      } else if (overlap) {
         HIP_TRY(c, hipEventRecord(c->cev[0], c->stream));
         HIP_TRY(c, hipStreamWaitEvent(c->cs, c->cev[0], 0));
         NCCL_TRY(c, ncclGroupStart());
@@ -1088,10 +1122,12 @@ static int enqueue_train(ddq_ctx* c, const ddq_step_cfg* cfg, const NetBuffers& 
   // exchange-free steps: fc4's weight update rides on the slab-reduce launch
   // (DDQ_VARIANT bit 512: off, A/B); per-kernel profiling keeps it separate
   const int ex = has_exchange(c, cfg) ? cfg->exchange : DDQ_EXCHANGE_NONE;
-  if (ex == DDQ_EXCHANGE_NONE && mark == nullptr && nb.conv_impl == 1 && !(nb.variant & 16) &&
-      !(nb.variant & 512) && fused_apply_ok(nb.L)) {
+  const bool ar_overlap = ex == DDQ_EXCHANGE_ALLREDUCE && cfg->overlap && c->comm;
+  if ((ex == DDQ_EXCHANGE_NONE || ar_overlap) && fused_apply_ok(nb.L)) {
     const ddq_update_cfg& u = cfg->update;
     nb.fa.on = 1;
+    nb.fa.ext = ar_overlap ? 1 : 0;
+    nb.fc4_wait = ar_overlap ? c->cev[2] : nullptr;
     nb.fa.rule = u.rule;
     nb.fa.period = cfg->target_period > 0 ? cfg->target_period : 0;
     nb.fa.lr = u.lr; nb.fa.decay = u.decay; nb.fa.eps = u.eps;
@@ -1102,12 +1138,10 @@ static int enqueue_train(ddq_ctx* c, const ddq_step_cfg* cfg, const NetBuffers& 
     // launch draws the next minibatch with it
     const Prefetch pf = make_prefetch(*pre, c->r_state, c->r_action, c->r_reward, c->r_nonterm,
                                       c->r_meta, cfg->seed);
-    const bool overlap = has_exchange(c, cfg) && cfg->exchange == DDQ_EXCHANGE_ALLREDUCE &&
-                         cfg->overlap && c->comm && mark == nullptr;
     // fused apply: the slab-reduce launch carries the draw + gather too
     TRY(enqueue_fwd_bwd_x(c, nb, mark, marg, cfg->target_period > 0 ? cfg->target_period : 0,
-                          c->r_meta, overlap, nb.fa.on ? &pf : nullptr));
-    return enqueue_exchange_apply(c, cfg, nb, mark, marg, overlap, nb.fa.on ? nullptr : &pf);
+                          c->r_meta, ar_overlap, nb.fa.on ? &pf : nullptr));
+    return enqueue_exchange_apply(c, cfg, nb, mark, marg, ar_overlap, nb.fa.on ? nullptr : &pf);
   }
   if (pre) {
     HIP_TRY(c, hipEventRecord(nb.ev[6], c->stream));
@@ -1117,11 +1151,9 @@ static int enqueue_train(ddq_ctx* c, const ddq_step_cfg* cfg, const NetBuffers& 
                              nb.side));
     HIP_TRY(c, hipEventRecord(nb.ev[7], nb.side));
   }
-  const bool overlap = has_exchange(c, cfg) && cfg->exchange == DDQ_EXCHANGE_ALLREDUCE &&
-                       cfg->overlap && c->comm && mark == nullptr;
   TRY(enqueue_fwd_bwd_x(c, nb, mark, marg, cfg->target_period > 0 ? cfg->target_period : 0, bump,
-                        overlap));
-  TRY(enqueue_exchange_apply(c, cfg, nb, mark, marg, overlap));
+                        ar_overlap));
+  TRY(enqueue_exchange_apply(c, cfg, nb, mark, marg, ar_overlap));
   if (pre) HIP_TRY(c, hipStreamWaitEvent(c->stream, nb.ev[7], 0));
   return DDQ_OK;
 }
@@ -1158,8 +1190,6 @@ static int initial_target_sync(ddq_ctx* c, const ddq_step_cfg* cfg) {
   if (cfg->target_period > 0 && c->applied % cfg->target_period == 0) {
     HIP_TRY(c, hipMemcpyAsync(c->nb.theta[1], c->nb.theta[0], c->nb.L.total * 4,
                               hipMemcpyDeviceToDevice, c->stream));
-    HIP_TRY(c, hipMemcpyAsync(c->nb.wk[1], c->nb.wk[0], c->nb.L.wk_total * 4,
-                              hipMemcpyDeviceToDevice, c->stream));
     HIP_TRY(c, hipMemcpyAsync(c->nb.wks[1], c->nb.wks[0], c->nb.L.wks_total * 3 * 2,
                               hipMemcpyDeviceToDevice, c->stream));
   }
@@ -1182,15 +1212,32 @@ static int check_step(ddq_ctx* c, const ddq_step_cfg* cfg) {
 }
 
 // ---------------- asynchronous param server (DDQ_EXCHANGE_ASYNC) ----------------
-// Worker side of a tick: the minibatch draw + gather and the forward/backward
-// on the model this worker last pulled (no apply bookkeeping: the owners keep
-// the iteration), into nb.grad, on the ctx stream.
+// The reference's workers free-run (main.py:61-112: fetch -> experience ->
+// full_pass -> push) against one server that applies every pushed gradient on
+// arrival (server.py:196-209) and copies Q -> P on a pull that sees
+// iteration % period == 0 (server.py:181-193).  Here rank r owns shard r of
+// the central model and its optimizer state; a TICK is one push: worker w's
+// gradient slices go to the owners, each owner applies its slice (iteration
+// += 1), the owners send worker w their shards (and the central P's when a
+// special update happened since w's last pull), and w computes its next
+// gradient on the model it pulled while the other ticks proceed.  Which
+// worker pushes at each tick is the arrival order: round-robin (the
+// deterministic test schedule, one step = W ticks) or ticket order (the
+// worker whose gradient is ready first; ddq_async_tick / ddq_group_async_run).
+
+// Worker side: the minibatch draw + gather and the forward/backward on the
+// model this worker last pulled (no apply bookkeeping: the owners keep the
+// iteration), into nb.grad, on the ctx stream; grad_ev marks it ready.
 static int async_compute(ddq_ctx* c, const ddq_step_cfg* cfg) {
   const NetBuffers& nb = c->nb;
   HIP_TRY(c, launch_sample(nb, c->r_meta, cfg->seed, c->stream));
   HIP_TRY(c, launch_gather(nb, c->r_state, c->r_action, c->r_reward, c->r_nonterm, c->r_meta,
                            c->stream));
-  return enqueue_fwd_bwd_x(c, nb, nullptr, nullptr, -1, nullptr, false);
+  TRY(enqueue_fwd_bwd_x(c, nb, nullptr, nullptr, -1, nullptr, false));
+  HIP_TRY(c, hipEventRecord(c->grad_ev, c->stream));
+  c->ready_seen = false;
+  c->grad_ev_captured = c->acapture;
+  return DDQ_OK;
 }
 
 // The special update (server.py:186-189) runs when a pull sees iteration %
@@ -1199,69 +1246,78 @@ static int async_compute(ddq_ctx* c, const ddq_step_cfg* cfg) {
 static bool async_pull_p(const ddq_step_cfg* cfg, int64_t last, int64_t now) {
   return cfg->target_period > 0 && now / cfg->target_period > last / cfg->target_period;
 }
-// the iteration worker (it - 1 - base) % W last pulled at, for its pull at
-// iteration it: one round earlier, or the common start (every rank knows it)
-static int64_t async_last_pull(const ddq_ctx* c, int64_t it) {
-  return it - c->nranks > c->async_base ? it - c->nranks : c->async_base;
-}
 
-// First async step: the owner copies start from this rank's replica (after
-// the pull at iteration 0, which is a special update), and the worker's
-// first gradient is computed on it.
-static int async_begin(ddq_ctx* c, const ddq_step_cfg* cfg, hipStream_t s) {
+// Start of the async exchange on this ctx (any earlier steps taken, the
+// replicas equal): the central model's shards start from this replica (after
+// the pull at the current iteration -- a special update when it is a
+// multiple of the period, e.g. 0), every worker pulled there, and the
+// worker's first gradient is computed on it.
+static int async_begin(ddq_ctx* c, const ddq_step_cfg* cfg) {
   const int64_t P = c->nb.L.total;
   if (!c->own) TRY(dalloc(c, &c->own, (size_t)P + kShardPad));
   if (!c->pown) TRY(dalloc(c, &c->pown, (size_t)P + kShardPad));
+  if (!c->grad_ev) {
+    HIP_TRY(c, hipEventCreateWithFlags(&c->grad_ev, hipEventDisableTiming));
+    HIP_TRY(c, hipEventCreateWithFlags(&c->tick_ev, hipEventDisableTiming));
+  }
   TRY(initial_target_sync(c, cfg));
   HIP_TRY(c, hipMemcpyAsync(c->own, c->nb.theta[0], P * 4, hipMemcpyDeviceToDevice, c->stream));
   HIP_TRY(c, hipMemcpyAsync(c->pown, c->nb.theta[1], P * 4, hipMemcpyDeviceToDevice, c->stream));
-  c->async_base = c->applied;
-  TRY(async_compute(c, cfg));
-  (void)s;
-  return DDQ_OK;
+  c->last_pull.assign(c->nranks, c->applied);
+  c->async_on = true;
+  // the owner duties run on the comm stream: it starts after the copies
+  HIP_TRY(c, hipEventRecord(c->cev[0], c->stream));
+  HIP_TRY(c, hipStreamWaitEvent(c->cs, c->cev[0], 0));
+  return async_compute(c, cfg);
 }
 
-// Owner side of a tick, on stream s: the received slice (in gsl) applied to
-// the owned shard on arrival (iteration += 1), and the central P shard
-// updated when this tick's pull is a special update.
-static int async_owner_apply(ddq_ctx* c, const ddq_step_cfg* cfg, int64_t it, hipStream_t s) {
+// Owner side of a tick, on the comm stream: the received slice (in gsl)
+// applied to the owned shard on arrival (iteration += 1, the launch's own
+// bookkeeping), and the central P shard updated when this tick's pull (at
+// iteration it) is a special update.
+static int async_owner_apply(ddq_ctx* c, const ddq_step_cfg* cfg, int64_t it) {
   const ddq_update_cfg& u = cfg->update;
   const int64_t L = c->shard_len, off = (int64_t)c->rank * L;
-  HIP_TRY(c, launch_book(c->nb, cfg->target_period > 0 ? cfg->target_period : 0, s));
   HIP_TRY(c, launch_apply_shard(c->nb, u.rule, u.lr, u.decay, u.eps, u.momentum, u.weight_decay,
-                                c->gsl, off, L, L, 1, s, c->own));
+                                c->gsl, off, L, L, 1, c->cs, c->own, c->applied == 0 ? 1 : 0));
   if (cfg->target_period > 0 && it % cfg->target_period == 0)
-    HIP_TRY(c, hipMemcpyAsync(c->pown + off, c->own + off, L * 4, hipMemcpyDeviceToDevice, s));
+    HIP_TRY(c, hipMemcpyAsync(c->pown + off, c->own + off, L * 4, hipMemcpyDeviceToDevice, c->cs));
   return DDQ_OK;
 }
 
 // Worker side after its pull (theta[0], and theta[1] when pull_p, hold the
-// central model): kernel layouts of Q (and P), then the next gradient.
+// central model; the ctx stream waited for them): kernel layouts of Q (and
+// P), then the next gradient.
 static int async_after_pull(ddq_ctx* c, const ddq_step_cfg* cfg, bool pull_p) {
   HIP_TRY(c, launch_refresh(c->nb, c->stream, 0));
   if (pull_p) {   // P's layouts from the pulled P weights
     NetBuffers pb = c->nb;
-    pb.theta[0] = c->nb.theta[1]; pb.wk[0] = c->nb.wk[1]; pb.wks[0] = c->nb.wks[1];
+    pb.theta[0] = c->nb.theta[1]; pb.wks[0] = c->nb.wks[1];
     HIP_TRY(c, launch_refresh(pb, c->stream, 0));
   }
   return async_compute(c, cfg);
 }
 
-// One round (W ticks) over RCCL: owner duties and the point-to-point pushes /
-// pulls on the comm stream, this rank's gradient on the ctx stream -- it
-// overlaps the other ranks' ticks.
-static int rccl_async_round(ddq_ctx* c, const ddq_step_cfg* cfg) {
+// Host bookkeeping of a tick (every rank / member: the same tick sequence).
+static void async_advance(ddq_ctx* c, int w, int64_t it) {
+  c->applied = it;
+  c->last_pull[w] = it;
+  c->async_ticks++;
+}
+
+// One tick over RCCL (worker w pushes): point-to-point pushes / pulls and the
+// owner apply on the comm stream, the pulling worker's next gradient on its
+// ctx stream -- it overlaps the later ticks' owner duties.
+static int rccl_async_tick(ddq_ctx* c, const ddq_step_cfg* cfg, int w) {
   const int W = c->nranks, r = c->rank;
   const int64_t L = c->shard_len;
   NetBuffers& nb = c->nb;
-  if (!c->cs) TRY(setup_shards(c, W));
-  if (c->steps == 0) TRY(async_begin(c, cfg, c->cs));
-  HIP_TRY(c, hipEventRecord(c->cev[0], c->stream));       // the gradient (and the copies)
-  for (int w = 0; w < W; ++w) {
-    const int64_t it = c->applied + w + 1;    // iteration after tick w's apply
-    const bool pull_p = async_pull_p(cfg, async_last_pull(c, it), it);
-    if (r == w) HIP_TRY(c, hipStreamWaitEvent(c->cs, c->cev[0], 0));
-    // push: worker w's gradient slices to their owners
+  const int64_t it = c->applied + 1;    // iteration after this tick's apply
+  const bool pull_p = async_pull_p(cfg, c->last_pull[w], it);
+  if (r == w && (!c->acapture || c->grad_ev_captured))
+    HIP_TRY(c, hipStreamWaitEvent(c->cs, c->grad_ev, 0));
+  // push: worker w's gradient slices to their owners
+  if (W > 1) {
     NCCL_TRY(c, ncclGroupStart());
     if (r == w) {
       for (int j = 0; j < W; ++j)
@@ -1270,11 +1326,13 @@ static int rccl_async_round(ddq_ctx* c, const ddq_step_cfg* cfg) {
       NCCL_TRY(c, ncclRecv(c->gsl, L, ncclFloat, w, c->comm, c->cs));
     }
     NCCL_TRY(c, ncclGroupEnd());
-    if (r == w)
-      HIP_TRY(c, hipMemcpyAsync(c->gsl, nb.grad + (size_t)r * L, L * 4, hipMemcpyDeviceToDevice,
-                                c->cs));
-    TRY(async_owner_apply(c, cfg, it, c->cs));
-    // pull: the owners' shards to worker w
+  }
+  if (r == w)
+    HIP_TRY(c, hipMemcpyAsync(c->gsl, nb.grad + (size_t)r * L, L * 4, hipMemcpyDeviceToDevice,
+                              c->cs));
+  TRY(async_owner_apply(c, cfg, it));
+  // pull: the owners' shards to worker w
+  if (W > 1) {
     NCCL_TRY(c, ncclGroupStart());
     if (r != w) {
       NCCL_TRY(c, ncclSend(c->own + (size_t)r * L, L, ncclFloat, w, c->comm, c->cs));
@@ -1288,20 +1346,180 @@ static int rccl_async_round(ddq_ctx* c, const ddq_step_cfg* cfg) {
       }
     }
     NCCL_TRY(c, ncclGroupEnd());
-    if (r == w) {
-      HIP_TRY(c, hipMemcpyAsync(nb.theta[0] + (size_t)r * L, c->own + (size_t)r * L, L * 4,
-                                hipMemcpyDeviceToDevice, c->cs));
-      if (pull_p)
-        HIP_TRY(c, hipMemcpyAsync(nb.theta[1] + (size_t)r * L, c->pown + (size_t)r * L, L * 4,
-                                  hipMemcpyDeviceToDevice, c->cs));
-      HIP_TRY(c, hipEventRecord(c->cev[1], c->cs));
-      HIP_TRY(c, hipStreamWaitEvent(c->stream, c->cev[1], 0));
-      TRY(async_after_pull(c, cfg, pull_p));
-    }
   }
-  // the step ends when this rank's owner duties are done as well
+  if (r == w) {
+    HIP_TRY(c, hipMemcpyAsync(nb.theta[0] + (size_t)r * L, c->own + (size_t)r * L, L * 4,
+                              hipMemcpyDeviceToDevice, c->cs));
+    if (pull_p)
+      HIP_TRY(c, hipMemcpyAsync(nb.theta[1] + (size_t)r * L, c->pown + (size_t)r * L, L * 4,
+                                hipMemcpyDeviceToDevice, c->cs));
+    HIP_TRY(c, hipEventRecord(c->tick_ev, c->cs));
+    HIP_TRY(c, hipStreamWaitEvent(c->stream, c->tick_ev, 0));
+    TRY(async_after_pull(c, cfg, pull_p));
+  }
+  async_advance(c, w, it);
+  return DDQ_OK;
+}
+
+// the ctx stream waits for the comm stream's owner duties so far
+static int async_join(ddq_ctx* c) {
   HIP_TRY(c, hipEventRecord(c->cev[1], c->cs));
   HIP_TRY(c, hipStreamWaitEvent(c->stream, c->cev[1], 0));
+  return DDQ_OK;
+}
+
+static int async_prepare(ddq_ctx* c, const ddq_step_cfg* cfg) {
+  if (c->local) return fail(c, DDQ_ESTATE, "in-process group members step with ddq_group_step");
+  if (!c->cs) TRY(setup_shards(c, c->nranks));
+  if (!c->async_on) TRY(async_begin(c, cfg));
+  return DDQ_OK;
+}
+
+// One round-robin round (W ticks, worker 0 .. W-1): a step of the async exchange.
+static int rccl_async_round(ddq_ctx* c, const ddq_step_cfg* cfg) {
+  for (int w = 0; w < c->nranks; ++w) TRY(rccl_async_tick(c, cfg, w));
+  return async_join(c);   // the step ends when this rank's owner duties are done
+}
+
+int ddq_async_begin(ddq_ctx* c, const ddq_step_cfg* cfg) {
+  TRY(check_step(c, cfg));
+  if (cfg->exchange != DDQ_EXCHANGE_ASYNC) return fail(c, DDQ_EINVAL, "cfg exchange is not async");
+  TRY(set_dev(c));
+  return async_prepare(c, cfg);
+}
+
+// Is this worker's gradient pushable: computed (grad_ev), and -- for an
+// emulated straggler -- straggle_us of host time since that was first seen.
+static int grad_ready(ddq_ctx* c, bool* ready) {
+  const hipError_t e = hipEventQuery(c->grad_ev);
+  if (e != hipSuccess && e != hipErrorNotReady)
+    return fail(c, DDQ_EHIP, "hipEventQuery: %s", hipGetErrorString(e));
+  *ready = false;
+  if (e != hipSuccess) return DDQ_OK;
+  const auto now = std::chrono::steady_clock::now();
+  if (!c->ready_seen) {
+    c->ready_seen = true;
+    c->ready_at = now;
+  }
+  *ready = now - c->ready_at >= std::chrono::microseconds(c->straggle_us);
+  return DDQ_OK;
+}
+
+int ddq_async_ready(ddq_ctx* c, int32_t* ready) {
+  if (!c || !ready) return fail(c, DDQ_EINVAL, "null argument");
+  if (!c->async_on) return fail(c, DDQ_ESTATE, "async exchange not begun (ddq_async_begin)");
+  TRY(set_dev(c));
+  bool r = false;
+  TRY(grad_ready(c, &r));
+  *ready = r ? 1 : 0;
+  return DDQ_OK;
+}
+
+int ddq_async_tick(ddq_ctx* c, const ddq_step_cfg* cfg, int32_t worker) {
+  TRY(check_step(c, cfg));
+  if (cfg->exchange != DDQ_EXCHANGE_ASYNC) return fail(c, DDQ_EINVAL, "cfg exchange is not async");
+  if (worker < 0 || worker >= c->nranks)
+    return fail(c, DDQ_EINVAL, "worker %d out of [0, %d)", worker, c->nranks);
+  TRY(set_dev(c));
+  TRY(async_prepare(c, cfg));
+  c->rr_rounds = 0;   // the round-robin graph's steady state no longer holds
+  return rccl_async_tick(c, cfg, worker);
+}
+
+// ---- round-robin rounds as hipGraphs ----
+// A round's launches depend on the host state only through the iteration's
+// residue mod the special-update period (which ticks pull P, which owners
+// copy Q -> P) and the workers' last pulls, which after one whole round-robin
+// round are one round back for everyone.  So K = period / gcd(W, period)
+// rounds (K W iterations, a multiple of the period) form a graph that is
+// valid whenever a round starts at the residue it was captured at; the host
+// bookkeeping of a replay is the captured ticks' (async_advance).  Rounds
+// before that alignment (and the remainder of a call) run eagerly.
+static constexpr int kAsyncGraphMaxRounds = 16;
+
+static int async_graph_rounds(const ddq_ctx* c, const ddq_step_cfg* cfg) {
+  if (cfg->target_period <= 0) return 1;
+  int a = c->nranks, b = cfg->target_period;
+  while (b) { const int t = a % b; a = b; b = t; }
+  return cfg->target_period / a;
+}
+
+static int64_t async_phase(const ddq_ctx* c, const ddq_step_cfg* cfg) {
+  return cfg->target_period > 0 ? c->applied % cfg->target_period : 0;
+}
+
+static int async_round_eager(ddq_ctx* c, const ddq_step_cfg* cfg) {
+  TRY(rccl_async_round(c, cfg));
+  c->steps++;
+  c->rr_rounds++;
+  return DDQ_OK;
+}
+
+static int ensure_async_graph(ddq_ctx* c, const ddq_step_cfg* cfg, int K) {
+  if (c->agexec && memcmp(&c->acfg, cfg, sizeof(*cfg)) == 0) return DDQ_OK;
+  if (c->agexec) hipGraphExecDestroy(c->agexec);
+  c->agexec = nullptr;
+  const int64_t applied = c->applied, ticks = c->async_ticks;
+  const std::vector<int64_t> last = c->last_pull;
+  HIP_TRY(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+  c->acapture = true;
+  c->grad_ev_captured = false;
+  // the comm stream joins the capture (its owner duties follow the graph's start)
+  int rc = DDQ_OK;
+  hipError_t e = hipEventRecord(c->cev[0], c->stream);
+  if (e == hipSuccess) e = hipStreamWaitEvent(c->cs, c->cev[0], 0);
+  if (e != hipSuccess) rc = fail(c, DDQ_EHIP, "async graph fork: %s", hipGetErrorString(e));
+  for (int k = 0; k < K && rc == DDQ_OK; ++k) rc = rccl_async_round(c, cfg);
+  hipGraph_t g = nullptr;
+  e = hipStreamEndCapture(c->stream, &g);
+  c->acapture = false;
+  c->applied = applied;             // the capture ran the ticks' host bookkeeping
+  c->async_ticks = ticks;
+  c->last_pull = last;
+  if (rc != DDQ_OK) { if (g) hipGraphDestroy(g); return rc; }
+  if (e != hipSuccess) return fail(c, DDQ_EHIP, "hipStreamEndCapture: %s", hipGetErrorString(e));
+  e = hipGraphInstantiate(&c->agexec, g, nullptr, nullptr, 0);
+  hipGraphDestroy(g);
+  if (e != hipSuccess) return fail(c, DDQ_EHIP, "hipGraphInstantiate: %s", hipGetErrorString(e));
+  HIP_TRY(c, hipGraphUpload(c->agexec, c->stream));
+  c->acfg = *cfg;
+  c->agraph_rounds = K;
+  c->agraph_phase = async_phase(c, cfg);
+  return DDQ_OK;
+}
+
+static int async_graph_steps(ddq_ctx* c, const ddq_step_cfg* cfg, int nsteps) {
+  TRY(async_prepare(c, cfg));
+  const int K = async_graph_rounds(c, cfg);
+  int i = 0;
+  if (K > kAsyncGraphMaxRounds) {
+    for (; i < nsteps; ++i) TRY(async_round_eager(c, cfg));
+    return DDQ_OK;
+  }
+  while (i < nsteps) {
+    const bool steady = c->rr_rounds >= 1;
+    if (steady && nsteps - i >= K &&
+        (c->agexec == nullptr || memcmp(&c->acfg, cfg, sizeof(*cfg)) != 0 ||
+         async_phase(c, cfg) == c->agraph_phase)) {
+      TRY(ensure_async_graph(c, cfg, K));
+      HIP_TRY(c, hipGraphLaunch(c->agexec, c->stream));
+      for (int k = 0; k < K; ++k)
+        for (int w = 0; w < c->nranks; ++w) async_advance(c, w, c->applied + 1);
+      c->steps += K;
+      c->rr_rounds += K;
+      i += K;
+      continue;
+    }
+    TRY(async_round_eager(c, cfg));
+    ++i;
+  }
+  return DDQ_OK;
+}
+
+int ddq_set_straggle(ddq_ctx* c, int64_t usec) {
+  if (!c) return fail(nullptr, DDQ_EINVAL, "null ctx");
+  if (usec < 0 || usec > 1000000) return fail(c, DDQ_EINVAL, "usec must be in [0, 1e6]");
+  c->straggle_us = usec;
   return DDQ_OK;
 }
 
@@ -1309,12 +1527,10 @@ int ddq_step_async(ddq_ctx* c, const ddq_step_cfg* cfg) {
   TRY(check_step(c, cfg));
   TRY(set_dev(c));
   if (is_async(c, cfg)) {
-    if (c->local) return fail(c, DDQ_ESTATE, "in-process group members step with ddq_group_step");
-    TRY(rccl_async_round(c, cfg));
-    c->steps++;
-    c->applied += step_inc(c, cfg);
-    return DDQ_OK;
+    TRY(async_prepare(c, cfg));
+    return async_round_eager(c, cfg);
   }
+  TRY(check_not_async(c));
   if (c->steps == 0) TRY(initial_target_sync(c, cfg));
   TRY(enqueue_step(c, cfg, nullptr, nullptr));
   c->steps++;
@@ -1346,8 +1562,8 @@ static int capture_steps(ddq_ctx* c, const ddq_step_cfg* cfg, int k, hipGraphExe
 static constexpr int kGraphSteps = 8;
 
 static int ensure_graph(ddq_ctx* c, const ddq_step_cfg* cfg) {
-  if (is_async(c, cfg))
-    return fail(c, DDQ_EINVAL, "the async exchange runs eager steps (ddq_step_async)");
+  if (is_async(c, cfg)) return DDQ_OK;   // captured when a round starts at its phase
+  TRY(check_not_async(c));
   if (!c->have_graph || memcmp(&c->gcfg, cfg, sizeof(*cfg)) != 0) {
     invalidate_graph(c);
     TRY(capture_steps(c, cfg, 1, &c->gexec));
@@ -1361,6 +1577,7 @@ static int ensure_graph(ddq_ctx* c, const ddq_step_cfg* cfg) {
 int ddq_step_graph_async(ddq_ctx* c, const ddq_step_cfg* cfg, int32_t nsteps) {
   TRY(check_step(c, cfg));
   TRY(set_dev(c));
+  if (is_async(c, cfg)) return async_graph_steps(c, cfg, nsteps);
   TRY(ensure_graph(c, cfg));
   if (c->steps == 0 && nsteps > 0) TRY(initial_target_sync(c, cfg));
   int i = 0;
@@ -1400,7 +1617,9 @@ static int capture_exec(ddq_ctx* c, hipGraphExec_t* out, const std::function<int
 
 static int ensure_pipe(ddq_ctx* c, const ddq_step_cfg* cfg) {
   if (is_async(c, cfg))
-    return fail(c, DDQ_EINVAL, "the async exchange runs eager steps (ddq_step_async)");
+    return fail(c, DDQ_EINVAL, "the async exchange runs round-robin rounds (ddq_step_async, "
+                               "ddq_step_graph_async) or ticks (ddq_async_tick)");
+  TRY(check_not_async(c));
   if (!c->mb2_state) {
     const int B = c->nb.B, S = c->nb.S;
     TRY(dalloc(c, &c->mb2_state, (size_t)B * S * S * 4));
@@ -1522,58 +1741,68 @@ int ddq_group_init(ddq_ctx** ctxs, int32_t W) {
   return DDQ_OK;
 }
 
-// One async round of an in-process group: rccl_async_round's schedule with
-// the point-to-point transfers as device copies, tick by tick (members
-// synchronised between the phases of a tick: a correctness path).
-static int group_async_round(ddq_ctx** ctxs, int W, const ddq_step_cfg* cfg) {
-  auto sync_all = [&]() -> int {
-    for (int r = 0; r < W; ++r) {
-      TRY(set_dev(ctxs[r]));
-      HIP_TRY(ctxs[r], hipStreamSynchronize(ctxs[r]->stream));
-    }
-    return DDQ_OK;
-  };
-  for (int r = 0; r < W; ++r)
-    if (ctxs[r]->steps == 0) {
-      TRY(set_dev(ctxs[r]));
-      TRY(async_begin(ctxs[r], cfg, ctxs[r]->stream));
-    }
+// In-process group ticks: rccl_async_tick with the point-to-point transfers
+// as device copies, ordered by events only (no host synchronisation): owner r
+// copies worker w's slice into its gsl on its comm stream once w's gradient is
+// ready, applies it, and copies its shard (and P's) into w's replica -- the
+// sender side of the pull, so its next apply cannot overtake the copy -- then
+// marks the tick; worker w's ctx stream waits for every owner's mark, and
+// recomputes.
+static int group_async_tick(ddq_ctx** ctxs, int W, const ddq_step_cfg* cfg, int w) {
+  ddq_ctx* cw = ctxs[w];
   const int64_t L = ctxs[0]->shard_len;
-  for (int w = 0; w < W; ++w) {
-    const int64_t it = ctxs[0]->applied + w + 1;
-    const bool pull_p = async_pull_p(cfg, async_last_pull(ctxs[0], it), it);
-    TRY(sync_all());
-    for (int r = 0; r < W; ++r) {   // push + owner apply
-      ddq_ctx* c = ctxs[r];
-      TRY(set_dev(c));
-      HIP_TRY(c, hipMemcpyAsync(c->gsl, ctxs[w]->nb.grad + (size_t)r * L, L * 4,
-                                hipMemcpyDeviceToDevice, c->stream));
-      TRY(async_owner_apply(c, cfg, it, c->stream));
-    }
-    TRY(sync_all());
-    ddq_ctx* cw = ctxs[w];           // pull
-    TRY(set_dev(cw));
-    for (int r = 0; r < W; ++r) {
-      HIP_TRY(cw, hipMemcpyAsync(cw->nb.theta[0] + (size_t)r * L, ctxs[r]->own + (size_t)r * L,
-                                 L * 4, hipMemcpyDeviceToDevice, cw->stream));
-      if (pull_p)
-        HIP_TRY(cw, hipMemcpyAsync(cw->nb.theta[1] + (size_t)r * L, ctxs[r]->pown + (size_t)r * L,
-                                   L * 4, hipMemcpyDeviceToDevice, cw->stream));
-    }
-    TRY(async_after_pull(cw, cfg, pull_p));
-  }
-  TRY(sync_all());
+  const int64_t it = ctxs[0]->applied + 1;
+  const bool pull_p = async_pull_p(cfg, ctxs[0]->last_pull[w], it);
   for (int r = 0; r < W; ++r) {
-    ctxs[r]->steps++;
-    ctxs[r]->applied += step_inc(ctxs[r], cfg);
+    ddq_ctx* c = ctxs[r];
+    TRY(set_dev(c));
+    HIP_TRY(c, hipStreamWaitEvent(c->cs, cw->grad_ev, 0));
+    HIP_TRY(c, hipMemcpyAsync(c->gsl, cw->nb.grad + (size_t)r * L, L * 4,
+                              hipMemcpyDeviceToDevice, c->cs));
+    TRY(async_owner_apply(c, cfg, it));
+    HIP_TRY(c, hipMemcpyAsync(cw->nb.theta[0] + (size_t)r * L, c->own + (size_t)r * L, L * 4,
+                              hipMemcpyDeviceToDevice, c->cs));
+    if (pull_p)
+      HIP_TRY(c, hipMemcpyAsync(cw->nb.theta[1] + (size_t)r * L, c->pown + (size_t)r * L, L * 4,
+                                hipMemcpyDeviceToDevice, c->cs));
+    HIP_TRY(c, hipEventRecord(c->tick_ev, c->cs));
+  }
+  TRY(set_dev(cw));
+  for (int r = 0; r < W; ++r) HIP_TRY(cw, hipStreamWaitEvent(cw->stream, ctxs[r]->tick_ev, 0));
+  TRY(async_after_pull(cw, cfg, pull_p));
+  for (int r = 0; r < W; ++r) async_advance(ctxs[r], w, it);
+  return DDQ_OK;
+}
+
+static int group_async_prepare(ddq_ctx** ctxs, int W, const ddq_step_cfg* cfg) {
+  for (int r = 0; r < W; ++r) {
+    if (ctxs[r]->async_on) continue;
+    TRY(set_dev(ctxs[r]));
+    TRY(async_begin(ctxs[r], cfg));
   }
   return DDQ_OK;
 }
 
-// One synchronous data-parallel step of an in-process group: the same
-// kernels and exchange semantics as RCCL ranks, with the collectives done as
-// device copies between the members' buffers, phase by phase.
-int ddq_group_step(ddq_ctx** ctxs, int32_t W, const ddq_step_cfg* cfg) {
+static int group_sync_all(ddq_ctx** ctxs, int W) {
+  for (int r = 0; r < W; ++r) {
+    ddq_ctx* c = ctxs[r];
+    TRY(set_dev(c));
+    HIP_TRY(c, hipStreamSynchronize(c->cs));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+  }
+  return DDQ_OK;
+}
+
+// One round-robin round of an in-process group (synchronised at its end).
+static int group_async_round(ddq_ctx** ctxs, int W, const ddq_step_cfg* cfg) {
+  TRY(group_async_prepare(ctxs, W, cfg));
+  for (int w = 0; w < W; ++w) TRY(group_async_tick(ctxs, W, cfg, w));
+  TRY(group_sync_all(ctxs, W));
+  for (int r = 0; r < W; ++r) ctxs[r]->steps++;
+  return DDQ_OK;
+}
+
+static int check_group(ddq_ctx** ctxs, int W, const ddq_step_cfg* cfg) {
   if (!ctxs || !cfg || W < 1) return fail(nullptr, DDQ_EINVAL, "bad argument");
   for (int r = 0; r < W; ++r) {
     ddq_ctx* c = ctxs[r];
@@ -1581,8 +1810,68 @@ int ddq_group_step(ddq_ctx** ctxs, int32_t W, const ddq_step_cfg* cfg) {
       return fail(c, DDQ_ESTATE, "ctx %d is not rank %d of a %d-member group", r, r, W);
     TRY(check_step(c, cfg));
   }
+  return DDQ_OK;
+}
+
+// Ticks in a given worker order (deterministic: the order of a ticket run, or
+// any test schedule), synchronised at the end.
+int ddq_group_async_ticks(ddq_ctx** ctxs, int32_t W, const ddq_step_cfg* cfg, int32_t n,
+                          const int32_t* order) {
+  TRY(check_group(ctxs, W, cfg));
+  if (cfg->exchange != DDQ_EXCHANGE_ASYNC) return fail(ctxs[0], DDQ_EINVAL, "cfg exchange is not async");
+  if (n < 0 || (n > 0 && !order)) return fail(ctxs[0], DDQ_EINVAL, "bad tick order");
+  for (int t = 0; t < n; ++t)
+    if (order[t] < 0 || order[t] >= W)
+      return fail(ctxs[0], DDQ_EINVAL, "tick %d: worker %d out of [0, %d)", t, order[t], W);
+  TRY(group_async_prepare(ctxs, W, cfg));
+  for (int t = 0; t < n; ++t) TRY(group_async_tick(ctxs, W, cfg, order[t]));
+  return group_sync_all(ctxs, W);
+}
+
+// Ticket order (arrival order) for an in-process group: the host polls the
+// members' gradient-ready events and gives the next ticket to the first
+// member found ready (the scan starts after the last ticket's holder), then
+// enqueues that tick.  Nothing waits on the device for a ticket: the order is
+// decided on the host, as the reference's single server decides it by the
+// order its HTTP handler takes modelLock (server.py:196-209).
+int ddq_group_async_run(ddq_ctx** ctxs, int32_t W, const ddq_step_cfg* cfg, int32_t npush,
+                        int32_t* order) {
+  TRY(check_group(ctxs, W, cfg));
+  if (cfg->exchange != DDQ_EXCHANGE_ASYNC) return fail(ctxs[0], DDQ_EINVAL, "cfg exchange is not async");
+  if (npush < 0) return fail(ctxs[0], DDQ_EINVAL, "npush must be >= 0");
+  TRY(group_async_prepare(ctxs, W, cfg));
+  int start = 0;
+  for (int t = 0; t < npush; ++t) {
+    int pick = -1;
+    for (int64_t spin = 0; pick < 0; ++spin) {
+      for (int k = 0; k < W && pick < 0; ++k) {
+        const int w = (start + k) % W;
+        TRY(set_dev(ctxs[w]));
+        bool r = false;
+        TRY(grad_ready(ctxs[w], &r));
+        if (r) pick = w;
+      }
+      if (pick < 0) {
+        if (spin > 2000000)   // ~minutes without any gradient finishing: a stall
+          return fail(ctxs[0], DDQ_EHIP, "async run: no gradient became ready");
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+      }
+    }
+    if (order) order[t] = pick;
+    TRY(group_async_tick(ctxs, W, cfg, pick));
+    start = (pick + 1) % W;
+  }
+  return group_sync_all(ctxs, W);
+}
+
+// One synchronous data-parallel step of an in-process group: the same
+// kernels and exchange semantics as RCCL ranks, with the collectives done as
+// device copies between the members' buffers, phase by phase.
+int ddq_group_step(ddq_ctx** ctxs, int32_t W, const ddq_step_cfg* cfg) {
+  TRY(check_group(ctxs, W, cfg));
   const int ex = cfg->exchange;
   if (ex == DDQ_EXCHANGE_ASYNC) return group_async_round(ctxs, W, cfg);
+  for (int r = 0; r < W; ++r) TRY(check_not_async(ctxs[r]));
   const ddq_update_cfg& u = cfg->update;
   const int64_t P = ctxs[0]->nb.L.total;
   std::vector<hipEvent_t> ev(W);
@@ -1711,6 +2000,7 @@ int ddq_profile_step(ddq_ctx* c, const ddq_step_cfg* cfg, char* names, float* us
   TRY(check_step(c, cfg));
   if (!n) return fail(c, DDQ_EINVAL, "null n");
   if (is_async(c, cfg)) return fail(c, DDQ_EINVAL, "profile steps take no async exchange");
+  TRY(check_not_async(c));
   TRY(set_dev(c));
   c->marks.clear();
   c->ev_used = 0;

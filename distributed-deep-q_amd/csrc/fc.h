@@ -249,17 +249,13 @@ __global__ __launch_bounds__(256) void fc4_fwd_split_kernel(const Fc4FwdArgs a) 
 inline int fc4_fwd_splits(int K) { return (K + kFc4KLen - 1) / kFc4KLen; }
 
 inline hipError_t launch_fc4_fwd_direct(const Fc4FwdArgs& a, hipStream_t st) {
-  bool sp = true;
-#ifdef DDQ_EXPERIMENTS
-  if (const char* e = getenv("DDQ_FC4_SPLIT")) sp = atoi(e) != 0;
-#endif
   if (a.B <= 32) {
-    hipLaunchKernelGGL(sp ? fc4_fwd_split_kernel<1> : fc4_fwd_direct_kernel<1>,
-                       dim3(512 / 128, fc4_fwd_splits(a.K), a.nz), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(fc4_fwd_split_kernel<1>, dim3(512 / 128, fc4_fwd_splits(a.K), a.nz),
+                       dim3(256), 0, st, a);
   } else {
     const int nbt = (a.B + 63) / 64;
-    hipLaunchKernelGGL(sp ? fc4_fwd_split_kernel<2> : fc4_fwd_direct_kernel<2>,
-                       dim3(512 / 128, fc4_fwd_splits(a.K), a.nz * nbt), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(fc4_fwd_split_kernel<2>, dim3(512 / 128, fc4_fwd_splits(a.K), a.nz * nbt),
+                       dim3(256), 0, st, a);
   }
   return hipGetLastError();
 }
@@ -386,19 +382,5 @@ __global__ __launch_bounds__(512) void fc4_dgrad_direct_kernel(const Fc4DgradArg
   fc4_dgrad_body<SPLIT>(a, red, blockIdx.x, blockIdx.y);
 }
 
-inline bool fc4_dgrad_split() {
-#ifdef DDQ_EXPERIMENTS
-  if (const char* e = getenv("DDQ_FC4D_SPLIT")) return atoi(e) != 0;
-#endif
-  return true;
-}
-
-inline hipError_t launch_fc4_dgrad_direct(const Fc4DgradArgs& a, hipStream_t st) {
-  dim3 grid(a.K / 32, (a.B + 31) / 32);
-  hipLaunchKernelGGL(fc4_dgrad_split() ? fc4_dgrad_direct_kernel<true>
-                                       : fc4_dgrad_direct_kernel<false>,
-                     grid, dim3(512), 0, st, a);
-  return hipGetLastError();
-}
 
 }  // namespace ddq

@@ -13,8 +13,6 @@ struct ParamLayout {
   int64_t w[5], b[5];      // offsets of layer weights / biases
   int64_t wn[5], bn[5];    // counts
   int64_t total;
-  int64_t wk_off[3];       // offsets of conv kernel-layout copies in the wk buffer
-  int64_t wk_total;
   int64_t wks_off[3];      // offsets of the split (3 x bf16) forward weights in a wks plane
   int64_t wkst_off;        // conv2 data-gradient split weights [ci][tap'][co] (Q only)
   int64_t wkst3_off;       // conv3 data-gradient split weights [ci][tap'][co] (Q only)
@@ -32,9 +30,15 @@ struct ReplayMeta {
   int32_t pad;
 };
 
-// Fused fc4-weight apply (exchange-free steps): the update rule of the step.
+// Fused apply: the update rule of the step.  ext = 0 (exchange-free steps):
+// the slab-reduce launch computes fc4's weight gradient tile by tile and
+// updates every parameter where its gradient becomes final.  ext = 1 (RCCL
+// all-reduce with overlap): fc4_bwd computes fc4's weight gradient, the comm
+// stream sums it over the ranks under the conv backward (fc4_wait), the
+// slab-reduce launch applies fc4's weights from it, and launch_apply the rest
+// after their (small) all-reduce.
 struct FusedApplyCfg {
-  int on;
+  int on, ext;
   int rule, period;
   float lr, decay, eps, momentum, wd;
 };
@@ -44,9 +48,10 @@ struct NetBuffers {
   // minibatch (NHWC frames; action one-hot (B,4); reward / non_terminal (B))
   float *state, *next_state, *action, *reward, *nonterm;
   int32_t* idx;
-  // activations per tower z (0 = Q on state, 1 = P on next_state); the
-  // forward convs read their input split (split.h), the Q backward fp32
-  float *pool1[2], *pool2[2], *pool3[2], *h4[2];
+  // activations per tower z (0 = Q on state, 1 = P on next_state): pool1 /
+  // pool2 only split (split.h: the next conv and the Q weight gradients read
+  // them split), pool3 fp32 in Caffe order (fc4's input)
+  float *pool3[2], *h4[2];
   __bf16 *pool1s[2], *pool2s[2];    // split pool1 / pool2 (3 planes, NHWC)
   uint8_t *mask1, *mask2, *mask3;   // Q tower only
   float* fc4_part;                  // [splits][2][B][512]
@@ -57,30 +62,30 @@ struct NetBuffers {
   // blobs
   float *q_out, *p_out, *q_sa, *p_sa, *target, *loss;
   // backward scratch
-  float *dh4, *dconv3, *dconv2, *dconv1;
+  float *dh4, *dconv3;               // dh4 (B,512); dconv3: fp32 pooled dpool3 (fc4 dgrad)
   __bf16 *dconv2s, *dconv1s;        // split pooled dpool2 / dpool1 (conv3 / conv2 data gradients)
   float* wpart;                     // conv wgrad slabs (3 layers, disjoint)
   int64_t wpart_off[3];
   int wsplits[3];
   int wnp[3];
-  // parameters: theta[z] flat Caffe layout; wk[z] conv kernel layout (fp32,
-  // the data gradients); wks[z] split kernel layout (the forward convs);
-  // grad; opt state
-  float *theta[2], *wk[2], *grad, *opt;
+  // parameters: theta[z] flat Caffe layout; wks[z] split kernel layouts (the
+  // forward convs; Q's also the data gradients' transposed copies); grad; opt
+  // state
+  float *theta[2], *grad, *opt;
   __bf16* wks[2];
   float *dqbuf, *lpart;             // head: per-sample dQ (B,4) and squared error (B)
   int32_t* opt_init;                // 0 until the first apply after a reset
   int64_t* iter;                    // applied updates (param-server iteration)
-  // second stream + events for concurrent wgrad / dgrad branches (optional)
+  // side stream + events: the next step's sample + gather beside a step whose
+  // apply launch cannot carry them (pipelined stepping, B > 256)
   hipStream_t side;
   hipEvent_t ev[8];
+  hipEvent_t fc4_wait;              // the slab-reduce launch waits for it (fa.ext)
   ParamLayout L;
   float gamma;
-  int conv_impl;                    // 0 = implicit-GEMM engine, 1 = direct (patch-in-LDS)
-  int variant;                      // tuning experiments (DDQ_VARIANT bits), 0 = default
   int fwd_only;                     // launch_forward: 0 = every layer, l + 1 = conv layer l only
   FusedApplyCfg fa;                 // on: head latches the apply flags, the slab reduce
-                                    // applies fc4's weights, launch_apply the rest
+                                    // applies (FusedApplyCfg)
   int book_inc;                     // param-server iterations per apply (1, or W: server mode)
 };
 
@@ -100,10 +105,12 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s, void (*ma
 hipError_t launch_head(const NetBuffers& nb, hipStream_t s, ReplayMeta* bump = nullptr);
 bool fused_apply_ok(const ParamLayout& L);
 struct Prefetch;
-// concurrent: run the weight-gradient GEMMs on nb.side beside the data-gradient chain.
-// pf (fused apply only): the next step's draw + gather as blocks of the slab-reduce launch.
+// book: the slab reduce also does the apply bookkeeping (target period
+// book_period); fc4_done: called right after the fc4 weight gradient is
+// enqueued (the overlapped all-reduce starts there); pf (fused apply only):
+// the next step's draw + gather as blocks of the slab-reduce launch.
 hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(void*, const char*),
-                           void* mark_arg, bool concurrent, bool book = false, int book_period = 0,
+                           void* mark_arg, bool book = false, int book_period = 0,
                            ReplayMeta* bump = nullptr, hipError_t (*fc4_done)(void*) = nullptr,
                            void* fc4_done_arg = nullptr, const Prefetch* pf = nullptr);
 // period > 0: also copy Q -> P when the next pull sees iteration % period == 0.
@@ -131,11 +138,13 @@ hipError_t launch_relayout(const NetBuffers& nb, int z, hipStream_t s);
 // applied in rank order; then, after the theta all-gather, launch_refresh
 // rebuilds the conv kernel layouts and performs a latched P <- Q sync.
 // theta: the parameters updated (default nb.theta[0]; the async exchange's
-// owner copy otherwise)
+// owner copy otherwise).  first >= 0: the rules' first-call flag from the host
+// and the apply's bookkeeping (iteration += 1) done by the launch itself
+// (async owner applies); -1: the flags latched by a prior launch_book.
 hipError_t launch_apply_shard(const NetBuffers& nb, int rule, float lr, float decay, float eps,
                               float momentum, float wd, const float* gsl, int64_t off,
                               int64_t len, int64_t slice, int W, hipStream_t s,
-                              float* theta = nullptr);
+                              float* theta = nullptr, int first = -1);
 // force_sync >= 0: P <- Q decided by the host instead of the latched flag
 hipError_t launch_refresh(const NetBuffers& nb, hipStream_t s, int force_sync = -1);
 // one apply's bookkeeping (first-call / sync latches, iteration += 1)
@@ -143,9 +152,9 @@ hipError_t launch_book(const NetBuffers& nb, int period, hipStream_t s);
 hipError_t launch_sum_slices(float* out, const float* in, int W, int64_t len, int64_t slice,
                              hipStream_t s);
 // Q-tower forward of n states (NHWC f32 in `in`) into scratch, argmax into out.
-hipError_t launch_act(const NetBuffers& nb, const float* in, int n, float* pool1, float* pool2,
-                      float* pool3, float* h4, float* part, float* qout, int32_t* actions,
-                      __bf16* pool1s, __bf16* pool2s, hipStream_t s);
+hipError_t launch_act(const NetBuffers& nb, const float* in, int n, float* pool3, float* h4,
+                      float* part, float* qout, int32_t* actions, __bf16* pool1s,
+                      __bf16* pool2s, hipStream_t s);
 // large-batch device draw (bitmap claim + ordered compaction) into idx[0..n)
 // and the Caffe-layout (n,4,S,S) f32 gather of replay.py:167-183
 hipError_t launch_sample_batch(ReplayMeta* meta, int64_t valid, int n, uint64_t seed,

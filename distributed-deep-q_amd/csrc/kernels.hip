@@ -1,10 +1,6 @@
 // deepq step kernels for MI355X (gfx950).  See DESIGN.md for the data layout
-// and the roofline of each kernel; layers.h for the implicit-GEMM problems.
+// and the roofline of each kernel.
 #include "kernels.h"
-#include "layers.h"
-#include "direct.h"
-#include "wgrad1.h"
-#include "wgradd.h"
 #include "wgrads.h"
 #include "fc.h"
 #include "split.h"
@@ -40,9 +36,6 @@ ParamLayout make_layout(int S) {
     L.b[i] = o; L.bn[i] = bn[i]; o += bn[i];
   }
   L.total = o;
-  int64_t q = 0;
-  for (int i = 0; i < 3; ++i) { L.wk_off[i] = q; q += wn[i]; }
-  L.wk_total = q;
   // split forward weights: conv1 [n][7][8][4] (kx 7 zero), conv2/3 [co][tap][ci]
   L.wks_off[0] = 0;
   L.wks_off[1] = kConv1WPlane;
@@ -503,18 +496,10 @@ hipError_t launch_u8_to_nhwc(const uint8_t* src, int n, int S, float* dst, hipSt
 // ---------------------------------------------------------------------------
 // Caffe (co,ci,ky,kx) -> kernel layout (co,ky,kx,ci) for the three convs
 // ---------------------------------------------------------------------------
-struct ConvDims { int64_t w_off, wk_off, wks_off; int cout, cin, ks; };
+struct ConvDims { int64_t w_off, wks_off; int cout, cin, ks; };
 
 // e: Caffe-order element (co, ci, ky, kx) of the layer's weight (< 2^31);
-// returns its offset in the kernel layout Wk[co][tap][ci].
-__device__ __forceinline__ int wk_local(const ConvDims& d, int e) {
-  const int kk = d.ks * d.ks, per = d.cin * kk;
-  const int co = e / per, rem = e - co * per;
-  const int ci = rem / kk, tap = rem - ci * kk;
-  return (co * kk + tap) * d.cin + ci;
-}
-
-// e as in wk_local; its offset in the split forward layout (split.h):
+// returns its offset in the split forward layout (split.h):
 // conv1 [co][ky][kx 0..7][ci] (kx 7 stays zero), conv2/3 [co][tap][ci]
 __device__ __forceinline__ int wks_local(const ConvDims& d, int e) {
   const int kk = d.ks * d.ks, per = d.cin * kk;
@@ -527,36 +512,32 @@ __device__ __forceinline__ int wks_local(const ConvDims& d, int e) {
   return (co * kk + tap) * d.cin + ci;
 }
 
-// conv weight element k (of layer d) now holds v: refresh the fp32 kernel
-// layout and the split forward layout (the split data gradient reads the
-// latter transposed)
-__device__ __forceinline__ void put_conv_weight(const ConvDims& d, int e, float v, float* wk,
-                                                __bf16* wks, int64_t wks_plane) {
-  wk[d.wk_off + wk_local(d, e)] = v;
+// conv weight element e (of layer d) now holds v: refresh its split forward
+// layout (the split data gradients read it transposed, head kernel)
+__device__ __forceinline__ void put_conv_weight(const ConvDims& d, int e, float v, __bf16* wks,
+                                                int64_t wks_plane) {
   store_split(wks, wks_plane, d.wks_off + wks_local(d, e), v);
 }
 
-__global__ void relayout_kernel(const float* __restrict__ theta, float* __restrict__ wk,
-                                __bf16* __restrict__ wks, int64_t wks_plane, ConvDims d0,
-                                ConvDims d1, ConvDims d2) {
+__global__ void relayout_kernel(const float* __restrict__ theta, __bf16* __restrict__ wks,
+                                int64_t wks_plane, ConvDims d0, ConvDims d1, ConvDims d2) {
   const int l = blockIdx.y;
   const ConvDims d = l == 0 ? d0 : (l == 1 ? d1 : d2);
   const int n = d.cout * d.cin * d.ks * d.ks;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x)
-    put_conv_weight(d, e, theta[d.w_off + e], wk, wks, wks_plane);
+    put_conv_weight(d, e, theta[d.w_off + e], wks, wks_plane);
 }
 
 static void conv_dims(const ParamLayout& L, ConvDims* d) {
   const int cout[3] = {32, 64, 64}, cin[3] = {4, 32, 64}, ks[3] = {7, 5, 3};
-  for (int i = 0; i < 3; ++i)
-    d[i] = {L.w[i], L.wk_off[i], L.wks_off[i], cout[i], cin[i], ks[i]};
+  for (int i = 0; i < 3; ++i) d[i] = {L.w[i], L.wks_off[i], cout[i], cin[i], ks[i]};
 }
 
 hipError_t launch_relayout(const NetBuffers& nb, int z, hipStream_t s) {
   ConvDims d[3];
   conv_dims(nb.L, d);
-  hipLaunchKernelGGL(relayout_kernel, dim3(64, 3), dim3(256), 0, s, nb.theta[z], nb.wk[z],
-                     nb.wks[z], nb.L.wks_total, d[0], d[1], d[2]);
+  hipLaunchKernelGGL(relayout_kernel, dim3(64, 3), dim3(256), 0, s, nb.theta[z], nb.wks[z],
+                     nb.L.wks_total, d[0], d[1], d[2]);
   return hipGetLastError();
 }
 
@@ -826,16 +807,16 @@ struct ApplyTail {
   const float* grad;
   float* opt;
   const int32_t* opt_init;   // [2] first call, [3] P<-Q sync due: latched before the launch
-  float* wk;
   float* thetaP;
-  float* wkP;
   __bf16* wks;               // split forward weights of Q / P (plane stride wks_plane)
   __bf16* wksP;
   int64_t wks_plane;
   int nfa;                   // slab reduce: fc4 apply blocks (the first of the launch)
   int rest;                  // slab reduce: also update conv / fc4-bias / fc5 params
+  int ext;                   // slab reduce: fc4's weight gradient is in grad already
+                             // (computed by fc4_bwd, summed over the ranks under the
+                             // conv backward): apply from it instead of computing it
   int64_t w5_off, b5_off, b4_off;
-  int skip;                  // experiment builds only: block roles to skip (timing A/B)
 };
 
 __device__ __forceinline__ void apply_at(const ApplyTail& t, const ApplyArgs& a, bool first,
@@ -962,7 +943,7 @@ hipError_t launch_head(const NetBuffers& nb, hipStream_t s, ReplayMeta* bump) {
 struct WredDims {
   int64_t w_off, b_off, part_off;
   int cout, cin, ks, splits, np, blk0;   // blk0: first workgroup of this layer
-  int64_t wk_off, wks_off;               // the layer's kernel / split layouts (fused apply)
+  int64_t wks_off;                       // the layer's split layout (fused apply)
   int G;                                 // waves per unit (1, 2 or 4)
 };
 
@@ -1012,8 +993,8 @@ __device__ __forceinline__ void apply_elems(const ApplyTail& t, const ApplyArgs&
     if (e0 >= 0 && e0 < (int64_t)d.cout * d.cin * d.ks * d.ks) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        put_conv_weight(d, (int)e0 + e, th[e], t.wk, t.wks, t.wks_plane);
-        if (sync) put_conv_weight(d, (int)e0 + e, th[e], t.wkP, t.wksP, t.wks_plane);
+        put_conv_weight(d, (int)e0 + e, th[e], t.wks, t.wks_plane);
+        if (sync) put_conv_weight(d, (int)e0 + e, th[e], t.wksP, t.wks_plane);
       }
     }
   }
@@ -1032,8 +1013,8 @@ __device__ __forceinline__ void apply_at(const ApplyTail& t, const ApplyArgs& a,
   if (a.rule != 0) t.opt[i] = st;
   if (sync) t.thetaP[i] = th;
   if (conv) {
-    put_conv_weight(cd, e, th, t.wk, t.wks, t.wks_plane);
-    if (sync) put_conv_weight(cd, e, th, t.wkP, t.wksP, t.wks_plane);
+    put_conv_weight(cd, e, th, t.wks, t.wks_plane);
+    if (sync) put_conv_weight(cd, e, th, t.wksP, t.wks_plane);
   }
 }
 
@@ -1108,12 +1089,20 @@ __device__ __forceinline__ void fc4_apply_tile(const ApplyTail& t, const ApplyAr
     if (a.rule != 0 && !first) s4[r] = *reinterpret_cast<const float4*>(t.opt + i0 + (int64_t)r * K);
   }
   float g[R][4];
-  fc4_wgrad_sum<R>(B, K, dh4, x, o0, k, g);
+  if (t.ext) {   // summed over the ranks already (all-reduce under the conv backward)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const float4 g4 = *reinterpret_cast<const float4*>(t.grad + i0 + (int64_t)r * K);
+      g[r][0] = g4.x; g[r][1] = g4.y; g[r][2] = g4.z; g[r][3] = g4.w;
+    }
+  } else {
+    fc4_wgrad_sum<R>(B, K, dh4, x, o0, k, g);
+  }
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int64_t i = i0 + (int64_t)r * K;
     const uint32_t ib = (uint32_t)(i * 4);
-    wt_store4(rg, ib, make_float4(g[r][0], g[r][1], g[r][2], g[r][3]));
+    if (!t.ext) wt_store4(rg, ib, make_float4(g[r][0], g[r][1], g[r][2], g[r][3]));
     float th[4] = {t4[r].x, t4[r].y, t4[r].z, t4[r].w};
     float st[4] = {s4[r].x, s4[r].y, s4[r].z, s4[r].w};
 #pragma unroll
@@ -1214,7 +1203,7 @@ __device__ __forceinline__ void wred_block(const float* __restrict__ part, float
   if (h == 0 && live) {
     grad[idx] = v;
     if (rest) {
-      const ConvDims cd{d.w_off, d.wk_off, d.wks_off, d.cout, d.cin, d.ks};
+      const ConvDims cd{d.w_off, d.wks_off, d.cout, d.cin, d.ks};
       const bool wt = n < kc;
       apply_at(fat, faa, first, sync, idx, v, th, st, !wt, wt, cd, (int)(idx - d.w_off));
     }
@@ -1233,14 +1222,14 @@ __global__ __launch_bounds__(256, 4) void wgrad_reduce_kernel(
     const float* __restrict__ fc4_x, int fc4_k) {
   __shared__ float red[4][4][64];
   if ((int)blockIdx.x < pf.ng) {   // fused apply: the next step's draw + gather first
-    if (!(fat.skip & 8)) prefetch_body(pf, blockIdx.x);
+    prefetch_body(pf, blockIdx.x);
     return;
   }
   int bid = blockIdx.x - pf.ng;
   if (fat.nfa > 0) {   // fused fc4-weight gradient + apply blocks come first: the
                        // longest HBM streams start before the reduce blocks
     if (bid < fat.nfa) {
-      if (!(fat.skip & 1)) fc4_apply_tile(fat, faa, hs.B, fc4_k, hs.dh4, fc4_x, bid);
+      fc4_apply_tile(fat, faa, hs.B, fc4_k, hs.dh4, fc4_x, bid);
       return;
     }
     bid -= fat.nfa;
@@ -1248,7 +1237,6 @@ __global__ __launch_bounds__(256, 4) void wgrad_reduce_kernel(
   if (opt_init && bid == 0 && threadIdx.x == 0)
     apply_book(iter, opt_init, book_period, bump, book_inc);
   const bool rest = fat.rest != 0;
-  if (fat.skip & (bid >= nub ? 2 : 4)) return;
   if (bid >= nub) {
     head_sums(bid - nub, hs.B, hs.dqbuf, hs.lpart, hs.h4q, hs.dh4, hs.loss, hs.gw5, hs.gb5,
               hs.gb4, rest, fat, faa);
@@ -1293,11 +1281,18 @@ __global__ void apply_book_kernel(int64_t* iter, int32_t* opt_init, int period) 
 // state held in registers across the W updates.  Only the first gradient of
 // the first apply takes the rules' first-call branch.  Conv kernel layouts and
 // the P tower are refreshed after the all-gather (refresh_kernel).
+// first >= 0: the rules' first-call flag given by the host (async owner
+// applies, whose bookkeeping is this kernel's: block 0 advances the iteration
+// and marks the state initialised -- nothing in the launch reads either)
 __global__ __launch_bounds__(256) void apply_shard_kernel(
     float* __restrict__ theta, const float* __restrict__ gsl, float* __restrict__ opt,
-    const int32_t* __restrict__ opt_init, int64_t off, int64_t len, int64_t slice, int W,
-    ApplyArgs a) {
-  const bool first = opt_init[2] != 0;
+    int32_t* __restrict__ opt_init, int64_t off, int64_t len, int64_t slice, int W,
+    ApplyArgs a, int first_host, int64_t* iter) {
+  const bool first = first_host >= 0 ? first_host != 0 : opt_init[2] != 0;
+  if (first_host >= 0 && blockIdx.x == 0 && threadIdx.x == 0) {
+    *iter += 1;
+    opt_init[0] = 1;
+  }
   const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (j >= len) return;
   const int64_t i = off + j;
@@ -1322,9 +1317,7 @@ __global__ __launch_bounds__(256) void apply_shard_kernel(
 // force >= 0: the P <- Q decision given by the host (async exchange pulls)
 __global__ __launch_bounds__(256) void refresh_kernel(const float* __restrict__ theta,
                                                       const int32_t* __restrict__ opt_init,
-                                                      float* __restrict__ wk,
-                                                      float* __restrict__ thetaP,
-                                                      float* __restrict__ wkP, __bf16* wks,
+                                                      float* __restrict__ thetaP, __bf16* wks,
                                                       __bf16* wksP, int64_t wks_plane,
                                                       ApplyArgs a, int force) {
   const bool sync = force >= 0 ? force != 0 : opt_init[3] != 0;
@@ -1341,8 +1334,8 @@ __global__ __launch_bounds__(256) void refresh_kernel(const float* __restrict__ 
     if (e0 >= 0 && e0 < (int64_t)d.cout * d.cin * d.ks * d.ks) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        put_conv_weight(d, (int)e0 + e, th[e], wk, wks, wks_plane);
-        if (sync) put_conv_weight(d, (int)e0 + e, th[e], wkP, wksP, wks_plane);
+        put_conv_weight(d, (int)e0 + e, th[e], wks, wks_plane);
+        if (sync) put_conv_weight(d, (int)e0 + e, th[e], wksP, wks_plane);
       }
     }
   }
@@ -1373,9 +1366,11 @@ static ApplyArgs apply_args(const NetBuffers& nb, int rule, float lr, float deca
 }
 
 static ApplyTail apply_tail(const NetBuffers& nb) {
-  return ApplyTail{nb.theta[0], nb.grad,  nb.opt,    nb.opt_init,      nb.wk[0],
-                   nb.theta[1], nb.wk[1], nb.wks[0], nb.wks[1], nb.L.wks_total, 0,
-                   0,           nb.L.w[4], nb.L.b[4], nb.L.b[3], 0};
+  ApplyTail t{};
+  t.theta = nb.theta[0]; t.grad = nb.grad; t.opt = nb.opt; t.opt_init = nb.opt_init;
+  t.thetaP = nb.theta[1]; t.wks = nb.wks[0]; t.wksP = nb.wks[1]; t.wks_plane = nb.L.wks_total;
+  t.w5_off = nb.L.w[4]; t.b5_off = nb.L.b[4]; t.b4_off = nb.L.b[3];
+  return t;
 }
 
 // The fused fc4-weight apply (NetBuffers::fa): fc4's weight gradient is final
@@ -1387,21 +1382,23 @@ bool fused_apply_ok(const ParamLayout& L) {
 
 hipError_t launch_apply_shard(const NetBuffers& nb, int rule, float lr, float decay, float eps,
                               float momentum, float wd, const float* gsl, int64_t off,
-                              int64_t len, int64_t slice, int W, hipStream_t s, float* theta) {
+                              int64_t len, int64_t slice, int W, hipStream_t s, float* theta,
+                              int first) {
   const ApplyArgs a = apply_args(nb, rule, lr, decay, eps, momentum, wd, 0);
   const int64_t blocks = (len / 4 + 255) / 256;
   if (blocks > 0)
     hipLaunchKernelGGL(apply_shard_kernel, dim3((uint32_t)blocks), dim3(256), 0, s,
                        theta ? theta : nb.theta[0], gsl, nb.opt, nb.opt_init, off, len, slice, W,
-                       a);
+                       a, first, nb.iter);
   return hipGetLastError();
 }
+
 
 hipError_t launch_refresh(const NetBuffers& nb, hipStream_t s, int force_sync) {
   const ApplyArgs a = apply_args(nb, 0, 0.f, 0.f, 0.f, 0.f, 0.f, 0);
   hipLaunchKernelGGL(refresh_kernel, dim3((uint32_t)((a.n / 4 + 255) / 256)), dim3(256), 0, s,
-                     nb.theta[0], nb.opt_init, nb.wk[0], nb.theta[1], nb.wk[1], nb.wks[0],
-                     nb.wks[1], nb.L.wks_total, a, force_sync);
+                     nb.theta[0], nb.opt_init, nb.theta[1], nb.wks[0], nb.wks[1],
+                     nb.L.wks_total, a, force_sync);
   return hipGetLastError();
 }
 
@@ -1437,99 +1434,47 @@ hipError_t launch_apply(const NetBuffers& nb, int rule, float lr, float decay, f
   if (pre) pf = *pre;
   ApplyArgs a = apply_args(nb, rule, lr, decay, eps, momentum, wd, period);
   if (!booked) hipLaunchKernelGGL(apply_book_kernel, dim3(1), dim3(1), 0, s, nb.iter, nb.opt_init, period);
-  // fused steps: the slab-reduce launch already updated every parameter
-  const int blocks = nb.fa.on ? 0 : (int)(((a.n - a.skip_len) / 4 + 255) / 256);
+  // fused steps: the slab-reduce launch already updated every parameter --
+  // or, with its fc4 gradient summed over the ranks under the conv backward
+  // (fa.ext), fc4's weights: the rest (summed after the reduce) here
+  if (nb.fa.on && nb.fa.ext) { a.skip_lo = nb.L.w[3]; a.skip_len = nb.L.wn[3]; }
+  const int blocks = (nb.fa.on && !nb.fa.ext) ? 0 : (int)(((a.n - a.skip_len) / 4 + 255) / 256);
   if (blocks + pf.ng == 0) return hipSuccess;
   hipLaunchKernelGGL(apply_kernel, dim3(blocks + pf.ng), dim3(256), 0, s, apply_tail(nb), a, pf);
   return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
-// GEMM configurations per layer (tuned at B = 32, S = 64)
+// layer geometry
 // ---------------------------------------------------------------------------
-using CfgConv1F = GemmCfg<128, 32, 28, 4, 1, 1>;
-using CfgConv2F = GemmCfg<128, 64, 32, 2, 2, 2>;
-using CfgConv3F = GemmCfg<64, 64, 32, 2, 2, 2>;
-using CfgFcF = GemmCfg<32, 64, 64, 1, 2, 2>;
-using CfgFcD = GemmCfg<32, 32, 64, 1, 1, 4>;
-using CfgFcW = GemmCfg<64, 64, 32, 2, 2, 1>;
-using CfgW1 = GemmCfg<32, 256, 32, 1, 4, 2>;
-using CfgW2 = GemmCfg<64, 128, 32, 2, 2, 2>;
-using CfgW3 = GemmCfg<64, 128, 32, 2, 2, 2>;
-using CfgD2 = GemmCfg<128, 32, 32, 4, 1, 2>;
-using CfgD3 = GemmCfg<64, 64, 32, 2, 2, 2>;
+int fc4_splits_for(int S) { return fc4_fwd_splits(64 * (S / 8) * (S / 8)); }
 
-constexpr int kFc4SplitLen = 128;
-constexpr int kWgradSplitLen[3] = {512, 1024, 256};
-constexpr int kWgradBN[3] = {CfgW1::BN, CfgW2::BN, CfgW3::BN};
-constexpr int kWgradBK[3] = {CfgW1::BK, CfgW2::BK, CfgW3::BK};
-
-// split-K: K per split is a multiple of BK, about `target`
-static inline int split_len(int K, int BK, int target, int* nsplit) {
-  int len = std::max(BK, (target / BK) * BK);
-  if (len >= K) { *nsplit = 1; return ((K + BK - 1) / BK) * BK; }
-  *nsplit = (K + len - 1) / len;
-  return len;
+// conv1 weight-gradient band height: the largest power of two <= 8 dividing
+// S (one slab per band)
+static int wgrad1_band(int S) {
+  int R = 8;
+  while (R > 1 && S % R != 0) R >>= 1;
+  return R;
 }
 
-int fc4_splits_for(int S) {
-  const int K = 64 * (S / 8) * (S / 8);
-  int ns;
-  split_len(K, CfgFcF::BK, kFc4SplitLen, &ns);
-  return ns;
-}
-
-int wgrad_splits_for(int layer, int B, int S, int* np, int impl) {
+// Slabs of the conv weight gradients and their pitch np (>= KC + 1: the bias
+// column, padded to 64 for the reduce's units).  conv1: one per band;
+// conv2 / conv3: one per row group (wgrads_groups).
+int wgrad_splits_for(int layer, int B, int S, int* np) {
   const int H = S >> layer;
-  const int K = B * H * H;
   const int KC[3] = {196, 800, 576};
-  *np = ((KC[layer] + 1 + kWgradBN[layer] - 1) / kWgradBN[layer]) * kWgradBN[layer];
-  if (layer == 0 && impl == 1) return B * (S / wgrad1_band(S, S));   // direct: one slab per band
-  if (impl == 1) {                                                    // direct: one slab per row group
-    const int nts[3] = {0, 2 * 5, 2 * 3};
-    int G, RPG;
-    int target = 512;
-    // tuning sweeps; conv3 measured 128: 25.0 us, 256: 16.0, 512: 15.2, 1024: 18.8
-#ifdef DDQ_EXPERIMENTS
-    const char* e = getenv(layer == 2 ? "DDQ_WG3_TARGET" : "DDQ_WG2_TARGET");
-    if (e && atoi(e) > 0) target = atoi(e);
-#endif
-    wgradd_groups(B * H, nts[layer], &G, &RPG, target);
-    return G;
-  }
-  int ns;
-  split_len(K, kWgradBK[layer], kWgradSplitLen[layer], &ns);
-  return ns;
-}
-
-
-
-// dgrad = forward conv of the layer's dconv with the transposed, flipped
-// kernel and padding KS-1-PAD (== PAD for the odd kernels of this net).
-static DirectArgs direct_dgrad_args(const float* dconv, const float* wk, const uint8_t* pmask,
-                                    float* pdconv, int B, int H, int pad) {
-  DirectArgs d{};
-  d.B = B; d.H = H; d.W = H; d.pad = pad;
-  d.in[0] = d.in[1] = dconv; d.wk[0] = d.wk[1] = wk;
-  d.pmask = pmask; d.pdconv = pdconv;
-  return d;
-}
-
-template <class P>
-static WgradDArgs wgradd_args(const P& p, int B, int G) {
-  WgradDArgs a;
-  a.B = B; a.H = p.H; a.W = p.W; a.G = G;
-  a.RPG = (B * p.H + G - 1) / G;
-  a.NP = p.NP; a.dconv = p.dconv; a.in = p.in; a.part = p.part;
-  a.droute = nullptr;
-  return a;
+  *np = ((KC[layer] + 1 + 63) / 64) * 64;
+  if (layer == 0) return B * (S / wgrad1_band(S));
+  const int nts[3] = {0, 2 * 5, 2 * 3};
+  int G, RPG;
+  wgrads_groups(B * H, nts[layer], &G, &RPG, 512);
+  return G;
 }
 
 // fc4 data gradient (blocks [0, nd): fc4_dgrad_body, 512 threads) beside the
-// fc4 weight gradient (blocks [nd, ...): the GEMM engine's FcWgrad, 256
-// threads; the other 4 waves end at once, which s_barrier does not wait for)
-// (threads 256..511 of a gradient block end at once, which s_barrier does
-// not wait for)
+// fc4 weight gradient (blocks [nd, ...): 256 threads; the other 4 waves end at
+// once, which s_barrier does not wait for).  nd = 0 blocks of the weight
+// gradient when the fused apply computes it tile by tile itself.
 template <bool SPLIT>
 __global__ __launch_bounds__(512) void fc4_bwd_kernel(const Fc4DgradArgs d, const float* x,
                                                       float* gw4, int nd, int ndx) {
@@ -1550,382 +1495,166 @@ __global__ __launch_bounds__(512) void fc4_bwd_kernel(const Fc4DgradArgs d, cons
         make_float4(g[r][0], g[r][1], g[r][2], g[r][3]);
 }
 
-// the fc4 weight gradient alone (profiled / concurrent steps)
-__global__ __launch_bounds__(256) void fc4_wgrad_kernel(int B, int K, const float* dh4,
-                                                        const float* x, float* gw4) {
-  float g[8][4];
-  int o0, k;
-  if (!fc4_wgrad_coords<8>(K, blockIdx.x, o0, k)) return;
-  fc4_wgrad_sum<8>(B, K, dh4, x, o0, k, g);
-#pragma unroll
-  for (int r = 0; r < 8; ++r)
-    *reinterpret_cast<float4*>(gw4 + (size_t)(o0 + r) * K + k) =
-        make_float4(g[r][0], g[r][1], g[r][2], g[r][3]);
-}
-
 hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
                           void (*mark)(void*, const char*), void* marg, bool out) {
   const ParamLayout& L = nb.L;
   const int B = nb.B, S = nb.S;
   auto M = [&](const char* n) { if (mark) mark(marg, n); };
+  const float* in[2] = {nb.state, nb.next_state};
   if (!nb.fwd_only || nb.fwd_only == 1) {
-    ConvFwd<4, 32, 7, 3> p;
-    p.nchw = 0;
-    p.M = B * S * S; p.N = 32; p.K = 196; p.ksplit_len = 196;
-    p.H = S; p.W = S; p.fWp = FastDiv(S / 2); p.fHp = FastDiv(S / 2);
-    p.in[0] = nb.state; p.in[1] = nb.next_state;
+    // conv1 (train_val.prototxt:39-78): bf16 matrix cores, fp32-exact
+    // (split.h): frames are exact in bf16, so 3 MFMAs per 32x32x16 block; the
+    // pooled output goes out split (conv2's input) and, for the Q tower, fp32
+    // (conv2's weight gradient)
+    Conv1Args c1{};
+    c1.B = B; c1.H = S; c1.W = S;
     for (int z = 0; z < 2; ++z) {
-      p.wk[z] = nb.wk[z] + L.wk_off[0]; p.bias[z] = nb.theta[z] + L.b[0];
-      p.out[z] = nb.pool1[z];
+      c1.in[z] = in[z];
+      c1.wk[z] = nb.wks[z] + L.wks_off[0];
+      c1.bias[z] = nb.theta[z] + L.b[0];
+      c1.out_split[z] = nb.pool1s[z];
     }
-    p.mask[0] = nb.mask1; p.mask[1] = nullptr;
+    c1.out[0] = c1.out[1] = nullptr;   // conv2 and conv2's weight gradient read it split
+    c1.out_elems = (int64_t)B * (S / 2) * (S / 2) * 32;
+    c1.mask[0] = nb.mask1; c1.mask[1] = nullptr;
     M("conv1_fwd");
-    if (nb.conv_impl == 1) {
-      // bf16 matrix cores, fp32-exact (split.h): frames are exact in bf16, so
-      // 3 MFMAs per 32x32x16 block; the pooled output goes out split (conv2's
-      // input) and, for the Q tower, fp32 (conv2's weight gradient).
-      // (ubench, both towers: 32x32 tiles / 16 waves 14.5 us, 16x32 / 8 waves
-      // 15.0, against 29.3 us for the f32-MFMA direct kernel)
-      Conv1Args c1{};
-      c1.B = B; c1.H = S; c1.W = S;
-      for (int z = 0; z < 2; ++z) {
-        c1.in[z] = p.in[z];
-        c1.wk[z] = nb.wks[z] + L.wks_off[0];
-        c1.bias[z] = p.bias[z];
-        c1.out_split[z] = nb.pool1s[z];
-      }
-      c1.out[0] = nb.pool1[0];   // the P tower needs no fp32 copy
-      c1.out[1] = nullptr;
-      c1.out_elems = (int64_t)B * (S / 2) * (S / 2) * 32;
-      c1.mask[0] = nb.mask1; c1.mask[1] = nullptr;
-      CHECK_LAUNCH((launch_split_conv1<32, 32, 16>(c1, nz, s, L.wks_total)));
-    } else {
-      CHECK_LAUNCH(launch_gemm<CfgConv1F>(p, nz, 1, s));
-    }
+    CHECK_LAUNCH((launch_split_conv1<32, 32, 16>(c1, nz, s, L.wks_total)));
   }
   if (!nb.fwd_only || nb.fwd_only == 2) {
+    // conv2 (train_val.prototxt:79-118): split bf16, 16x16 tiles, 16 waves of
+    // one 32x32 block each
     const int H = S / 2;
-    ConvFwd<32, 64, 5, 2> p;
-    p.nchw = 0;
-    p.M = B * H * H; p.N = 64; p.K = 800; p.ksplit_len = 800;
-    p.H = H; p.W = H; p.fWp = FastDiv(H / 2); p.fHp = FastDiv(H / 2);
+    SplitArgs a2{};
+    a2.B = B; a2.H = H; a2.W = H; a2.pad = 2;
     for (int z = 0; z < 2; ++z) {
-      p.in[z] = nb.pool1[z]; p.wk[z] = nb.wk[z] + L.wk_off[1]; p.bias[z] = nb.theta[z] + L.b[1];
-      p.out[z] = nb.pool2[z];
+      a2.in[z] = nb.pool1s[z];
+      a2.wk[z] = nb.wks[z] + L.wks_off[1];
+      a2.bias[z] = nb.theta[z] + L.b[1];
+      a2.out_split[z] = nb.pool2s[z];
     }
-    p.mask[0] = nb.mask2; p.mask[1] = nullptr;
+    a2.in_elems = (int64_t)B * H * H * 32;
+    a2.wk_elems = L.wks_total;
+    a2.out[0] = a2.out[1] = nullptr;   // conv3 and conv3's weight gradient read it split
+    a2.out_elems = (int64_t)B * (H / 2) * (H / 2) * 64;
+    a2.mask[0] = nb.mask2; a2.mask[1] = nullptr;
     M("conv2_fwd");
-    if (nb.conv_impl == 1) {
-      // split bf16 (split.h): 16x16 tiles, 16 waves of one 32x32 block each
-      // (ubench, both towers: 33.9 us against 53.9 for the f32-MFMA kernel;
-      // 8 waves of 32x64: 34.3; 8x16 tiles: 43)
-      SplitArgs a2{};
-      a2.B = B; a2.H = H; a2.W = H; a2.pad = 2;
-      for (int z = 0; z < 2; ++z) {
-        a2.in[z] = nb.pool1s[z];
-        a2.wk[z] = nb.wks[z] + L.wks_off[1];
-        a2.bias[z] = p.bias[z];
-        a2.out_split[z] = nb.pool2s[z];
-      }
-      a2.in_elems = (int64_t)B * H * H * 32;
-      a2.wk_elems = L.wks_total;
-      a2.out[0] = nb.pool2[0];   // fp32 for the Q tower only (conv3's weight gradient)
-      a2.out[1] = nullptr;
-      a2.out_elems = (int64_t)B * (H / 2) * (H / 2) * 64;
-      a2.mask[0] = nb.mask2; a2.mask[1] = nullptr;
-      // (k groups here -- 4x2 waves x 2 groups, 2 m tiles a wave -- measured
-      // 32.2 against 31.4 us: the 16 waves already cover the LDS latency)
-      CHECK_LAUNCH((launch_split_conv<32, 32, 64, 5, 16, 16, 8, 2, 1, false>(a2, nz, s)));
-    } else {
-      CHECK_LAUNCH(launch_gemm<CfgConv2F>(p, nz, 1, s));
-    }
+    CHECK_LAUNCH((launch_split_conv<32, 32, 64, 5, 16, 16, 8, 2, 1, false>(a2, nz, s)));
   }
   if (!nb.fwd_only || nb.fwd_only == 3) {
+    // conv3 (train_val.prototxt:119-158): split bf16, 8x8 tiles, two k groups
+    // of 4 waves; pool3 (= fc4's input) fp32 in Caffe order, routing bytes
+    // NHWC (the backward expands dpool3 through them)
     const int H = S / 4;
-    ConvFwd<64, 64, 3, 1> p;
-    p.M = B * H * H; p.N = 64; p.K = 576; p.ksplit_len = 576;
-    p.H = H; p.W = H; p.fWp = FastDiv(H / 2); p.fHp = FastDiv(H / 2);
+    SplitArgs a3{};
+    a3.B = B; a3.H = H; a3.W = H; a3.pad = 1;
     for (int z = 0; z < 2; ++z) {
-      p.in[z] = nb.pool2[z]; p.wk[z] = nb.wk[z] + L.wk_off[2]; p.bias[z] = nb.theta[z] + L.b[2];
-      p.out[z] = nb.pool3[z];
+      a3.in[z] = nb.pool2s[z];
+      a3.wk[z] = nb.wks[z] + L.wks_off[2];
+      a3.bias[z] = nb.theta[z] + L.b[2];
+      a3.out[z] = nb.pool3[z];
     }
-    p.mask[0] = nb.mask3; p.mask[1] = nullptr;
-    p.nchw = 1; p.fHWp = FastDiv((H / 2) * (H / 2));   // pool3 = fc4 input in Caffe order
+    a3.in_elems = (int64_t)B * H * H * 64;
+    a3.wk_elems = L.wks_total;
+    a3.nchw = 1;
+    a3.mask[0] = nb.mask3; a3.mask[1] = nullptr;
     M("conv3_fwd");
-    if (nb.conv_impl == 1) {
-      // split bf16: 8x8 tiles, 4 waves (ubench 12.1 us against 14.5 f32);
-      // pool3 (= fc4's input) fp32 in Caffe order, routing bytes NHWC (the
-      // backward expands dpool3 through them)
-      SplitArgs a3{};
-      a3.B = B; a3.H = H; a3.W = H; a3.pad = 1;
-      for (int z = 0; z < 2; ++z) {
-        a3.in[z] = nb.pool2s[z];
-        a3.wk[z] = nb.wks[z] + L.wks_off[2];
-        a3.bias[z] = p.bias[z];
-        a3.out[z] = nb.pool3[z];
-      }
-      a3.in_elems = (int64_t)B * H * H * 64;
-      a3.wk_elems = L.wks_total;
-      a3.nchw = 1;
-      a3.mask[0] = nb.mask3; a3.mask[1] = nullptr;
-      // two k groups of 4 waves (2 waves per SIMD on the LDS-bound single
-      // workgroup per CU): 12.6 -> 11.3 us; four groups measured the same
-      CHECK_LAUNCH((launch_split_conv<64, 64, 64, 3, 8, 8, 2, 2, 2, false>(a3, nz, s)));
-    } else {
-      CHECK_LAUNCH(launch_gemm<CfgConv3F>(p, nz, 1, s));
-    }
+    CHECK_LAUNCH((launch_split_conv<64, 64, 64, 3, 8, 8, 2, 2, 2, false>(a3, nz, s)));
   }
   if (nb.fwd_only) return hipSuccess;   // ddq_time_layer: one conv layer
-  {
-    const int s4 = S / 8;
-    FcFwd p;
-    p.M = B; p.N = kFc4; p.K = 64 * s4 * s4;
-    int ns;
-    p.ksplit_len = split_len(p.K, CfgFcF::BK, kFc4SplitLen, &ns);
-    for (int z = 0; z < 2; ++z) { p.x[z] = nb.pool3[z]; p.w[z] = nb.theta[z] + L.w[3]; }
-    p.part = nb.fc4_part; p.nz = nz;
-    M("fc4_fwd");
-    if (!(nb.variant & 4)) {   // register-direct (bit 4: LDS GEMM engine, A/B)
-      Fc4FwdArgs f;
-      f.B = B; f.K = p.K; f.nz = nz; f.part = nb.fc4_part;
-      for (int z = 0; z < 2; ++z) { f.x[z] = p.x[z]; f.w[z] = p.w[z]; }
-      CHECK_LAUNCH(launch_fc4_fwd_direct(f, s));
-    } else {
-      CHECK_LAUNCH(launch_gemm<CfgFcF>(p, nz, ns, s));
-    }
-    if (!out) return hipSuccess;   // training: reduce + Q_out fused into the head kernel
-    M("fc4_reduce_out");
-    hipLaunchKernelGGL(fc4_reduce_out_kernel, dim3(B, nz), dim3(kFc4), 0, s, nb.fc4_part, ns, nz,
-                       B, nb.theta[0] + L.b[3], nb.theta[1] + L.b[3], nb.theta[0] + L.w[4],
-                       nb.theta[0] + L.b[4], nb.theta[1] + L.w[4], nb.theta[1] + L.b[4],
-                       nb.h4[0], nb.h4[1], nb.q_out, nb.p_out);
-    CHECK_LAUNCH(hipGetLastError());
-  }
+  // fc4 (train_val.prototxt:159-185): split bf16 MFMA register-direct, split-K
+  // partials (reduced by the head kernel, or by fc4_reduce_out below)
+  const int s4 = S / 8;
+  Fc4FwdArgs f;
+  f.B = B; f.K = 64 * s4 * s4; f.nz = nz; f.part = nb.fc4_part;
+  for (int z = 0; z < 2; ++z) { f.x[z] = nb.pool3[z]; f.w[z] = nb.theta[z] + L.w[3]; }
+  M("fc4_fwd");
+  CHECK_LAUNCH(launch_fc4_fwd_direct(f, s));
+  if (!out) return hipSuccess;   // training: reduce + Q_out fused into the head kernel
+  M("fc4_reduce_out");
+  hipLaunchKernelGGL(fc4_reduce_out_kernel, dim3(B, nz), dim3(kFc4), 0, s, nb.fc4_part,
+                     fc4_fwd_splits(f.K), nz, B, nb.theta[0] + L.b[3], nb.theta[1] + L.b[3],
+                     nb.theta[0] + L.w[4], nb.theta[0] + L.b[4], nb.theta[1] + L.w[4],
+                     nb.theta[1] + L.b[4], nb.h4[0], nb.h4[1], nb.q_out, nb.p_out);
+  CHECK_LAUNCH(hipGetLastError());
   return hipSuccess;
 }
 
-// conv3 weight gradient (blocks [0, nw): wgradd body, 4 waves) beside the
-// conv3 data gradient (blocks [nw, ...): register-B direct dgrad, 6 waves;
-// wgrad blocks end their extra 2 waves at once).  Both only need dpool3 and
-// are latency-bound alone (about 25 % of the MFMA roof each); the shared
-// launch was meant to overlap their prologues and tails (A/B only, see the
-// launch site).
-using Conv3DgradCfg = DirectCfg<64, 64, 3, 4, 8, 1, 2, true, false, 3, true>;
-__global__ __launch_bounds__(Conv3DgradCfg::kThreads) void conv3_bwd_kernel(const WgradDArgs w,
-                                                                            const DirectArgs d,
-                                                                            int nw, int ntiles) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int bid = blockIdx.x;
-  if (bid < nw) {
-    if (threadIdx.x >= 256) return;
-    wgradd_body<64, 64, 3, 1, true>(w, sm, bid);
-    return;
-  }
-  const int i = bid - nw;
-  direct_conv_body<64, 64, 3, 4, 8, 1, 2, true, false, 3, true>(d, sm, i % ntiles, i / ntiles, 0);
-}
-
 hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(void*, const char*),
-                           void* marg, bool concurrent, bool book, int book_period,
-                           ReplayMeta* bump, hipError_t (*fc4_done)(void*), void* fc4_done_arg,
+                           void* marg, bool book, int book_period, ReplayMeta* bump,
+                           hipError_t (*fc4_done)(void*), void* fc4_done_arg,
                            const Prefetch* pre) {
   const ParamLayout& L = nb.L;
   const int B = nb.B, S = nb.S;
   const int s4 = S / 8;
   auto M = [&](const char* n) { if (mark) mark(marg, n); };
-  // weight-gradient GEMMs depend only on the data-gradient chain's outputs:
-  // fork them onto the side stream so they overlap the chain.
-  const hipStream_t sw = concurrent ? nb.side : s;
-  int nev = 0;
-  auto fork = [&]() -> hipError_t {
-    if (!concurrent) return hipSuccess;
-    hipError_t e = hipEventRecord(nb.ev[nev], s);
-    if (e == hipSuccess) e = hipStreamWaitEvent(nb.side, nb.ev[nev], 0);
-    ++nev;
-    return e;
-  };
-  // fc4 dgrad and fc4 wgrad both need only dh4 (the head's output): one
-  // launch runs them side by side (dgrad blocks first -- they feed conv3),
-  // instead of two serial latency-bound launches.
-  const bool fc4_fused = !concurrent && !mark && !(nb.variant & 8);
-  if (fc4_fused) {
+  {  // fc4 (train_val.prototxt:159-185): data gradient -> pooled dpool3, and
+     // the weight gradient unless the fused apply computes it itself
     Fc4DgradArgs f;
     f.B = B; f.K = 64 * s4 * s4; f.s4 = s4; f.fS4sq = FastDiv(s4 * s4); f.fS4 = FastDiv(s4);
     f.dh4 = nb.dh4; f.w4 = nb.theta[0] + L.w[3]; f.mask3 = nb.mask3; f.dconv3 = nb.dconv3;
-    f.pooled = nb.conv_impl == 1;
-    f.dsplit = nullptr;   // conv3's weight gradient splits the fp32 dpool3 itself
+    f.pooled = 1;
+    f.dsplit = nullptr;   // conv3's gradients split the fp32 dpool3 themselves
     const int ndx = f.K / 32, nd = ndx * ((B + 31) / 32);
-    // the fused apply computes the fc4 weight gradient tile by tile itself
-    const int nw = nb.fa.on ? 0 : fc4_wgrad_blocks<8>(f.K);
-    hipLaunchKernelGGL(fc4_dgrad_split() ? fc4_bwd_kernel<true> : fc4_bwd_kernel<false>,
-                       dim3(nd + nw), dim3(512), 0, s, f, nb.pool3[0],
+    const int nw = (nb.fa.on && !nb.fa.ext) ? 0 : fc4_wgrad_blocks<8>(f.K);
+    M("fc4_bwd");
+    hipLaunchKernelGGL(fc4_bwd_kernel<true>, dim3(nd + nw), dim3(512), 0, s, f, nb.pool3[0],
                        nb.grad + L.w[3], nd, ndx);
     CHECK_LAUNCH(hipGetLastError());
-    if (fc4_done) CHECK_LAUNCH(fc4_done(fc4_done_arg));
-  }
-  if (!fc4_fused) {  // fc4 dgrad -> dconv3
-    FcDgrad p;
-    p.M = B; p.N = 64 * s4 * s4; p.K = kFc4; p.ksplit_len = kFc4;
-    p.s4 = s4; p.s4sq = s4 * s4; p.fS4sq = FastDiv(s4 * s4); p.fS4 = FastDiv(s4);
-    p.dh4 = nb.dh4; p.w4 = nb.theta[0] + L.w[3]; p.mask3 = nb.mask3; p.dconv3 = nb.dconv3;
-    p.pooled = nb.conv_impl == 1;
-    CHECK_LAUNCH(fork());   // side: fc4 wgrad needs only dh4 (head) -> fork before dgrad
-    M("fc4_dgrad");
-    if (!(nb.variant & 8)) {   // register-direct (bit 8: LDS GEMM engine, A/B)
-      Fc4DgradArgs f;
-      f.B = B; f.K = p.N; f.s4 = s4; f.fS4sq = p.fS4sq; f.fS4 = p.fS4;
-      f.dh4 = nb.dh4; f.w4 = p.w4; f.mask3 = nb.mask3; f.dconv3 = nb.dconv3;
-      f.pooled = p.pooled;
-      f.dsplit = nullptr;
-      CHECK_LAUNCH(launch_fc4_dgrad_direct(f, s));
-    } else {
-      CHECK_LAUNCH(launch_gemm<CfgFcD>(p, 1, 1, s));
-    }
-  }
-  if (!fc4_fused) {  // fc4 wgrad
-    const int K4 = 64 * s4 * s4;
-    M("fc4_wgrad");
-    hipLaunchKernelGGL(fc4_wgrad_kernel, dim3(fc4_wgrad_blocks<8>(K4)), dim3(256), 0, sw, B, K4,
-                       nb.dh4, nb.pool3[0], nb.grad + L.w[3]);
-    CHECK_LAUNCH(hipGetLastError());
     // the fc4 weight gradient (the bulk of the flat gradient) is final here:
-    // the caller may start reducing it under the conv backward
+    // the caller may start reducing it over the ranks under the conv backward
     if (fc4_done) CHECK_LAUNCH(fc4_done(fc4_done_arg));
-    CHECK_LAUNCH(fork());   // side waits for fc4 dgrad (dconv3)
   }
-  // conv3 wgrad and dgrad in one launch: opt-in A/B (DDQ_VARIANT bit 32).
-  // Measured slower: 32.6 us against 15.2 + 15.3 separately -- the shared
-  // launch runs both bodies at the larger register count (199 VGPRs, 2 waves
-  // per SIMD), so a 6-wave dgrad workgroup leaves no room beside it.
-  const bool conv3_fused = !concurrent && !mark && nb.conv_impl == 1 && (nb.variant & 32);
-  if (conv3_fused) {
+  {  // conv3 weight gradient (split bf16, wgrads.h): the fp32 pooled dpool3 of
+     // the fc4 data gradient expanded through pool3's routing bytes and split
+     // while the rows are staged, against the split pool2
     const int H = S / 4;
-    ConvWgrad<64, 64, 3, 1> p;
-    p.M = 64; p.N = 577; p.K = B * H * H;
-    int ns;
-    p.ksplit_len = split_len(p.K, kWgradBK[2], kWgradSplitLen[2], &ns);
-    p.rowtile = (H % kWgradBK[2]) == 0;
-    p.H = H; p.W = H; p.fW = FastDiv(H); p.fH = FastDiv(H);
-    p.NP = nb.wnp[2]; p.dconv = nb.dconv3; p.in = nb.pool2[0]; p.part = nb.wpart + nb.wpart_off[2];
-    WgradDArgs wa = wgradd_args(p, B, nb.wsplits[2]);
-    wa.droute = nb.mask3;
-    const int nw = (wa.G + 7) / 8 * 8 * 2 * 3;
-    DirectArgs d = direct_dgrad_args(nb.dconv3, nb.wk[0] + L.wk_off[2], nb.mask2, nb.dconv2, B, H, 1);
-    d.in_route = nb.mask3;
-    d.pd_pooled = 1;
-    d.tiles_x = (H + 7) / 8;
-    const int ntiles = d.tiles_x * ((H + 3) / 4);
-    const size_t wsm = wgradd_smem_bytes<64, 1>(H);
-    const size_t dsm = (size_t)Conv3DgradCfg::kSmem * 4;
-    hipLaunchKernelGGL(conv3_bwd_kernel, dim3(nw + ntiles * B), dim3(Conv3DgradCfg::kThreads),
-                       wsm > dsm ? wsm : dsm, s, wa, d, nw, ntiles);
-    CHECK_LAUNCH(hipGetLastError());
-  }
-  if (!conv3_fused) {  // conv3 wgrad
-    const int H = S / 4;
-    ConvWgrad<64, 64, 3, 1> p;
-    p.M = 64; p.N = 577; p.K = B * H * H;
-    int ns;
-    p.ksplit_len = split_len(p.K, kWgradBK[2], kWgradSplitLen[2], &ns);
-    p.rowtile = (H % kWgradBK[2]) == 0;
-    p.H = H; p.W = H; p.fW = FastDiv(H); p.fH = FastDiv(H);
-    p.NP = nb.wnp[2]; p.dconv = nb.dconv3; p.in = nb.pool2[0]; p.part = nb.wpart + nb.wpart_off[2];
+    WgradSArgs ws{};
+    ws.B = B; ws.H = H; ws.W = H; ws.G = nb.wsplits[2];
+    ws.RPG = (B * H + ws.G - 1) / ws.G; ws.NP = nb.wnp[2];
+    ws.in = nb.pool2s[0]; ws.in_elems = (int64_t)B * H * H * 64;
+    ws.dpool_f32 = nb.dconv3;
+    ws.droute = nb.mask3; ws.part = nb.wpart + nb.wpart_off[2];
     M("conv3_wgrad");
-    if (nb.conv_impl == 1) {
-      // split bf16 (wgrads.h): the pooled gradient of fc4's dgrad, expanded
-      // through pool3's routing bytes while the rows are staged, against the
-      // split pool2
-      WgradDArgs wd = wgradd_args(p, B, nb.wsplits[2]);
-      WgradSArgs ws{};
-      ws.B = B; ws.H = H; ws.W = H; ws.G = wd.G; ws.RPG = wd.RPG; ws.NP = wd.NP;
-      ws.in = nb.pool2s[0]; ws.in_elems = (int64_t)B * H * H * 64;
-      // the fp32 pooled dpool3 of the fc4 data gradient, split while staged
-      ws.dpool_f32 = nb.dconv3;
-      ws.droute = nb.mask3; ws.part = p.part;
-      CHECK_LAUNCH((launch_wgrads<64, 64, 3, 1, true>(ws, sw)));
-    } else {
-      CHECK_LAUNCH(launch_gemm<CfgW3>(p, 1, ns, sw));
-    }
+    CHECK_LAUNCH((launch_wgrads<64, 64, 3, 1, true>(ws, s)));
   }
-  if (!conv3_fused) {  // conv3 dgrad -> dconv2
+  {  // conv3 data gradient -> split pooled dpool2 (split bf16 on conv3's
+     // transposed + flipped split weights, rebuilt by the head kernel; the fp32
+     // dpool3 expanded through pool3's routing and split while staged; 4x8
+     // tiles x four k groups)
     const int H = S / 4;
-    ConvDgrad<64, 64, 3, 1> p;
-    p.M = B * H * H; p.N = 64; p.K = 576; p.ksplit_len = 576;
-    p.H = H; p.W = H; p.fW = FastDiv(H); p.fH = FastDiv(H);
-    p.dconv = nb.dconv3; p.wk = nb.wk[0] + L.wk_off[2]; p.pmask = nb.mask2; p.pdconv = nb.dconv2;
+    SplitArgs a{};
+    a.B = B; a.H = H; a.W = H; a.pad = 1;
+    a.in_f32 = nb.dconv3; a.in_route = nb.mask3;
+    a.wk[0] = nb.wks[0] + L.wkst3_off; a.wk_elems = L.wks_total;
+    a.pd_split = nb.dconv2s; a.pd_elems = (int64_t)B * H * H * 64;
     M("conv3_dgrad");
-    if (nb.conv_impl == 1) {
-      // split bf16 on conv3's transposed + flipped split weights (built by the
-      // head), the fp32 pooled dpool3 of the fc4 data gradient expanded
-      // through pool3's routing bytes and split while the patch is staged;
-      // 4x8-pixel tiles (256 workgroups) x four k groups (8 waves): 12.5 ->
-      // 8.5 us against the f32 direct kernel (4 waves, register-B).  The
-      // pool2-output gradient leaves pooled and split only (conv2's weight /
-      // data gradients expand it through mask2).
-      SplitArgs a{};
-      a.B = B; a.H = H; a.W = H; a.pad = 1;
-      a.in_f32 = nb.dconv3; a.in_route = nb.mask3;
-      a.wk[0] = nb.wks[0] + L.wkst3_off; a.wk_elems = L.wks_total;
-      a.pd_split = nb.dconv2s; a.pd_elems = (int64_t)B * H * H * 64;
-      CHECK_LAUNCH((launch_split_conv<64, 64, 64, 3, 4, 8, 1, 2, 4, true>(a, 1, s)));
-    } else {
-      CHECK_LAUNCH(launch_gemm<CfgD3>(p, 1, 1, s));
-    }
-    CHECK_LAUNCH(fork());   // side waits for conv3 dgrad (dconv2)
+    CHECK_LAUNCH((launch_split_conv<64, 64, 64, 3, 4, 8, 1, 2, 4, true>(a, 1, s)));
   }
-  {  // conv2 wgrad
+  {  // conv2 weight gradient (split bf16, wgrads.h) on the split pooled dpool2
+     // and the split pool1
     const int H = S / 2;
-    ConvWgrad<32, 64, 5, 2> p;
-    p.M = 64; p.N = 801; p.K = B * H * H;
-    int ns;
-    p.ksplit_len = split_len(p.K, kWgradBK[1], kWgradSplitLen[1], &ns);
-    p.rowtile = (H % kWgradBK[1]) == 0;
-    p.H = H; p.W = H; p.fW = FastDiv(H); p.fH = FastDiv(H);
-    p.NP = nb.wnp[1]; p.dconv = nb.dconv2; p.in = nb.pool1[0]; p.part = nb.wpart + nb.wpart_off[1];
+    WgradSArgs ws{};
+    ws.B = B; ws.H = H; ws.W = H; ws.G = nb.wsplits[1];
+    ws.RPG = (B * H + ws.G - 1) / ws.G; ws.NP = nb.wnp[1];
+    ws.in = nb.pool1s[0]; ws.in_elems = (int64_t)B * H * H * 32;
+    ws.dpool = nb.dconv2s; ws.d_elems = (int64_t)B * (H / 2) * (H / 2) * 64;
+    ws.droute = nb.mask2; ws.part = nb.wpart + nb.wpart_off[1];
     M("conv2_wgrad");
-    if (nb.conv_impl == 1) {
-      // split bf16 (wgrads.h) on the split pooled dpool2 (conv3 dgrad) and pool1
-      WgradDArgs wd = wgradd_args(p, B, nb.wsplits[1]);
-      WgradSArgs ws{};
-      ws.B = B; ws.H = H; ws.W = H; ws.G = wd.G; ws.RPG = wd.RPG; ws.NP = wd.NP;
-      ws.in = nb.pool1s[0]; ws.in_elems = (int64_t)B * H * H * 32;
-      ws.dpool = nb.dconv2s; ws.d_elems = (int64_t)B * (H / 2) * (H / 2) * 64;
-      ws.droute = nb.mask2; ws.part = p.part;
-      CHECK_LAUNCH((launch_wgrads<32, 64, 5, 2>(ws, sw)));
-    } else {
-      CHECK_LAUNCH(launch_gemm<CfgW2>(p, 1, ns, sw));
-    }
+    CHECK_LAUNCH((launch_wgrads<32, 64, 5, 2>(ws, s)));
   }
-  {  // conv2 dgrad -> dconv1
+  {  // conv2 data gradient -> split pooled dpool1 (split bf16, DGRAD): the
+     // split pooled dpool2 expanded through mask2 while staged, the transposed
+     // split weights the head kernel rebuilt, one 64-channel chunk, 8x16-pixel
+     // tiles, four k groups (their sums meet in LDS in fixed order)
     const int H = S / 2;
-    ConvDgrad<32, 64, 5, 2> p;
-    p.M = B * H * H; p.N = 32; p.K = 1600; p.ksplit_len = 1600;
-    p.H = H; p.W = H; p.fW = FastDiv(H); p.fH = FastDiv(H);
-    p.dconv = nb.dconv2; p.wk = nb.wk[0] + L.wk_off[1]; p.pmask = nb.mask1; p.pdconv = nb.dconv1;
+    SplitArgs a{};
+    a.B = B; a.H = H; a.W = H; a.pad = 2;
+    a.in[0] = nb.dconv2s; a.in_elems = (int64_t)B * (H / 2) * (H / 2) * 64;
+    a.wk[0] = nb.wks[0] + L.wkst_off; a.wk_elems = L.wks_total;
+    a.in_route = nb.mask2;
+    a.pd_split = nb.dconv1s; a.pd_elems = (int64_t)B * H * H * 32;
     M("conv2_dgrad");
-    if (nb.conv_impl == 1) {
-      // split bf16 (split.h, DGRAD): the split pooled dpool2 (conv3 dgrad)
-      // expanded through mask2 while staged, the transposed split weights the
-      // head kernel rebuilt, one 64-channel chunk (the patch
-      // is staged once: 25 weight steps), 8x16-pixel tiles; the pool1-output
-      // gradient leaves split and pooled (4.2 MB per plane instead of the
-      // 16.8 MB un-pooled image) for the conv1 wgrad, which expands it through
-      // mask1.  (The fp32 direct kernel: 32.5 us; 32-channel chunks: 35.5,
-      // 16x16 tiles (128 workgroups): 31.8, this: 23.2 -- ubench.)
-      SplitArgs a{};
-      a.B = B; a.H = H; a.W = H; a.pad = 2;
-      a.in[0] = nb.dconv2s; a.in_elems = (int64_t)B * (H / 2) * (H / 2) * 64;
-      a.wk[0] = nb.wks[0] + L.wkst_off; a.wk_elems = L.wks_total;
-      a.in_route = nb.mask2;
-      a.pd_split = nb.dconv1s; a.pd_elems = (int64_t)B * H * H * 32;
-      // four k groups (one 16-channel k-step of every tap each): 16 waves on
-      // the CU's single workgroup instead of 4 -- 28.8 -> 20.9 us (two groups
-      // 23.3); the groups' sums meet in LDS in fixed order and every group
-      // stores a quarter of the epilogue
-      CHECK_LAUNCH((launch_split_conv<64, 64, 32, 5, 8, 16, 4, 1, 4, true>(a, 1, s)));
-    } else {
-      CHECK_LAUNCH(launch_gemm<CfgD2>(p, 1, 1, s));
-    }
+    CHECK_LAUNCH((launch_split_conv<64, 64, 32, 5, 8, 16, 4, 1, 4, true>(a, 1, s)));
   }
   // slab-reduce geometry: layer l's blocks start at d[l].blk0
   WredDims d[3];
@@ -1936,36 +1665,20 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     const int sp = nb.wsplits[l];
     const int G = sp <= kWredCh ? 1 : (sp <= 2 * kWredCh ? 2 : 4);
     d[l] = {L.w[l], L.b[l], nb.wpart_off[l], cout[l], cin[l], ks[l], sp, nb.wnp[l],
-            blk, L.wk_off[l], L.wks_off[l], G};
+            blk, L.wks_off[l], G};
     blk += cout[l] * (nb.wnp[l] / 64) * G / 4;   // units per layer: a multiple of 32
   }
-  {  // conv1 wgrad
-    ConvWgrad<4, 32, 7, 3> p;
-    p.M = 32; p.N = 197; p.K = B * S * S;
-    int ns;
-    p.ksplit_len = split_len(p.K, kWgradBK[0], kWgradSplitLen[0], &ns);
-    p.rowtile = (S % kWgradBK[0]) == 0;
-    p.H = S; p.W = S; p.fW = FastDiv(S); p.fH = FastDiv(S);
-    p.NP = nb.wnp[0]; p.dconv = nb.dconv1; p.in = nb.state; p.part = nb.wpart + nb.wpart_off[0];
+  {  // conv1 weight gradient (split3, wgrads.h): the split pooled dpool1
+     // (conv2 dgrad) against the frames, three MFMAs per (tap row, 16 pixels)
+    Wgrad1SArgs w{};
+    w.B = B; w.H = S; w.W = S; w.R = wgrad1_band(S); w.NP = nb.wnp[0];
+    w.dpool = nb.dconv1s; w.d_elems = (int64_t)B * (S / 2) * (S / 2) * 32;
+    w.droute = nb.mask1; w.in = nb.state; w.part = nb.wpart + nb.wpart_off[0];
     M("conv1_wgrad");
-    if (nb.conv_impl == 1) {
-      // split bf16 (wgrads.h): the split pooled dpool1 (conv2 dgrad) against
-      // the frames, three MFMAs per (tap row, 16 pixels)
-      Wgrad1SArgs w{};
-      w.B = B; w.H = S; w.W = S; w.R = wgrad1_band(S, S); w.NP = nb.wnp[0];
-      w.dpool = nb.dconv1s; w.d_elems = (int64_t)B * (S / 2) * (S / 2) * 32;
-      w.droute = nb.mask1; w.in = nb.state; w.part = p.part;
-      CHECK_LAUNCH(launch_wgrad1s(w, s));
-    } else {
-      CHECK_LAUNCH(launch_gemm<CfgW1>(p, 1, ns, s));
-    }
+    CHECK_LAUNCH(launch_wgrad1s(w, s));
   }
-  {  // slab reduce -> grads (Caffe layout)
-    if (concurrent) {       // join the side stream
-      CHECK_LAUNCH(hipEventRecord(nb.ev[nev], nb.side));
-      CHECK_LAUNCH(hipStreamWaitEvent(s, nb.ev[nev], 0));
-      ++nev;
-    }
+  {  // slab reduce -> grads (Caffe layout) [+ the fused apply + next draw]
+    if (nb.fc4_wait) CHECK_LAUNCH(hipStreamWaitEvent(s, nb.fc4_wait, 0));
     M("wgrad_reduce");
     HeadSums hs{0, B, nb.dqbuf, nb.lpart, nb.h4[0], nb.dh4, nb.loss, nb.grad + L.w[4],
                 nb.grad + L.b[4], nb.grad + L.b[3]};
@@ -1980,11 +1693,11 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
       faa.hi = L.b[3];
       nfa = fc4_wgrad_blocks<kFc4ApplyR>(64 * s4 * s4);
       fat.nfa = nfa;
-      fat.rest = 1;   // and everything else where its gradient is reduced
+      fat.ext = nb.fa.ext;
+      // and everything else where its gradient is reduced -- unless the rest
+      // must be summed over the ranks first (ext: apply launch after that)
+      fat.rest = !nb.fa.ext;
     }
-#ifdef DDQ_EXPERIMENTS
-    if (const char* e = getenv("DDQ_WRED_SKIP")) fat.skip = atoi(e);
-#endif
     Prefetch pf{};
     if (pre && nb.fa.on) pf = *pre;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(pf.ng + nub + kFc4 / 64 + nfa), dim3(256), 0, s,
@@ -2010,15 +1723,15 @@ __global__ void argmax_kernel(int n, const float* __restrict__ qout, int32_t* __
   actions[b] = best;
 }
 
-hipError_t launch_act(const NetBuffers& nb, const float* in, int n, float* pool1, float* pool2,
-                      float* pool3, float* h4, float* part, float* qout, int32_t* actions,
-                      __bf16* pool1s, __bf16* pool2s, hipStream_t s) {
+hipError_t launch_act(const NetBuffers& nb, const float* in, int n, float* pool3, float* h4,
+                      float* part, float* qout, int32_t* actions, __bf16* pool1s,
+                      __bf16* pool2s, hipStream_t s) {
   NetBuffers a = nb;
   a.B = n;
   a.state = const_cast<float*>(in);
   a.next_state = const_cast<float*>(in);
-  a.pool1[0] = pool1; a.pool2[0] = pool2; a.pool3[0] = pool3; a.h4[0] = h4;
-  a.pool1[1] = pool1; a.pool2[1] = pool2; a.pool3[1] = pool3; a.h4[1] = h4;
+  a.pool3[0] = pool3; a.h4[0] = h4;
+  a.pool3[1] = pool3; a.h4[1] = h4;
   a.pool1s[0] = a.pool1s[1] = pool1s; a.pool2s[0] = a.pool2s[1] = pool2s;
   a.mask1 = a.mask2 = a.mask3 = nullptr;
   a.fc4_part = part;

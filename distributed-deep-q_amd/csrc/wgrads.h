@@ -21,9 +21,21 @@
 // the ky == 0 workgroups.
 #pragma once
 #include "split.h"
-#include "wgradd.h"
 
 namespace ddq {
+
+// Row groups (= slabs) of a weight gradient over `rows` image rows: about
+// `target` workgroups over the nts (co block, tap row) pairs, whole XCD
+// rounds (the kernels' decode deals a group's workgroups to one XCD).
+inline void wgrads_groups(int rows, int nts, int* G, int* RPG, int target = 512) {
+  int g = target / nts;
+  if (g >= 16) g &= ~7;
+  if (g < 1) g = 1;
+  if (g > rows) g = rows;
+  const int rpg = (rows + g - 1) / g;
+  *RPG = rpg;
+  *G = (rows + rpg - 1) / rpg;
+}
 
 typedef short i16x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));

@@ -48,7 +48,7 @@ class StepCfg(ctypes.Structure):
                 ("overlap", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 EXCHANGES = {"none": 0, "allreduce": 1, "sharded": 2, "server": 3, "async": 4}
 
 
@@ -111,6 +111,14 @@ _SIGS = {
     "ddq_step_count": (_i64, [_P]),
     "ddq_group_init": (ctypes.c_int, [ctypes.POINTER(_P), _i32]),
     "ddq_group_step": (ctypes.c_int, [ctypes.POINTER(_P), _i32, ctypes.POINTER(StepCfg)]),
+    "ddq_group_async_run": (ctypes.c_int, [ctypes.POINTER(_P), _i32, ctypes.POINTER(StepCfg), _i32,
+                                           _P]),
+    "ddq_group_async_ticks": (ctypes.c_int, [ctypes.POINTER(_P), _i32, ctypes.POINTER(StepCfg),
+                                             _i32, _P]),
+    "ddq_async_begin": (ctypes.c_int, [_P, ctypes.POINTER(StepCfg)]),
+    "ddq_async_ready": (ctypes.c_int, [_P, ctypes.POINTER(_i32)]),
+    "ddq_async_tick": (ctypes.c_int, [_P, ctypes.POINTER(StepCfg), _i32]),
+    "ddq_set_straggle": (ctypes.c_int, [_P, _i64]),
     "ddq_profile_step": (ctypes.c_int, [_P, ctypes.POINTER(StepCfg), _P, _fp, _i32,
                                         ctypes.POINTER(_i32)]),
     "ddq_time_layer": (ctypes.c_int, [_P, ctypes.c_char_p, _i32, _fp]),

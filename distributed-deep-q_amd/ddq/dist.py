@@ -13,6 +13,7 @@ round trip (baristanet.py:105-123, server.py:196-209) replaced by xGMI.
 from __future__ import annotations
 
 import os
+import time
 
 
 def env_ranks():
@@ -96,3 +97,70 @@ def choose_step_mode(net, cfg, modes, log=None):
         if all_ranks_ok(ok):
             return name, overlap
     raise RuntimeError("no step mode could be prepared on every rank")
+
+
+def ticket_store(world, rank=0, prefix="ddq/async"):
+    """The key-value store that hands out async tickets: the default process
+    group's store (a TCPStore every rank reaches) when one is initialised,
+    an in-process HashStore for a single rank."""
+    import torch.distributed as dist
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        from torch.distributed import distributed_c10d as c10d
+        return dist.PrefixStore(prefix, c10d._get_default_store())
+    if world > 1:
+        raise RuntimeError("ticket_store: world > 1 needs an initialised process group")
+    return dist.PrefixStore(prefix, dist.HashStore())
+
+
+class AsyncTicketLoop:
+    """Arrival-order pushes of the asynchronous param server over RCCL ranks
+    (include/ddq_hip.h DDQ_EXCHANGE_ASYNC, ddq_async_tick).
+
+    The reference's workers push whenever their gradient is ready and the
+    one server applies pushes in the order they arrive (main.py:61-112,
+    server.py:196-209).  Here a rank whose gradient is ready
+    (``net.async_ready()``) takes the next ticket from a shared store (an
+    atomic counter: ``store.add``) and publishes ``tk/<t> = rank``; every rank
+    executes tick t as soon as its owner is known, in ticket order, so all
+    ranks enqueue the same RCCL send / recv sequence.  A fast worker takes
+    several tickets while a slow one takes one.  No device ever waits for a
+    ticket: the order is decided on the host, the ticks are enqueued
+    asynchronously and the gradient of the next tick computes meanwhile.
+    """
+
+    def __init__(self, net, cfg, store, rank, world):
+        self.net, self.cfg, self.store = net, cfg, store
+        self.rank, self.world = int(rank), int(world)
+        self.next = 0            # next ticket to execute
+        self.holding = False     # this rank holds a ticket not yet executed
+
+    def run(self, npush, poll_s=20e-6, timeout_s=600.0):
+        """Execute the next npush ticks (whoever pushes); returns their workers."""
+        net, store = self.net, self.store
+        net.async_begin(self.cfg)
+        order = []
+        end = self.next + int(npush)
+        idle_since = time.perf_counter()
+        while self.next < end:
+            progressed = False
+            if not self.holding and net.async_ready():
+                t = store.add("ticket", 1) - 1
+                store.set("tk/%d" % t, str(self.rank))
+                self.holding = True
+                progressed = True
+            key = "tk/%d" % self.next
+            if store.check([key]):
+                w = int(store.get(key))
+                net.async_tick(self.cfg, w)
+                order.append(w)
+                if w == self.rank:
+                    self.holding = False
+                self.next += 1
+                progressed = True
+            if progressed:
+                idle_since = time.perf_counter()
+            else:
+                if time.perf_counter() - idle_since > timeout_s:
+                    raise RuntimeError("async ticket loop: no progress for %.0f s" % timeout_s)
+                time.sleep(poll_s)
+        return order

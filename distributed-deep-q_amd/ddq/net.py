@@ -405,5 +405,47 @@ class DeepQNet:
         if rc != 0:
             check(rc, nets[0].ctx)
 
+    @staticmethod
+    def group_async_run(nets, cfg, npush, arr=None):
+        """Ticket-order async exchange of an in-process group: npush pushes,
+        each by the member whose gradient was ready first.  Returns the order."""
+        import numpy as np
+        lib = _lib.load()
+        if arr is None:
+            arr = (ctypes.c_void_p * len(nets))(*[n.ctx.value for n in nets])
+        order = np.zeros(max(int(npush), 1), np.int32)
+        rc = lib.ddq_group_async_run(arr, len(nets), ctypes.byref(cfg), int(npush), ptr(order))
+        if rc != 0:
+            check(rc, nets[0].ctx)
+        return order[:int(npush)]
+
+    @staticmethod
+    def group_async_ticks(nets, cfg, order, arr=None):
+        """Async ticks of an in-process group in the given worker order."""
+        import numpy as np
+        lib = _lib.load()
+        if arr is None:
+            arr = (ctypes.c_void_p * len(nets))(*[n.ctx.value for n in nets])
+        o = np.ascontiguousarray(order, np.int32)
+        rc = lib.ddq_group_async_ticks(arr, len(nets), ctypes.byref(cfg), int(o.size),
+                                       ptr(o) if o.size else None)
+        if rc != 0:
+            check(rc, nets[0].ctx)
+
+    def async_begin(self, cfg):
+        self._check(self.lib.ddq_async_begin(self.ctx, ctypes.byref(cfg)))
+
+    def async_ready(self):
+        r = _lib._i32()
+        self._check(self.lib.ddq_async_ready(self.ctx, ctypes.byref(r)))
+        return bool(r.value)
+
+    def async_tick(self, cfg, worker):
+        self._check(self.lib.ddq_async_tick(self.ctx, ctypes.byref(cfg), int(worker)))
+
+    def set_straggle(self, usec):
+        """Delay every gradient of this worker by usec (straggler emulation)."""
+        self._check(self.lib.ddq_set_straggle(self.ctx, int(usec)))
+
     def allreduce_grads(self):
         self._check(self.lib.ddq_allreduce_grads(self.ctx))

@@ -111,11 +111,12 @@ class ReplayDataset:
         filled unless they are the bound network's own input buffers."""
         idx = self.draw_indices(sample_size)
         if sample_size != self._net.batch:
-            raise ValueError("sample size %d != network batch %d" % (sample_size, self._net.batch))
-        self._net.replay_sample(np.asarray(idx, np.int32))
-        if getattr(state, "_ddq_device_bound", False):
-            return
-        st, ac, rw, ns, nt = self._net.read_minibatch()
+            st, ac, rw, ns, nt = self._gather_any(np.asarray(idx, np.int32))
+        else:
+            self._net.replay_sample(np.asarray(idx, np.int32))
+            if getattr(state, "_ddq_device_bound", False):
+                return
+            st, ac, rw, ns, nt = self._net.read_minibatch()
         state[...] = st.reshape(state.shape)
         next_state[...] = ns.reshape(next_state.shape)
         if action.ndim > 1 and action.shape[1] > 1:
@@ -124,6 +125,19 @@ class ReplayDataset:
             action[...] = np.argmax(ac.reshape(len(idx), -1), axis=1).reshape(action.shape)
         reward.flat[:] = rw.ravel()
         non_terminal.flat[:] = nt.ravel()
+
+    def _gather_any(self, idx):
+        """Any sample size (the reference gathers into caller arrays of any
+        length, replay.py:167-183): the Caffe-layout batch gather
+        (ddq_replay_gather_batch_async) into device buffers, then to the host."""
+        import torch
+        n = int(idx.size)
+        bufs = self._net.batch_buffers(n)
+        bufs["idx"].copy_(torch.from_numpy(idx))
+        torch.cuda.current_stream(bufs["idx"].device).synchronize()   # before the ctx stream reads
+        self._net.replay_gather_batch(bufs)                          # checks (and syncs) the ctx
+        return tuple(bufs[k].cpu().numpy() for k in ("state", "action", "reward", "next_state",
+                                                      "non_terminal"))
 
     def sample(self, sample_size):
         """Tuple form (the reference's ``sample`` is broken, replay.py:135-136;

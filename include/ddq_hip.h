@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define DDQ_ABI_VERSION 3
+#define DDQ_ABI_VERSION 4
 
 enum ddq_status {
   DDQ_OK = 0,
@@ -105,16 +105,19 @@ enum ddq_exchange {
    * the server applies gradients on arrival; iteration += W per step; then
    * all-gather of theta.  Staleness within a step: 0..W-1 updates. */
   DDQ_EXCHANGE_SERVER = 3,
-  /* Asynchronous param server (server.py:181-209 with free-running workers)
-   * on a deterministic round-robin arrival schedule: rank r owns shard r of
-   * the central model (and its optimizer state); one step = one round of W
-   * ticks; at tick w worker w pushes the gradient it computed on the model
-   * it last pulled, the owners apply it on arrival (iteration += 1), worker
-   * w pulls the owners' shards (and the central P tower when a
-   * special-update pull happened since its last pull) and immediately
-   * computes its next gradient while the other ranks' ticks proceed.
-   * Staleness: W-1 updates, from the arrival order.  Eager steps only
-   * (ddq_step_async / ddq_group_step). */
+  /* Asynchronous param server (server.py:181-209 with free-running workers,
+   * main.py:61-112): rank r owns shard r of the central model (and its
+   * optimizer state).  A TICK is one push: worker w sends the gradient it
+   * computed on the model it last pulled, the owners apply it on arrival
+   * (iteration += 1), worker w pulls the owners' shards (and the central P
+   * tower when a special-update pull happened since its last pull) and
+   * immediately computes its next gradient while later ticks proceed.  The
+   * arrival order is either round-robin (the deterministic schedule: one
+   * step of ddq_step_async / ddq_step_graph_async / ddq_group_step = W ticks,
+   * staleness W-1) or ticket order (ddq_async_tick with the worker whose
+   * gradient was ready first, ddq_group_async_run): a fast worker pushes
+   * more often than a slow one, as in the reference.  Once begun on a ctx,
+   * only async steps / ticks run there. */
   DDQ_EXCHANGE_ASYNC = 4
 };
 
@@ -283,6 +286,33 @@ int ddq_group_init(ddq_ctx** ctxs, int32_t nranks);
 int ddq_group_step(ddq_ctx** ctxs, int32_t nranks, const ddq_step_cfg* cfg);
 /* Steps taken so far (drives the target-sync period). */
 int64_t ddq_step_count(const ddq_ctx* ctx);
+
+/* ---------------- asynchronous param server in arrival order ------------ */
+/* (DDQ_EXCHANGE_ASYNC, server.py:196-209 applying pushes as they arrive.)
+ * ddq_async_begin: the central model's shards start from this replica and the
+ * worker computes its first gradient (implicit in the calls below).
+ * ddq_async_ready: *ready = 1 once this worker's gradient is computed (it may
+ * take the next ticket).  ddq_async_tick: enqueue tick `worker` -- every rank
+ * calls it with the same worker sequence (the tickets, e.g. from a TCP store:
+ * ddq/dist.py AsyncTicketLoop); enqueued, no sync (ddq_synchronize waits for
+ * the owner duties too). */
+int ddq_async_begin(ddq_ctx* ctx, const ddq_step_cfg* cfg);
+int ddq_async_ready(ddq_ctx* ctx, int32_t* ready);
+int ddq_async_tick(ddq_ctx* ctx, const ddq_step_cfg* cfg, int32_t worker);
+/* In-process group in ticket order: npush ticks, each given to the first
+ * member (after the previous ticket's holder) whose gradient is ready, polled
+ * on the host; order[t] (nullable) receives tick t's worker.  Synchronous. */
+int ddq_group_async_run(ddq_ctx** ctxs, int32_t nranks, const ddq_step_cfg* cfg, int32_t npush,
+                        int32_t* order);
+/* The same ticks in a given worker order (deterministic replay of a ticket
+ * run, or any schedule).  Synchronous. */
+int ddq_group_async_ticks(ddq_ctx** ctxs, int32_t nranks, const ddq_step_cfg* cfg, int32_t n,
+                          const int32_t* order);
+/* Straggler emulation (fault injection, cf. the dummy driver's injected
+ * failures, baristanet.py:125-133): every gradient this worker computes
+ * becomes pushable (ddq_async_ready, ticket runs) usec of host time after it
+ * is computed -- a slow worker loop, without occupying the GPU.  0 disables. */
+int ddq_set_straggle(ddq_ctx* ctx, int64_t usec);
 
 /* ---------------- measurement ------------------------------------------ */
 /* Kernel ids for ddq_profile_step. */

@@ -56,7 +56,27 @@ def test_struct_layouts_match_header():
 
 
 def test_abi_version(lib):
-    assert lib.ddq_abi_version() == 3
+    assert lib.ddq_abi_version() == 4
+
+
+@pytest.mark.parametrize("batch,frame,ok", [(1024, 256, True), (1024, 512, False),
+                                            (128, 1016, True), (131, 1016, False),
+                                            (1, 1024, False)])
+def test_create_rejects_sizes_past_32bit_offsets(lib, batch, frame, ok):
+    """ddq_create refuses shapes whose tensors exceed the kernels' 32-bit
+    buffer offsets (16 B S^2 and 2^11 S^2 bytes < 2^31), before it looks for
+    a device: those sizes fail with DDQ_EINVAL on any host."""
+    from ddq import _lib
+    desc = _lib.NetDesc(batch, frame, 4, 4, 0.85)
+    ctx = ctypes.c_void_p()
+    rc = lib.ddq_create(ctypes.byref(ctx), 0, ctypes.byref(desc))
+    if ok:
+        assert rc != _lib.DDQ_EINVAL or b"32-bit" not in lib.ddq_last_error(None)
+        if rc == 0:
+            lib.ddq_destroy(ctx)
+    else:
+        assert rc == _lib.DDQ_EINVAL
+        assert b"32-bit" in lib.ddq_last_error(None)
 
 
 def test_no_gpu_fails_loudly(lib):

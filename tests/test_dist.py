@@ -338,3 +338,68 @@ def test_gloo_async_round_robin_matches_server_replay(world):
         np.testing.assert_allclose(pv, pview[r], rtol=1e-6, atol=1e-7)
     # staleness: the workers' views differ (each pulled at a different tick)
     assert not np.array_equal(res[0][1], res[1][1])
+
+
+class _FakeAsyncNet:
+    """The ddq_async_* surface of a worker whose gradient takes `compute_s`:
+    it is ready that long after its last pull (its own tick)."""
+
+    def __init__(self, rank, compute_s):
+        import time
+        self.rank, self.compute_s, self.time = rank, compute_s, time
+        self.ticks = []
+        self.pulled = None
+
+    def async_begin(self, cfg):
+        if self.pulled is None:
+            self.pulled = self.time.perf_counter()
+
+    def async_ready(self):
+        return self.time.perf_counter() - self.pulled >= self.compute_s
+
+    def async_tick(self, cfg, w):
+        self.ticks.append(w)
+        if w == self.rank:
+            self.pulled = self.time.perf_counter()
+
+
+def _ticket_worker(rank, world, port, npush, out):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "distributed-deep-q_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from ddq import dist as ddist
+    ddist.init_process_group(rank, world, "gloo")
+    net = _FakeAsyncNet(rank, 0.002 if rank == 0 else 0.012)
+    loop = ddist.AsyncTicketLoop(net, None, ddist.ticket_store(world, rank), rank, world)
+    order = loop.run(npush // 2) + loop.run(npush - npush // 2)   # two calls: state carries
+    out.put((rank, order, net.ticks))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_async_ticket_order(world):
+    """AsyncTicketLoop (the arrival-order async exchange's host side): every
+    rank executes the same tick sequence, each ticket owned by the rank that
+    took it when its gradient was ready, so the fast rank 0 pushes more often
+    than the slow ones -- server.py applying pushes as they arrive."""
+    npush = 30
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ticket_worker, args=(r, world, port, npush, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=300) for _ in range(world)), key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    orders = [r[1] for r in res]
+    assert all(o == orders[0] for o in orders)
+    assert all(r[2] == orders[0] for r in res)        # the ticks each rank enqueued
+    assert len(orders[0]) == npush
+    counts = np.bincount(orders[0], minlength=world)
+    assert counts[0] > max(counts[1:]) and min(counts) >= 1, counts

@@ -1,0 +1,176 @@
+"""GPU: the asynchronous param server (DDQ_EXCHANGE_ASYNC) in arrival order.
+
+* Ticket order (ddq_group_async_run): a straggling member (ddq_set_straggle)
+  pushes less often than the others -- the reference's free-running workers
+  (main.py:61-112) against one server applying pushes on arrival
+  (server.py:196-209) -- and the ticket run is bit-identical to the same ticks
+  replayed deterministically in its recorded order.
+* Any order (ddq_group_async_ticks) against server.py replayed tick by tick
+  (tests/_async_check.py): an irregular schedule in which one worker pushes
+  three times in a row, with special updates inside it.
+* RCCL with a 1-rank communicator: ticket ticks (ddq_async_tick) and the
+  graph-captured round-robin rounds (ddq_step_graph_async) equal plain steps
+  bit-exactly (staleness 0 at W = 1).
+"""
+import numpy as np
+import pytest
+
+from _async_check import run_checked
+
+pytestmark = pytest.mark.gpu
+
+S, B, N = 16, 8, 120
+
+
+@pytest.fixture(scope="module")
+def ddq():
+    import ddq as m
+    return m
+
+
+@pytest.fixture(scope="module")
+def ref():
+    from oracle import ref_numpy
+    return ref_numpy
+
+
+def member_data(r):
+    rng = np.random.default_rng(r)
+    return (rng.integers(0, 256, (N, 4, S, S)).astype(np.uint8),
+            rng.integers(0, 4, N).astype(np.uint8),
+            rng.integers(-1, 2, N).astype(np.int16),
+            (rng.random(N) > 0.1).astype(np.uint8))
+
+
+def make_group(ddq, W, log=64):
+    from ddq.params import init_params_flat
+    theta = init_params_flat(S, seed=42)
+    nets, data = [], []
+    for r in range(W):
+        n = ddq.DeepQNet(batch=B, frame=S)
+        n.set_flat(0, theta)
+        n.set_flat(1, theta)
+        n.replay_create(N)
+        d = member_data(r)
+        n.replay_import(*d, 0, N)
+        n.index_log_enable(log)
+        nets.append(n)
+        data.append(d)
+    arr = ddq.DeepQNet.group_init(nets)
+    return nets, arr, theta, data
+
+
+def minibatch_fn(nets, data):
+    def mb(r, draw):
+        st, ac, rw, nt = data[r]
+        idx = nets[r].index_log(draw, 1)[0].astype(np.int64)
+        nx = np.where(idx + 1 == N, 0, idx + 1)
+        a = np.zeros((B, 4, 1, 1), np.float32)
+        a[np.arange(B), ac[nx], 0, 0] = 1
+        return (st[idx].astype(np.float32), a, rw[nx].astype(np.float32).reshape(B, 1, 1, 1),
+                st[nx].astype(np.float32), nt[nx].astype(np.float32).reshape(B, 1, 1, 1))
+    return mb
+
+
+@pytest.mark.parametrize("rule", ["rmsprop", "sgd"])
+def test_group_async_any_order_matches_server_replay(ddq, ref, rule):
+    W, lr, period = 3, 1e-4, 4
+    order = [0, 2, 2, 2, 1, 0, 1, 2, 0, 0]
+    nets, arr, theta, data = make_group(ddq, W)
+    try:
+        cfg = nets[0].step_cfg(rule, lr=lr, target_period=period, exchange="async", seed=5)
+        run_checked(ddq, ref, nets, arr, cfg, order, minibatch_fn(nets, data), rule, lr,
+                    period, theta, what="%s " % rule)
+    finally:
+        for n in nets:
+            n.close()
+
+
+def test_group_async_ticket_order_straggler(ddq):
+    """A member 3 ms slower per gradient takes fewer tickets; the ticket run
+    equals a deterministic replay of its recorded order bit for bit."""
+    W, npush = 3, 18
+    groups = [make_group(ddq, W) for _ in range(2)]
+    try:
+        (nets, arr, _, _), (nets2, arr2, _, _) = groups
+        nets[1].set_straggle(3000)
+        cfg = nets[0].step_cfg("rmsprop", lr=1e-4, target_period=4, exchange="async", seed=7)
+        order = ddq.DeepQNet.group_async_run(nets, cfg, npush, arr)
+        counts = np.bincount(order, minlength=W)
+        assert counts.sum() == npush
+        assert counts[1] < counts[0] and counts[1] < counts[2], order
+        ddq.DeepQNet.group_async_ticks(nets2, cfg, order, arr2)
+        for a, b in zip(nets, nets2):
+            for z in (0, 1):
+                np.testing.assert_array_equal(a.get_flat(z), b.get_flat(z))
+            np.testing.assert_array_equal(a.optimizer_state(), b.optimizer_state())
+            np.testing.assert_array_equal(a.get_grads_flat(), b.get_grads_flat())
+    finally:
+        for nets_, _, _, _ in groups:
+            for n in nets_:
+                n.close()
+
+
+def test_group_async_refuses_other_steps_once_begun(ddq):
+    from ddq._lib import DDQError
+    nets, arr, _, _ = make_group(ddq, 2)
+    try:
+        cfg = nets[0].step_cfg("sgd", lr=1e-3, target_period=0, exchange="async", seed=1)
+        ddq.DeepQNet.group_step(nets, cfg, arr)
+        sync = nets[0].step_cfg("sgd", lr=1e-3, target_period=0, exchange="server", seed=1)
+        with pytest.raises(DDQError):
+            ddq.DeepQNet.group_step(nets, sync, arr)
+    finally:
+        for n in nets:
+            n.close()
+
+
+def _world1_nets(ddq, count, seed=6):
+    from ddq.params import init_params_flat
+    theta = init_params_flat(S, seed=42)
+    rng = np.random.default_rng(seed)
+    st = rng.integers(0, 256, (N, 4, S, S)).astype(np.uint8)
+    ac = rng.integers(0, 4, N).astype(np.uint8)
+    rw = rng.integers(-1, 2, N).astype(np.int16)
+    nt = (rng.random(N) > 0.1).astype(np.uint8)
+    nets = [ddq.DeepQNet(batch=B, frame=S) for _ in range(count)]
+    for n in nets:
+        n.set_flat(0, theta)
+        n.set_flat(1, theta)
+        n.replay_create(N)
+        n.replay_import(st, ac, rw, nt, 0, N)
+    return nets
+
+
+@pytest.mark.parametrize("period", [3, 0])
+def test_rccl_world1_async_ticks_and_graph_equal_plain_steps(ddq, period):
+    """W = 1: staleness 0, so R pushes are R plain steps.  Net 0: ticket ticks
+    (ddq_async_tick after ddq_async_ready); net 1: round-robin rounds as
+    graphs (period / gcd(1, period) rounds per graph, eager rounds to align);
+    net 2: plain exchange-free steps."""
+    R = 13
+    nets = _world1_nets(ddq, 3)
+    try:
+        for n in nets[:2]:
+            n.comm_init(ddq.DeepQNet.comm_unique_id(), 1, 0)
+        acfg = nets[0].step_cfg("rmsprop", lr=1e-4, target_period=period, exchange="async", seed=9)
+        nets[0].async_begin(acfg)
+        for _ in range(R):
+            while not nets[0].async_ready():
+                pass
+            nets[0].async_tick(acfg, 0)
+        nets[1].step_graph(acfg, 4)
+        nets[1].step_graph(acfg, R - 4)
+        plain = nets[2].step_cfg("rmsprop", lr=1e-4, target_period=period, exchange="none", seed=9)
+        for _ in range(R):
+            nets[2].step(plain)
+        for n in nets:
+            n.synchronize()
+        for z in (0, 1):
+            np.testing.assert_array_equal(nets[0].get_flat(z), nets[2].get_flat(z))
+            np.testing.assert_array_equal(nets[1].get_flat(z), nets[2].get_flat(z))
+        np.testing.assert_array_equal(nets[0].optimizer_state(), nets[2].optimizer_state())
+        np.testing.assert_array_equal(nets[1].optimizer_state(), nets[2].optimizer_state())
+    finally:
+        for n in nets:
+            n.close()

@@ -33,9 +33,11 @@ oracle.  So:
   of those 31 steps, started from the GPU's own state, matches the oracle's
   step (gradients, theta_Q, theta_P, optimizer state, loss) at rtol 1e-4
   with the GPU's max-pool routing adopted only at proven near-ties.
-* ``test_shipped_chain_free_running``: the first 6 steps of the chain from the
-  common initial state against a free-running oracle (before the first
-  near-tie), rtol 1e-4 on theta_Q, theta_P, the cache and the loss.
+* ``test_shipped_chain_free_running``: the chain from the common initial
+  state against a free-running oracle, rtol 1e-4 on theta_Q, theta_P, the
+  cache and the loss: 6 rmsprop steps (its lagged cache divides by earlier
+  gradients, amplifying fp32-vs-fp64 differences of near-zero elements) and
+  24 sgd steps (two P <- Q syncs).
 """
 import numpy as np
 import pytest
@@ -170,7 +172,7 @@ def test_shipped_chain_teacher_forced(ref_mod, ring, rule, lr, calls):
     assert float(chain.blob("loss")) == float(eager.blob("loss"))
 
 
-@pytest.mark.parametrize("rule,lr,calls", [("rmsprop", 1e-4, (1, 5)), ("sgd", 1e-2, (6,))])
+@pytest.mark.parametrize("rule,lr,calls", [("rmsprop", 1e-4, (1, 5)), ("sgd", 1e-2, (16, 8))])
 def test_shipped_chain_free_running(ref_mod, ring, rule, lr, calls):
     import ddq
     from ddq.params import init_params_flat

@@ -46,6 +46,17 @@ def test_replay_dataset_dropin_matches_oracle(tmp_path):
     exp = r.gather(idx)
     for got, want in zip(arrs, exp):
         np.testing.assert_array_equal(got, want)
+    # any sample size, as the reference's caller arrays allow (replay.py:144-183)
+    for n in (1, 3, 20):
+        out = [np.zeros((n, 4, S, S), np.float32), np.zeros((n, 4, 1, 1), np.float32),
+               np.zeros((n, 1, 1, 1), np.float32), np.zeros((n, 4, S, S), np.float32),
+               np.zeros((n, 1, 1, 1), np.float32)]
+        random.seed(10 + n)
+        ds.sample_direct(*out, n)
+        random.seed(10 + n)
+        exp = r.gather(ds.draw_indices(n))
+        for got, want in zip(out, exp):
+            np.testing.assert_array_equal(got, want)
     with pytest.raises(ValueError):
         ds.sample_direct(*arrs, 1000)
     # persistence round trip (replay.py:185-192 persists, reopen appends)

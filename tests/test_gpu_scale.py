@@ -15,6 +15,10 @@ bench initialisation: seed-42 Gaussian fillers, zero biases):
 * C5: 8 members x 1M-slot 64x64 rings (8 x 16.4 GB in HBM), the server
   exchange over two steps as above, then a 4096-transition device draw +
   gather per member checked row by row against its tiled pool.
+* C5 as BASELINE.json states it -- 8 ASYNC workers with 1M-slot rings: two
+  round-robin rounds (16 pushes, special update every 10 iterations) checked
+  tick by tick against server.py replayed in the same arrival order
+  (tests/_async_check.py), then a ticket-order run (ddq_group_async_run).
 """
 import numpy as np
 import pytest
@@ -52,7 +56,7 @@ def pools(S, pool, seed):
     return st, ac, rw, nt.astype(np.uint8)
 
 
-def make_members(ddq, N, pool):
+def make_members(ddq, N, pool, log=0):
     from ddq.params import init_params_flat
     theta = init_params_flat(S, seed=42)
     nets, data = [], []
@@ -63,6 +67,8 @@ def make_members(ddq, N, pool):
         n.replay_create(N)
         d = pools(S, pool, seed=500 + r)          # each member its own shard contents
         n.replay_fill_tiled(*d, 0, N)
+        if log:
+            n.index_log_enable(log)
         nets.append(n)
         data.append(d)
     return nets, data, theta
@@ -178,3 +184,40 @@ def test_c5_eight_members_million_slot_rings(ddq, ref):
     finally:
         for net in nets:
             net.close()
+
+
+def test_c5_eight_async_workers_million_slot_rings(ddq, ref):
+    from _async_check import run_checked
+    N, pool = 1 << 20, 1024
+    nets, data, theta = make_members(ddq, N, pool=pool, log=64)
+    try:
+        arr = ddq.DeepQNet.group_init(nets)
+
+        def minibatch(r, draw):        # member r's draw: its tiled pool at the logged indices
+            st, ac, rw, nt = data[r]
+            idx = nets[r].index_log(draw, 1)[0].astype(np.int64)
+            nx = np.where(idx + 1 == N, 0, idx + 1)
+            a = np.zeros((B, 4, 1, 1), np.float32)
+            a[np.arange(B), ac[nx % pool], 0, 0] = 1
+            return (st[idx % pool].astype(np.float32), a,
+                    rw[nx % pool].astype(np.float32).reshape(B, 1, 1, 1),
+                    st[nx % pool].astype(np.float32),
+                    nt[nx % pool].astype(np.float32).reshape(B, 1, 1, 1))
+        lr, period = 1e-4, 10
+        cfg = nets[0].step_cfg("rmsprop", lr=lr, target_period=period, exchange="async", seed=77)
+        order = list(range(W)) * 2                 # two round-robin rounds
+        # every gradient is checked at the first pushes; later ones 1 in 3
+        run_checked(ddq, ref, nets, arr, cfg, order, minibatch, "rmsprop", lr, period, theta,
+                    grad_check=lambda t, w: (t < 0 and w < 2) or (t >= 0 and t % 3 == 0),
+                    what="C5 ")
+        # arrival order: 24 more pushes by whichever worker is ready first
+        before = [n.get_flat(0) for n in nets]
+        got = ddq.DeepQNet.group_async_run(nets, cfg, 24, arr)
+        assert len(got) == 24 and set(got.tolist()) <= set(range(W))
+        for n, b in zip(nets, before):
+            th = n.get_flat(0)
+            assert np.isfinite(th).all()
+        assert any(not np.array_equal(n.get_flat(0), b) for n, b in zip(nets, before))
+    finally:
+        for n in nets:
+            n.close()
