@@ -285,17 +285,21 @@ struct Fc4DgradArgs {
 // SPLIT: the 32 f32 MFMAs of a wave (64 cycles each) as 24 bf16 ones on
 // fp32-exact split operands (split.h; 32 cycles each): step s of a 32-n block
 // pairs n = 16h + 8s + e of both operands, as fc4_fwd_split_kernel.
-template <bool SPLIT>
+// KCW kc columns per block (32, or 16 -- the MFMA's other 16 columns read
+// nothing and are dropped): K / 16 blocks fill the 256 CUs at 64x64, where
+// K / 32 = 128 blocks streamed W4 on half of them (1.3 TB/s).
+template <bool SPLIT, int KCW = 32>
 __device__ __forceinline__ void fc4_dgrad_body(const Fc4DgradArgs& a, float (*red)[1024], int bx,
                                                int by) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int l31 = lane & 31, h = lane >> 5;
-  const int kc0 = bx * 32, b0 = by * 32;
+  const int kc0 = bx * KCW, b0 = by * 32;
   const int K = a.K;
   const int nbase = w * 64 + h * 16;
   const __amdgpu_buffer_rsrc_t ra = fc_rsrc(a.dh4, (uint32_t)(a.B * 512 * 4));
   const __amdgpu_buffer_rsrc_t rb = fc_rsrc(a.w4, (uint32_t)(512 * K * 4));
   const uint32_t aoff = (uint32_t)((b0 + l31) * 512 + nbase) * 4;   // rows b >= B read 0
+  const bool bcol = l31 < KCW;                                       // (wave-varying, no branch)
   const uint32_t boff = (uint32_t)(nbase * K + kc0 + l31) * 4;
 
   float4 av[2][4];
@@ -305,7 +309,8 @@ __device__ __forceinline__ void fc4_dgrad_body(const Fc4DgradArgs& a, float (*re
 #pragma unroll
     for (int i = 0; i < 4; ++i) av[blk][i] = fc_ld4(ra, aoff + (blk * 32 + 4 * i) * 4);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) bv[blk][j] = fc_ld1(rb, boff + (uint32_t)((blk * 32 + j) * K) * 4);
+    for (int j = 0; j < 16; ++j)
+      bv[blk][j] = fc_ld1(rb, bcol ? boff + (uint32_t)((blk * 32 + j) * K) * 4 : kFcOOB);
   }
   __builtin_amdgcn_sched_barrier(0);   // keep every load ahead of the first MFMA
   f32x16 acc;
@@ -357,7 +362,7 @@ __device__ __forceinline__ void fc4_dgrad_body(const Fc4DgradArgs& a, float (*re
     const int r = e >> 6, ln = e & 63;
     const int bb = b0 + fc_acc_row(r, ln);
     const int kc = kc0 + (ln & 31);
-    if (bb >= a.B) continue;
+    if (bb >= a.B || (ln & 31) >= KCW) continue;
     uint32_t ch, p, py, px;
     a.fS4sq.divmod((uint32_t)kc, ch, p);
     if (a.pooled) {   // one store per element instead of four (three of them zeros)

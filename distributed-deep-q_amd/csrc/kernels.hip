@@ -5,6 +5,13 @@
 #include "fc.h"
 #include "split.h"
 
+// A/B timing experiments only (make variant DEFS=-DDDQ_AB_SKIP=..., tools/ab):
+// block roles of the slab-reduce launch that return at once (1 fc4 apply
+// tiles, 2 slab units, 4 head sums, 8 prefetch).  0 in the product build.
+#ifndef DDQ_AB_SKIP
+#define DDQ_AB_SKIP 0
+#endif
+
 namespace ddq {
 
 // first failing launch site of the last failed launch sequence (api.hip
@@ -1222,14 +1229,14 @@ __global__ __launch_bounds__(256, 4) void wgrad_reduce_kernel(
     const float* __restrict__ fc4_x, int fc4_k) {
   __shared__ float red[4][4][64];
   if ((int)blockIdx.x < pf.ng) {   // fused apply: the next step's draw + gather first
-    prefetch_body(pf, blockIdx.x);
+    if (!(DDQ_AB_SKIP & 8)) prefetch_body(pf, blockIdx.x);
     return;
   }
   int bid = blockIdx.x - pf.ng;
   if (fat.nfa > 0) {   // fused fc4-weight gradient + apply blocks come first: the
                        // longest HBM streams start before the reduce blocks
     if (bid < fat.nfa) {
-      fc4_apply_tile(fat, faa, hs.B, fc4_k, hs.dh4, fc4_x, bid);
+      if (!(DDQ_AB_SKIP & 1)) fc4_apply_tile(fat, faa, hs.B, fc4_k, hs.dh4, fc4_x, bid);
       return;
     }
     bid -= fat.nfa;
@@ -1237,6 +1244,7 @@ __global__ __launch_bounds__(256, 4) void wgrad_reduce_kernel(
   if (opt_init && bid == 0 && threadIdx.x == 0)
     apply_book(iter, opt_init, book_period, bump, book_inc);
   const bool rest = fat.rest != 0;
+  if (DDQ_AB_SKIP & (bid >= nub ? 4 : 2)) return;
   if (bid >= nub) {
     head_sums(bid - nub, hs.B, hs.dqbuf, hs.lpart, hs.h4q, hs.dh4, hs.loss, hs.gw5, hs.gb5,
               hs.gb4, rest, fat, faa);
@@ -1475,13 +1483,13 @@ int wgrad_splits_for(int layer, int B, int S, int* np) {
 // fc4 weight gradient (blocks [nd, ...): 256 threads; the other 4 waves end at
 // once, which s_barrier does not wait for).  nd = 0 blocks of the weight
 // gradient when the fused apply computes it tile by tile itself.
-template <bool SPLIT>
+template <bool SPLIT, int KCW>
 __global__ __launch_bounds__(512) void fc4_bwd_kernel(const Fc4DgradArgs d, const float* x,
                                                       float* gw4, int nd, int ndx) {
   __shared__ __attribute__((aligned(16))) float smem[8 * 1024];
   const int bid = blockIdx.x;
   if (bid < nd) {
-    fc4_dgrad_body<SPLIT>(d, reinterpret_cast<float(*)[1024]>(smem), bid % ndx, bid / ndx);
+    fc4_dgrad_body<SPLIT, KCW>(d, reinterpret_cast<float(*)[1024]>(smem), bid % ndx, bid / ndx);
     return;
   }
   if (threadIdx.x >= 256) return;
@@ -1594,11 +1602,13 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     f.dh4 = nb.dh4; f.w4 = nb.theta[0] + L.w[3]; f.mask3 = nb.mask3; f.dconv3 = nb.dconv3;
     f.pooled = 1;
     f.dsplit = nullptr;   // conv3's gradients split the fp32 dpool3 themselves
-    const int ndx = f.K / 32, nd = ndx * ((B + 31) / 32);
+    // 16-column blocks when 32-column ones would not give every CU one
+    const bool narrow = (f.K / 32) * ((B + 31) / 32) < 256;
+    const int ndx = f.K / (narrow ? 16 : 32), nd = ndx * ((B + 31) / 32);
     const int nw = (nb.fa.on && !nb.fa.ext) ? 0 : fc4_wgrad_blocks<8>(f.K);
     M("fc4_bwd");
-    hipLaunchKernelGGL(fc4_bwd_kernel<true>, dim3(nd + nw), dim3(512), 0, s, f, nb.pool3[0],
-                       nb.grad + L.w[3], nd, ndx);
+    hipLaunchKernelGGL((narrow ? fc4_bwd_kernel<true, 16> : fc4_bwd_kernel<true, 32>),
+                       dim3(nd + nw), dim3(512), 0, s, f, nb.pool3[0], nb.grad + L.w[3], nd, ndx);
     CHECK_LAUNCH(hipGetLastError());
     // the fc4 weight gradient (the bulk of the flat gradient) is final here:
     // the caller may start reducing it over the ranks under the conv backward

@@ -672,9 +672,18 @@ __global__ __launch_bounds__(64 * WM) void split_conv1_kernel(const Conv1Args a)
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const __bf16* pa = patch + abase[i] + ky * C::RS + 16 * g;
-        const uint2 lo = *reinterpret_cast<const uint2*>(pa);
-        const uint2 hi = *reinterpret_cast<const uint2*>(pa + 4);
-        u32x4 av4 = {lo.x, lo.y, hi.x, hi.y};
+        // two ds_read_b64 (2 LDS cycles each, conflict-free at RS == 64 mod
+        // 128): left adjacent, hipcc merges them into one ds_read2_b64 (4 x
+        // 16-lane groups on 32 banks: rows y and y+1 of a window collide,
+        // 16 cycles -- 35 % of conv1's LDS cycles were conflicts)
+        typedef __attribute__((address_space(3))) const u32x2 lds_u2;
+        typedef __attribute__((address_space(3))) const char lds_c;
+        lds_u2* la = (lds_u2*)pa;
+        uint32_t hi_off = 8;                       // bytes; opaque: no merge
+        asm volatile("" : "+v"(hi_off));
+        const u32x2 lo = *la;
+        const u32x2 hi = *(lds_u2*)((lds_c*)la + hi_off);
+        u32x4 av4 = {lo[0], lo[1], hi[0], hi[1]};
         const bf16x8 av = *reinterpret_cast<bf16x8*>(&av4);
         cor[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv[2], cor[i], 0, 0, 0);
         cor[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv[1], cor[i], 0, 0, 0);

@@ -11,7 +11,10 @@ import os
 
 import numpy as np
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libddq_hip.so")
+# DDQ_LIB_PATH: an A/B variant build (tools/ab, `make variant`); the product
+# path is the in-tree library
+LIB_PATH = os.environ.get("DDQ_LIB_PATH") or \
+    os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libddq_hip.so")
 
 DDQ_OK, DDQ_EINVAL, DDQ_ENOMEM, DDQ_EHIP, DDQ_ERCCL, DDQ_ESTATE, DDQ_ERANGE = 0, -1, -2, -3, -4, -5, -6
 RULES = {"sgd": 0, "rmsprop": 1, "adagrad": 2, "momentum": 3}
