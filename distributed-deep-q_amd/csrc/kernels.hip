@@ -663,7 +663,9 @@ __global__ __launch_bounds__(512) void fc4_head_kernel(
   float q[8];
   // every operand that does not depend on the partial sums is loaded first,
   // and the partials 32 splits x 2 towers per round (one round at 64x64):
-  // the kernel is a chain of memory latencies, not of work
+  // the kernel is a chain of memory latencies, not of work (a quarter of the
+  // partials -- 4-wave k-split fc4 forward workgroups -- measured the same
+  // 6.4 us here and 6.5 against 6.1 us for the forward)
   float bias4[2], w5v[2][4];
 #pragma unroll
   for (int z = 0; z < 2; ++z) {
@@ -1614,31 +1616,32 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     // the caller may start reducing it over the ranks under the conv backward
     if (fc4_done) CHECK_LAUNCH(fc4_done(fc4_done_arg));
   }
-  {  // conv3 weight gradient (split bf16, wgrads.h): the fp32 pooled dpool3 of
-     // the fc4 data gradient expanded through pool3's routing bytes and split
-     // while the rows are staged, against the split pool2
-    const int H = S / 4;
-    WgradSArgs ws{};
-    ws.B = B; ws.H = H; ws.W = H; ws.G = nb.wsplits[2];
-    ws.RPG = (B * H + ws.G - 1) / ws.G; ws.NP = nb.wnp[2];
-    ws.in = nb.pool2s[0]; ws.in_elems = (int64_t)B * H * H * 64;
-    ws.dpool_f32 = nb.dconv3;
-    ws.droute = nb.mask3; ws.part = nb.wpart + nb.wpart_off[2];
-    M("conv3_wgrad");
-    CHECK_LAUNCH((launch_wgrads<64, 64, 3, 1, true>(ws, s)));
-  }
   {  // conv3 data gradient -> split pooled dpool2 (split bf16 on conv3's
      // transposed + flipped split weights, rebuilt by the head kernel; the fp32
      // dpool3 expanded through pool3's routing and split while staged; 4x8
-     // tiles x four k groups)
+     // tiles x four k groups).  Its staging also writes the expanded split
+     // dconv3 (the tiles' own pixels, 16-byte stores) for the weight gradient.
     const int H = S / 4;
     SplitArgs a{};
     a.B = B; a.H = H; a.W = H; a.pad = 1;
     a.in_f32 = nb.dconv3; a.in_route = nb.mask3;
     a.wk[0] = nb.wks[0] + L.wkst3_off; a.wk_elems = L.wks_total;
     a.pd_split = nb.dconv2s; a.pd_elems = (int64_t)B * H * H * 64;
+    a.xsplit = nb.dconv3s; a.x_elems = (int64_t)B * H * H * 64;
     M("conv3_dgrad");
     CHECK_LAUNCH((launch_split_conv<64, 64, 64, 3, 4, 8, 1, 2, 4, true>(a, 1, s)));
+  }
+  {  // conv3 weight gradient (split bf16, wgrads.h): rows of the expanded split
+     // dconv3 (pure copies) against the split pool2
+    const int H = S / 4;
+    WgradSArgs ws{};
+    ws.B = B; ws.H = H; ws.W = H; ws.G = nb.wsplits[2];
+    ws.RPG = (B * H + ws.G - 1) / ws.G; ws.NP = nb.wnp[2];
+    ws.in = nb.pool2s[0]; ws.in_elems = (int64_t)B * H * H * 64;
+    ws.dfull = nb.dconv3s; ws.d_elems = (int64_t)B * H * H * 64;
+    ws.droute = nb.mask3; ws.part = nb.wpart + nb.wpart_off[2];
+    M("conv3_wgrad");
+    CHECK_LAUNCH((launch_wgrads<64, 64, 3, 1, 2>(ws, s)));
   }
   {  // conv2 weight gradient (split bf16, wgrads.h) on the split pooled dpool2
      // and the split pool1

@@ -180,6 +180,9 @@ struct SplitArgs {
   float* pd;                 // dgrad: fp32 gradient of the previous pool output (nullable)
   __bf16* pd_split;          // dgrad: split gradient of the previous pool output (nullable)
   int64_t pd_elems;
+  __bf16* xsplit;            // dgrad, one channel chunk: the staged source expanded and
+  int64_t x_elems;           // split, NHWC (B,H,W,CPT), written once (nullable) -- the
+                             // layer's weight gradient then copies rows (wgrads DSRC 2)
 };
 
 // Epilogue of a direct conv tile (accumulator rows window-major: a lane's 4
@@ -404,6 +407,24 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
   ws0.store(wbuf, tid);
   if (NSTEP > 1) wload(ws1, 1);
   __syncthreads();
+  if (DGRAD && NCH == 1 && a.xsplit) {   // the tile's own pixels of the staged source
+    constexpr int NV = TY * TX * (CPT / 8);
+#pragma unroll
+    for (int i = 0; i < (3 * NV + C::kThreads - 1) / C::kThreads; ++i) {
+      const int f = tid + i * C::kThreads;
+      if (f < 3 * NV) {
+        const int p = f / NV, r = f - p * NV;
+        const int pix = r / (CPT / 8), c8 = r % (CPT / 8);
+        const int ty = pix / TX, tx = pix % TX;
+        const int gy = y0 + ty, gx = x0 + tx;
+        if (gy < a.H && gx < a.W)
+          *reinterpret_cast<u32x4*>(a.xsplit + p * a.x_elems +
+                                    (((size_t)b * a.H + gy) * a.W + gx) * CPT + 8 * c8) =
+              *reinterpret_cast<const u32x4*>(patch + p * C::kPlane + (ty + a.pad) * C::RS +
+                                              (tx + a.pad) * C::CS + 8 * c8);
+      }
+    }
+  }
 
   // ---- per-lane operand offsets (bf16 units) ----
   const int l31 = lane & 31, h = lane >> 5;

@@ -50,9 +50,11 @@ struct WgradSArgs {
   int64_t d_elems;
   const uint8_t* droute;    // its NHWC routing bytes
   float* part;              // [G][COUT][NP]
-  const float* dpool_f32;   // DF32 instances: the pooled gradient in fp32 instead
-                            // (split while staged; conv3's, from the fc4 data
-                            // gradient, whose split stores cost 2.7 us there)
+  const float* dpool_f32;   // DSRC 1: the pooled gradient in fp32 instead
+                            // (split while staged)
+  const __bf16* dfull;      // DSRC 2: the gradient already expanded and split,
+                            // NHWC (B,H,W,COUT), plane stride d_elems (conv3's:
+                            // a side output of its data gradient's staging)
 };
 
 // LDS geometry of one wave's region (bf16 units).  Pixel strides keep the
@@ -80,8 +82,12 @@ __device__ __forceinline__ bf16x8 tr_pair(const __bf16* p0, const __bf16* p1) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int CIN, int COUT, int KS, int PAD, int WMAX, bool DF32>
+// DSRC: the dconv rows' source -- 0: pooled split + routing bytes (conv2's),
+// 1: pooled fp32 + routing bytes, split while staged, 2: expanded split
+// (dfull: pure 16-byte copies, no VALU per element)
+template <int CIN, int COUT, int KS, int PAD, int WMAX, int DSRC>
 __device__ __forceinline__ void wgrads_body(const WgradSArgs& a, char* smem, int L) {
+  constexpr bool DF32 = DSRC == 1;
   constexpr int NCB = CIN / 32;
   constexpr int T = KS * NCB;
   constexpr int KC = KS * KS * CIN;
@@ -142,7 +148,8 @@ __device__ __forceinline__ void wgrads_body(const WgradSArgs& a, char* smem, int
   // one routing load per pixel chunk for the three planes.
   constexpr int CC = CIN / 8, PPP = 64 / CC;
   constexpr int NPI = (WMAX + PPP - 1) / PPP;
-  constexpr int NPD = (WMAX / 2 + 15) / 16;
+  // dconv chunks per lane: pooled pixels (16 a pass), or DSRC 2 full-width pixels
+  constexpr int NPD = DSRC == 2 ? (WMAX + 15) / 16 : (WMAX / 2 + 15) / 16;
   const int ic8 = lane % CC, ipx = lane / CC;
   const int dc8 = lane & 3, dpx = lane >> 2;
   struct Regs {
@@ -165,13 +172,16 @@ __device__ __forceinline__ void wgrads_body(const WgradSArgs& a, char* smem, int
       __builtin_amdgcn_make_buffer_rsrc((void*)(a.in + a.in_elems), (short)0, (int)ib, 0x00020000),
       __builtin_amdgcn_make_buffer_rsrc((void*)(a.in + 2 * a.in_elems), (short)0, (int)ib,
                                         0x00020000)};
-  const uint32_t db = (uint32_t)(a.B * (H >> 1) * (W >> 1) * COUT);   // elements of a plane
+  // elements of a plane of the dconv source
+  const uint32_t db = DSRC == 2 ? (uint32_t)(a.B * H * W * COUT)
+                                : (uint32_t)(a.B * (H >> 1) * (W >> 1) * COUT);
+  const __bf16* dsp = DSRC == 2 ? a.dfull : a.dpool;
   const __amdgpu_buffer_rsrc_t rd_g[3] = {
-      __builtin_amdgcn_make_buffer_rsrc((void*)(DF32 ? (const void*)a.dpool_f32 : (const void*)a.dpool),
+      __builtin_amdgcn_make_buffer_rsrc((void*)(DF32 ? (const void*)a.dpool_f32 : (const void*)dsp),
                                         (short)0, (int)(DF32 ? db * 4 : db * 2), 0x00020000),
-      __builtin_amdgcn_make_buffer_rsrc((void*)(DF32 ? nullptr : a.dpool + a.d_elems), (short)0,
+      __builtin_amdgcn_make_buffer_rsrc((void*)(DF32 ? nullptr : dsp + a.d_elems), (short)0,
                                         (int)(db * 2), 0x00020000),
-      __builtin_amdgcn_make_buffer_rsrc((void*)(DF32 ? nullptr : a.dpool + 2 * a.d_elems), (short)0,
+      __builtin_amdgcn_make_buffer_rsrc((void*)(DF32 ? nullptr : dsp + 2 * a.d_elems), (short)0,
                                         (int)(db * 2), 0x00020000)};
   const __amdgpu_buffer_rsrc_t rm_g =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.droute, (short)0, (int)db, 0x00020000);
@@ -188,6 +198,21 @@ __device__ __forceinline__ void wgrads_body(const WgradSArgs& a, char* smem, int
 #pragma unroll
       for (int p = 0; p < 3; ++p)
         R.i[p][u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rin_g[p], (int)o, 0, 0));
+    }
+    if (DSRC == 2) {   // expanded split rows: 16-byte copies
+      const uint32_t o0 = (uint32_t)(((lb * H + ly) * W + dpx) * COUT + cb * 32 + 8 * dc8);
+#pragma unroll
+      for (int u = 0; u < NPD; ++u) {
+        const bool ok = live && dpx + 16 * u < W;
+        const uint32_t o = o0 + (uint32_t)(u * 16 * COUT);
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          R.d[p][u] = __builtin_bit_cast(
+              u32x4, __builtin_amdgcn_raw_buffer_load_b128(rd_g[p], (int)(ok ? o * 2 : kOOB), 0, 0));
+      }
+      ly += 4;
+      if (ly >= H) { ly -= H; ++lb; }
+      return;
     }
     const uint32_t o0 =
         (uint32_t)(((lb * (H >> 1) + (ly >> 1)) * (W >> 1) + dpx) * COUT + cb * 32 + 8 * dc8);
@@ -241,8 +266,26 @@ __device__ __forceinline__ void wgrads_body(const WgradSArgs& a, char* smem, int
         for (int p = 0; p < 3; ++p)
           *reinterpret_cast<u32x4*>(rin + p * ipl + (ipx + u * PPP + PAD) * Geo::PSI + 8 * ic8) =
               R.i[p][u];
+    if (DSRC == 2) {
 #pragma unroll
-    for (int u = 0; u < NPD; ++u) {
+      for (int u = 0; u < NPD; ++u) {
+        const int px = dpx + 16 * u;
+        if (px >= W) continue;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          *reinterpret_cast<u32x4*>(rd + p * dpl + px * Geo::PSD + 8 * dc8) = R.d[p][u];
+          if (ky == 0) {   // bias: fp32 value = sum of the three planes
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              bsum[2 * e] += __builtin_bit_cast(float, R.d[p][u][e] << 16);
+              bsum[2 * e + 1] += __builtin_bit_cast(float, R.d[p][u][e] & 0xffff0000u);
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < (DSRC == 2 ? 0 : NPD); ++u) {
       const int px = dpx + 16 * u;
       if (px >= (W >> 1)) continue;
 #pragma unroll
@@ -376,11 +419,11 @@ __device__ __forceinline__ void wgrads_body(const WgradSArgs& a, char* smem, int
 
 // two waves per SIMD (<= 256 registers): the other wave's MFMAs cover each
 // wave's row staging and LDS round trips
-template <int CIN, int COUT, int KS, int PAD, int WMAX, bool DF32>
+template <int CIN, int COUT, int KS, int PAD, int WMAX, int DSRC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void wgrads_kernel(
     const WgradSArgs a) {
   extern __shared__ __attribute__((aligned(16))) char sm_wgs[];
-  wgrads_body<CIN, COUT, KS, PAD, WMAX, DF32>(a, sm_wgs, blockIdx.x);
+  wgrads_body<CIN, COUT, KS, PAD, WMAX, DSRC>(a, sm_wgs, blockIdx.x);
 }
 
 template <int CIN, int PAD>
@@ -389,11 +432,11 @@ inline size_t wgrads_smem_bytes(int W) {
   return f > 4 * 16 * 64 * 4 + 0 ? f : 4 * 16 * 64 * 4;   // >= the 4-wave reduction image
 }
 
-template <int CIN, int COUT, int KS, int PAD, int WMAX, bool DF32>
+template <int CIN, int COUT, int KS, int PAD, int WMAX, int DSRC>
 inline hipError_t launch_wgrads_w(const WgradSArgs& a, hipStream_t st) {
   const size_t shm = wgrads_smem_bytes<CIN, PAD>(a.W);
   if (shm > 160 * 1024) return hipErrorInvalidValue;
-  auto kern = wgrads_kernel<CIN, COUT, KS, PAD, WMAX, DF32>;
+  auto kern = wgrads_kernel<CIN, COUT, KS, PAD, WMAX, DSRC>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -407,11 +450,11 @@ inline hipError_t launch_wgrads_w(const WgradSArgs& a, hipStream_t st) {
 }
 
 // the staging registers are sized for the widest row the instance takes
-template <int CIN, int COUT, int KS, int PAD, bool DF32 = false>
+template <int CIN, int COUT, int KS, int PAD, int DSRC = 0>
 inline hipError_t launch_wgrads(const WgradSArgs& a, hipStream_t st) {
-  if (a.W <= 16) return launch_wgrads_w<CIN, COUT, KS, PAD, 16, DF32>(a, st);
-  if (a.W <= 32) return launch_wgrads_w<CIN, COUT, KS, PAD, 32, DF32>(a, st);
-  if (a.W <= 64) return launch_wgrads_w<CIN, COUT, KS, PAD, 64, DF32>(a, st);
+  if (a.W <= 16) return launch_wgrads_w<CIN, COUT, KS, PAD, 16, DSRC>(a, st);
+  if (a.W <= 32) return launch_wgrads_w<CIN, COUT, KS, PAD, 32, DSRC>(a, st);
+  if (a.W <= 64) return launch_wgrads_w<CIN, COUT, KS, PAD, 64, DSRC>(a, st);
   return hipErrorInvalidValue;   // frames > 128 (conv2) / 256 (conv3): not supported
 }
 
