@@ -1459,6 +1459,87 @@ hipError_t launch_apply(const NetBuffers& nb, int rule, float lr, float decay, f
 // ---------------------------------------------------------------------------
 int fc4_splits_for(int S) { return fc4_fwd_splits(64 * (S / 8) * (S / 8)); }
 
+// Tile menus of the direct convolutions.  A tile's rows (its pixels, padded to
+// whole 32-row blocks: split.h SplitCfg::NWIN) are the MFMA work of one
+// workgroup; the frame's edge tiles of a fixed 16 x 16 tile wasted up to 2.56x
+// of it (conv2 at S = 40: four 16 x 16 tiles on a 20 x 20 map).  Per layer and
+// map side the cheapest option is taken: tiles x (rows + 32), the 32 standing
+// for a workgroup's fixed costs (weight ring, prologue); the first option (the
+// tuned tile of the exact 64 x 64 / 128 x 128 frames) is left only for one at
+// least 10 % cheaper.
+struct TileOpt {
+  int ty, tx, rows;
+};
+template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK>
+constexpr TileOpt split_tile() {
+  return {TY, TX, WM * SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK>::TM * 32};
+}
+template <int TY, int TX, int WM>
+constexpr TileOpt conv1_tile() { return {TY, TX, WM * Conv1Cfg<TY, TX, WM>::TM * 32}; }
+
+template <class T, int n>
+static const T& pick_tile(const T (&menu)[n], int H, int W) {
+  auto cost = [&](const TileOpt& o) {
+    return (int64_t)((H + o.ty - 1) / o.ty) * ((W + o.tx - 1) / o.tx) * (o.rows + 32);
+  };
+  const int64_t c0 = cost(menu[0].opt);
+  int best = 0;
+  int64_t bc = c0;
+  for (int i = 1; i < n; ++i) {
+    const int64_t c = cost(menu[i].opt);
+    if (10 * c < 9 * c0 && c < bc) { bc = c; best = i; }
+  }
+  return menu[best];
+}
+
+struct SplitMenu {
+  TileOpt opt;
+  hipError_t (*launch)(SplitArgs, int, hipStream_t);
+};
+#define DDQ_SPLIT_TILE(CPT, CP, N, KS, TY, TX, WM, WN, WK, DG)              \
+  SplitMenu {                                                              \
+    split_tile<CPT, CP, N, KS, TY, TX, WM, WN, WK>(),                      \
+        &launch_split_conv<CPT, CP, N, KS, TY, TX, WM, WN, WK, DG>          \
+  }
+// conv2 forward (32 -> 64, 5x5): 16 waves of one 32x32 block on 16 x 16
+static const SplitMenu kConv2Fwd[] = {
+    DDQ_SPLIT_TILE(32, 32, 64, 5, 16, 16, 8, 2, 1, false),
+    DDQ_SPLIT_TILE(32, 32, 64, 5, 10, 20, 7, 2, 1, false),
+    DDQ_SPLIT_TILE(32, 32, 64, 5, 12, 12, 5, 2, 1, false),
+    DDQ_SPLIT_TILE(32, 32, 64, 5, 8, 8, 2, 2, 1, false),
+    DDQ_SPLIT_TILE(32, 32, 64, 5, 8, 26, 7, 2, 1, false),
+    DDQ_SPLIT_TILE(32, 32, 64, 5, 14, 14, 7, 2, 1, false)};
+// conv3 forward (64 -> 64, 3x3): two k groups on 8 x 8
+static const SplitMenu kConv3Fwd[] = {
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 8, 8, 2, 2, 2, false),
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 10, 10, 4, 2, 2, false),
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 12, 12, 5, 2, 1, false),
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 18, 4, 2, 2, false),
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 4, 4, 1, 2, 2, false),
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 26, 5, 2, 1, false)};
+// conv3 data gradient: four k groups on 4 x 8
+static const SplitMenu kConv3Dgrad[] = {
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 4, 8, 1, 2, 4, true),
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 10, 2, 2, 4, true),
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 26, 5, 2, 1, true)};
+// conv2 data gradient (64 -> 32): four k groups on 8 x 16
+static const SplitMenu kConv2Dgrad[] = {
+    DDQ_SPLIT_TILE(64, 64, 32, 5, 8, 16, 4, 1, 4, true),
+    DDQ_SPLIT_TILE(64, 64, 32, 5, 8, 20, 5, 1, 2, true),
+    DDQ_SPLIT_TILE(64, 64, 32, 5, 12, 12, 5, 1, 2, true),
+    DDQ_SPLIT_TILE(64, 64, 32, 5, 8, 8, 2, 1, 4, true)};
+#undef DDQ_SPLIT_TILE
+
+struct Conv1Menu {
+  TileOpt opt;
+  hipError_t (*launch)(Conv1Args, int, hipStream_t, int64_t);
+};
+#define DDQ_CONV1_TILE(TY, TX, WM) \
+  Conv1Menu { conv1_tile<TY, TX, WM>(), &launch_split_conv1<TY, TX, WM> }
+static const Conv1Menu kConv1Fwd[] = {DDQ_CONV1_TILE(32, 32, 16), DDQ_CONV1_TILE(20, 20, 13),
+                                      DDQ_CONV1_TILE(16, 16, 8), DDQ_CONV1_TILE(24, 24, 9)};
+#undef DDQ_CONV1_TILE
+
 // conv1 weight-gradient band height: the largest power of two <= 8 dividing
 // S (one slab per band)
 static int wgrad1_band(int S) {
@@ -1528,11 +1609,11 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     c1.out_elems = (int64_t)B * (S / 2) * (S / 2) * 32;
     c1.mask[0] = nb.mask1; c1.mask[1] = nullptr;
     M("conv1_fwd");
-    CHECK_LAUNCH((launch_split_conv1<32, 32, 16>(c1, nz, s, L.wks_total)));
+    CHECK_LAUNCH(pick_tile(kConv1Fwd, S, S).launch(c1, nz, s, L.wks_total));
   }
   if (!nb.fwd_only || nb.fwd_only == 2) {
     // conv2 (train_val.prototxt:79-118): split bf16, 16x16 tiles, 16 waves of
-    // one 32x32 block each
+    // one 32x32 block each (kConv2Fwd: edge-fitting tiles on other maps)
     const int H = S / 2;
     SplitArgs a2{};
     a2.B = B; a2.H = H; a2.W = H; a2.pad = 2;
@@ -1548,10 +1629,10 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     a2.out_elems = (int64_t)B * (H / 2) * (H / 2) * 64;
     a2.mask[0] = nb.mask2; a2.mask[1] = nullptr;
     M("conv2_fwd");
-    CHECK_LAUNCH((launch_split_conv<32, 32, 64, 5, 16, 16, 8, 2, 1, false>(a2, nz, s)));
+    CHECK_LAUNCH(pick_tile(kConv2Fwd, H, H).launch(a2, nz, s));
   }
   if (!nb.fwd_only || nb.fwd_only == 3) {
-    // conv3 (train_val.prototxt:119-158): split bf16, 8x8 tiles, two k groups
+    // conv3 (train_val.prototxt:119-158): split bf16, 8x8 tiles (kConv3Fwd), two k groups
     // of 4 waves; pool3 (= fc4's input) fp32 in Caffe order, routing bytes
     // NHWC (the backward expands dpool3 through them)
     const int H = S / 4;
@@ -1568,7 +1649,7 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     a3.nchw = 1;
     a3.mask[0] = nb.mask3; a3.mask[1] = nullptr;
     M("conv3_fwd");
-    CHECK_LAUNCH((launch_split_conv<64, 64, 64, 3, 8, 8, 2, 2, 2, false>(a3, nz, s)));
+    CHECK_LAUNCH(pick_tile(kConv3Fwd, H, H).launch(a3, nz, s));
   }
   if (nb.fwd_only) return hipSuccess;   // ddq_time_layer: one conv layer
   // fc4 (train_val.prototxt:159-185): split bf16 MFMA register-direct, split-K
@@ -1618,7 +1699,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
   }
   {  // conv3 data gradient -> split pooled dpool2 (split bf16 on conv3's
      // transposed + flipped split weights, rebuilt by the head kernel; the fp32
-     // dpool3 expanded through pool3's routing and split while staged; 4x8
+     // dpool3 expanded through pool3's routing and split while staged; 4x8 (kConv3Dgrad)
      // tiles x four k groups).  Its staging also writes the expanded split
      // dconv3 (the tiles' own pixels, 16-byte stores) for the weight gradient.
     const int H = S / 4;
@@ -1629,7 +1710,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     a.pd_split = nb.dconv2s; a.pd_elems = (int64_t)B * H * H * 64;
     a.xsplit = nb.dconv3s; a.x_elems = (int64_t)B * H * H * 64;
     M("conv3_dgrad");
-    CHECK_LAUNCH((launch_split_conv<64, 64, 64, 3, 4, 8, 1, 2, 4, true>(a, 1, s)));
+    CHECK_LAUNCH(pick_tile(kConv3Dgrad, H, H).launch(a, 1, s));
   }
   {  // conv3 weight gradient (split bf16, wgrads.h): rows of the expanded split
      // dconv3 (pure copies) against the split pool2
@@ -1657,7 +1738,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
   }
   {  // conv2 data gradient -> split pooled dpool1 (split bf16, DGRAD): the
      // split pooled dpool2 expanded through mask2 while staged, the transposed
-     // split weights the head kernel rebuilt, one 64-channel chunk, 8x16-pixel
+     // split weights the head kernel rebuilt, one 64-channel chunk, 8x16-pixel (kConv2Dgrad)
      // tiles, four k groups (their sums meet in LDS in fixed order)
     const int H = S / 2;
     SplitArgs a{};
@@ -1667,7 +1748,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     a.in_route = nb.mask2;
     a.pd_split = nb.dconv1s; a.pd_elems = (int64_t)B * H * H * 32;
     M("conv2_dgrad");
-    CHECK_LAUNCH((launch_split_conv<64, 64, 32, 5, 8, 16, 4, 1, 4, true>(a, 1, s)));
+    CHECK_LAUNCH(pick_tile(kConv2Dgrad, H, H).launch(a, 1, s));
   }
   // slab-reduce geometry: layer l's blocks start at d[l].blk0
   WredDims d[3];

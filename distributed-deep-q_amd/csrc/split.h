@@ -108,7 +108,12 @@ struct SplitCfg {
   static constexpr int kGroup = 64 * WM * WN * WK;                     // all waves stage
   static constexpr int kThreads = kGroup;
   static constexpr int KSW = KSTEP / WK;                              // k-steps per wave
-  static constexpr int TM = TY * TX / WM / 32;
+  // 32-row blocks per wave: the tile's NWIN pooling windows (8 per block),
+  // padded to WM * TM * 8 -- padding rows read window 0 and are dropped by
+  // the epilogue, so a tile need not hold a multiple of 32 pixels (10 x 20,
+  // 10 x 10, ... tiles that fit the frame's edge: kernels.hip pick_tile)
+  static constexpr int NWIN = TY * TX / 4;
+  static constexpr int TM = (NWIN + 8 * WM - 1) / (8 * WM);
   static constexpr int TN = N / WN / 32;
   static constexpr int kPlane = PH * RS;                              // bf16 per patch plane
   static constexpr int kWSlot = N * CW;                               // bf16 per weight plane
@@ -116,7 +121,8 @@ struct SplitCfg {
   static constexpr int kWB = 2 * 3 * kWSlot * 2;                      // two-slot ring
   static constexpr int kSmemB = kPatchB + kWB;
   static_assert(CPT % CP == 0 && CP % 16 == 0 && TY % 2 == 0 && TX % 2 == 0, "shape");
-  static_assert(TM >= 1 && TN >= 1 && TY * TX == WM * TM * 32 && N == WN * TN * 32, "wave tile");
+  static_assert(TM >= 1 && TN >= 1 && (WM * TM - 1) * 8 < NWIN && N == WN * TN * 32, "wave tile");
+  static_assert(kGroup <= 1024, "workgroup size");
   static_assert(kSmemB <= 160 * 1024, "LDS budget");
   static_assert(KSTEP % WK == 0, "k split");
   // every k group's accumulators for the fixed-order sums of the epilogue
@@ -194,7 +200,7 @@ struct SplitArgs {
 //         split (the consumer routes it through that pool's mask).
 // With WK k groups, group wkg finishes the windows gi (rows 4gi..4gi+3) with
 // gi % WK == wkg.
-template <int TM, int TN, int TX, int N, bool DGRAD, int WK = 1>
+template <int TM, int TN, int TX, int N, bool DGRAD, int WK = 1, int NWIN = 1 << 30>
 __device__ __forceinline__ void split_epilogue(const SplitArgs& a, const f32x16 (&acc)[TM][TN],
                                                int b, int z, int y0, int x0, int wmi, int wni,
                                                int l31, int h, int wkg = 0) {
@@ -215,6 +221,7 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, const f32x16 
         for (int g = 0; g < 4; ++g) {
           if (g % WK != wkg) continue;
           const int win = (mb + 8 * g + 4 * h) >> 2;
+          if (win >= NWIN) continue;                // padding rows
           const int pyy = y0 / 2 + win / (TX / 2), pxx = x0 / 2 + win % (TX / 2);
           if (pyy >= Hp || pxx >= Wp) continue;
           const float v0 = acc[i][j][4 * g + 0] + bvv, v1 = acc[i][j][4 * g + 1] + bvv;
@@ -238,6 +245,7 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, const f32x16 
           if ((r >> 2) % WK != wkg) continue;
           const int m = mb + (r & 3) + 8 * (r >> 2) + 4 * h;
           const int win = m >> 2;
+          if (win >= NWIN) continue;                // padding rows
           const int y = y0 + 2 * (win / (TX / 2)) + ((m >> 1) & 1);
           const int x = x0 + 2 * (win % (TX / 2)) + (m & 1);
           if (y >= a.H || x >= a.W) continue;
@@ -436,7 +444,7 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int m = wmi * TM * 32 + 32 * i + l31;
-    const int win = m >> 2, dy = (m >> 1) & 1, dx = m & 1;
+    const int win = (m >> 2) < C::NWIN ? m >> 2 : 0, dy = (m >> 1) & 1, dx = m & 1;
     const int wy = win / (TX / 2), wx = win % (TX / 2);
     abase[i] = (2 * wy + dy) * C::RS + (2 * wx + dx) * C::CS + h * 8 + 16 * C::KSW * wkg;
   }
@@ -542,7 +550,7 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
         }
       }
   }
-  split_epilogue<TM, TN, TX, N, DGRAD, WK>(a, acc, b, z, y0, x0, wmi, wni, l31, h, wkg);
+  split_epilogue<TM, TN, TX, N, DGRAD, WK, C::NWIN>(a, acc, b, z, y0, x0, wmi, wni, l31, h, wkg);
 }
 
 template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, bool DGRAD>
@@ -604,8 +612,10 @@ struct Conv1Cfg {
   static constexpr int kPatchB = PH * RS * 2;
   static constexpr int kWB = 3 * 32 * CW * 2;
   static constexpr int kSmemB = kPatchB + kWB;
-  static constexpr int TM = TY * TX / WM / 32;
-  static_assert(TM >= 1 && TY * TX == WM * TM * 32 && TX % 16 == 0, "tile");
+  static constexpr int NWIN = TY * TX / 4;                             // padded as SplitCfg
+  static constexpr int TM = (NWIN + 8 * WM - 1) / (8 * WM);
+  static_assert(TM >= 1 && (WM * TM - 1) * 8 < NWIN && TX % 2 == 0 && TY % 2 == 0 && WM <= 16,
+                "tile");
   static_assert(kSmemB <= 160 * 1024, "LDS");
 };
 
@@ -672,7 +682,7 @@ __global__ __launch_bounds__(64 * WM) void split_conv1_kernel(const Conv1Args a)
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int m = wid * TM * 32 + 32 * i + l31;
-    const int win = m >> 2, dy = (m >> 1) & 1, dx = m & 1;
+    const int win = (m >> 2) < C::NWIN ? m >> 2 : 0, dy = (m >> 1) & 1, dx = m & 1;
     const int wy = win / (TX / 2), wx = win % (TX / 2);
     abase[i] = (2 * wy + dy) * C::RS + (2 * wx + dx + 2 * h) * 4;
   }
@@ -721,7 +731,7 @@ __global__ __launch_bounds__(64 * WM) void split_conv1_kernel(const Conv1Args a)
   e.out_split[0] = a.out_split[0]; e.out_split[1] = a.out_split[1];
   e.out_elems = a.out_elems;
   e.mask[0] = a.mask[0]; e.mask[1] = a.mask[1];
-  split_epilogue<TM, 1, TX, 32, false>(e, acc, b, z, y0, x0, wid, 0, l31, h);
+  split_epilogue<TM, 1, TX, 32, false, 1, C::NWIN>(e, acc, b, z, y0, x0, wid, 0, l31, h);
 }
 
 template <int TY, int TX, int WM>
