@@ -5,6 +5,14 @@
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+// A/B timing experiments only (make variant DEFS=-DDDQ_AB_SKIP=..., tools/ab):
+// work that returns at once -- slab-reduce launch roles (1 fc4 apply tiles,
+// 2 slab units, 4 head sums, 8 prefetch); conv2 forward phases (16 the tap
+// loop, 32 the epilogue stores, 64 the patch staging).  0 in the product build.
+#ifndef DDQ_AB_SKIP
+#define DDQ_AB_SKIP 0
+#endif
+
 namespace ddq {
 
 constexpr int kWave = 64;          // CDNA wavefront

@@ -5,13 +5,6 @@
 #include "fc.h"
 #include "split.h"
 
-// A/B timing experiments only (make variant DEFS=-DDDQ_AB_SKIP=..., tools/ab):
-// block roles of the slab-reduce launch that return at once (1 fc4 apply
-// tiles, 2 slab units, 4 head sums, 8 prefetch).  0 in the product build.
-#ifndef DDQ_AB_SKIP
-#define DDQ_AB_SKIP 0
-#endif
-
 namespace ddq {
 
 // first failing launch site of the last failed launch sequence (api.hip

@@ -202,9 +202,9 @@ struct SplitArgs {
 // gi % WK == wkg.
 template <int TM, int TN, int TX, int N, bool DGRAD, int WK = 1, int NWIN = 1 << 30>
 __device__ __forceinline__ void split_epilogue(const SplitArgs& a, const f32x16 (&acc)[TM][TN],
-                                               int b, int z, int y0, int x0, int wmi, int wni,
-                                               int l31, int h, int wkg = 0) {
-  const float* __restrict__ biasz = z ? a.bias[1] : a.bias[0];
+                                               const float (&bpre)[TN], int b, int z, int y0,
+                                               int x0, int wmi, int wni, int l31, int h,
+                                               int wkg = 0) {
   float* __restrict__ outz = z ? a.out[1] : a.out[0];
   __bf16* __restrict__ osplit = z ? a.out_split[1] : a.out_split[0];
   uint8_t* __restrict__ maskz = z ? a.mask[1] : a.mask[0];
@@ -216,7 +216,7 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, const f32x16 
       const int n = wni * TN * 32 + 32 * j + l31;
       if (!DGRAD) {
         const int Hp = a.H >> 1, Wp = a.W >> 1;
-        const float bvv = biasz[n];
+        const float bvv = bpre[j];   // loaded at the kernel's start
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           if (g % WK != wkg) continue;
@@ -235,6 +235,7 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, const f32x16 
           const size_t onhwc = (((size_t)b * Hp + pyy) * Wp + pxx) * N + n;
           // (plain stores: write-through measured no faster here, and slower
           // for the scattered NCHW pool3 and the routing bytes)
+          if ((DDQ_AB_SKIP & 128) && a.B > 0) continue;   // A/B: no stores
           if (outz) outz[a.nchw ? (((size_t)b * N + n) * Hp + pyy) * Wp + pxx : onhwc] = o;
           if (osplit) store_split(osplit, a.out_elems, onhwc, o);
           if (maskz) maskz[onhwc] = (uint8_t)(pos ? arg : 4);
@@ -258,6 +259,120 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, const f32x16 
   }
 }
 
+// Forward epilogue through LDS: the pooled values of the tile (split planes
+// or fp32, and the routing bytes) are first gathered in LDS in the output's
+// own order, then copied out as whole 16-byte vectors (the accumulator layout
+// gives 2-byte stores of 64-byte segments per plane and lane group and, for
+// conv3's NCHW fp32 pool3, one 256-byte-strided dword per lane).  The stores
+// of these one-round launches all leave at the end (A/B without them: conv1 /
+// conv2 / conv3 forward -2.9 / -4.7 / -1.4 us); the 16-byte write-through form
+// recovers ~1 us of it, the rest is the bytes themselves.  Every wave must have
+// finished reading the patch / ring (the barrier at the top).  LDS: NWIN * N *
+// 7 bytes.  One of out / out_split per launch (the forward passes never ask
+// for both).
+template <int TM, int TN, int TX, int N, int WK, int NWIN, int NT>
+__device__ __forceinline__ void split_epilogue_fwd_lds(const SplitArgs& a,
+                                                       const f32x16 (&acc)[TM][TN],
+                                                       const float (&bpre)[TN], char* smem, int b,
+                                                       int z, int y0, int x0, int wmi, int wni,
+                                                       int l31, int h, int wkg, int tid) {
+  float* __restrict__ outz = z ? a.out[1] : a.out[0];
+  __bf16* __restrict__ osplit = z ? a.out_split[1] : a.out_split[0];
+  uint8_t* __restrict__ maskz = z ? a.mask[1] : a.mask[0];
+  __bf16* sv = reinterpret_cast<__bf16*>(smem);                   // [3][NWIN][N] bf16 or
+  float* fv = reinterpret_cast<float*>(smem);                     // [NWIN][N] fp32
+  uint8_t* sm = reinterpret_cast<uint8_t*>(smem) + NWIN * N * 6;  // [NWIN][N]
+  const bool split = osplit != nullptr;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int mb = wmi * TM * 32 + 32 * i;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = wni * TN * 32 + 32 * j + l31;
+      const float bvv = bpre[j];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        if (g % WK != wkg) continue;
+        const int win = (mb + 8 * g + 4 * h) >> 2;
+        if (win >= NWIN) continue;                // padding rows
+        const float v0 = acc[i][j][4 * g + 0] + bvv, v1 = acc[i][j][4 * g + 1] + bvv;
+        const float v2 = acc[i][j][4 * g + 2] + bvv, v3 = acc[i][j][4 * g + 3] + bvv;
+        float mx = v0; int arg = 0;
+        if (v1 > mx) { mx = v1; arg = 1; }
+        if (v2 > mx) { mx = v2; arg = 2; }
+        if (v3 > mx) { mx = v3; arg = 3; }
+        const bool pos = mx > 0.f;
+        const float o = pos ? mx : 0.f;
+        const int e = win * N + n;
+        if (split) {
+          __bf16 hh, mm, ll;
+          split3(o, hh, mm, ll);
+          sv[e] = hh;
+          sv[NWIN * N + e] = mm;
+          sv[2 * NWIN * N + e] = ll;
+        } else {
+          fv[e] = o;
+        }
+        sm[e] = (uint8_t)(pos ? arg : 4);
+      }
+    }
+  }
+  __syncthreads();
+  if ((DDQ_AB_SKIP & 128) && a.B > 0) return;   // A/B: no stores
+  const int Hp = a.H >> 1, Wp = a.W >> 1;
+  auto pix = [&](int win, int& off) {           // pooled NHWC pixel of window win
+    const int pyy = y0 / 2 + win / (TX / 2), pxx = x0 / 2 + win % (TX / 2);
+    off = (b * Hp + pyy) * Wp + pxx;
+    return pyy < Hp && pxx < Wp;
+  };
+  // write-through (sc1) 16-byte stores: the lines go to memory as they are
+  // written instead of at the kernel's end (conv1 / conv2 forward -0.9 / -0.5
+  // us against plain stores of the same vectors)
+  if (split) {
+    constexpr int VPW = N / 8;                  // 16-byte vectors per window and plane
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      const __amdgpu_buffer_rsrc_t rs = wt_rsrc(osplit + p * a.out_elems, (uint32_t)(a.out_elems * 2));
+      for (int f = tid; f < NWIN * VPW; f += NT) {
+        const int win = f / VPW, c = f % VPW;
+        int off;
+        if (!pix(win, off)) continue;
+        __builtin_amdgcn_raw_buffer_store_b128(
+            *reinterpret_cast<const u32x4*>(sv + (p * NWIN + win) * N + 8 * c), rs,
+            (off * N + 8 * c) * 2, 0, 16);
+      }
+    }
+  } else if (outz) {
+    if (a.nchw) {   // Caffe (B, N, Hp, Wp): consecutive lanes walk a window row
+      for (int f = tid; f < N * NWIN; f += NT) {
+        const int n = f / NWIN, win = f % NWIN;
+        const int pyy = y0 / 2 + win / (TX / 2), pxx = x0 / 2 + win % (TX / 2);
+        if (pyy < Hp && pxx < Wp) outz[(((size_t)b * N + n) * Hp + pyy) * Wp + pxx] = fv[win * N + n];
+      }
+    } else {
+      for (int f = tid; f < NWIN * (N / 4); f += NT) {
+        const int win = f / (N / 4), c = f % (N / 4);
+        int off;
+        if (pix(win, off))
+          *reinterpret_cast<float4*>(outz + (size_t)off * N + 4 * c) =
+              *reinterpret_cast<const float4*>(fv + win * N + 4 * c);
+      }
+    }
+  }
+  if (maskz) {
+    constexpr int VPM = N / 16;                 // 16-byte vectors of routing bytes per window
+    const __amdgpu_buffer_rsrc_t rm = wt_rsrc(maskz, (uint32_t)(a.B * Hp * Wp * N));
+    for (int f = tid; f < NWIN * VPM; f += NT) {
+      const int win = f / VPM, c = f % VPM;
+      int off;
+      if (!pix(win, off)) continue;
+      __builtin_amdgcn_raw_buffer_store_b128(
+          *reinterpret_cast<const u32x4*>(sm + win * N + 16 * c), rm, off * N + 16 * c, 0, 16);
+    }
+  }
+}
+
 template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, bool DGRAD>
 __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, int bx, int by,
                                                 int bz) {
@@ -271,6 +386,14 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
   const int y0 = ty * TY, x0 = tx * TX;
   const __bf16* __restrict__ in = z ? a.in[1] : a.in[0];
   const __bf16* __restrict__ wk = z ? a.wk[1] : a.wk[0];
+  // the bias of the lane's output channels (fwd), loaded now: at the epilogue
+  // its latency was exposed once per workgroup after the last MFMA
+  float bpre[C::TN];
+#pragma unroll
+  for (int j = 0; j < C::TN; ++j)
+    bpre[j] = DGRAD ? 0.f
+                    : (z ? a.bias[1] : a.bias[0])[((wid % (WM * WN)) % WN) * C::TN * 32 + 32 * j +
+                                                  (lane & 31)];
 
   // ---- stage the halo patch of channel chunk ch (3 planes, zero outside) ----
   // Batches of 8 vectors per thread: every load of a batch is issued before
@@ -286,52 +409,58 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
                                                (int)(src_elems * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t rroute =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.in_route, (short)0, (int)src_elems, 0x00020000);
+  constexpr int NV = C::PH * C::PW * (CP / 8);             // 16-byte vectors per plane
+  constexpr int NIT = (3 * NV + C::kThreads - 1) / C::kThreads;
+  constexpr int BAT = NIT < 8 ? NIT : 8;
+  auto patch_load = [&](int ch, int i0, u32x4 (&v)[BAT], int (&dst)[BAT]) {
+#pragma unroll
+    for (int u = 0; u < BAT; ++u) {
+      const int f0 = tid + (i0 + u) * C::kThreads;
+      const bool live = i0 + u < NIT && f0 < 3 * NV;
+      const int f = live ? f0 : 0;
+      const int p = f / NV, r = f - p * NV;
+      const int pix = r / (CP / 8), c8 = r % (CP / 8);
+      const int py = pix / C::PW, px = pix % C::PW;
+      const int gy = y0 - a.pad + py, gx = x0 - a.pad + px;
+      const bool in_img = live && (unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W;
+      dst[u] = live ? p * C::kPlane + py * C::RS + px * C::CS + 8 * c8 : -1;
+      // bounds-checked buffer loads: outside the image (or past the
+      // items) the offset is out of range and the vector reads 0 -- no
+      // branch, select or 64-bit address per vector
+      if (DGRAD) {   // pooled source: expand through the routing bytes
+        const uint32_t o = (uint32_t)(((b * (a.H >> 1) + (gy >> 1)) * (a.W >> 1) + (gx >> 1)) * CPT +
+                                      ch * CP + 8 * c8);
+        const u32x4 uw = __builtin_bit_cast(
+            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rin[p], (int)(in_img ? o * 2 : kOOB), 0, 0));
+        const u32x2 m = __builtin_bit_cast(
+            u32x2, __builtin_amdgcn_raw_buffer_load_b64(rroute, (int)(in_img ? o : kOOB), 0, 0));
+        const uint32_t q = ((gy & 1) << 1) | (gx & 1);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {   // bf16 pair e = channels 2e, 2e+1 (zeros route nothing)
+          const uint32_t mw = m[e >> 1];
+          const uint32_t r0 = (mw >> (16 * (e & 1))) & 0xff;
+          const uint32_t r1 = (mw >> (16 * (e & 1) + 8)) & 0xff;
+          v[u][e] = (r0 == q ? (uw[e] & 0xffffu) : 0u) | (r1 == q ? (uw[e] & 0xffff0000u) : 0u);
+        }
+      } else {
+        const uint32_t o = (uint32_t)(((b * a.H + gy) * a.W + gx) * CPT + ch * CP + 8 * c8);
+        v[u] = __builtin_bit_cast(
+            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rin[p], (int)(in_img ? o * 2 : kOOB), 0, 0));
+      }
+    }
+  };
+  auto patch_store = [&](__bf16* buf, const u32x4 (&v)[BAT], const int (&dst)[BAT]) {
+#pragma unroll
+    for (int u = 0; u < BAT; ++u)
+      if (dst[u] >= 0) *reinterpret_cast<u32x4*>(buf + dst[u]) = v[u];
+  };
   auto stage_patch_split = [&](int ch) {
-    constexpr int NV = C::PH * C::PW * (CP / 8);           // 16-byte vectors per plane
-    constexpr int NIT = (3 * NV + C::kThreads - 1) / C::kThreads;
-    constexpr int BAT = 8;
 #pragma unroll
     for (int i0 = 0; i0 < NIT; i0 += BAT) {
       u32x4 v[BAT];
       int dst[BAT];
-#pragma unroll
-      for (int u = 0; u < BAT; ++u) {
-        const int f0 = tid + (i0 + u) * C::kThreads;
-        const bool live = i0 + u < NIT && f0 < 3 * NV;
-        const int f = live ? f0 : 0;
-        const int p = f / NV, r = f - p * NV;
-        const int pix = r / (CP / 8), c8 = r % (CP / 8);
-        const int py = pix / C::PW, px = pix % C::PW;
-        const int gy = y0 - a.pad + py, gx = x0 - a.pad + px;
-        const bool in_img = live && (unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W;
-        dst[u] = live ? p * C::kPlane + py * C::RS + px * C::CS + 8 * c8 : -1;
-        // bounds-checked buffer loads: outside the image (or past the
-        // items) the offset is out of range and the vector reads 0 -- no
-        // branch, select or 64-bit address per vector
-        if (DGRAD) {   // pooled source: expand through the routing bytes
-          const uint32_t o = (uint32_t)(((b * (a.H >> 1) + (gy >> 1)) * (a.W >> 1) + (gx >> 1)) * CPT +
-                                        ch * CP + 8 * c8);
-          const u32x4 uw = __builtin_bit_cast(
-              u32x4, __builtin_amdgcn_raw_buffer_load_b128(rin[p], (int)(in_img ? o * 2 : kOOB), 0, 0));
-          const u32x2 m = __builtin_bit_cast(
-              u32x2, __builtin_amdgcn_raw_buffer_load_b64(rroute, (int)(in_img ? o : kOOB), 0, 0));
-          const uint32_t q = ((gy & 1) << 1) | (gx & 1);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {   // bf16 pair e = channels 2e, 2e+1 (zeros route nothing)
-            const uint32_t mw = m[e >> 1];
-            const uint32_t r0 = (mw >> (16 * (e & 1))) & 0xff;
-            const uint32_t r1 = (mw >> (16 * (e & 1) + 8)) & 0xff;
-            v[u][e] = (r0 == q ? (uw[e] & 0xffffu) : 0u) | (r1 == q ? (uw[e] & 0xffff0000u) : 0u);
-          }
-        } else {
-          const uint32_t o = (uint32_t)(((b * a.H + gy) * a.W + gx) * CPT + ch * CP + 8 * c8);
-          v[u] = __builtin_bit_cast(
-              u32x4, __builtin_amdgcn_raw_buffer_load_b128(rin[p], (int)(in_img ? o * 2 : kOOB), 0, 0));
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < BAT; ++u)
-        if (dst[u] >= 0) *reinterpret_cast<u32x4*>(patch + dst[u]) = v[u];
+      patch_load(ch, i0, v, dst);
+      patch_store(patch, v, dst);
     }
   };
 
@@ -410,7 +539,8 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
     const int sc = st < NSTEP ? st : NSTEP - 1;
     w.load(wk, a.wk_elems, sc / T, sc % T, tid);
   };
-  stage_patch(0);
+  constexpr bool kAbC2f = !DGRAD && CPT == 32;   // A/B: conv2 forward only
+  if (!(kAbC2f && (DDQ_AB_SKIP & 64))) stage_patch(0);
   wload(ws0, 0);
   ws0.store(wbuf, tid);
   if (NSTEP > 1) wload(ws1, 1);
@@ -462,8 +592,9 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
       for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; cor[i][j][r] = 0.f; }
 
   // one step: the MFMAs of tap t of the resident chunk on ring slot `slot`
-  auto tap_step = [&](int t, int slot) {
+  auto tap_step = [&](int s, int slot) {
     const __bf16* wb = wbuf + slot * 3 * C::kWSlot;
+    const int t = s % T;
     const int ky = t / KS, kx = t % KS;
     const __bf16* pa = patch + ky * C::RS + kx * C::CS;
 #pragma unroll
@@ -506,19 +637,19 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
     w.store(wbuf + ((s + 1) & 1) * 3 * C::kWSlot, tid);
     __syncthreads();
   };
-  for (int s = 0; s < NSTEP; s += 2) {
+  for (int s = 0; s < ((kAbC2f && (DDQ_AB_SKIP & 16)) ? 0 : NSTEP); s += 2) {
     if (s + 2 < NSTEP) {
       wload(ws0, s + 2);
       __builtin_amdgcn_sched_barrier(0);
     }
-    tap_step(s % T, 0);
+    tap_step(s, 0);
     if (s + 1 >= NSTEP) break;
     step_end(ws1, s);
     if (s + 3 < NSTEP) {
       wload(ws1, s + 3);
       __builtin_amdgcn_sched_barrier(0);
     }
-    tap_step((s + 1) % T, 1);
+    tap_step(s + 1, 1);
     if (s + 2 >= NSTEP) break;
     step_end(ws0, s + 1);
   }
@@ -550,7 +681,14 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
         }
       }
   }
-  split_epilogue<TM, TN, TX, N, DGRAD, WK, C::NWIN>(a, acc, b, z, y0, x0, wmi, wni, l31, h, wkg);
+  if (kAbC2f && (DDQ_AB_SKIP & 32) && a.B > 0) return;   // (kept MFMAs: B unknown)
+  if constexpr (!DGRAD && C::NWIN * N * 7 <= C::kSmemB) {
+    split_epilogue_fwd_lds<TM, TN, TX, N, WK, C::NWIN, C::kThreads>(a, acc, bpre, smem, b, z, y0,
+                                                                    x0, wmi, wni, l31, h, wkg, tid);
+    return;
+  }
+  split_epilogue<TM, TN, TX, N, DGRAD, WK, C::NWIN>(a, acc, bpre, b, z, y0, x0, wmi, wni, l31, h,
+                                                    wkg);
 }
 
 template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, bool DGRAD>
@@ -571,6 +709,10 @@ inline hipError_t launch_split_conv(SplitArgs a, int nz, hipStream_t st) {
     if (e != hipSuccess) return e;
     attr = true;
   }
+  // the forward epilogue writes one of the fp32 / split outputs (see
+  // split_epilogue_fwd_lds)
+  if (!DGRAD && ((a.out[0] && a.out_split[0]) || (a.out[1] && a.out_split[1])))
+    return hipErrorInvalidValue;
   a.tiles_x = (a.W + TX - 1) / TX;
   const int tiles_y = (a.H + TY - 1) / TY;
   hipLaunchKernelGGL(kern, dim3(tiles_y * a.tiles_x, a.B, nz), dim3(C::kThreads), C::kSmemB, st,
@@ -633,6 +775,7 @@ __global__ __launch_bounds__(64 * WM) void split_conv1_kernel(const Conv1Args a)
   const float* __restrict__ in = z ? a.in[1] : a.in[0];
   const __bf16* __restrict__ wk = z ? a.wk[1] : a.wk[0];
   constexpr int kThreads = 64 * WM;
+  const float bias_pre = (z ? a.bias[1] : a.bias[0])[lane & 31];   // the epilogue's, early
   // patch: one pixel (4 channels) per item, fp32 -> bf16 (exact), loads first
   {
     constexpr int NP = C::PH * C::PW;
@@ -687,6 +830,7 @@ __global__ __launch_bounds__(64 * WM) void split_conv1_kernel(const Conv1Args a)
     abase[i] = (2 * wy + dy) * C::RS + (2 * wx + dx + 2 * h) * 4;
   }
   const int bbase = l31 * C::CW + h * 8;
+  const float bpre[1] = {bias_pre};
   f32x16 acc[TM][1], cor[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -726,17 +870,21 @@ __global__ __launch_bounds__(64 * WM) void split_conv1_kernel(const Conv1Args a)
   for (int i = 0; i < TM; ++i) acc[i][0] += cor[i];
   SplitArgs e{};
   e.B = a.B; e.H = a.H; e.W = a.W;
-  e.bias[0] = a.bias[0]; e.bias[1] = a.bias[1];
   e.out[0] = a.out[0]; e.out[1] = a.out[1];
   e.out_split[0] = a.out_split[0]; e.out_split[1] = a.out_split[1];
   e.out_elems = a.out_elems;
   e.mask[0] = a.mask[0]; e.mask[1] = a.mask[1];
-  split_epilogue<TM, 1, TX, 32, false, 1, C::NWIN>(e, acc, b, z, y0, x0, wid, 0, l31, h);
+  if constexpr (C::NWIN * 32 * 7 <= C::kSmemB)
+    split_epilogue_fwd_lds<TM, 1, TX, 32, 1, C::NWIN, 64 * WM>(e, acc, bpre, sm_c1, b, z, y0, x0,
+                                                               wid, 0, l31, h, 0, tid);
+  else
+    split_epilogue<TM, 1, TX, 32, false, 1, C::NWIN>(e, acc, bpre, b, z, y0, x0, wid, 0, l31, h);
 }
 
 template <int TY, int TX, int WM>
 inline hipError_t launch_split_conv1(Conv1Args a, int nz, hipStream_t st, int64_t wk_elems) {
   a.wk_elems = wk_elems;
+  if ((a.out[0] && a.out_split[0]) || (a.out[1] && a.out_split[1])) return hipErrorInvalidValue;
   using C = Conv1Cfg<TY, TX, WM>;
   auto kern = split_conv1_kernel<TY, TX, WM>;
   static bool attr = false;
