@@ -48,8 +48,8 @@ def kernel_flops(B, S):
     c3 = 2.0 * B * s3 * s3 * 64 * 576
     fc = 2.0 * B * 512 * k4
     return {"conv1_fwd": 2 * c1, "conv2_fwd": 2 * c2, "conv3_fwd": 2 * c3, "fc4_fwd": 2 * fc,
-            "fc4_bwd": fc, "conv3_wgrad": c3, "conv3_dgrad": c3,
-            "conv2_wgrad": c2, "conv2_dgrad": c2, "conv1_wgrad": c1}
+            "fc4_bwd": fc, "conv3_dgrad": c3, "conv23_wgrad": c2 + c3, "conv2_dgrad": c2,
+            "conv1_wgrad": c1}
 
 
 # rocprof kernel symbol (prefix) of each profiled step kernel
@@ -61,9 +61,8 @@ KERNEL_SYMBOL = {
     "fc4_fwd": "void ddq::fc4_fwd_split_kernel",
     "head": "ddq::fc4_head_kernel",
     "fc4_bwd": "void ddq::fc4_bwd_kernel",
-    "conv3_wgrad": "void ddq::wgrads_kernel<64, 64, 3, 1",
     "conv3_dgrad": "void ddq::split_conv_kernel<64, 64, 64, 3, 4, 8,",
-    "conv2_wgrad": "void ddq::wgrads_kernel<32, 64, 5, 2",
+    "conv23_wgrad": "void ddq::wgrads_pair_kernel",
     "conv2_dgrad": "void ddq::split_conv_kernel<64, 64, 32, 5,",
     "conv1_wgrad": "void ddq::wgrad1s_kernel",
     "wgrad_reduce": "ddq::wgrad_reduce_kernel",
@@ -77,7 +76,7 @@ KERNEL_SYMBOL = {
 # dense peak over the products per f32 product (the f32 MFMA peak for "f32").
 KERNEL_ARITH = {
     "conv1_fwd": "split3", "conv2_fwd": "split", "conv3_fwd": "split",
-    "conv1_wgrad": "split3", "conv2_wgrad": "split", "conv3_wgrad": "split",
+    "conv1_wgrad": "split3", "conv23_wgrad": "split",
     "conv2_dgrad": "split", "conv3_dgrad": "split", "fc4_fwd": "split", "fc4_bwd": "split",
 }
 BF16_MFMA_PEAK = 2.5e15       # MI355X_MICROARCH.md: dense bf16

@@ -1706,28 +1706,24 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     CHECK_LAUNCH(pick_tile(kConv3Dgrad, H, H).launch(a, 1, s));
   }
   {  // conv3 weight gradient (split bf16, wgrads.h): rows of the expanded split
-     // dconv3 (pure copies) against the split pool2
-    const int H = S / 4;
-    WgradSArgs ws{};
-    ws.B = B; ws.H = H; ws.W = H; ws.G = nb.wsplits[2];
-    ws.RPG = (B * H + ws.G - 1) / ws.G; ws.NP = nb.wnp[2];
-    ws.in = nb.pool2s[0]; ws.in_elems = (int64_t)B * H * H * 64;
-    ws.dfull = nb.dconv3s; ws.d_elems = (int64_t)B * H * H * 64;
-    ws.droute = nb.mask3; ws.part = nb.wpart + nb.wpart_off[2];
-    M("conv3_wgrad");
-    CHECK_LAUNCH((launch_wgrads<64, 64, 3, 1, 2>(ws, s)));
-  }
-  {  // conv2 weight gradient (split bf16, wgrads.h) on the split pooled dpool2
-     // and the split pool1
-    const int H = S / 2;
-    WgradSArgs ws{};
-    ws.B = B; ws.H = H; ws.W = H; ws.G = nb.wsplits[1];
-    ws.RPG = (B * H + ws.G - 1) / ws.G; ws.NP = nb.wnp[1];
-    ws.in = nb.pool1s[0]; ws.in_elems = (int64_t)B * H * H * 32;
-    ws.dpool = nb.dconv2s; ws.d_elems = (int64_t)B * (H / 2) * (H / 2) * 64;
-    ws.droute = nb.mask2; ws.part = nb.wpart + nb.wpart_off[1];
-    M("conv2_wgrad");
-    CHECK_LAUNCH((launch_wgrads<32, 64, 5, 2>(ws, s)));
+     // dconv3 (pure copies) against the split pool2; conv2's on the split
+     // pooled dpool2 and the split pool1
+    WgradSArgs w3{}, w2{};
+    const int H3 = S / 4, H2 = S / 2;
+    w3.B = B; w3.H = H3; w3.W = H3; w3.G = nb.wsplits[2];
+    w3.RPG = (B * H3 + w3.G - 1) / w3.G; w3.NP = nb.wnp[2];
+    w3.in = nb.pool2s[0]; w3.in_elems = (int64_t)B * H3 * H3 * 64;
+    w3.dfull = nb.dconv3s; w3.d_elems = (int64_t)B * H3 * H3 * 64;
+    w3.droute = nb.mask3; w3.part = nb.wpart + nb.wpart_off[2];
+    w2.B = B; w2.H = H2; w2.W = H2; w2.G = nb.wsplits[1];
+    w2.RPG = (B * H2 + w2.G - 1) / w2.G; w2.NP = nb.wnp[1];
+    w2.in = nb.pool1s[0]; w2.in_elems = (int64_t)B * H2 * H2 * 32;
+    w2.dpool = nb.dconv2s; w2.d_elems = (int64_t)B * (H2 / 2) * (H2 / 2) * 64;
+    w2.droute = nb.mask2; w2.part = nb.wpart + nb.wpart_off[1];
+    // one launch (wgrads_pair_kernel, conv2's blocks first): 35.2 -> 30.2 us
+    // against the two launches, same-box kernel trace
+    M("conv23_wgrad");
+    CHECK_LAUNCH(launch_wgrads_conv23(w2, w3, s));
   }
   {  // conv2 data gradient -> split pooled dpool1 (split bf16, DGRAD): the
      // split pooled dpool2 expanded through mask2 while staged, the transposed

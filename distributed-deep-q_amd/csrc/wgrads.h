@@ -417,26 +417,38 @@ __device__ __forceinline__ void wgrads_body(const WgradSArgs& a, char* smem, int
   }
 }
 
-// two waves per SIMD (<= 256 registers): the other wave's MFMAs cover each
-// wave's row staging and LDS round trips
-template <int CIN, int COUT, int KS, int PAD, int WMAX, int DSRC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void wgrads_kernel(
-    const WgradSArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char sm_wgs[];
-  wgrads_body<CIN, COUT, KS, PAD, WMAX, DSRC>(a, sm_wgs, blockIdx.x);
-}
-
 template <int CIN, int PAD>
 inline size_t wgrads_smem_bytes(int W) {
   const size_t f = (size_t)4 * WgradSGeom<CIN, PAD>::region(W) * 2;
   return f > 4 * 16 * 64 * 4 + 0 ? f : 4 * 16 * 64 * 4;   // >= the 4-wave reduction image
 }
 
-template <int CIN, int COUT, int KS, int PAD, int WMAX, int DSRC>
-inline hipError_t launch_wgrads_w(const WgradSArgs& a, hipStream_t st) {
-  const size_t shm = wgrads_smem_bytes<CIN, PAD>(a.W);
+// Two weight gradients in one launch (conv2's and conv3's: both need only the
+// data gradient conv3's data-gradient launch wrote): blocks [0, n0) are the
+// first's, the rest the second's -- one kernel boundary fewer, and the second's
+// workgroups fill the CUs the first's tail leaves idle.  n0 is a multiple of 8,
+// so each keeps its XCD-aware decode.  LDS: the larger of the two.  Two waves
+// per SIMD (<= 256 registers): the other wave's MFMAs cover each wave's row
+// staging and LDS round trips.
+template <int CIN0, int COUT0, int KS0, int PAD0, int WMAX0, int DSRC0, int CIN1, int COUT1,
+          int KS1, int PAD1, int WMAX1, int DSRC1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void wgrads_pair_kernel(
+    const WgradSArgs a0, const WgradSArgs a1, int n0) {
+  extern __shared__ __attribute__((aligned(16))) char sm_wgp[];
+  if ((int)blockIdx.x < n0)
+    wgrads_body<CIN0, COUT0, KS0, PAD0, WMAX0, DSRC0>(a0, sm_wgp, blockIdx.x);
+  else
+    wgrads_body<CIN1, COUT1, KS1, PAD1, WMAX1, DSRC1>(a1, sm_wgp, blockIdx.x - n0);
+}
+
+template <int CIN0, int COUT0, int KS0, int PAD0, int WMAX0, int DSRC0, int CIN1, int COUT1,
+          int KS1, int PAD1, int WMAX1, int DSRC1>
+inline hipError_t launch_wgrads_pair_w(const WgradSArgs& a0, const WgradSArgs& a1, hipStream_t st) {
+  const size_t s0 = wgrads_smem_bytes<CIN0, PAD0>(a0.W), s1 = wgrads_smem_bytes<CIN1, PAD1>(a1.W);
+  const size_t shm = s0 > s1 ? s0 : s1;
   if (shm > 160 * 1024) return hipErrorInvalidValue;
-  auto kern = wgrads_kernel<CIN, COUT, KS, PAD, WMAX, DSRC>;
+  auto kern = wgrads_pair_kernel<CIN0, COUT0, KS0, PAD0, WMAX0, DSRC0, CIN1, COUT1, KS1, PAD1,
+                                 WMAX1, DSRC1>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -444,18 +456,19 @@ inline hipError_t launch_wgrads_w(const WgradSArgs& a, hipStream_t st) {
     if (e != hipSuccess) return e;
     attr = true;
   }
-  const int g8 = (a.G + 7) / 8 * 8;
-  hipLaunchKernelGGL(kern, dim3(g8 * (COUT / 32) * KS), dim3(256), shm, st, a);
+  const int n0 = (a0.G + 7) / 8 * 8 * (COUT0 / 32) * KS0;
+  const int n1 = (a1.G + 7) / 8 * 8 * (COUT1 / 32) * KS1;
+  hipLaunchKernelGGL(kern, dim3(n0 + n1), dim3(256), shm, st, a0, a1, n0);
   return hipGetLastError();
 }
 
-// the staging registers are sized for the widest row the instance takes
-template <int CIN, int COUT, int KS, int PAD, int DSRC = 0>
-inline hipError_t launch_wgrads(const WgradSArgs& a, hipStream_t st) {
-  if (a.W <= 16) return launch_wgrads_w<CIN, COUT, KS, PAD, 16, DSRC>(a, st);
-  if (a.W <= 32) return launch_wgrads_w<CIN, COUT, KS, PAD, 32, DSRC>(a, st);
-  if (a.W <= 64) return launch_wgrads_w<CIN, COUT, KS, PAD, 64, DSRC>(a, st);
-  return hipErrorInvalidValue;   // frames > 128 (conv2) / 256 (conv3): not supported
+// conv2's (on the split pooled dpool2) + conv3's (on the expanded split
+// dconv3); the staging registers are sized for the widest row of each
+inline hipError_t launch_wgrads_conv23(const WgradSArgs& a2, const WgradSArgs& a3, hipStream_t st) {
+  if (a2.W <= 16) return launch_wgrads_pair_w<32, 64, 5, 2, 16, 0, 64, 64, 3, 1, 16, 2>(a2, a3, st);
+  if (a2.W <= 32) return launch_wgrads_pair_w<32, 64, 5, 2, 32, 0, 64, 64, 3, 1, 16, 2>(a2, a3, st);
+  if (a2.W <= 64) return launch_wgrads_pair_w<32, 64, 5, 2, 64, 0, 64, 64, 3, 1, 32, 2>(a2, a3, st);
+  return hipErrorInvalidValue;   // frames > 128: not supported
 }
 
 }  // namespace ddq

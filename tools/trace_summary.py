@@ -12,19 +12,15 @@ import statistics
 import sys
 
 SHORT = [("sample_gather_kernel", "sample"), ("split_conv1_kernel", "c1f"),
-         ("split_conv_kernel<32, 32, 64, 5", "c2f"),
-         ("split_conv_kernel<64, 64, 64, 3, 8, 8, 2, 2,", "c3f"),
-         ("split_conv_kernel<64, 64, 64, 3, 4, 8,", "c3d"),
-         ("split_conv_kernel<64, 64, 32, 5", "c2d"),
+         ("c2f", "c2f"), ("c3f", "c3f"), ("c3d", "c3d"), ("c2d", "c2d"),
+         ("wgrads_pair_kernel", "c23w"),
          ("wgrads_kernel<64, 64, 3", "c3w"), ("wgrads_kernel<32, 64, 5", "c2w"),
          ("wgrad1s_kernel", "c1w"),
-         ("direct_conv_kernel<4, 32, 7", "c1f"),
-         ("direct_conv_kernel<32, 64, 5", "c2f"), ("direct_conv_kernel<64, 64, 3, 8, 8, 2, 2, false", "c3f"),
-         ("fc4_fwd_direct", "fc4f"), ("fc4_fwd_split", "fc4f"), ("fc4_head", "head"), ("fc4_dgrad_direct", "fc4d"),
-         ("fc4_bwd_kernel", "fc4bwd"), ("FcWgrad", "fc4w"), ("wgradd_kernel<64, 64, 3", "c3w"),
-         ("direct_conv_kernel<64, 64, 3, 8, 8, 2, 2, true", "c3d"), ("wgradd_kernel<32, 64, 5", "c2w"),
-         ("direct_conv_kernel<64, 32, 5", "c2d"), ("wgrad1_kernel", "c1w"),
+         ("fc4_fwd_split", "fc4f"), ("fc4_head", "head"), ("fc4_bwd_kernel", "fc4bwd"),
          ("wgrad_reduce_kernel", "wred"), ("apply_kernel", "apply")]
+# split_conv_kernel<CPT, CP, N, KS, ..., DGRAD>: any tile of the per-map menus
+SPLIT = {(32, 64, 5, "false"): "c2f", (64, 64, 3, "false"): "c3f", (64, 64, 3, "true"): "c3d",
+         (64, 32, 5, "true"): "c2d"}
 
 
 def main():
@@ -34,12 +30,9 @@ def main():
     per = collections.defaultdict(list)
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
-        m = re.search(r"direct_conv_kernel<(\d+), (\d+), (\d+),.*?(true|false), (true|false)", name)
-        if m:   # any tile config: classify by (CP, N, KS, DGRAD)
-            cp, n, ks, dg = int(m.group(1)), int(m.group(2)), int(m.group(3)), m.group(4) == "true"
-            short = {(4, 32, 7): "c1f", (32, 64, 5): "c2f", (64, 32, 5): "c2d"}.get((cp, n, ks))
-            if ks == 3:
-                short = "c3d" if dg else "c3f"
+        m = re.search(r"split_conv_kernel<(\d+), \d+, (\d+), (\d+),.*(true|false)>", name)
+        if m:
+            short = SPLIT.get((int(m.group(1)), int(m.group(2)), int(m.group(3)), m.group(4)))
             if short:
                 per[short].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
             continue
