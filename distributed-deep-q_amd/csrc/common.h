@@ -12,6 +12,27 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #ifndef DDQ_AB_SKIP
 #define DDQ_AB_SKIP 0
 #endif
+// A/B: force a conv tile-menu entry (kernels.hip pick_tile), -1 = the cost model's
+#ifndef DDQ_AB_TILE_C1F
+#define DDQ_AB_TILE_C1F -1
+#endif
+#ifndef DDQ_AB_TILE_C2F
+#define DDQ_AB_TILE_C2F -1
+#endif
+#ifndef DDQ_AB_TILE_C3F
+#define DDQ_AB_TILE_C3F -1
+#endif
+#ifndef DDQ_AB_TILE_C3D
+#define DDQ_AB_TILE_C3D -1
+#endif
+#ifndef DDQ_AB_TILE_C2D
+#define DDQ_AB_TILE_C2D -1
+#endif
+// conv2 forward as the persistent pipelined kernel (split.h
+// split_conv_pipe_body) on maps whose side is a multiple of 16
+#ifndef DDQ_CONV2_PIPE
+#define DDQ_CONV2_PIPE 0
+#endif
 
 namespace ddq {
 

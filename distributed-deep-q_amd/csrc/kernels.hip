@@ -1471,7 +1471,8 @@ template <int TY, int TX, int WM>
 constexpr TileOpt conv1_tile() { return {TY, TX, WM * Conv1Cfg<TY, TX, WM>::TM * 32}; }
 
 template <class T, int n>
-static const T& pick_tile(const T (&menu)[n], int H, int W) {
+static const T& pick_tile(const T (&menu)[n], int H, int W, int force = -1) {
+  if (force >= 0 && force < n) return menu[force];   // A/B: DDQ_AB_TILE_*
   auto cost = [&](const TileOpt& o) {
     return (int64_t)((H + o.ty - 1) / o.ty) * ((W + o.tx - 1) / o.tx) * (o.rows + 32);
   };
@@ -1602,7 +1603,7 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     c1.out_elems = (int64_t)B * (S / 2) * (S / 2) * 32;
     c1.mask[0] = nb.mask1; c1.mask[1] = nullptr;
     M("conv1_fwd");
-    CHECK_LAUNCH(pick_tile(kConv1Fwd, S, S).launch(c1, nz, s, L.wks_total));
+    CHECK_LAUNCH(pick_tile(kConv1Fwd, S, S, DDQ_AB_TILE_C1F).launch(c1, nz, s, L.wks_total));
   }
   if (!nb.fwd_only || nb.fwd_only == 2) {
     // conv2 (train_val.prototxt:79-118): split bf16, 16x16 tiles, 16 waves of
@@ -1622,7 +1623,10 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     a2.out_elems = (int64_t)B * (H / 2) * (H / 2) * 64;
     a2.mask[0] = nb.mask2; a2.mask[1] = nullptr;
     M("conv2_fwd");
-    CHECK_LAUNCH(pick_tile(kConv2Fwd, H, H).launch(a2, nz, s));
+    if (DDQ_CONV2_PIPE && H % 8 == 0 && H % 16 == 0)
+      CHECK_LAUNCH((launch_split_conv_pipe<32, 64, 5, 8, 16, 4, 2>(a2, nz, s)));
+    else
+      CHECK_LAUNCH(pick_tile(kConv2Fwd, H, H, DDQ_AB_TILE_C2F).launch(a2, nz, s));
   }
   if (!nb.fwd_only || nb.fwd_only == 3) {
     // conv3 (train_val.prototxt:119-158): split bf16, 8x8 tiles (kConv3Fwd), two k groups
@@ -1642,7 +1646,7 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     a3.nchw = 1;
     a3.mask[0] = nb.mask3; a3.mask[1] = nullptr;
     M("conv3_fwd");
-    CHECK_LAUNCH(pick_tile(kConv3Fwd, H, H).launch(a3, nz, s));
+    CHECK_LAUNCH(pick_tile(kConv3Fwd, H, H, DDQ_AB_TILE_C3F).launch(a3, nz, s));
   }
   if (nb.fwd_only) return hipSuccess;   // ddq_time_layer: one conv layer
   // fc4 (train_val.prototxt:159-185): split bf16 MFMA register-direct, split-K
@@ -1703,7 +1707,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     a.pd_split = nb.dconv2s; a.pd_elems = (int64_t)B * H * H * 64;
     a.xsplit = nb.dconv3s; a.x_elems = (int64_t)B * H * H * 64;
     M("conv3_dgrad");
-    CHECK_LAUNCH(pick_tile(kConv3Dgrad, H, H).launch(a, 1, s));
+    CHECK_LAUNCH(pick_tile(kConv3Dgrad, H, H, DDQ_AB_TILE_C3D).launch(a, 1, s));
   }
   {  // conv3 weight gradient (split bf16, wgrads.h): rows of the expanded split
      // dconv3 (pure copies) against the split pool2; conv2's on the split
@@ -1737,7 +1741,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     a.in_route = nb.mask2;
     a.pd_split = nb.dconv1s; a.pd_elems = (int64_t)B * H * H * 32;
     M("conv2_dgrad");
-    CHECK_LAUNCH(pick_tile(kConv2Dgrad, H, H).launch(a, 1, s));
+    CHECK_LAUNCH(pick_tile(kConv2Dgrad, H, H, DDQ_AB_TILE_C2D).launch(a, 1, s));
   }
   // slab-reduce geometry: layer l's blocks start at d[l].blk0
   WredDims d[3];

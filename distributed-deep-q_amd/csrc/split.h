@@ -721,6 +721,256 @@ inline hipError_t launch_split_conv(SplitArgs a, int nz, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------------------
+// Persistent, software-pipelined forward convolution (one channel chunk,
+// CPT == CP).  The one-round launch above stages its halo patch with nothing
+// to overlap it (every CU loads at once, then computes) and stores its pooled
+// outputs at the end (every CU stores at once).  Here a workgroup per CU slot
+// loops over tiles t = blockIdx.x, +gridDim.x, ... with two patch buffers:
+//  * the next tile's patch is loaded into registers when a tile starts and
+//    committed to the other buffer at tap kCommit (the buffer's last reader,
+//    the previous tile's epilogue, finished before that tile's last barrier);
+//  * a tile's epilogue gathers its pooled outputs in its own patch buffer and
+//    stores them while the next tile's first taps run;
+//  * the weight ring runs on the global step g = (local tile li, tap g % T):
+//    slot g & 1, tower of tile li, so tile boundaries cost no ring refill.
+// Tiles are numbered tower-major ((z, b, ty, tx)), so the tower of local tile
+// li is just blockIdx.x + li * gridDim.x >= tiles per tower.  Per output
+// element the accumulation order (tap, k-step, the six products) is that of
+// split_conv_body: the outputs are bit-identical.
+// ---------------------------------------------------------------------------
+template <int CPT, int N, int KS, int TY, int TX, int WM, int WN>
+struct SplitPipeCfg {
+  using C = SplitCfg<CPT, CPT, N, KS, TY, TX, WM, WN, 1>;
+  static constexpr int kSmemB = 2 * C::kPatchB + C::kWB;
+  static constexpr int kCommit = C::T / 2;   // tap at which the next patch is stored
+  static_assert(kSmemB <= 160 * 1024, "LDS budget (two patch buffers + ring)");
+  static_assert(C::NWIN * N * 7 <= C::kPatchB, "epilogue gather fits a patch buffer");
+};
+
+template <int CPT, int N, int KS, int TY, int TX, int WM, int WN>
+__device__ __forceinline__ void split_conv_pipe_body(const SplitArgs& a, char* smem, int ntiles,
+                                                     int tpi, int tpt) {
+  using P = SplitPipeCfg<CPT, N, KS, TY, TX, WM, WN>;
+  using C = typename P::C;
+  constexpr int TM = C::TM, TN = C::TN, T = C::T;
+  constexpr int kPB = C::kPatchB / 2;                     // bf16 per patch buffer
+  __bf16* const patch0 = reinterpret_cast<__bf16*>(smem);
+  __bf16* const wbuf = reinterpret_cast<__bf16*>(smem + 2 * C::kPatchB);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int l31 = lane & 31, h = lane >> 5;
+  const int G = gridDim.x, bx = blockIdx.x;
+  const int nmine = bx < ntiles ? (ntiles - 1 - bx) / G + 1 : 0;
+  if (nmine == 0) return;
+  const int nstep = nmine * T;
+  auto tower = [&](int li) { return bx + li * G >= tpt ? 1 : 0; };
+  // (b, y0, x0) of local tile li (runtime divisions: once per tile)
+  auto coords = [&](int li, int& b, int& y0, int& x0) {
+    int t = bx + li * G;
+    if (t >= tpt) t -= tpt;
+    b = t / tpi;
+    const int r = t - b * tpi;
+    const int ty = r / a.tiles_x;
+    y0 = ty * TY;
+    x0 = (r - ty * a.tiles_x) * TX;
+  };
+
+  // ---- halo patch of a tile: bounds-checked buffer loads into registers ----
+  constexpr uint32_t kOOB = 0x80000000u;
+  const uint32_t src_bytes = (uint32_t)(a.B * a.H * a.W * CPT) * 2u;
+  constexpr int NV = C::PH * C::PW * (CPT / 8);           // 16-byte vectors per plane
+  constexpr int NIT = (NV + C::kThreads - 1) / C::kThreads;
+  u32x4 pv[3][NIT];
+  int pdst[NIT];
+  auto patch_issue = [&](int li) {
+    const bool live = li < nmine;
+    int b = 0, y0 = 0, x0 = 0;
+    if (live) coords(li, b, y0, x0);
+    const __bf16* in = (live && tower(li)) ? a.in[1] : a.in[0];
+#pragma unroll
+    for (int u = 0; u < NIT; ++u) {
+      const int f0 = tid + u * C::kThreads;
+      const bool ok = live && f0 < NV;
+      const int f = ok ? f0 : 0;
+      const int pix = f / (CPT / 8), c8 = f % (CPT / 8);
+      const int py = pix / C::PW, px = pix % C::PW;
+      const int gy = y0 - a.pad + py, gx = x0 - a.pad + px;
+      const bool in_img = ok && (unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W;
+      pdst[u] = ok ? py * C::RS + px * C::CS + 8 * c8 : -1;
+      const uint32_t o = in_img ? (uint32_t)(((b * a.H + gy) * a.W + gx) * CPT + 8 * c8) * 2u : kOOB;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(in + p * a.in_elems), (short)0, (int)src_bytes, 0x00020000);
+        pv[p][u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o, 0, 0));
+      }
+    }
+  };
+  auto patch_commit = [&](int li) {
+    __bf16* buf = patch0 + (li & 1) * kPB;
+#pragma unroll
+    for (int u = 0; u < NIT; ++u)
+      if (pdst[u] >= 0)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) *reinterpret_cast<u32x4*>(buf + p * C::kPlane + pdst[u]) = pv[p][u];
+  };
+
+  // ---- weights of global step g (tile g / T, tap g % T), clamped ----
+  SplitWStage<C, CPT, CPT, N> ws0, ws1;
+  auto wload = [&](SplitWStage<C, CPT, CPT, N>& w, int g) {
+    const int gc = g < nstep ? g : nstep - 1;
+    const int li = gc / T;
+    w.load(tower(li) ? a.wk[1] : a.wk[0], a.wk_elems, 0, gc - li * T, tid);
+  };
+
+  // ---- per-lane operand offsets (split_conv_body, one k group) ----
+  const int wmi = wid / WN, wni = wid % WN;
+  int abase[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = wmi * TM * 32 + 32 * i + l31;
+    const int win = (m >> 2) < C::NWIN ? m >> 2 : 0, dy = (m >> 1) & 1, dx = m & 1;
+    const int wy = win / (TX / 2), wx = win % (TX / 2);
+    abase[i] = (2 * wy + dy) * C::RS + (2 * wx + dx) * C::CS + h * 8;
+  }
+  int bbase[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) bbase[j] = (wni * TN * 32 + 32 * j + l31) * C::CW + h * 8;
+  float bpre[TN];
+  auto bias_load = [&](int li) {
+    const float* bz = tower(li < nmine ? li : 0) ? a.bias[1] : a.bias[0];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bpre[j] = bz[wni * TN * 32 + 32 * j + l31];
+  };
+
+  f32x16 acc[TM][TN], cor[TM][TN];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; cor[i][j][r] = 0.f; }
+  };
+  auto tap_step = [&](int t, const __bf16* patch, int slot) {
+    const __bf16* wb = wbuf + slot * 3 * C::kWSlot;
+    const int ky = t / KS, kx = t % KS;
+    const __bf16* pa = patch + ky * C::RS + kx * C::CS;
+#pragma unroll
+    for (int g = 0; g < C::KSTEP; ++g) {
+      bf16x8 av[3][TM], bv[3][TN];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          av[p][i] = *reinterpret_cast<const bf16x8*>(pa + p * C::kPlane + abase[i] + 16 * g);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          bv[p][j] = *reinterpret_cast<const bf16x8*>(wb + p * C::kWSlot + bbase[j] + 16 * g);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2][i], bv[0][j], cor[i][j], 0, 0, 0);
+          cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[1][j], cor[i][j], 0, 0, 0);
+          cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[2][j], cor[i][j], 0, 0, 0);
+          cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[0][j], cor[i][j], 0, 0, 0);
+          cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[1][j], cor[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[0][j], acc[i][j], 0, 0, 0);
+        }
+    }
+  };
+  // one global step: the MFMAs of (tile li, tap t) from ring slot g & 1; at
+  // tap kCommit the next tile's patch goes to the other buffer; at the last
+  // tap the epilogue (LDS gather in this tile's buffer, 16-byte stores), the
+  // next-next tile's patch loads and the next tile's bias; then the ring slot
+  // of step g + 1 and the step's barrier.
+  auto step = [&](int g, SplitWStage<C, CPT, CPT, N>& wnext) {
+    const int li = g / T, t = g - li * T;
+    __bf16* const patch = patch0 + (li & 1) * kPB;
+    tap_step(t, patch, g & 1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (t == P::kCommit && li + 1 < nmine) patch_commit(li + 1);
+    if (t == T - 1) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] += cor[i][j];
+      int b, y0, x0;
+      coords(li, b, y0, x0);
+      split_epilogue_fwd_lds<TM, TN, TX, N, 1, C::NWIN, C::kThreads>(
+          a, acc, bpre, reinterpret_cast<char*>(patch), b, tower(li), y0, x0, wmi, wni, l31, h, 0,
+          tid);
+      zero_acc();
+      if (li + 2 < nmine) patch_issue(li + 2);
+      bias_load(li + 1);
+    }
+    if (g + 1 < nstep) {
+      wnext.store(wbuf + ((g + 1) & 1) * 3 * C::kWSlot, tid);
+      __syncthreads();
+    }
+  };
+
+  // prologue: tile 0's patch and bias, ring slot 0, step 1's weights, tile 1's patch loads
+  patch_issue(0);
+  patch_commit(0);
+  bias_load(0);
+  wload(ws0, 0);
+  ws0.store(wbuf, tid);
+  if (nstep > 1) wload(ws1, 1);
+  patch_issue(1);
+  zero_acc();
+  __syncthreads();
+  for (int g = 0; g < nstep; g += 2) {
+    if (g + 2 < nstep) {
+      wload(ws0, g + 2);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    step(g, ws1);
+    if (g + 1 >= nstep) break;
+    if (g + 3 < nstep) {
+      wload(ws1, g + 3);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    step(g + 1, ws0);
+  }
+}
+
+template <int CPT, int N, int KS, int TY, int TX, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void split_conv_pipe_kernel(const SplitArgs a, int ntiles,
+                                                                       int tpi, int tpt) {
+  extern __shared__ __attribute__((aligned(16))) char sm_pipe[];
+  split_conv_pipe_body<CPT, N, KS, TY, TX, WM, WN>(a, sm_pipe, ntiles, tpi, tpt);
+}
+
+// grid: one workgroup per CU (the two patch buffers take the LDS), at most
+// one per tile
+template <int CPT, int N, int KS, int TY, int TX, int WM, int WN>
+inline hipError_t launch_split_conv_pipe(SplitArgs a, int nz, hipStream_t st) {
+  using P = SplitPipeCfg<CPT, N, KS, TY, TX, WM, WN>;
+  auto kern = split_conv_pipe_kernel<CPT, N, KS, TY, TX, WM, WN>;
+  static int ncu = 0;
+  if (!ncu) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, P::kSmemB);
+    if (e != hipSuccess) return e;
+    int dev = 0;
+    if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+    int n = 0;
+    if ((e = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
+      return e;
+    ncu = n > 0 ? n : 256;
+  }
+  if ((a.out[0] && a.out_split[0]) || (a.out[1] && a.out_split[1])) return hipErrorInvalidValue;
+  a.tiles_x = (a.W + TX - 1) / TX;
+  const int tiles_y = (a.H + TY - 1) / TY;
+  const int tpi = tiles_y * a.tiles_x, tpt = tpi * a.B, ntiles = tpt * nz;
+  const int grid = ntiles < ncu ? ntiles : ncu;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(P::C::kThreads), P::kSmemB, st, a, ntiles, tpi, tpt);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // conv1 (4 -> 32 channels, 7x7, pad 3) on the bf16 matrix cores.  Its input
 // is the replay frames: integers 0..255, exact in bf16, so A has ONE plane
 // and a product needs only three MFMAs (a.b0, a.b1, a.b2).  K of a kernel row
