@@ -33,6 +33,11 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #ifndef DDQ_CONV2_PIPE
 #define DDQ_CONV2_PIPE 0
 #endif
+// conv1 forward as the persistent pipelined kernel (split.h
+// split_conv1_pipe_kernel, 16 x 16 tiles) on frames whose side is a multiple of 16
+#ifndef DDQ_CONV1_PIPE
+#define DDQ_CONV1_PIPE 0
+#endif
 
 namespace ddq {
 

@@ -1603,7 +1603,10 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     c1.out_elems = (int64_t)B * (S / 2) * (S / 2) * 32;
     c1.mask[0] = nb.mask1; c1.mask[1] = nullptr;
     M("conv1_fwd");
-    CHECK_LAUNCH(pick_tile(kConv1Fwd, S, S, DDQ_AB_TILE_C1F).launch(c1, nz, s, L.wks_total));
+    if (DDQ_CONV1_PIPE && S % 16 == 0)
+      CHECK_LAUNCH((launch_split_conv1_pipe<16, 16, 8>(c1, nz, s, L.wks_total)));
+    else
+      CHECK_LAUNCH(pick_tile(kConv1Fwd, S, S, DDQ_AB_TILE_C1F).launch(c1, nz, s, L.wks_total));
   }
   if (!nb.fwd_only || nb.fwd_only == 2) {
     // conv2 (train_val.prototxt:79-118): split bf16, 16x16 tiles, 16 waves of

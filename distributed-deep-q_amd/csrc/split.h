@@ -1131,6 +1131,204 @@ __global__ __launch_bounds__(64 * WM) void split_conv1_kernel(const Conv1Args a)
     split_epilogue<TM, 1, TX, 32, false, 1, C::NWIN>(e, acc, bpre, b, z, y0, x0, wid, 0, l31, h);
 }
 
+// Persistent pipelined conv1 (split_conv_pipe_body's scheme): a workgroup
+// keeps the split weights of its tower resident, owns a contiguous run of
+// tiles (tower-major numbering: at most one weight restage per workgroup),
+// loads the next tile's frames into registers while a tile computes, commits
+// them to the other patch buffer after tap row 3, and gathers / stores its
+// pooled outputs from a buffer of their own while the next tile computes.
+template <int TY, int TX, int WM>
+struct Conv1PipeCfg {
+  using C = Conv1Cfg<TY, TX, WM>;
+  static constexpr int kGatherB = C::NWIN * 32 * 7;
+  static constexpr int kSmemB = C::kWB + 2 * C::kPatchB + kGatherB;
+  static_assert(kSmemB <= 160 * 1024, "LDS");
+};
+
+template <int TY, int TX, int WM>
+__global__ __launch_bounds__(64 * WM) __attribute__((amdgpu_waves_per_eu(4))) void split_conv1_pipe_kernel(const Conv1Args a, int ntiles,
+                                                                   int per, int tpi, int tpt) {
+  using P = Conv1PipeCfg<TY, TX, WM>;
+  using C = typename P::C;
+  constexpr int TM = C::TM;
+  constexpr int kThreads = 64 * WM;
+  extern __shared__ __attribute__((aligned(16))) char sm_c1p[];
+  __bf16* const wbuf = reinterpret_cast<__bf16*>(sm_c1p);
+  __bf16* const patch0 = reinterpret_cast<__bf16*>(sm_c1p + C::kWB);
+  char* const gather = sm_c1p + C::kWB + 2 * C::kPatchB;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int l31 = lane & 31, h = lane >> 5;
+  const int t0 = blockIdx.x * per;
+  const int nmine = ntiles - t0 < per ? ntiles - t0 : per;
+  if (nmine <= 0) return;
+  auto coords = [&](int li, int& z, int& b, int& y0, int& x0) {
+    int t = t0 + li;
+    z = t >= tpt ? 1 : 0;
+    if (z) t -= tpt;
+    b = t / tpi;
+    const int r = t - b * tpi;
+    const int ty = r / a.tiles_x;
+    y0 = ty * TY;
+    x0 = (r - ty * a.tiles_x) * TX;
+  };
+  // frames of a tile: one pixel (4 channels, fp32 -> exact bf16) per item
+  constexpr int NP = C::PH * C::PW;
+  constexpr int NIT = (NP + kThreads - 1) / kThreads;
+  float4 pv[NIT];
+  auto patch_issue = [&](int li) {
+    const bool live = li < nmine;
+    int z = 0, b = 0, y0 = 0, x0 = 0;
+    if (live) coords(li, z, b, y0, x0);
+    const float* __restrict__ in = z ? a.in[1] : a.in[0];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int f = tid + it * kThreads;
+      const int py = f / C::PW, px = f % C::PW;
+      const int gy = y0 - 3 + py, gx = x0 - 3 + px;
+      pv[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (live && f < NP && px < TX + 6 && (unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W)
+        pv[it] = *reinterpret_cast<const float4*>(in + (((size_t)b * a.H + gy) * a.W + gx) * 4);
+    }
+  };
+  auto patch_commit = [&](int li) {
+    __bf16* const patch = patch0 + (li & 1) * (C::kPatchB / 2);
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int f = tid + it * kThreads;
+      if (f < NP) {
+        const int py = f / C::PW, px = f % C::PW;
+        __bf16 q[4] = {(__bf16)pv[it].x, (__bf16)pv[it].y, (__bf16)pv[it].z, (__bf16)pv[it].w};
+        *reinterpret_cast<uint2*>(patch + py * C::RS + px * 4) = *reinterpret_cast<uint2*>(q);
+      }
+    }
+  };
+  auto stage_weights = [&](int z) {
+    const __bf16* __restrict__ wk = z ? a.wk[1] : a.wk[0];
+    constexpr int NW = 3 * kConv1WPlane / 8;
+    constexpr int WIT = (NW + kThreads - 1) / kThreads;
+    u32x4 w[WIT];
+#pragma unroll
+    for (int it = 0; it < WIT; ++it) {
+      const int f0 = tid + it * kThreads;
+      const int f = f0 < NW ? f0 : NW - 1;
+      const int p = f / (kConv1WPlane / 8), r = f % (kConv1WPlane / 8);
+      w[it] = *reinterpret_cast<const u32x4*>(wk + p * a.wk_elems + 8 * (size_t)r);
+    }
+#pragma unroll
+    for (int it = 0; it < WIT; ++it) {
+      const int f0 = tid + it * kThreads;
+      const int f = f0 < NW ? f0 : NW - 1;
+      const int p = f / (kConv1WPlane / 8), r = f % (kConv1WPlane / 8);
+      const int n = r / 28, q8 = r % 28;
+      *reinterpret_cast<u32x4*>(wbuf + (p * 32 + n) * C::CW + 8 * q8) = w[it];
+    }
+  };
+  int abase[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = wid * TM * 32 + 32 * i + l31;
+    const int win = (m >> 2) < C::NWIN ? m >> 2 : 0, dy = (m >> 1) & 1, dx = m & 1;
+    const int wy = win / (TX / 2), wx = win % (TX / 2);
+    abase[i] = (2 * wy + dy) * C::RS + (2 * wx + dx + 2 * h) * 4;
+  }
+  const int bbase = l31 * C::CW + h * 8;
+  SplitArgs e{};
+  e.B = a.B; e.H = a.H; e.W = a.W;
+  e.out[0] = a.out[0]; e.out[1] = a.out[1];
+  e.out_split[0] = a.out_split[0]; e.out_split[1] = a.out_split[1];
+  e.out_elems = a.out_elems;
+  e.mask[0] = a.mask[0]; e.mask[1] = a.mask[1];
+
+  int zc, bq, yq, xq;
+  coords(0, zc, bq, yq, xq);
+  patch_issue(0);
+  stage_weights(zc);
+  patch_commit(0);
+  patch_issue(1);
+  __syncthreads();
+  for (int li = 0; li < nmine; ++li) {
+    int z, b, y0, x0;
+    coords(li, z, b, y0, x0);
+    if (z != zc) {   // tower change (once at most): the epilogue's barriers fenced every reader
+      stage_weights(z);
+      __syncthreads();
+      zc = z;
+    }
+    const float bpre[1] = {(z ? a.bias[1] : a.bias[0])[l31]};
+    const __bf16* const patch = patch0 + (li & 1) * (C::kPatchB / 2);
+    f32x16 acc[TM][1], cor[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { acc[i][0][r] = 0.f; cor[i][r] = 0.f; }
+#pragma unroll
+    for (int ky = 0; ky < 7; ++ky) {
+      if (ky == 4 && li + 1 < nmine) {   // the next tile's frames (their loads have landed)
+        __builtin_amdgcn_sched_barrier(0);
+        patch_commit(li + 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        bf16x8 bv[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          bv[p] = *reinterpret_cast<const bf16x8*>(wbuf + p * 32 * C::CW + bbase + ky * 32 + 16 * g);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const __bf16* pa = patch + abase[i] + ky * C::RS + 16 * g;
+          typedef __attribute__((address_space(3))) const u32x2 lds_u2;
+          typedef __attribute__((address_space(3))) const char lds_c;
+          lds_u2* la = (lds_u2*)pa;
+          uint32_t hi_off = 8;                       // separate ds_read_b64 (split_conv1_kernel)
+          asm volatile("" : "+v"(hi_off));
+          const u32x2 lo = *la;
+          const u32x2 hi = *(lds_u2*)((lds_c*)la + hi_off);
+          u32x4 av4 = {lo[0], lo[1], hi[0], hi[1]};
+          const bf16x8 av = *reinterpret_cast<bf16x8*>(&av4);
+          cor[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv[2], cor[i], 0, 0, 0);
+          cor[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv[1], cor[i], 0, 0, 0);
+          acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv[0], acc[i][0], 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[i][0] += cor[i];
+    // gather buffer: its previous readers (the last tile's stores) read it
+    // before that epilogue's end; the barrier at the top of this one fences
+    // every wave's patch reads of this tile as well
+    split_epilogue_fwd_lds<TM, 1, TX, 32, 1, C::NWIN, kThreads>(e, acc, bpre, gather, b, z, y0, x0,
+                                                                wid, 0, l31, h, 0, tid);
+    if (li + 2 < nmine) patch_issue(li + 2);
+  }
+}
+
+template <int TY, int TX, int WM>
+inline hipError_t launch_split_conv1_pipe(Conv1Args a, int nz, hipStream_t st, int64_t wk_elems) {
+  using P = Conv1PipeCfg<TY, TX, WM>;
+  a.wk_elems = wk_elems;
+  if ((a.out[0] && a.out_split[0]) || (a.out[1] && a.out_split[1])) return hipErrorInvalidValue;
+  auto kern = split_conv1_pipe_kernel<TY, TX, WM>;
+  static int slots = 0;
+  if (!slots) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, P::kSmemB);
+    if (e != hipSuccess) return e;
+    int dev = 0, n = 0;
+    if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+    if ((e = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
+      return e;
+    slots = (n > 0 ? n : 256) * ((160 * 1024) / P::kSmemB);   // workgroups resident at once
+  }
+  a.tiles_x = (a.W + TX - 1) / TX;
+  const int tiles_y = (a.H + TY - 1) / TY;
+  const int tpi = tiles_y * a.tiles_x, tpt = tpi * a.B, ntiles = tpt * nz;
+  const int per = (ntiles + slots - 1) / slots;
+  const int grid = (ntiles + per - 1) / per;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WM), P::kSmemB, st, a, ntiles, per, tpi, tpt);
+  return hipGetLastError();
+}
+
 template <int TY, int TX, int WM>
 inline hipError_t launch_split_conv1(Conv1Args a, int nz, hipStream_t st, int64_t wk_elems) {
   a.wk_elems = wk_elems;
