@@ -289,6 +289,7 @@ int ddq_create(ddq_ctx** out, int device, const ddq_net_desc* desc) {
     TRY(dalloc(c, &nb.opt, (size_t)P + kShardPad));
     nb.book_inc = 1;
     TRY(dalloc(c, &nb.opt_init, 4));
+    TRY(dalloc(c, &nb.chain, 4));
     TRY(dalloc(c, &nb.iter, 1));
     // acting scratch (n <= B)
     TRY(dalloc(c, &c->act_u8, (size_t)B * 4 * S * S));

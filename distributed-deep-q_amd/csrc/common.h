@@ -35,6 +35,11 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #endif
 // conv1 forward as the persistent pipelined kernel (split.h
 // split_conv1_pipe_kernel, 16 x 16 tiles) on frames whose side is a multiple of 16
+// fc4 forward, head and fc4 data gradient as one launch with intra-launch
+// hand-offs (kernels.hip fc4_chain_kernel)
+#ifndef DDQ_FC4_CHAIN
+#define DDQ_FC4_CHAIN 0
+#endif
 #ifndef DDQ_CONV1_PIPE
 #define DDQ_CONV1_PIPE 0
 #endif

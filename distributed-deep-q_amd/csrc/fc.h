@@ -29,6 +29,12 @@ __device__ __forceinline__ float4 fc_ld4(__amdgpu_buffer_rsrc_t r, uint32_t off)
   auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
   return *reinterpret_cast<float4*>(&v);
 }
+// sc1 (L2-served, L1 bypassed): bytes another workgroup of the same launch
+// stored sc1 and signalled for (fc4 chain, MI355X_MICROARCH.md hand-off table)
+__device__ __forceinline__ float4 fc_ld4_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 16);
+  return *reinterpret_cast<float4*>(&v);
+}
 __device__ __forceinline__ float fc_ld1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   auto v = __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
   return __builtin_bit_cast(float, v);
@@ -154,15 +160,22 @@ __device__ __forceinline__ void split8(const float4& lo, const float4& hi, bf16x
   }
 }
 
+// NWF waves per workgroup (32 n each: block bx covers n 32 NWF bx ..); the x
+// tile in `smem` (3 planes of BT*32 rows of XSB bf16: fc4_fwd_smem_bytes)
 template <int BT>
-__global__ __launch_bounds__(256) void fc4_fwd_split_kernel(const Fc4FwdArgs a) {
+constexpr int fc4_fwd_smem_bytes() { return 3 * BT * 32 * (kFc4KLen + 8) * 2; }
+
+template <int BT, int NWF = 4>
+__device__ __forceinline__ void fc4_fwd_split_body(const Fc4FwdArgs& a, char* smem, int bx,
+                                                   int by, int bzz) {
   constexpr int XSB = kFc4KLen + 8;     // bf16 per LDS row (272 B)
-  __shared__ __attribute__((aligned(16))) __bf16 xs[3][BT * 32 * XSB];
+  constexpr int NT = 64 * NWF;
+  __bf16 (*xs)[BT * 32 * XSB] = reinterpret_cast<__bf16 (*)[BT * 32 * XSB]>(smem);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int l31 = lane & 31, h = lane >> 5;
-  const int z = blockIdx.z % a.nz, split = blockIdx.y;
-  const int bt0 = (blockIdx.z / a.nz) * (BT * 32);
-  const int n0 = blockIdx.x * 128 + w * 32;
+  const int z = bzz % a.nz, split = by;
+  const int bt0 = (bzz / a.nz) * (BT * 32);
+  const int n0 = bx * (32 * NWF) + w * 32;
   const int K = a.K;
   const int k0 = split * kFc4KLen;
   const __amdgpu_buffer_rsrc_t rw = fc_rsrc(z ? a.w[1] : a.w[0], (uint32_t)(512 * K * 4));
@@ -176,12 +189,12 @@ __global__ __launch_bounds__(256) void fc4_fwd_split_kernel(const Fc4FwdArgs a) 
     for (int r = 0; r < 16; ++r) { acc[t][r] = 0.f; cor[t][r] = 0.f; }
 
   constexpr int kC4 = kFc4KLen / 4;
-  constexpr int NX = BT * 32 * kC4 / 256;
-  static_assert(NX * 256 == BT * 32 * kC4, "x tile / workgroup");
+  constexpr int NX = BT * 32 * kC4 / NT;
+  static_assert(NX * NT == BT * 32 * kC4, "x tile / workgroup");
   float4 xv[NX];
 #pragma unroll
   for (int it = 0; it < NX; ++it) {
-    const int f = threadIdx.x + 256 * it;
+    const int f = threadIdx.x + NT * it;
     const int r = f / kC4, c4 = f % kC4;
     const int k = k0 + 4 * c4;
     xv[it] = fc_ld4(rx, k < K ? (uint32_t)((bt0 + r) * K + k) * 4 : kFcOOB);
@@ -196,7 +209,7 @@ __global__ __launch_bounds__(256) void fc4_fwd_split_kernel(const Fc4FwdArgs a) 
   }
 #pragma unroll
   for (int it = 0; it < NX; ++it) {
-    const int f = threadIdx.x + 256 * it;
+    const int f = threadIdx.x + NT * it;
     const int o = (f / kC4) * XSB + 4 * (f % kC4);
     const float v[4] = {xv[it].x, xv[it].y, xv[it].z, xv[it].w};
     typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -234,8 +247,8 @@ __global__ __launch_bounds__(256) void fc4_fwd_split_kernel(const Fc4FwdArgs a) 
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[t], 0, 0, 0);
       }
     }
-  const __amdgpu_buffer_rsrc_t rp =
-      wt_rsrc(a.part, (uint32_t)((size_t)gridDim.y * a.nz * a.B * 512 * 4));
+  const __amdgpu_buffer_rsrc_t rp = wt_rsrc(
+      a.part, (uint32_t)((size_t)((a.K + kFc4KLen - 1) / kFc4KLen) * a.nz * a.B * 512 * 4));
   const uint32_t dbase = (uint32_t)((((size_t)(split * a.nz + z) * a.B) * 512 + n0 + l31) * 4);
 #pragma unroll
   for (int t = 0; t < BT; ++t)
@@ -244,6 +257,12 @@ __global__ __launch_bounds__(256) void fc4_fwd_split_kernel(const Fc4FwdArgs a) 
       const int b = bt0 + t * 32 + fc_acc_row(r, lane);
       if (b < a.B) wt_store(rp, dbase + (uint32_t)b * 2048, acc[t][r] + cor[t][r]);
     }
+}
+
+template <int BT>
+__global__ __launch_bounds__(256) void fc4_fwd_split_kernel(const Fc4FwdArgs a) {
+  __shared__ __attribute__((aligned(16))) char xs[fc4_fwd_smem_bytes<BT>()];
+  fc4_fwd_split_body<BT>(a, xs, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
 inline int fc4_fwd_splits(int K) { return (K + kFc4KLen - 1) / kFc4KLen; }
@@ -288,9 +307,14 @@ struct Fc4DgradArgs {
 // KCW kc columns per block (32, or 16 -- the MFMA's other 16 columns read
 // nothing and are dropped): K / 16 blocks fill the 256 CUs at 64x64, where
 // K / 32 = 128 blocks streamed W4 on half of them (1.3 TB/s).
-template <bool SPLIT, int KCW = 32>
+struct NoWait {
+  __device__ void operator()() const {}
+};
+// SC1 + wait (fc4 chain): the W4 loads are issued, then wait() (dh4 is being
+// produced by other workgroups of the launch), then the dh4 loads (sc1)
+template <bool SPLIT, int KCW = 32, bool SC1 = false, class Wait = NoWait>
 __device__ __forceinline__ void fc4_dgrad_body(const Fc4DgradArgs& a, float (*red)[1024], int bx,
-                                               int by) {
+                                               int by, const Wait& wait = Wait()) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int l31 = lane & 31, h = lane >> 5;
   const int kc0 = bx * KCW, b0 = by * 32;
@@ -305,13 +329,17 @@ __device__ __forceinline__ void fc4_dgrad_body(const Fc4DgradArgs& a, float (*re
   float4 av[2][4];
   float bv[2][16];
 #pragma unroll
-  for (int blk = 0; blk < 2; ++blk) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) av[blk][i] = fc_ld4(ra, aoff + (blk * 32 + 4 * i) * 4);
+  for (int blk = 0; blk < 2; ++blk)
 #pragma unroll
     for (int j = 0; j < 16; ++j)
       bv[blk][j] = fc_ld1(rb, bcol ? boff + (uint32_t)((blk * 32 + j) * K) * 4 : kFcOOB);
-  }
+  wait();
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      av[blk][i] = SC1 ? fc_ld4_sc1(ra, aoff + (blk * 32 + 4 * i) * 4)
+                       : fc_ld4(ra, aoff + (blk * 32 + 4 * i) * 4);
   __builtin_amdgcn_sched_barrier(0);   // keep every load ahead of the first MFMA
   f32x16 acc;
 #pragma unroll

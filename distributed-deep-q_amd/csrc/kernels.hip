@@ -604,10 +604,11 @@ __global__ __launch_bounds__(512) void fc4_reduce_out_kernel(
 // LDS, coalesced both ways.  The head is a latency-bound 32-block launch, so
 // these blocks ride for free; every step runs its head after the previous
 // apply changed the weights and before its conv data gradients.
+constexpr int kWkstSmemB = 3 * 64 * (64 + 2) * 2;   // the larger (CI = 64) tile
 template <int CI, int T>
 __device__ __forceinline__ void wkst_tap(const __bf16* __restrict__ wks, int64_t plane,
-                                         int64_t src_off, int64_t dst_off, int t) {
-  __shared__ uint16_t tile[3][64][CI + 2];
+                                         int64_t src_off, int64_t dst_off, int t, char* smem) {
+  uint16_t (*tile)[64][CI + 2] = reinterpret_cast<uint16_t (*)[64][CI + 2]>(smem);
   constexpr int E = 64 * CI;
   const uint16_t* src = reinterpret_cast<const uint16_t*>(wks) + src_off;
   uint16_t* dst = reinterpret_cast<uint16_t*>(const_cast<__bf16*>(wks)) + dst_off;
@@ -622,25 +623,82 @@ __device__ __forceinline__ void wkst_tap(const __bf16* __restrict__ wks, int64_t
   }
 }
 
-__global__ __launch_bounds__(512) void fc4_head_kernel(
-    const float* __restrict__ part, int splits, int B, float gamma,
-    const float* __restrict__ thq, const float* __restrict__ thp, int64_t b4_off, int64_t w5_off,
-    int64_t b5_off, const float* __restrict__ action, const float* __restrict__ reward,
-    const float* __restrict__ nonterm, float* __restrict__ h4q, float* __restrict__ h4p,
-    float* __restrict__ outq, float* __restrict__ outp, float* q_sa_o, float* p_sa_o,
-    float* target_o, float* __restrict__ dqbuf, float* __restrict__ lpart,
-    float* __restrict__ dh4, int32_t* latch, const int64_t* iter, int period, int inc,
-    ReplayMeta* bump, const __bf16* wks, int64_t wks_plane, int64_t wks2_off, int64_t wkst_off,
-    int64_t wks3_off, int64_t wkst3_off) {
+struct HeadArgs {
+  const float* part;
+  int splits, B;
+  float gamma;
+  const float *thq, *thp;
+  int64_t b4_off, w5_off, b5_off;
+  const float *action, *reward, *nonterm;
+  float *h4q, *h4p, *outq, *outp, *q_sa_o, *p_sa_o, *target_o, *dqbuf, *lpart, *dh4;
+  int32_t* latch;
+  const int64_t* iter;
+  int period, inc;
+  ReplayMeta* bump;
+  const __bf16* wks;
+  int64_t wks_plane, wks2_off, wkst_off, wks3_off, wkst3_off;
+};
+
+// Intra-launch hand-off (fc4 chain): the storing workgroup's bytes are all
+// sc1 stores; every wave waits for them, then one lane adds to the counter
+// (MI355X_MICROARCH.md hand-off table, first row).  The consumer polls the
+// counter with sc1 loads (one lane), the workgroup joins at a barrier, and
+// every load of the handed-off bytes is an sc1 load.  A poll that has not
+// matched after 0.2 s gives up and raises err (wrong results, no hang).
+__device__ __forceinline__ void chain_signal(int32_t* ctr) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void chain_wait(const int32_t* ctr, int target, int32_t* err) {
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+}
+
+// One head block b (SC1: chain mode -- wait() before the partials, sc1
+// partial loads and dh4 stores, then the signal on done)
+template <bool SC1 = false, class Wait = NoWait>
+__device__ __forceinline__ void head_body(const HeadArgs& H, int b, char* smem,
+                                          const Wait& wait = Wait(), int32_t* done = nullptr) {
+  const float* __restrict__ part = H.part;
+  const int splits = H.splits, B = H.B;
+  const float gamma = H.gamma;
+  const float* __restrict__ thq = H.thq;
+  const float* __restrict__ thp = H.thp;
+  const int64_t b4_off = H.b4_off, w5_off = H.w5_off, b5_off = H.b5_off;
+  const float* __restrict__ action = H.action;
+  const float* __restrict__ reward = H.reward;
+  const float* __restrict__ nonterm = H.nonterm;
+  float* __restrict__ h4q = H.h4q;
+  float* __restrict__ h4p = H.h4p;
+  float* __restrict__ outq = H.outq;
+  float* __restrict__ outp = H.outp;
+  float *q_sa_o = H.q_sa_o, *p_sa_o = H.p_sa_o, *target_o = H.target_o;
+  float* __restrict__ dqbuf = H.dqbuf;
+  float* __restrict__ lpart = H.lpart;
+  float* __restrict__ dh4 = H.dh4;
+  int32_t* latch = H.latch;
+  const int64_t* iter = H.iter;
+  const int period = H.period, inc = H.inc;
+  ReplayMeta* bump = H.bump;
   __shared__ float red[8][8];
   __shared__ float qp[8];
-  const int b = blockIdx.x, n = threadIdx.x, w = n >> 6;
+  const int n = threadIdx.x, w = n >> 6;
   if (b >= B + 25) {
-    wkst_tap<64, 9>(wks, wks_plane, wks3_off, wkst3_off, b - B - 25);
+    wkst_tap<64, 9>(H.wks, H.wks_plane, H.wks3_off, H.wkst3_off, b - B - 25, smem);
     return;
   }
   if (b >= B) {
-    wkst_tap<32, 25>(wks, wks_plane, wks2_off, wkst_off, b - B);
+    wkst_tap<32, 25>(H.wks, H.wks_plane, H.wks2_off, H.wkst_off, b - B, smem);
     return;
   }
   // fused apply: latch the step's apply flags now (the values apply_book
@@ -671,18 +729,29 @@ __global__ __launch_bounds__(512) void fc4_head_kernel(
 #pragma unroll
   for (int a = 0; a < 4; ++a) acv[a] = action[b * 4 + a];
   const float ntb = nonterm[b], rwb = reward[b];
+  wait();
   // split-K partial sums of both towers, summed in split order
   float acc2[2] = {0.f, 0.f};
   {
     const float* p0 = part + (size_t)b * kFc4 + n;
     const float* p1 = part + ((size_t)B + b) * kFc4 + n;
+    const __amdgpu_buffer_rsrc_t rpt =
+        __builtin_amdgcn_make_buffer_rsrc((void*)part, (short)0, (int)(splits * stride * 4), 0x00020000);
+    const uint32_t o0 = (uint32_t)((size_t)b * kFc4 + n) * 4, o1 = (uint32_t)(((size_t)B + b) * kFc4 + n) * 4;
     for (int s = 0; s < splits; s += 32) {
       float v[2][32];
 #pragma unroll
       for (int u = 0; u < 32; ++u) {           // clamped, unconditional loads
         const int su = min(s + u, splits - 1);
-        v[0][u] = p0[su * stride];
-        v[1][u] = p1[su * stride];
+        if (SC1) {
+          v[0][u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                  rpt, (int)(o0 + (uint32_t)(su * stride) * 4), 0, 16));
+          v[1][u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                  rpt, (int)(o1 + (uint32_t)(su * stride) * 4), 0, 16));
+        } else {
+          v[0][u] = p0[su * stride];
+          v[1][u] = p1[su * stride];
+        }
       }
 #pragma unroll
       for (int u = 0; u < 32; ++u) {
@@ -739,7 +808,18 @@ __global__ __launch_bounds__(512) void fc4_head_kernel(
     for (int a = 0; a < 4; ++a) dqbuf[b * 4 + a] = dq[a];
   }
   const float v = dq[0] * w5v[0][0] + dq[1] * w5v[0][1] + dq[2] * w5v[0][2] + dq[3] * w5v[0][3];
-  dh4[(size_t)b * kFc4 + n] = h[0] > 0.f ? v : 0.f;              // ReLU backward
+  const float dv = h[0] > 0.f ? v : 0.f;                         // ReLU backward
+  if (SC1) {
+    wt_store(wt_rsrc(dh4, (uint32_t)((size_t)B * kFc4 * 4)), (uint32_t)((size_t)b * kFc4 + n) * 4, dv);
+    chain_signal(done);
+  } else {
+    dh4[(size_t)b * kFc4 + n] = dv;
+  }
+}
+
+__global__ __launch_bounds__(512) void fc4_head_kernel(const HeadArgs H) {
+  __shared__ __attribute__((aligned(16))) char smem[kWkstSmemB];
+  head_body(H, blockIdx.x, smem);
 }
 
 // Cross-sample head sums, run by the 8 trailing blocks of the wgrad slab
@@ -924,15 +1004,115 @@ __device__ __forceinline__ void head_sums(int hb, int B, const float* __restrict
   }
 }
 
-hipError_t launch_head(const NetBuffers& nb, hipStream_t s, ReplayMeta* bump) {
+static HeadArgs head_args(const NetBuffers& nb, ReplayMeta* bump) {
   const ParamLayout& L = nb.L;
-  hipLaunchKernelGGL(fc4_head_kernel, dim3(nb.B + 25 + 9), dim3(kFc4), 0, s, nb.fc4_part, nb.fc4_splits,
-                     nb.B, nb.gamma, nb.theta[0], nb.theta[1], L.b[3], L.w[4], L.b[4], nb.action,
-                     nb.reward, nb.nonterm, nb.h4[0], nb.h4[1], nb.q_out, nb.p_out, nb.q_sa,
-                     nb.p_sa, nb.target, nb.dqbuf, nb.lpart, nb.dh4,
-                     nb.fa.on ? nb.opt_init : nullptr, nb.iter, nb.fa.period, nb.book_inc,
-                     nb.fa.on ? bump : nullptr, nb.wks[0], L.wks_total, L.wks_off[1], L.wkst_off,
-                     L.wks_off[2], L.wkst3_off);
+  return HeadArgs{nb.fc4_part, nb.fc4_splits, nb.B, nb.gamma, nb.theta[0], nb.theta[1], L.b[3],
+                  L.w[4], L.b[4], nb.action, nb.reward, nb.nonterm, nb.h4[0], nb.h4[1], nb.q_out,
+                  nb.p_out, nb.q_sa, nb.p_sa, nb.target, nb.dqbuf, nb.lpart, nb.dh4,
+                  nb.fa.on ? nb.opt_init : nullptr, nb.iter, nb.fa.period, nb.book_inc,
+                  nb.fa.on ? bump : nullptr, nb.wks[0], L.wks_total, L.wks_off[1], L.wkst_off,
+                  L.wks_off[2], L.wkst3_off};
+}
+
+// ---------------------------------------------------------------------------
+// fc4 chain: fc4 forward -> head -> fc4 data gradient as ONE launch
+// (train_val.prototxt:159-483 forward + backward to dpool3).  Three block
+// ranges, each waiting for the one before through a counter (chain_signal /
+// chain_wait); a range only waits for lower block indices, which every XCD
+// dispatches first, so the chain cannot deadlock whatever fits at once.  What
+// it buys: the data gradient's W4 stream (8.4 MB) is issued at dispatch, under
+// the forward's (16.8 MB) and the head's latency chain, and two launch
+// boundaries go.  The last data-gradient block zeroes the counters for the
+// next launch (every wait of this launch has then matched).  Training steps
+// with the fused apply (nw = 0) and B <= 32 only (fc4_chain_ok).
+// ---------------------------------------------------------------------------
+struct Fc4ChainArgs {
+  Fc4FwdArgs f;
+  int nF;                 // forward blocks [0, nF): 8 waves x 32 n, split-K partials
+  HeadArgs h;
+  int nH;                 // head blocks: B samples (they signal) + 34 weight transposes
+  Fc4DgradArgs d;
+  int ndx, nD;            // data-gradient blocks
+  int32_t* ctr;           // [0] forward blocks done, [1] head samples done,
+                          // [2] data-gradient blocks done, [3] timeout flag (sticky)
+};
+constexpr int kChainFwdN = 256;   // n per forward block (8 waves)
+constexpr int kChainSmemB = 32 * 1024;
+static_assert(kChainSmemB >= fc4_fwd_smem_bytes<1>() && kChainSmemB >= kWkstSmemB &&
+                  kChainSmemB >= 8 * 1024 * 4,
+              "chain LDS");
+
+template <int KCW>
+__global__ __launch_bounds__(512) void fc4_chain_kernel(const Fc4ChainArgs c) {
+  extern __shared__ __attribute__((aligned(16))) char sm_ch[];
+  int bid = blockIdx.x;
+  if (bid < c.nF) {
+    const int nxb = kFc4 / kChainFwdN, spl = (c.f.K + kFc4KLen - 1) / kFc4KLen;
+    fc4_fwd_split_body<1, kChainFwdN / 32>(c.f, sm_ch, bid % nxb, (bid / nxb) % spl,
+                                           bid / (nxb * spl));
+    chain_signal(c.ctr + 0);
+    return;
+  }
+  bid -= c.nF;
+  if (bid < c.nH) {
+    int32_t* err = c.ctr + 3;
+    const int32_t* fdone = c.ctr;
+    const int nF = c.nF;
+    head_body<true>(c.h, bid, sm_ch, [=]() { chain_wait(fdone, nF, err); }, c.ctr + 1);
+    return;
+  }
+  bid -= c.nH;
+  {
+    int32_t* err = c.ctr + 3;
+    const int32_t* hdone = c.ctr + 1;
+    const int B = c.h.B;
+    fc4_dgrad_body<true, KCW, true>(c.d, reinterpret_cast<float (*)[1024]>(sm_ch), bid % c.ndx,
+                                    bid / c.ndx, [=]() { chain_wait(hdone, B, err); });
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 &&
+      __hip_atomic_fetch_add(c.ctr + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == c.nD - 1) {
+    __hip_atomic_store(c.ctr + 0, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(c.ctr + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(c.ctr + 2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+bool fc4_chain_ok(const NetBuffers& nb) {
+  return DDQ_FC4_CHAIN && nb.chain && nb.B <= 32 && nb.fa.on && !nb.fa.ext && !nb.fwd_only;
+}
+
+static Fc4DgradArgs fc4_dgrad_args(const NetBuffers& nb, bool& narrow, int& ndx, int& nd) {
+  const int s4 = nb.S / 8, B = nb.B;
+  Fc4DgradArgs f;
+  f.B = B; f.K = 64 * s4 * s4; f.s4 = s4; f.fS4sq = FastDiv(s4 * s4); f.fS4 = FastDiv(s4);
+  f.dh4 = nb.dh4; f.w4 = nb.theta[0] + nb.L.w[3]; f.mask3 = nb.mask3; f.dconv3 = nb.dconv3;
+  f.pooled = 1;
+  f.dsplit = nullptr;   // conv3's gradients split the fp32 dpool3 themselves
+  // 16-column blocks when 32-column ones would not give every CU one
+  narrow = (f.K / 32) * ((B + 31) / 32) < 256;
+  ndx = f.K / (narrow ? 16 : 32);
+  nd = ndx * ((B + 31) / 32);
+  return f;
+}
+
+hipError_t launch_head(const NetBuffers& nb, hipStream_t s, ReplayMeta* bump) {
+  if (fc4_chain_ok(nb)) {
+    Fc4ChainArgs c;
+    const int s4 = nb.S / 8;
+    c.f.B = nb.B; c.f.K = 64 * s4 * s4; c.f.nz = 2; c.f.part = nb.fc4_part;
+    for (int z = 0; z < 2; ++z) { c.f.x[z] = nb.pool3[z]; c.f.w[z] = nb.theta[z] + nb.L.w[3]; }
+    c.nF = (kFc4 / kChainFwdN) * fc4_fwd_splits(c.f.K) * 2;
+    c.h = head_args(nb, bump);
+    c.nH = nb.B + 25 + 9;
+    bool narrow;
+    c.d = fc4_dgrad_args(nb, narrow, c.ndx, c.nD);
+    c.ctr = nb.chain;
+    auto kern = narrow ? fc4_chain_kernel<16> : fc4_chain_kernel<32>;
+    hipLaunchKernelGGL(kern, dim3(c.nF + c.nH + c.nD), dim3(512), kChainSmemB, s, c);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(fc4_head_kernel, dim3(nb.B + 25 + 9), dim3(kFc4), 0, s, head_args(nb, bump));
   return hipGetLastError();
 }
 
@@ -1652,6 +1832,7 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     CHECK_LAUNCH(pick_tile(kConv3Fwd, H, H, DDQ_AB_TILE_C3F).launch(a3, nz, s));
   }
   if (nb.fwd_only) return hipSuccess;   // ddq_time_layer: one conv layer
+  if (!out && fc4_chain_ok(nb)) return hipSuccess;   // the head launch runs fc4 (fc4 chain)
   // fc4 (train_val.prototxt:159-185): split bf16 MFMA register-direct, split-K
   // partials (reduced by the head kernel, or by fc4_reduce_out below)
   const int s4 = S / 8;
@@ -1678,25 +1859,21 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
   const int B = nb.B, S = nb.S;
   const int s4 = S / 8;
   auto M = [&](const char* n) { if (mark) mark(marg, n); };
-  {  // fc4 (train_val.prototxt:159-185): data gradient -> pooled dpool3, and
-     // the weight gradient unless the fused apply computes it itself
-    Fc4DgradArgs f;
-    f.B = B; f.K = 64 * s4 * s4; f.s4 = s4; f.fS4sq = FastDiv(s4 * s4); f.fS4 = FastDiv(s4);
-    f.dh4 = nb.dh4; f.w4 = nb.theta[0] + L.w[3]; f.mask3 = nb.mask3; f.dconv3 = nb.dconv3;
-    f.pooled = 1;
-    f.dsplit = nullptr;   // conv3's gradients split the fp32 dpool3 themselves
-    // 16-column blocks when 32-column ones would not give every CU one
-    const bool narrow = (f.K / 32) * ((B + 31) / 32) < 256;
-    const int ndx = f.K / (narrow ? 16 : 32), nd = ndx * ((B + 31) / 32);
+  if (!fc4_chain_ok(nb)) {  // fc4 (train_val.prototxt:159-185): data gradient -> pooled
+     // dpool3, and the weight gradient unless the fused apply computes it itself
+     // (the fc4 chain ran the data gradient in the head launch)
+    bool narrow;
+    int ndx, nd;
+    Fc4DgradArgs f = fc4_dgrad_args(nb, narrow, ndx, nd);
     const int nw = (nb.fa.on && !nb.fa.ext) ? 0 : fc4_wgrad_blocks<8>(f.K);
     M("fc4_bwd");
     hipLaunchKernelGGL((narrow ? fc4_bwd_kernel<true, 16> : fc4_bwd_kernel<true, 32>),
                        dim3(nd + nw), dim3(512), 0, s, f, nb.pool3[0], nb.grad + L.w[3], nd, ndx);
     CHECK_LAUNCH(hipGetLastError());
-    // the fc4 weight gradient (the bulk of the flat gradient) is final here:
-    // the caller may start reducing it over the ranks under the conv backward
-    if (fc4_done) CHECK_LAUNCH(fc4_done(fc4_done_arg));
   }
+  // the fc4 weight gradient (the bulk of the flat gradient) is final here:
+  // the caller may start reducing it over the ranks under the conv backward
+  if (fc4_done) CHECK_LAUNCH(fc4_done(fc4_done_arg));
   {  // conv3 data gradient -> split pooled dpool2 (split bf16 on conv3's
      // transposed + flipped split weights, rebuilt by the head kernel; the fp32
      // dpool3 expanded through pool3's routing and split while staged; 4x8 (kConv3Dgrad)
