@@ -28,6 +28,14 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #ifndef DDQ_AB_TILE_C2D
 #define DDQ_AB_TILE_C2D -1
 #endif
+// A/B: workgroups the conv2 / conv3 weight gradients aim at (kernels.hip
+// wgrad_splits_for: fewer = fewer, larger slabs)
+#ifndef DDQ_AB_WG_TARGET2
+#define DDQ_AB_WG_TARGET2 512
+#endif
+#ifndef DDQ_AB_WG_TARGET3
+#define DDQ_AB_WG_TARGET3 512
+#endif
 // conv2 forward as the persistent pipelined kernel (split.h
 // split_conv_pipe_body) on maps whose side is a multiple of 16
 #ifndef DDQ_CONV2_PIPE
@@ -39,6 +47,10 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // hand-offs (kernels.hip fc4_chain_kernel)
 #ifndef DDQ_FC4_CHAIN
 #define DDQ_FC4_CHAIN 0
+#endif
+// conv2 data gradient as the persistent pipelined kernel (two 32-channel chunks)
+#ifndef DDQ_C2D_PIPE
+#define DDQ_C2D_PIPE 0
 #endif
 #ifndef DDQ_CONV1_PIPE
 #define DDQ_CONV1_PIPE 0

@@ -1731,8 +1731,9 @@ int wgrad_splits_for(int layer, int B, int S, int* np) {
   *np = ((KC[layer] + 1 + 63) / 64) * 64;
   if (layer == 0) return B * (S / wgrad1_band(S));
   const int nts[3] = {0, 2 * 5, 2 * 3};
+  const int target[3] = {0, DDQ_AB_WG_TARGET2, DDQ_AB_WG_TARGET3};
   int G, RPG;
-  wgrads_groups(B * H, nts[layer], &G, &RPG, 512);
+  wgrads_groups(B * H, nts[layer], &G, &RPG, target[layer]);
   return G;
 }
 
@@ -1807,7 +1808,7 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     a2.mask[0] = nb.mask2; a2.mask[1] = nullptr;
     M("conv2_fwd");
     if (DDQ_CONV2_PIPE && H % 8 == 0 && H % 16 == 0)
-      CHECK_LAUNCH((launch_split_conv_pipe<32, 64, 5, 8, 16, 4, 2>(a2, nz, s)));
+      CHECK_LAUNCH((launch_split_conv_pipe<32, 32, 64, 5, 8, 16, 4, 2, 1, false>(a2, nz, s)));
     else
       CHECK_LAUNCH(pick_tile(kConv2Fwd, H, H, DDQ_AB_TILE_C2F).launch(a2, nz, s));
   }
@@ -1921,7 +1922,10 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     a.in_route = nb.mask2;
     a.pd_split = nb.dconv1s; a.pd_elems = (int64_t)B * H * H * 32;
     M("conv2_dgrad");
-    CHECK_LAUNCH(pick_tile(kConv2Dgrad, H, H, DDQ_AB_TILE_C2D).launch(a, 1, s));
+    if (DDQ_C2D_PIPE && H % 8 == 0 && H % 16 == 0)   // two 32-channel chunks, pipelined
+      CHECK_LAUNCH((launch_split_conv_pipe<64, 32, 32, 5, 8, 16, 4, 1, 2, true>(a, 1, s)));
+    else
+      CHECK_LAUNCH(pick_tile(kConv2Dgrad, H, H, DDQ_AB_TILE_C2D).launch(a, 1, s));
   }
   // slab-reduce geometry: layer l's blocks start at d[l].blk0
   WredDims d[3];

@@ -721,38 +721,44 @@ inline hipError_t launch_split_conv(SplitArgs a, int nz, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------------------
-// Persistent, software-pipelined forward convolution (one channel chunk,
-// CPT == CP).  The one-round launch above stages its halo patch with nothing
-// to overlap it (every CU loads at once, then computes) and stores its pooled
-// outputs at the end (every CU stores at once).  Here a workgroup per CU slot
-// loops over tiles t = blockIdx.x, +gridDim.x, ... with two patch buffers:
-//  * the next tile's patch is loaded into registers when a tile starts and
-//    committed to the other buffer at tap kCommit (the buffer's last reader,
-//    the previous tile's epilogue, finished before that tile's last barrier);
-//  * a tile's epilogue gathers its pooled outputs in its own patch buffer and
-//    stores them while the next tile's first taps run;
-//  * the weight ring runs on the global step g = (local tile li, tap g % T):
-//    slot g & 1, tower of tile li, so tile boundaries cost no ring refill.
+// Persistent, software-pipelined direct convolution.  The one-round launch
+// above stages its halo patch with nothing to overlap it (every CU loads at
+// once, then computes) and stores its outputs at the end (every CU stores at
+// once).  Here a workgroup per CU slot loops over units u = (tile, channel
+// chunk) of its tiles t = blockIdx.x, +gridDim.x, ... with two patch buffers:
+//  * unit u + 1's patch is loaded into registers when unit u starts (DGRAD:
+//    the pooled source and its routing bytes) and committed to the other
+//    buffer at tap kCommit of unit u (expanded through the routing bytes
+//    there); that buffer's last reader, unit u - 1 (or its epilogue),
+//    finished before unit u's first barrier;
+//  * a tile's epilogue runs after its last unit: the k groups meet in that
+//    unit's (now free) patch buffer, the forward gathers its pooled outputs
+//    there too, and the stores drain while the next tile's first taps run;
+//  * the weight ring runs on the global step g = (unit g / T, tap g % T):
+//    slot g & 1, chunk and tower of that unit, so unit boundaries cost no
+//    ring refill.
 // Tiles are numbered tower-major ((z, b, ty, tx)), so the tower of local tile
 // li is just blockIdx.x + li * gridDim.x >= tiles per tower.  Per output
-// element the accumulation order (tap, k-step, the six products) is that of
-// split_conv_body: the outputs are bit-identical.
+// element the accumulation order (chunk, tap, k-step, the six products, the k
+// groups in order) is that of split_conv_body with the same CP / WK: the
+// outputs are bit-identical to that configuration's.
 // ---------------------------------------------------------------------------
-template <int CPT, int N, int KS, int TY, int TX, int WM, int WN>
+template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, bool DGRAD>
 struct SplitPipeCfg {
-  using C = SplitCfg<CPT, CPT, N, KS, TY, TX, WM, WN, 1>;
+  using C = SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK>;
   static constexpr int kSmemB = 2 * C::kPatchB + C::kWB;
   static constexpr int kCommit = C::T / 2;   // tap at which the next patch is stored
   static_assert(kSmemB <= 160 * 1024, "LDS budget (two patch buffers + ring)");
-  static_assert(C::NWIN * N * 7 <= C::kPatchB, "epilogue gather fits a patch buffer");
+  static_assert(DGRAD || C::NWIN * N * 7 <= C::kPatchB, "epilogue gather fits a patch buffer");
+  static_assert(WK == 1 || WK * WM * WN * 16 * 64 * 4 <= C::kPatchB, "k groups meet in a buffer");
 };
 
-template <int CPT, int N, int KS, int TY, int TX, int WM, int WN>
+template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, bool DGRAD>
 __device__ __forceinline__ void split_conv_pipe_body(const SplitArgs& a, char* smem, int ntiles,
                                                      int tpi, int tpt) {
-  using P = SplitPipeCfg<CPT, N, KS, TY, TX, WM, WN>;
+  using P = SplitPipeCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK, DGRAD>;
   using C = typename P::C;
-  constexpr int TM = C::TM, TN = C::TN, T = C::T;
+  constexpr int TM = C::TM, TN = C::TN, T = C::T, NCH = C::NCH;
   constexpr int kPB = C::kPatchB / 2;                     // bf16 per patch buffer
   __bf16* const patch0 = reinterpret_cast<__bf16*>(smem);
   __bf16* const wbuf = reinterpret_cast<__bf16*>(smem + 2 * C::kPatchB);
@@ -761,9 +767,10 @@ __device__ __forceinline__ void split_conv_pipe_body(const SplitArgs& a, char* s
   const int G = gridDim.x, bx = blockIdx.x;
   const int nmine = bx < ntiles ? (ntiles - 1 - bx) / G + 1 : 0;
   if (nmine == 0) return;
-  const int nstep = nmine * T;
+  const int nunit = nmine * NCH;
+  const int nstep = nunit * T;
   auto tower = [&](int li) { return bx + li * G >= tpt ? 1 : 0; };
-  // (b, y0, x0) of local tile li (runtime divisions: once per tile)
+  // (b, y0, x0) of local tile li (runtime divisions: once per unit)
   auto coords = [&](int li, int& b, int& y0, int& x0) {
     int t = bx + li * G;
     if (t >= tpt) t -= tpt;
@@ -774,69 +781,102 @@ __device__ __forceinline__ void split_conv_pipe_body(const SplitArgs& a, char* s
     x0 = (r - ty * a.tiles_x) * TX;
   };
 
-  // ---- halo patch of a tile: bounds-checked buffer loads into registers ----
+  // ---- halo patch of a unit: bounds-checked buffer loads into registers ----
   constexpr uint32_t kOOB = 0x80000000u;
-  const uint32_t src_bytes = (uint32_t)(a.B * a.H * a.W * CPT) * 2u;
-  constexpr int NV = C::PH * C::PW * (CPT / 8);           // 16-byte vectors per plane
+  // plane extent of the split source: (B, H, W, CPT), pooled (B, H/2, W/2, CPT) for DGRAD
+  const uint32_t src_elems = DGRAD ? (uint32_t)(a.B * (a.H >> 1) * (a.W >> 1) * CPT)
+                                   : (uint32_t)(a.B * a.H * a.W * CPT);
+  constexpr int NV = C::PH * C::PW * (CP / 8);            // 16-byte vectors per plane
   constexpr int NIT = (NV + C::kThreads - 1) / C::kThreads;
   u32x4 pv[3][NIT];
+  u32x2 pm[DGRAD ? NIT : 1];                              // DGRAD: routing bytes
   int pdst[NIT];
-  auto patch_issue = [&](int li) {
-    const bool live = li < nmine;
+  uint32_t pq[DGRAD ? NIT : 1];                           // DGRAD: quadrant of the pixel
+  auto patch_issue = [&](int u) {
+    const bool live = u < nunit;
+    const int li = live ? u / NCH : 0, ch = live ? u - li * NCH : 0;
     int b = 0, y0 = 0, x0 = 0;
     if (live) coords(li, b, y0, x0);
     const __bf16* in = (live && tower(li)) ? a.in[1] : a.in[0];
 #pragma unroll
-    for (int u = 0; u < NIT; ++u) {
-      const int f0 = tid + u * C::kThreads;
+    for (int it = 0; it < NIT; ++it) {
+      const int f0 = tid + it * C::kThreads;
       const bool ok = live && f0 < NV;
       const int f = ok ? f0 : 0;
-      const int pix = f / (CPT / 8), c8 = f % (CPT / 8);
+      const int pix = f / (CP / 8), c8 = f % (CP / 8);
       const int py = pix / C::PW, px = pix % C::PW;
       const int gy = y0 - a.pad + py, gx = x0 - a.pad + px;
       const bool in_img = ok && (unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W;
-      pdst[u] = ok ? py * C::RS + px * C::CS + 8 * c8 : -1;
-      const uint32_t o = in_img ? (uint32_t)(((b * a.H + gy) * a.W + gx) * CPT + 8 * c8) * 2u : kOOB;
+      pdst[it] = ok ? py * C::RS + px * C::CS + 8 * c8 : -1;
+      const uint32_t o = DGRAD ? (uint32_t)(((b * (a.H >> 1) + (gy >> 1)) * (a.W >> 1) + (gx >> 1)) *
+                                                CPT + ch * CP + 8 * c8)
+                               : (uint32_t)(((b * a.H + gy) * a.W + gx) * CPT + ch * CP + 8 * c8);
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(in + p * a.in_elems), (short)0, (int)src_bytes, 0x00020000);
-        pv[p][u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o, 0, 0));
+            (void*)(in + p * a.in_elems), (short)0, (int)(src_elems * 2), 0x00020000);
+        pv[p][it] = __builtin_bit_cast(
+            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(in_img ? o * 2 : kOOB), 0, 0));
+      }
+      if constexpr (DGRAD) {
+        const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)a.in_route, (short)0, (int)src_elems, 0x00020000);
+        pm[it] = __builtin_bit_cast(
+            u32x2, __builtin_amdgcn_raw_buffer_load_b64(rr, (int)(in_img ? o : kOOB), 0, 0));
+        pq[it] = ((gy & 1) << 1) | (gx & 1);
       }
     }
   };
-  auto patch_commit = [&](int li) {
-    __bf16* buf = patch0 + (li & 1) * kPB;
+  auto patch_commit = [&](int u) {
+    __bf16* buf = patch0 + (u & 1) * kPB;
 #pragma unroll
-    for (int u = 0; u < NIT; ++u)
-      if (pdst[u] >= 0)
+    for (int it = 0; it < NIT; ++it) {
+      if (pdst[it] < 0) continue;
 #pragma unroll
-        for (int p = 0; p < 3; ++p) *reinterpret_cast<u32x4*>(buf + p * C::kPlane + pdst[u]) = pv[p][u];
+      for (int p = 0; p < 3; ++p) {
+        u32x4 v = pv[p][it];
+        if constexpr (DGRAD) {   // expand: the value at its routed quadrant, 0 elsewhere
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const uint32_t mw = pm[it][e >> 1];
+            const uint32_t r0 = (mw >> (16 * (e & 1))) & 0xff;
+            const uint32_t r1 = (mw >> (16 * (e & 1) + 8)) & 0xff;
+            v[e] = (r0 == pq[it] ? (v[e] & 0xffffu) : 0u) | (r1 == pq[it] ? (v[e] & 0xffff0000u) : 0u);
+          }
+        }
+        *reinterpret_cast<u32x4*>(buf + p * C::kPlane + pdst[it]) = v;
+      }
+    }
   };
 
-  // ---- weights of global step g (tile g / T, tap g % T), clamped ----
-  SplitWStage<C, CPT, CPT, N> ws0, ws1;
-  auto wload = [&](SplitWStage<C, CPT, CPT, N>& w, int g) {
+  // ---- weights of global step g (unit g / T, tap g % T), clamped ----
+  SplitWStage<C, CPT, CP, N> ws0, ws1;
+  auto wload = [&](SplitWStage<C, CPT, CP, N>& w, int g) {
     const int gc = g < nstep ? g : nstep - 1;
-    const int li = gc / T;
-    w.load(tower(li) ? a.wk[1] : a.wk[0], a.wk_elems, 0, gc - li * T, tid);
+    const int u = gc / T, li = u / NCH;
+    w.load(tower(li) ? a.wk[1] : a.wk[0], a.wk_elems, u - li * NCH, gc - u * T, tid);
   };
 
-  // ---- per-lane operand offsets (split_conv_body, one k group) ----
-  const int wmi = wid / WN, wni = wid % WN;
+  // ---- per-lane operand offsets (split_conv_body) ----
+  const int wkg = wid / (WM * WN), wmn = wid % (WM * WN);
+  const int wmi = wmn / WN, wni = wmn % WN;
   int abase[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int m = wmi * TM * 32 + 32 * i + l31;
     const int win = (m >> 2) < C::NWIN ? m >> 2 : 0, dy = (m >> 1) & 1, dx = m & 1;
     const int wy = win / (TX / 2), wx = win % (TX / 2);
-    abase[i] = (2 * wy + dy) * C::RS + (2 * wx + dx) * C::CS + h * 8;
+    abase[i] = (2 * wy + dy) * C::RS + (2 * wx + dx) * C::CS + h * 8 + 16 * C::KSW * wkg;
   }
   int bbase[TN];
 #pragma unroll
-  for (int j = 0; j < TN; ++j) bbase[j] = (wni * TN * 32 + 32 * j + l31) * C::CW + h * 8;
+  for (int j = 0; j < TN; ++j)
+    bbase[j] = (wni * TN * 32 + 32 * j + l31) * C::CW + h * 8 + 16 * C::KSW * wkg;
   float bpre[TN];
   auto bias_load = [&](int li) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bpre[j] = 0.f;
+    if (DGRAD) return;
     const float* bz = tower(li < nmine ? li : 0) ? a.bias[1] : a.bias[0];
 #pragma unroll
     for (int j = 0; j < TN; ++j) bpre[j] = bz[wni * TN * 32 + 32 * j + l31];
@@ -856,7 +896,7 @@ __device__ __forceinline__ void split_conv_pipe_body(const SplitArgs& a, char* s
     const int ky = t / KS, kx = t % KS;
     const __bf16* pa = patch + ky * C::RS + kx * C::CS;
 #pragma unroll
-    for (int g = 0; g < C::KSTEP; ++g) {
+    for (int g = 0; g < C::KSW; ++g) {
       bf16x8 av[3][TM], bv[3][TN];
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
@@ -880,30 +920,61 @@ __device__ __forceinline__ void split_conv_pipe_body(const SplitArgs& a, char* s
         }
     }
   };
-  // one global step: the MFMAs of (tile li, tap t) from ring slot g & 1; at
-  // tap kCommit the next tile's patch goes to the other buffer; at the last
-  // tap the epilogue (LDS gather in this tile's buffer, 16-byte stores), the
-  // next-next tile's patch loads and the next tile's bias; then the ring slot
-  // of step g + 1 and the step's barrier.
-  auto step = [&](int g, SplitWStage<C, CPT, CPT, N>& wnext) {
-    const int li = g / T, t = g - li * T;
-    __bf16* const patch = patch0 + (li & 1) * kPB;
-    tap_step(t, patch, g & 1);
-    __builtin_amdgcn_sched_barrier(0);
-    if (t == P::kCommit && li + 1 < nmine) patch_commit(li + 1);
-    if (t == T - 1) {
+  // the end of a tile (after its last unit's last tap): k groups meet, epilogue
+  auto tile_end = [&](int li, __bf16* freebuf) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] += cor[i][j];
+    if (WK > 1) {   // as split_conv_body, in the finished unit's patch buffer
+      float* red = reinterpret_cast<float*>(freebuf);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] += cor[i][j];
-      int b, y0, x0;
-      coords(li, b, y0, x0);
-      split_epilogue_fwd_lds<TM, TN, TX, N, 1, C::NWIN, C::kThreads>(
-          a, acc, bpre, reinterpret_cast<char*>(patch), b, tower(li), y0, x0, wmi, wni, l31, h, 0,
-          tid);
-      zero_acc();
-      if (li + 2 < nmine) patch_issue(li + 2);
-      bias_load(li + 1);
+        for (int j = 0; j < TN; ++j) {
+          __syncthreads();
+#pragma unroll
+          for (int r = 0; r < 16; ++r) red[((wkg * WM * WN + wmn) * 16 + r) * 64 + lane] = acc[i][j][r];
+          __syncthreads();
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            if ((r >> 2) % WK != wkg) continue;
+            float v = 0.f;
+#pragma unroll
+            for (int k = 0; k < WK; ++k) v += red[((k * WM * WN + wmn) * 16 + r) * 64 + lane];
+            acc[i][j][r] = v;
+          }
+        }
+    }
+    int b, y0, x0;
+    coords(li, b, y0, x0);
+    if constexpr (DGRAD)
+      split_epilogue<TM, TN, TX, N, true, WK, C::NWIN>(a, acc, bpre, b, 0, y0, x0, wmi, wni, l31,
+                                                       h, wkg);
+    else
+      split_epilogue_fwd_lds<TM, TN, TX, N, WK, C::NWIN, C::kThreads>(
+          a, acc, bpre, reinterpret_cast<char*>(freebuf), b, tower(li), y0, x0, wmi, wni, l31, h,
+          wkg, tid);
+  };
+  // one global step: the MFMAs of (unit u, tap t) from ring slot g & 1; at
+  // tap kCommit the next unit's patch goes to the other buffer; at the last
+  // tap the next-next unit's patch loads (and at a tile's last unit its
+  // epilogue and the next tile's bias); then the ring slot of step g + 1 and
+  // the step's barrier.
+  auto step = [&](int g, SplitWStage<C, CPT, CP, N>& wnext) {
+    const int u = g / T, t = g - u * T;
+    __bf16* const patch = patch0 + (u & 1) * kPB;
+    tap_step(t, patch, g & 1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (t == P::kCommit && u + 1 < nunit) patch_commit(u + 1);
+    if (t == T - 1) {
+      const int li = u / NCH;
+      if (u - li * NCH == NCH - 1) {
+        tile_end(li, patch);
+        zero_acc();
+        bias_load(li + 1);
+      }
+      if (u + 2 < nunit) patch_issue(u + 2);
     }
     if (g + 1 < nstep) {
       wnext.store(wbuf + ((g + 1) & 1) * 3 * C::kWSlot, tid);
@@ -911,7 +982,8 @@ __device__ __forceinline__ void split_conv_pipe_body(const SplitArgs& a, char* s
     }
   };
 
-  // prologue: tile 0's patch and bias, ring slot 0, step 1's weights, tile 1's patch loads
+  // prologue: unit 0's patch, tile 0's bias, ring slot 0, step 1's weights,
+  // unit 1's patch loads
   patch_issue(0);
   patch_commit(0);
   bias_load(0);
@@ -936,19 +1008,20 @@ __device__ __forceinline__ void split_conv_pipe_body(const SplitArgs& a, char* s
   }
 }
 
-template <int CPT, int N, int KS, int TY, int TX, int WM, int WN>
-__global__ __launch_bounds__(64 * WM * WN) void split_conv_pipe_kernel(const SplitArgs a, int ntiles,
-                                                                       int tpi, int tpt) {
+template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, bool DGRAD>
+__global__ __launch_bounds__(64 * WM * WN * WK) void split_conv_pipe_kernel(const SplitArgs a,
+                                                                            int ntiles, int tpi,
+                                                                            int tpt) {
   extern __shared__ __attribute__((aligned(16))) char sm_pipe[];
-  split_conv_pipe_body<CPT, N, KS, TY, TX, WM, WN>(a, sm_pipe, ntiles, tpi, tpt);
+  split_conv_pipe_body<CPT, CP, N, KS, TY, TX, WM, WN, WK, DGRAD>(a, sm_pipe, ntiles, tpi, tpt);
 }
 
 // grid: one workgroup per CU (the two patch buffers take the LDS), at most
 // one per tile
-template <int CPT, int N, int KS, int TY, int TX, int WM, int WN>
+template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, bool DGRAD>
 inline hipError_t launch_split_conv_pipe(SplitArgs a, int nz, hipStream_t st) {
-  using P = SplitPipeCfg<CPT, N, KS, TY, TX, WM, WN>;
-  auto kern = split_conv_pipe_kernel<CPT, N, KS, TY, TX, WM, WN>;
+  using P = SplitPipeCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK, DGRAD>;
+  auto kern = split_conv_pipe_kernel<CPT, CP, N, KS, TY, TX, WM, WN, WK, DGRAD>;
   static int ncu = 0;
   if (!ncu) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -961,7 +1034,9 @@ inline hipError_t launch_split_conv_pipe(SplitArgs a, int nz, hipStream_t st) {
       return e;
     ncu = n > 0 ? n : 256;
   }
-  if ((a.out[0] && a.out_split[0]) || (a.out[1] && a.out_split[1])) return hipErrorInvalidValue;
+  if (!DGRAD && ((a.out[0] && a.out_split[0]) || (a.out[1] && a.out_split[1])))
+    return hipErrorInvalidValue;
+  if (DGRAD && (a.in_f32 || a.xsplit)) return hipErrorInvalidValue;   // split_conv_body only
   a.tiles_x = (a.W + TX - 1) / TX;
   const int tiles_y = (a.H + TY - 1) / TY;
   const int tpi = tiles_y * a.tiles_x, tpt = tpi * a.B, ntiles = tpt * nz;
