@@ -34,26 +34,31 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #define DDQ_AB_WG_TARGET2 512
 #endif
 #ifndef DDQ_AB_WG_TARGET3
-#define DDQ_AB_WG_TARGET3 512
+#define DDQ_AB_WG_TARGET3 256   // 40 slabs at 64x64 B=32: pair 30.0 -> 28.2 us, reduce 21.9 -> 19.2
 #endif
-// conv2 forward as the persistent pipelined kernel (split.h
-// split_conv_pipe_body) on maps whose side is a multiple of 16
+// A/B: the conv1 weight gradient's largest band height (kernels.hip wgrad1_band)
+#ifndef DDQ_AB_W1BAND
+#define DDQ_AB_W1BAND 8
+#endif
+// Measured and rejected (same-box A/B, 64x64 B=32, rocprofv3 averages; 0 in
+// the product build, where their kernels are not even instantiated):
+//  DDQ_CONV2_PIPE  conv2 forward as the persistent pipelined kernel (split.h
+//                  split_conv_pipe_body, 8 x 16 tiles, 8 waves): 30.8 -> 52.0 us
+//  DDQ_C2D_PIPE    conv2 data gradient likewise (two 32-channel chunks): 20.5 -> 36.5 us
+//  DDQ_CONV1_PIPE  conv1 forward likewise (split_conv1_pipe_kernel): 12.2 -> 12.9 us
+//  DDQ_FC4_CHAIN   fc4 forward + head + fc4 data gradient as one launch with
+//                  intra-launch counter hand-offs (fc4_chain_kernel): 19.8 -> 31.2 us
 #ifndef DDQ_CONV2_PIPE
 #define DDQ_CONV2_PIPE 0
 #endif
-// conv1 forward as the persistent pipelined kernel (split.h
-// split_conv1_pipe_kernel, 16 x 16 tiles) on frames whose side is a multiple of 16
-// fc4 forward, head and fc4 data gradient as one launch with intra-launch
-// hand-offs (kernels.hip fc4_chain_kernel)
-#ifndef DDQ_FC4_CHAIN
-#define DDQ_FC4_CHAIN 0
-#endif
-// conv2 data gradient as the persistent pipelined kernel (two 32-channel chunks)
 #ifndef DDQ_C2D_PIPE
 #define DDQ_C2D_PIPE 0
 #endif
 #ifndef DDQ_CONV1_PIPE
 #define DDQ_CONV1_PIPE 0
+#endif
+#ifndef DDQ_FC4_CHAIN
+#define DDQ_FC4_CHAIN 0
 #endif
 
 namespace ddq {

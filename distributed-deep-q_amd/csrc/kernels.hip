@@ -1097,6 +1097,7 @@ static Fc4DgradArgs fc4_dgrad_args(const NetBuffers& nb, bool& narrow, int& ndx,
 }
 
 hipError_t launch_head(const NetBuffers& nb, hipStream_t s, ReplayMeta* bump) {
+#if DDQ_FC4_CHAIN
   if (fc4_chain_ok(nb)) {
     Fc4ChainArgs c;
     const int s4 = nb.S / 8;
@@ -1112,6 +1113,7 @@ hipError_t launch_head(const NetBuffers& nb, hipStream_t s, ReplayMeta* bump) {
     hipLaunchKernelGGL(kern, dim3(c.nF + c.nH + c.nD), dim3(512), kChainSmemB, s, c);
     return hipGetLastError();
   }
+#endif
   hipLaunchKernelGGL(fc4_head_kernel, dim3(nb.B + 25 + 9), dim3(kFc4), 0, s, head_args(nb, bump));
   return hipGetLastError();
 }
@@ -1714,10 +1716,10 @@ static const Conv1Menu kConv1Fwd[] = {DDQ_CONV1_TILE(32, 32, 16), DDQ_CONV1_TILE
                                       DDQ_CONV1_TILE(16, 16, 8), DDQ_CONV1_TILE(24, 24, 9)};
 #undef DDQ_CONV1_TILE
 
-// conv1 weight-gradient band height: the largest power of two <= 8 dividing
+// conv1 weight-gradient band height: the largest power of two <= DDQ_AB_W1BAND (8) dividing
 // S (one slab per band)
 static int wgrad1_band(int S) {
-  int R = 8;
+  int R = DDQ_AB_W1BAND;
   while (R > 1 && S % R != 0) R >>= 1;
   return R;
 }
@@ -1784,9 +1786,11 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     c1.out_elems = (int64_t)B * (S / 2) * (S / 2) * 32;
     c1.mask[0] = nb.mask1; c1.mask[1] = nullptr;
     M("conv1_fwd");
-    if (DDQ_CONV1_PIPE && S % 16 == 0)
+#if DDQ_CONV1_PIPE
+    if (S % 16 == 0)
       CHECK_LAUNCH((launch_split_conv1_pipe<16, 16, 8>(c1, nz, s, L.wks_total)));
     else
+#endif
       CHECK_LAUNCH(pick_tile(kConv1Fwd, S, S, DDQ_AB_TILE_C1F).launch(c1, nz, s, L.wks_total));
   }
   if (!nb.fwd_only || nb.fwd_only == 2) {
@@ -1807,9 +1811,11 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     a2.out_elems = (int64_t)B * (H / 2) * (H / 2) * 64;
     a2.mask[0] = nb.mask2; a2.mask[1] = nullptr;
     M("conv2_fwd");
-    if (DDQ_CONV2_PIPE && H % 8 == 0 && H % 16 == 0)
+#if DDQ_CONV2_PIPE
+    if (H % 16 == 0)
       CHECK_LAUNCH((launch_split_conv_pipe<32, 32, 64, 5, 8, 16, 4, 2, 1, false>(a2, nz, s)));
     else
+#endif
       CHECK_LAUNCH(pick_tile(kConv2Fwd, H, H, DDQ_AB_TILE_C2F).launch(a2, nz, s));
   }
   if (!nb.fwd_only || nb.fwd_only == 3) {
@@ -1922,9 +1928,11 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     a.in_route = nb.mask2;
     a.pd_split = nb.dconv1s; a.pd_elems = (int64_t)B * H * H * 32;
     M("conv2_dgrad");
-    if (DDQ_C2D_PIPE && H % 8 == 0 && H % 16 == 0)   // two 32-channel chunks, pipelined
+#if DDQ_C2D_PIPE
+    if (H % 16 == 0)   // two 32-channel chunks, pipelined
       CHECK_LAUNCH((launch_split_conv_pipe<64, 32, 32, 5, 8, 16, 4, 1, 2, true>(a, 1, s)));
     else
+#endif
       CHECK_LAUNCH(pick_tile(kConv2Dgrad, H, H, DDQ_AB_TILE_C2D).launch(a, 1, s));
   }
   // slab-reduce geometry: layer l's blocks start at d[l].blk0
