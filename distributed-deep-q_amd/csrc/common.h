@@ -40,6 +40,11 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #ifndef DDQ_AB_W1BAND
 #define DDQ_AB_W1BAND 8
 #endif
+// the fused fc4-weight apply as blocks of the conv2 / conv3 weight-gradient
+// launch instead of the slab-reduce launch (kernels.hip wgrads_pair_fa_kernel)
+#ifndef DDQ_FA_IN_PAIR
+#define DDQ_FA_IN_PAIR 0
+#endif
 // Measured and rejected (same-box A/B, 64x64 B=32, rocprofv3 averages; 0 in
 // the product build, where their kernels are not even instantiated):
 //  DDQ_CONV2_PIPE  conv2 forward as the persistent pipelined kernel (split.h

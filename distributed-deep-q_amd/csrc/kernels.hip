@@ -1558,6 +1558,71 @@ static ApplyTail apply_tail(const NetBuffers& nb) {
   return t;
 }
 
+// conv2 + conv3 weight gradients (wgrads_pair_kernel) with the fused fc4-weight
+// apply blocks (fc4_apply_tile) interleaved in chunks of 8 blocks: the
+// HBM-bound apply streams (42 MB at 64x64) run under the MFMA-bound weight
+// gradients instead of in the slab-reduce launch.  Chunk c is an apply chunk
+// when c is odd and apply chunks remain; every wgrad chunk keeps its block
+// index mod 8 (the XCD-aware decode of wgrads_body).  Legal here: fc4's
+// weight gradient needs dh4 (head) and pool3 (forward) only, nothing later in
+// the step reads W4, and the apply flags were latched by the head.
+template <int CIN0, int COUT0, int KS0, int PAD0, int WMAX0, int DSRC0, int CIN1, int COUT1,
+          int KS1, int PAD1, int WMAX1, int DSRC1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void wgrads_pair_fa_kernel(
+    const WgradSArgs a0, const WgradSArgs a1, int n0, int nfa, ApplyTail fat, ApplyArgs faa,
+    int B, int K, const float* dh4, const float* x) {
+  extern __shared__ __attribute__((aligned(16))) char sm_wgpa[];
+  const int c = blockIdx.x >> 3, nac = nfa >> 3;
+  if ((c & 1) && (c >> 1) < nac) {
+    fc4_apply_tile(fat, faa, B, K, dh4, x, (c >> 1) * 8 + (blockIdx.x & 7));
+    return;
+  }
+  const int L = (c - min((c + 1) >> 1, nac)) * 8 + (blockIdx.x & 7);
+  if (L < n0)
+    wgrads_body<CIN0, COUT0, KS0, PAD0, WMAX0, DSRC0>(a0, sm_wgpa, L);
+  else
+    wgrads_body<CIN1, COUT1, KS1, PAD1, WMAX1, DSRC1>(a1, sm_wgpa, L - n0);
+}
+
+template <int CIN0, int COUT0, int KS0, int PAD0, int WMAX0, int DSRC0, int CIN1, int COUT1,
+          int KS1, int PAD1, int WMAX1, int DSRC1>
+static hipError_t launch_wgrads_pair_fa_w(const WgradSArgs& a0, const WgradSArgs& a1, int nfa,
+                                          const ApplyTail& fat, const ApplyArgs& faa, int B, int K,
+                                          const float* dh4, const float* x, hipStream_t st) {
+  const size_t s0 = wgrads_smem_bytes<CIN0, PAD0>(a0.W), s1 = wgrads_smem_bytes<CIN1, PAD1>(a1.W);
+  const size_t shm = s0 > s1 ? s0 : s1;
+  if (shm > 160 * 1024 || nfa % 8) return hipErrorInvalidValue;
+  auto kern = wgrads_pair_fa_kernel<CIN0, COUT0, KS0, PAD0, WMAX0, DSRC0, CIN1, COUT1, KS1, PAD1,
+                                    WMAX1, DSRC1>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int n0 = (a0.G + 7) / 8 * 8 * (COUT0 / 32) * KS0;
+  const int n1 = (a1.G + 7) / 8 * 8 * (COUT1 / 32) * KS1;
+  hipLaunchKernelGGL(kern, dim3(n0 + n1 + nfa), dim3(256), shm, st, a0, a1, n0, nfa, fat, faa, B, K,
+                     dh4, x);
+  return hipGetLastError();
+}
+
+static hipError_t launch_wgrads_conv23_fa(const WgradSArgs& a2, const WgradSArgs& a3, int nfa,
+                                          const ApplyTail& fat, const ApplyArgs& faa, int B, int K,
+                                          const float* dh4, const float* x, hipStream_t st) {
+  if (a2.W <= 16)
+    return launch_wgrads_pair_fa_w<32, 64, 5, 2, 16, 0, 64, 64, 3, 1, 16, 2>(a2, a3, nfa, fat, faa, B,
+                                                                             K, dh4, x, st);
+  if (a2.W <= 32)
+    return launch_wgrads_pair_fa_w<32, 64, 5, 2, 32, 0, 64, 64, 3, 1, 16, 2>(a2, a3, nfa, fat, faa, B,
+                                                                             K, dh4, x, st);
+  if (a2.W <= 64)
+    return launch_wgrads_pair_fa_w<32, 64, 5, 2, 64, 0, 64, 64, 3, 1, 32, 2>(a2, a3, nfa, fat, faa, B,
+                                                                             K, dh4, x, st);
+  return hipErrorInvalidValue;
+}
+
 // The fused fc4-weight apply (NetBuffers::fa): fc4's weight gradient is final
 // after the fc4 backward, so its update runs as extra blocks of the slab-
 // reduce launch and the apply launch keeps the rest of the parameters.
@@ -1896,6 +1961,11 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     M("conv3_dgrad");
     CHECK_LAUNCH(pick_tile(kConv3Dgrad, H, H, DDQ_AB_TILE_C3D).launch(a, 1, s));
   }
+  // exchange-free fused steps: the fc4-weight apply rides on the weight-gradient
+  // pair launch (DDQ_FA_IN_PAIR) instead of the slab-reduce launch
+  const bool fa_in_pair = DDQ_FA_IN_PAIR && nb.fa.on && !nb.fa.ext &&
+                          fc4_wgrad_blocks<kFc4ApplyR>(64 * s4 * s4) % 8 == 0;
+  const int nfa_pair = fa_in_pair ? fc4_wgrad_blocks<kFc4ApplyR>(64 * s4 * s4) : 0;
   {  // conv3 weight gradient (split bf16, wgrads.h): rows of the expanded split
      // dconv3 (pure copies) against the split pool2; conv2's on the split
      // pooled dpool2 and the split pool1
@@ -1914,7 +1984,20 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     // one launch (wgrads_pair_kernel, conv2's blocks first): 35.2 -> 30.2 us
     // against the two launches, same-box kernel trace
     M("conv23_wgrad");
-    CHECK_LAUNCH(launch_wgrads_conv23(w2, w3, s));
+    if (fa_in_pair) {   // + the fused fc4-weight apply blocks (wgrads_pair_fa_kernel)
+      ApplyTail fat = apply_tail(nb);
+      ApplyArgs faa = apply_args(nb, nb.fa.rule, nb.fa.lr, nb.fa.decay, nb.fa.eps, nb.fa.momentum,
+                                 nb.fa.wd, nb.fa.period);
+      faa.lo = L.w[3];
+      faa.hi = L.b[3];
+      fat.nfa = nfa_pair;
+      fat.ext = 0;
+      fat.rest = 1;
+      CHECK_LAUNCH(launch_wgrads_conv23_fa(w2, w3, nfa_pair, fat, faa, B, 64 * s4 * s4, nb.dh4,
+                                           nb.pool3[0], s));
+    } else {
+      CHECK_LAUNCH(launch_wgrads_conv23(w2, w3, s));
+    }
   }
   {  // conv2 data gradient -> split pooled dpool1 (split bf16, DGRAD): the
      // split pooled dpool2 expanded through mask2 while staged, the transposed
@@ -1970,7 +2053,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     if (nb.fa.on) {   // fc4 weights [w4, b4): its gradient is final since fc4_bwd
       faa.lo = L.w[3];
       faa.hi = L.b[3];
-      nfa = fc4_wgrad_blocks<kFc4ApplyR>(64 * s4 * s4);
+      nfa = fa_in_pair ? 0 : fc4_wgrad_blocks<kFc4ApplyR>(64 * s4 * s4);
       fat.nfa = nfa;
       fat.ext = nb.fa.ext;
       // and everything else where its gradient is reduced -- unless the rest
