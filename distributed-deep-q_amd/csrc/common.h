@@ -31,7 +31,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // A/B: workgroups the conv2 / conv3 weight gradients aim at (kernels.hip
 // wgrad_splits_for: fewer = fewer, larger slabs)
 #ifndef DDQ_AB_WG_TARGET2
-#define DDQ_AB_WG_TARGET2 512
+#define DDQ_AB_WG_TARGET2 256   // 24 slabs at 64x64 B=32: pair 28.4 -> 27.7 us, 6098 -> 6165 updates/s A/B
 #endif
 #ifndef DDQ_AB_WG_TARGET3
 #define DDQ_AB_WG_TARGET3 256   // 40 slabs at 64x64 B=32: pair 30.0 -> 28.2 us, reduce 21.9 -> 19.2
@@ -40,10 +40,9 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #ifndef DDQ_AB_W1BAND
 #define DDQ_AB_W1BAND 8
 #endif
-// the fused fc4-weight apply as blocks of the conv2 / conv3 weight-gradient
-// launch instead of the slab-reduce launch (kernels.hip wgrads_pair_fa_kernel)
-#ifndef DDQ_FA_IN_PAIR
-#define DDQ_FA_IN_PAIR 0
+// A/B: waves of a conv1 weight-gradient workgroup (wgrads.h launch_wgrad1s_w)
+#ifndef DDQ_AB_W1NW
+#define DDQ_AB_W1NW 4
 #endif
 // Measured and rejected (same-box A/B, 64x64 B=32, rocprofv3 averages; 0 in
 // the product build, where their kernels are not even instantiated):
@@ -53,6 +52,9 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 //  DDQ_CONV1_PIPE  conv1 forward likewise (split_conv1_pipe_kernel): 12.2 -> 12.9 us
 //  DDQ_FC4_CHAIN   fc4 forward + head + fc4 data gradient as one launch with
 //                  intra-launch counter hand-offs (fc4_chain_kernel): 19.8 -> 31.2 us
+//  DDQ_FA_IN_PAIR  the fused fc4-weight apply blocks interleaved into the conv2 / conv3
+//                  weight-gradient launch (wgrads_pair_fa_kernel): reduce 19.2 -> 12.2 us
+//                  but the pair 28.4 -> 44.4 us (6098 -> 5797 updates/s)
 #ifndef DDQ_CONV2_PIPE
 #define DDQ_CONV2_PIPE 0
 #endif
@@ -64,6 +66,9 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #endif
 #ifndef DDQ_FC4_CHAIN
 #define DDQ_FC4_CHAIN 0
+#endif
+#ifndef DDQ_FA_IN_PAIR
+#define DDQ_FA_IN_PAIR 0
 #endif
 
 namespace ddq {

@@ -1558,6 +1558,7 @@ static ApplyTail apply_tail(const NetBuffers& nb) {
   return t;
 }
 
+#if DDQ_FA_IN_PAIR
 // conv2 + conv3 weight gradients (wgrads_pair_kernel) with the fused fc4-weight
 // apply blocks (fc4_apply_tile) interleaved in chunks of 8 blocks: the
 // HBM-bound apply streams (42 MB at 64x64) run under the MFMA-bound weight
@@ -1622,6 +1623,7 @@ static hipError_t launch_wgrads_conv23_fa(const WgradSArgs& a2, const WgradSArgs
                                                                              K, dh4, x, st);
   return hipErrorInvalidValue;
 }
+#endif
 
 // The fused fc4-weight apply (NetBuffers::fa): fc4's weight gradient is final
 // after the fc4 backward, so its update runs as extra blocks of the slab-
@@ -1984,6 +1986,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     // one launch (wgrads_pair_kernel, conv2's blocks first): 35.2 -> 30.2 us
     // against the two launches, same-box kernel trace
     M("conv23_wgrad");
+#if DDQ_FA_IN_PAIR
     if (fa_in_pair) {   // + the fused fc4-weight apply blocks (wgrads_pair_fa_kernel)
       ApplyTail fat = apply_tail(nb);
       ApplyArgs faa = apply_args(nb, nb.fa.rule, nb.fa.lr, nb.fa.decay, nb.fa.eps, nb.fa.momentum,
@@ -1995,7 +1998,9 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
       fat.rest = 1;
       CHECK_LAUNCH(launch_wgrads_conv23_fa(w2, w3, nfa_pair, fat, faa, B, 64 * s4 * s4, nb.dh4,
                                            nb.pool3[0], s));
-    } else {
+    } else
+#endif
+    {
       CHECK_LAUNCH(launch_wgrads_conv23(w2, w3, s));
     }
   }

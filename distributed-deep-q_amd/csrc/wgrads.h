@@ -708,7 +708,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
 // the kernel is VALU-bound on the routing expansion, not latency-bound)
 template <int WMAX>
 inline hipError_t launch_wgrad1s_w(const Wgrad1SArgs& a, hipStream_t st) {
-  constexpr int NW = WMAX <= 64 ? 4 : 2;   // two staged rows per wave: LDS
+  constexpr int NW = WMAX <= 64 ? DDQ_AB_W1NW : 2;   // two staged rows per wave: LDS
   using Geo = Wgrad1SGeom<WMAX, NW>;
   const size_t shm = Geo::bytes(a.W, a.R);
   if (shm > 160 * 1024) return hipErrorInvalidValue;
