@@ -44,6 +44,10 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #ifndef DDQ_AB_W1NW
 #define DDQ_AB_W1NW 4
 #endif
+// A/B: k per fc4-forward split (fc.h kFc4KLen; the head sums K / kFc4KLen partials)
+#ifndef DDQ_AB_FC4_KLEN
+#define DDQ_AB_FC4_KLEN 128
+#endif
 // Measured and rejected (same-box A/B, 64x64 B=32, rocprofv3 averages; 0 in
 // the product build, where their kernels are not even instantiated):
 //  DDQ_CONV2_PIPE  conv2 forward as the persistent pipelined kernel (split.h

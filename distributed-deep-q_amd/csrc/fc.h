@@ -46,7 +46,7 @@ constexpr uint32_t kFcOOB = 0x80000000u;
 // grid (512/128, splits, nz), 4 waves; wave w owns n0 = 128*bx + 32*w, all b.
 // x = pool3 in Caffe NCHW order (B, K); W4 Caffe (512, K).  K % 32 == 0.
 // ---------------------------------------------------------------------------
-constexpr int kFc4KLen = 128;     // k per split
+constexpr int kFc4KLen = DDQ_AB_FC4_KLEN;     // k per split (128)
 
 struct Fc4FwdArgs {
   int B, K, nz;

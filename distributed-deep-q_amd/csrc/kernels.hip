@@ -1026,6 +1026,7 @@ static HeadArgs head_args(const NetBuffers& nb, ReplayMeta* bump) {
 // next launch (every wait of this launch has then matched).  Training steps
 // with the fused apply (nw = 0) and B <= 32 only (fc4_chain_ok).
 // ---------------------------------------------------------------------------
+#if DDQ_FC4_CHAIN
 struct Fc4ChainArgs {
   Fc4FwdArgs f;
   int nF;                 // forward blocks [0, nF): 8 waves x 32 n, split-K partials
@@ -1077,6 +1078,8 @@ __global__ __launch_bounds__(512) void fc4_chain_kernel(const Fc4ChainArgs c) {
     __hip_atomic_store(c.ctr + 2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
+
+#endif
 
 bool fc4_chain_ok(const NetBuffers& nb) {
   return DDQ_FC4_CHAIN && nb.chain && nb.B <= 32 && nb.fa.on && !nb.fa.ext && !nb.fwd_only;
