@@ -48,6 +48,11 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #ifndef DDQ_AB_FC4_KLEN
 #define DDQ_AB_FC4_KLEN 128
 #endif
+// A/B: the conv1 weight gradient stages one conv row of a pooled row at a time
+// (3 LDS planes per wave instead of 6: two workgroups per CU)
+#ifndef DDQ_AB_W1SEQ
+#define DDQ_AB_W1SEQ 0
+#endif
 // Measured and rejected (same-box A/B, 64x64 B=32, rocprofv3 averages; 0 in
 // the product build, where their kernels are not even instantiated):
 //  DDQ_CONV2_PIPE  conv2 forward as the persistent pipelined kernel (split.h

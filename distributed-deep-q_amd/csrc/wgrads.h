@@ -505,8 +505,11 @@ struct Wgrad1SGeom {
   static __host__ __device__ int d_plane(int W) { return ((W + 15) & ~15) * PSD; }
   // the halo patch + the NW waves' dconv row pairs; at least the image of the
   // final cross-wave sums (NW x 16 x 64 floats)
+  // dconv rows staged per wave: both conv rows of a pooled row (6 planes), or
+  // one at a time (3 planes, DDQ_AB_W1SEQ: half the LDS, two workgroups per CU)
+  static constexpr int kRowPlanes = DDQ_AB_W1SEQ ? 3 : 6;
   static __host__ __device__ size_t bytes(int W, int R) {
-    const size_t a = ((size_t)(R + 6) * in_row(W) + NW * 6 * d_plane(W)) * 2;
+    const size_t a = ((size_t)(R + 6) * in_row(W) + NW * kRowPlanes * d_plane(W)) * 2;
     return a > (size_t)NW * 16 * 64 * 4 ? a : (size_t)NW * 16 * 64 * 4;
   }
 };
@@ -521,7 +524,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
   const int l31 = lane & 31, h = lane >> 5;
   const int irow = Geo::in_row(W), dpl = Geo::d_plane(W);
   __bf16* patch = reinterpret_cast<__bf16*>(sm_w1);                 // [R+6][irow]
-  __bf16* rd = patch + (R + 6) * irow + w * 6 * dpl;                // this wave's [2][3][W16][32]
+  __bf16* rd = patch + (R + 6) * irow + w * Geo::kRowPlanes * dpl;  // this wave's [2 or 1][3][W16][32]
   const int bands = H / R;
   const int band = blockIdx.x;
   const int b = band / bands, y0 = (band % bands) * R;
@@ -537,7 +540,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
     *reinterpret_cast<uint2*>(patch + py * irow + 4 * px) = *reinterpret_cast<uint2*>(q);
   }
   // dconv tail pixels (W..W16) stay zero
-  for (int i = lane; i < 6 * (((W + 15) & ~15) - W) * 4; i += 64) {
+  for (int i = lane; i < Geo::kRowPlanes * (((W + 15) & ~15) - W) * 4; i += 64) {
     const int per = (((W + 15) & ~15) - W) * 4;
     const int p = i / per, r = i - p * per;
     reinterpret_cast<u32x4*>(rd + p * dpl + W * Geo::PSD)[r] = u32x4{0u, 0u, 0u, 0u};
@@ -588,7 +591,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
             u32x4, __builtin_amdgcn_raw_buffer_load_b128(rd_g[p], (int)(ok ? o * 2 : kOOB), 0, 0));
     }
   };
-  auto store = [&](const Regs& G) {
+  // dys: the conv rows (dy bits) whose quadrants are stored now; bias with dy 0
+  auto store = [&](const Regs& G, int dys) {
 #pragma unroll
     for (int u = 0; u < NPD; ++u) {
       const int px = dpx + 16 * u;
@@ -602,6 +606,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {   // quadrant q = 2 dy + dx
+        if (!((dys >> (q >> 1)) & 1)) continue;
         uint32_t keep[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e)
@@ -611,10 +616,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
           u32x4 o;
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[e] = G.d[p][u][e] & keep[e];
-          *reinterpret_cast<u32x4*>(rd + ((q >> 1) * 3 + p) * dpl + (2 * px + (q & 1)) * Geo::PSD +
-                                    8 * dc8) = o;
+          *reinterpret_cast<u32x4*>(rd + ((Geo::kRowPlanes == 6 ? (q >> 1) : 0) * 3 + p) * dpl +
+                                    (2 * px + (q & 1)) * Geo::PSD + 8 * dc8) = o;
         }
       }
+      if (!(dys & 1)) continue;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {   // bias: every routed value once
         const uint32_t any = (ra[e] != 4u ? 0xffffu : 0u) | (rb[e] != 4u ? 0xffff0000u : 0u);
@@ -638,13 +644,18 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
   Regs g;
   if (2 * w < R) load(g, w);
   for (int k = w; 2 * k < R; k += NW) {
-    store(g);
+    Regs cur = g;
+    if (Geo::kRowPlanes == 6) store(cur, 3);
     load(g, k + NW);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int dy = 0; dy < 2; ++dy) {
+      if (Geo::kRowPlanes == 3) {   // this conv row's quadrants into the wave's 3 planes
+        if (dy) __builtin_amdgcn_wave_barrier();   // row 0's reads done (wave-private region)
+        store(cur, 1 << dy);
+      }
       const int r = 2 * k + dy;
-      const __bf16* rdr = rd + dy * 3 * dpl;
+      const __bf16* rdr = rd + (Geo::kRowPlanes == 6 ? dy : 0) * 3 * dpl;
 #pragma unroll
       for (int s = 0; s < WMAX / 16; ++s) {
         if (16 * s >= W) break;
