@@ -301,10 +301,39 @@ def kernel_roofline(avg_us, B, S, P):
             out[k] = {"GBps": round(by / (us * 1e-6) / 1e9, 1),
                       "frac": round(by / (us * 1e-6) / HBM_PEAK, 3)}
         elif k == "apply":
-            by = 20 * P
-            out[k] = {"GBps": round(by / (us * 1e-6) / 1e9, 1),
+            # fused steps: every parameter is applied inside the slab-reduce
+            # launch; this launch only carries the next step's draw + gather
+            by = 2 * B * 4 * S * S * 5 + B * 24
+            out[k] = {"GBps": round(by / (us * 1e-6) / 1e9, 1), "role": "prefetch gather",
+                      "frac": round(by / (us * 1e-6) / HBM_PEAK, 3)}
+        elif k == "wgrad_reduce":
+            # slab reads + the fused rmsprop apply of every parameter (theta,
+            # state read + written, gradient written: 20 P; fc4's x tile and
+            # dh4 come from L2)
+            by = slab_bytes(B, S) + 20 * P
+            out[k] = {"GBps": round(by / (us * 1e-6) / 1e9, 1), "bound": "hbm",
                       "frac": round(by / (us * 1e-6) / HBM_PEAK, 3)}
     return out
+
+
+def slab_bytes(B, S, target2=256, target3=256):
+    """fp32 weight-gradient slab bytes per step (kernels.hip wgrad_splits_for /
+    wgrads.h wgrads_groups at the product's group targets, csrc/common.h)."""
+    def groups(rows, nts, target):
+        g = max(1, target // nts)
+        if g >= 16:
+            g &= ~7
+        g = max(1, min(g, rows))
+        rpg = -(-rows // g)
+        return -(-rows // rpg)
+    band = 8
+    while band > 1 and S % band:
+        band //= 2
+    np_ = lambda kc: -(-(kc + 1) // 64) * 64
+    g1 = B * (S // band)
+    g2 = groups(B * S // 2, 10, target2)
+    g3 = groups(B * S // 4, 6, target3)
+    return 4 * (g1 * 32 * np_(196) + g2 * 64 * np_(800) + g3 * 64 * np_(576))
 
 
 def acting_rate(net, cfg, S, iters=200, seed=5):

@@ -53,6 +53,11 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #ifndef DDQ_AB_W1SEQ
 #define DDQ_AB_W1SEQ 0
 #endif
+// the slab-reduce launch dispatches its 8 head-sum blocks right after the
+// prefetch blocks instead of last (kernels.hip wgrad_reduce_kernel)
+#ifndef DDQ_REDUCE_HEAD_FIRST
+#define DDQ_REDUCE_HEAD_FIRST 0
+#endif
 // Measured and rejected (same-box A/B, 64x64 B=32, rocprofv3 averages; 0 in
 // the product build, where their kernels are not even instantiated):
 //  DDQ_CONV2_PIPE  conv2 forward as the persistent pipelined kernel (split.h

@@ -1413,6 +1413,18 @@ __global__ __launch_bounds__(256, 4) void wgrad_reduce_kernel(
     return;
   }
   int bid = blockIdx.x - pf.ng;
+  const bool rest = fat.rest != 0;
+  if (DDQ_REDUCE_HEAD_FIRST) {   // the head sums' dependent latency chains next
+    if (bid < kFc4 / 64) {
+      if (opt_init && bid == 0 && threadIdx.x == 0)
+        apply_book(iter, opt_init, book_period, bump, book_inc);
+      if (DDQ_AB_SKIP & 4) return;
+      head_sums(bid, hs.B, hs.dqbuf, hs.lpart, hs.h4q, hs.dh4, hs.loss, hs.gw5, hs.gb5, hs.gb4,
+                rest, fat, faa);
+      return;
+    }
+    bid -= kFc4 / 64;
+  }
   if (fat.nfa > 0) {   // fused fc4-weight gradient + apply blocks come first: the
                        // longest HBM streams start before the reduce blocks
     if (bid < fat.nfa) {
@@ -1421,9 +1433,8 @@ __global__ __launch_bounds__(256, 4) void wgrad_reduce_kernel(
     }
     bid -= fat.nfa;
   }
-  if (opt_init && bid == 0 && threadIdx.x == 0)
+  if (!DDQ_REDUCE_HEAD_FIRST && opt_init && bid == 0 && threadIdx.x == 0)
     apply_book(iter, opt_init, book_period, bump, book_inc);
-  const bool rest = fat.rest != 0;
   if (DDQ_AB_SKIP & (bid >= nub ? 4 : 2)) return;
   if (bid >= nub) {
     head_sums(bid - nub, hs.B, hs.dqbuf, hs.lpart, hs.h4q, hs.dh4, hs.loss, hs.gw5, hs.gb5,
