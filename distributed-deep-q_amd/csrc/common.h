@@ -58,6 +58,11 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #ifndef DDQ_REDUCE_HEAD_FIRST
 #define DDQ_REDUCE_HEAD_FIRST 0
 #endif
+// conflict-free LDS stores of 32-channel weight rows and patch pixels
+// (split.h SplitWStage::row)
+#ifndef DDQ_LDS_ROWPERM
+#define DDQ_LDS_ROWPERM 0
+#endif
 // Measured and rejected (same-box A/B, 64x64 B=32, rocprofv3 averages; 0 in
 // the product build, where their kernels are not even instantiated):
 //  DDQ_CONV2_PIPE  conv2 forward as the persistent pipelined kernel (split.h

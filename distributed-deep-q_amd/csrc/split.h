@@ -141,6 +141,17 @@ struct SplitWStage {
   static constexpr int kPer = (3 * WV + C::kGroup - 1) / C::kGroup;
   static_assert(kPer <= 12, "weight staging registers");
   u32x4 r[kPer];
+  // ds_write_b128 serves 8 contiguous lanes per LDS cycle on banks (a/4) mod
+  // 32.  With 32-channel rows (4 vectors, row stride CW = 40 bf16 = 20 dwords)
+  // lanes 4-7 hit the banks of lanes 0-3 when they write row n + 1; writing
+  // rows n and n + 4 instead (80 dwords apart: the other 16 banks) is
+  // conflict-free -- a permutation of the rows within blocks of 8, the same
+  // for the load and the store of a lane (DDQ_LDS_ROWPERM)
+  static __device__ __forceinline__ int row(int q) {
+    const int n0 = q / (CP / 8);
+    if (!DDQ_LDS_ROWPERM || CP != 32) return n0;
+    return (n0 & ~7) | ((n0 & 7) >> 1) | ((n0 & 1) << 2);
+  }
 
   __device__ __forceinline__ void load(const __bf16* __restrict__ wk, int64_t E, int ch, int t,
                                        int tid) {
@@ -149,18 +160,21 @@ struct SplitWStage {
       const int f0 = tid + S * C::kGroup;
       const int f = (3 * WV) % C::kGroup == 0 || f0 < 3 * WV ? f0 : 3 * WV - 1;
       const int p = f / WV, q = f - p * WV;
-      const int n = q / (CP / 8), c8 = q % (CP / 8);
+      const int n = row(q), c8 = q % (CP / 8);
       r[S] = *reinterpret_cast<const u32x4*>(wk + p * E + ((size_t)n * C::T + t) * CPT + ch * CP +
                                              8 * c8);
     }
   }
   __device__ __forceinline__ void store(__bf16* dst, int tid) const {
 #pragma unroll
-    for (int S = 0; S < kPer; ++S) {   // clamped lanes rewrite the last vector: no branch
+    for (int S = 0; S < kPer; ++S) {
       const int f0 = tid + S * C::kGroup;
+      // lanes past the vectors store nothing (whole waves at these sizes:
+      // a uniform branch); they used to rewrite the last vector
+      if (DDQ_LDS_ROWPERM && (3 * WV) % C::kGroup != 0 && f0 >= 3 * WV) continue;
       const int f = (3 * WV) % C::kGroup == 0 || f0 < 3 * WV ? f0 : 3 * WV - 1;
       const int p = f / WV, q = f - p * WV;
-      const int n = q / (CP / 8), c8 = q % (CP / 8);
+      const int n = row(q), c8 = q % (CP / 8);
       *reinterpret_cast<u32x4*>(dst + p * C::kWSlot + n * C::CW + 8 * c8) = r[S];
     }
   }
@@ -419,7 +433,13 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
       const bool live = i0 + u < NIT && f0 < 3 * NV;
       const int f = live ? f0 : 0;
       const int p = f / NV, r = f - p * NV;
-      const int pix = r / (CP / 8), c8 = r % (CP / 8);
+      const int pix0 = r / (CP / 8), c8 = r % (CP / 8);
+      // 32-channel pixels (20 dwords apart): pixels q and q + 4 share an
+      // 8-lane store group instead of q and q + 1 (SplitWStage::row)
+      constexpr int NPX = C::PH * C::PW;
+      const int pix = (DDQ_LDS_ROWPERM && CP == 32 && pix0 < (NPX & ~7))
+                          ? (pix0 & ~7) | ((pix0 & 7) >> 1) | ((pix0 & 1) << 2)
+                          : pix0;
       const int py = pix / C::PW, px = pix % C::PW;
       const int gy = y0 - a.pad + py, gx = x0 - a.pad + px;
       const bool in_img = live && (unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W;
