@@ -63,6 +63,9 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #ifndef DDQ_LDS_ROWPERM
 #define DDQ_LDS_ROWPERM 0
 #endif
+#ifndef DDQ_AB_C3F_WIDE
+#define DDQ_AB_C3F_WIDE 0
+#endif
 // Measured and rejected (same-box A/B, 64x64 B=32, rocprofv3 averages; 0 in
 // the product build, where their kernels are not even instantiated):
 //  DDQ_CONV2_PIPE  conv2 forward as the persistent pipelined kernel (split.h

@@ -1917,7 +1917,11 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     a3.nchw = 1;
     a3.mask[0] = nb.mask3; a3.mask[1] = nullptr;
     M("conv3_fwd");
+#if DDQ_AB_C3F_WIDE   // A/B: 8 x 16 tiles, 16 waves (half the workgroups, half the weight streaming)
+    CHECK_LAUNCH((launch_split_conv<64, 64, 64, 3, 8, 16, 4, 2, 2, false>(a3, nz, s)));
+#else
     CHECK_LAUNCH(pick_tile(kConv3Fwd, H, H, DDQ_AB_TILE_C3F).launch(a3, nz, s));
+#endif
   }
   if (nb.fwd_only) return hipSuccess;   // ddq_time_layer: one conv layer
   if (!out && fc4_chain_ok(nb)) return hipSuccess;   // the head launch runs fc4 (fc4 chain)
