@@ -1985,7 +1985,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
   // pair launch (DDQ_FA_IN_PAIR) instead of the slab-reduce launch
   const bool fa_in_pair = DDQ_FA_IN_PAIR && nb.fa.on && !nb.fa.ext &&
                           fc4_wgrad_blocks<kFc4ApplyR>(64 * s4 * s4) % 8 == 0;
-  const int nfa_pair = fa_in_pair ? fc4_wgrad_blocks<kFc4ApplyR>(64 * s4 * s4) : 0;
+  [[maybe_unused]] const int nfa_pair = fa_in_pair ? fc4_wgrad_blocks<kFc4ApplyR>(64 * s4 * s4) : 0;
   {  // conv3 weight gradient (split bf16, wgrads.h): rows of the expanded split
      // dconv3 (pure copies) against the split pool2; conv2's on the split
      // pooled dpool2 and the split pool1
