@@ -66,6 +66,10 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #ifndef DDQ_AB_C3F_WIDE
 #define DDQ_AB_C3F_WIDE 0
 #endif
+// fc4 data gradient: the two 16-column blocks of a 128-byte W4 line on one XCD
+#ifndef DDQ_FC4BWD_XCD
+#define DDQ_FC4BWD_XCD 0
+#endif
 // Measured and rejected (same-box A/B, 64x64 B=32, rocprofv3 averages; 0 in
 // the product build, where their kernels are not even instantiated):
 //  DDQ_CONV2_PIPE  conv2 forward as the persistent pipelined kernel (split.h

@@ -1830,7 +1830,15 @@ __global__ __launch_bounds__(512) void fc4_bwd_kernel(const Fc4DgradArgs d, cons
   __shared__ __attribute__((aligned(16))) float smem[8 * 1024];
   const int bid = blockIdx.x;
   if (bid < nd) {
-    fc4_dgrad_body<SPLIT, KCW>(d, reinterpret_cast<float(*)[1024]>(smem), bid % ndx, bid / ndx);
+    int lb = bid;
+    if (DDQ_FC4BWD_XCD && KCW == 16 && nd % 16 == 0) {
+      // 16-column blocks 2m and 2m+1 read the two halves of the same 128-byte
+      // W4 lines: dispatch them to one XCD (workgroup i runs on XCD i % 8), so
+      // that XCD's L2 fetches each line once
+      const int xcd = bid & 7, q = bid >> 3;
+      lb = 16 * (q >> 1) + 2 * xcd + (q & 1);
+    }
+    fc4_dgrad_body<SPLIT, KCW>(d, reinterpret_cast<float(*)[1024]>(smem), lb % ndx, lb / ndx);
     return;
   }
   if (threadIdx.x >= 256) return;
