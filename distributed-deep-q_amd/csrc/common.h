@@ -44,31 +44,37 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #ifndef DDQ_AB_W1NW
 #define DDQ_AB_W1NW 4
 #endif
-// A/B: k per fc4-forward split (fc.h kFc4KLen; the head sums K / kFc4KLen partials)
+// A/B: k per fc4-forward split (fc.h kFc4KLen; the head sums K / kFc4KLen partials);
+// measured: 64 -> head 6.6 -> 8.4 us, 256 -> fc4 forward 6.0 -> 8.7 us (128 kept)
 #ifndef DDQ_AB_FC4_KLEN
 #define DDQ_AB_FC4_KLEN 128
 #endif
 // A/B: the conv1 weight gradient stages one conv row of a pooled row at a time
-// (3 LDS planes per wave instead of 6: two workgroups per CU)
+// (3 LDS planes per wave instead of 6: two workgroups per CU); measured:
+// conv1 weight gradient 14.2 -> 15.6 us (256 workgroups never pair on a CU)
 #ifndef DDQ_AB_W1SEQ
 #define DDQ_AB_W1SEQ 0
 #endif
 // the slab-reduce launch dispatches its 8 head-sum blocks right after the
-// prefetch blocks instead of last (kernels.hip wgrad_reduce_kernel)
+// prefetch blocks instead of last (kernels.hip wgrad_reduce_kernel); 1 in the
+// product build: reduce 19.4 -> 16.4 us, 6108 -> 6250 updates/s (same-box A/B)
 #ifndef DDQ_REDUCE_HEAD_FIRST
-#define DDQ_REDUCE_HEAD_FIRST 0
+#define DDQ_REDUCE_HEAD_FIRST 1
 #endif
 // conflict-free LDS stores of 32-channel weight rows and patch pixels
-// (split.h SplitWStage::row)
+// (split.h SplitWStage::row); 1 in the product build (timing-neutral:
+// conv2 forward 30.4 -> 30.2 us, within the A/B's noise)
 #ifndef DDQ_LDS_ROWPERM
-#define DDQ_LDS_ROWPERM 0
+#define DDQ_LDS_ROWPERM 1
 #endif
+// A/B: conv3 forward on 8 x 16 tiles, 16 waves; measured 11.2 -> 14.6 us
 #ifndef DDQ_AB_C3F_WIDE
 #define DDQ_AB_C3F_WIDE 0
 #endif
-// fc4 data gradient: the two 16-column blocks of a 128-byte W4 line on one XCD
+// fc4 data gradient: the two 16-column blocks of a 128-byte W4 line on one XCD;
+// 1 in the product build: 7.1 -> 6.5 us
 #ifndef DDQ_FC4BWD_XCD
-#define DDQ_FC4BWD_XCD 0
+#define DDQ_FC4BWD_XCD 1
 #endif
 // Measured and rejected (same-box A/B, 64x64 B=32, rocprofv3 averages; 0 in
 // the product build, where their kernels are not even instantiated):
