@@ -61,6 +61,11 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #ifndef DDQ_REDUCE_HEAD_FIRST
 #define DDQ_REDUCE_HEAD_FIRST 1
 #endif
+// A/B (with DDQ_REDUCE_HEAD_FIRST): the slab units dispatched before the fused
+// fc4 apply tiles
+#ifndef DDQ_REDUCE_SLABS_FIRST
+#define DDQ_REDUCE_SLABS_FIRST 0
+#endif
 // conflict-free LDS stores of 32-channel weight rows and patch pixels
 // (split.h SplitWStage::row); 1 in the product build (timing-neutral:
 // conv2 forward 30.4 -> 30.2 us, within the A/B's noise)

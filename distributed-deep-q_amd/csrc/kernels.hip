@@ -1425,6 +1425,22 @@ __global__ __launch_bounds__(256, 4) void wgrad_reduce_kernel(
     }
     bid -= kFc4 / 64;
   }
+  if (DDQ_REDUCE_HEAD_FIRST && DDQ_REDUCE_SLABS_FIRST && fat.nfa > 0) {
+    // the slab units' latency chains ahead of the fc4 apply tiles' HBM streams
+    if (bid < nub) {
+      if (DDQ_AB_SKIP & 2) return;
+      const WredDims& d = bid >= d1.blk0 ? d1 : (bid >= d2.blk0 ? d2 : d0);
+      if (d.G == 1)
+        wred_block<1>(part, grad, d, bid - d.blk0, red, rest, fat, faa);
+      else if (d.G == 2)
+        wred_block<2>(part, grad, d, bid - d.blk0, red, rest, fat, faa);
+      else
+        wred_block<4>(part, grad, d, bid - d.blk0, red, rest, fat, faa);
+      return;
+    }
+    if (!(DDQ_AB_SKIP & 1)) fc4_apply_tile(fat, faa, hs.B, fc4_k, hs.dh4, fc4_x, bid - nub);
+    return;
+  }
   if (fat.nfa > 0) {   // fused fc4-weight gradient + apply blocks come first: the
                        // longest HBM streams start before the reduce blocks
     if (bid < fat.nfa) {

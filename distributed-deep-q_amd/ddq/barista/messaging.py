@@ -1,12 +1,17 @@
-"""Wire format between a Barista worker and the parameter server, byte-compatible
-with barista/messaging.py (reference):
+"""Wire format between a Barista worker and the parameter server, compatible with
+barista/messaging.py (reference) -- framing and fp32 payload byte-identical, the
+header an equivalent pickle (see below):
 
 * model message (server -> worker, messaging.py:13-40):
     struct.pack('ii', iteration, hlen) + header + raw fp32 blobs
 * gradient / net message (worker -> server, messaging.py:43-79):
     struct.pack('i', hlen) + header + raw fp32 blobs of the ``Q*`` params only
-* header: pickle (protocol 2, what Python 2 ``cPickle.dumps(.., -1)`` writes)
-  of an OrderedDict {param name: [blob shape, ...]} in parameter order; the
+* header: pickle (protocol 2, the protocol Python 2 ``cPickle.dumps(.., -1)``
+  writes) of an OrderedDict {param name: [blob shape, ...]} in parameter order.
+  Python 2 cPickle decodes it to the same OrderedDict, but the bytes are not
+  cPickle's own (BINUNICODE names against SHORT_BINSTRING, Python 3's memo
+  numbering), so the length prefix (this header's own length) differs too;
+  the reference never compares header bytes, it decodes them.  The
   loaders use only element counts (:111-112) or reshape to the header shapes
   (:159-161).
 

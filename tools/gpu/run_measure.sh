@@ -6,6 +6,8 @@ mkdir -p gpurun_out
 R=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -o run -- python3 $R/bench.py --steps 200 --warmup 20 --profile-steps 5 --no-cpu-baseline --no-gather-stress --no-sweep > $R/gpurun_out/prof_bench.json 2> $R/gpurun_out/prof.err
+# the step alone (no exchange-path launches in the averages)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_step -o run -- python3 $R/bench.py --steps 200 --warmup 20 --profile-steps 5 --no-cpu-baseline --no-gather-stress --no-sweep --no-exchange-paths > $R/gpurun_out/prof_step_bench.json 2> $R/gpurun_out/prof_step.err
 i=0
 while read -r line; do
   i=$((i + 1))

@@ -9,5 +9,6 @@ cp gpurun_out/gpu_tests.log gpurun_out/bench_full.json gpurun_out/bench_acting.j
    gpurun_out/prof_bench.json gpurun_out/pmc_summary.txt gpurun_out/pmc.json \
    gpurun_out/trace_summary.txt gpurun_out/measure.log gpurun_out/keep/
 cp gpurun_out/prof/run_kernel_stats.csv gpurun_out/keep/kernel_stats.csv
+cp gpurun_out/prof_step/run_kernel_stats.csv gpurun_out/keep/kernel_stats_step.csv
 find gpurun_out -mindepth 1 -maxdepth 1 ! -name keep -exec rm -rf {} +
 ls -la gpurun_out/keep
