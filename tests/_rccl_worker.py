@@ -1,0 +1,56 @@
+"""One rank of tests/test_gpu_zz_rccl_multi.py: W processes, rank r on GPU r,
+an RCCL communicator over all of them (gloo only broadcasts its id), R steps
+of one exchange, then the rank's Q / P parameters, optimizer state and last
+gradient saved for the parent to compare with an in-process group.
+
+usage: RANK=r WORLD_SIZE=W MASTER_ADDR=127.0.0.1 MASTER_PORT=p \
+       python tests/_rccl_worker.py EXCHANGE ROUNDS OUT.npz
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "distributed-deep-q_amd"))
+
+S, B, N, SEED, PERIOD, LR = 16, 8, 120, 5, 4, 1e-4
+
+
+def member_data(r):
+    """The replay contents of member r (tests/test_gpu_exchange.py make_group)."""
+    rng = np.random.default_rng(r)
+    return (rng.integers(0, 256, (N, 4, S, S)).astype(np.uint8),
+            rng.integers(0, 4, N).astype(np.uint8),
+            rng.integers(-1, 2, N).astype(np.int16),
+            (rng.random(N) > 0.1).astype(np.uint8))
+
+
+def main():
+    exchange, rounds, out = sys.argv[1], int(sys.argv[2]), sys.argv[3]
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import ddq
+    from ddq import dist as ddist
+    from ddq.params import init_params_flat
+    theta = init_params_flat(S, seed=42)
+    n = ddq.DeepQNet(batch=B, frame=S, device=rank)
+    n.set_flat(0, theta)
+    n.set_flat(1, theta)
+    n.replay_create(N)
+    n.replay_import(*member_data(rank), 0, N)
+    ddist.setup_comm(n, rank, world)
+    cfg = n.step_cfg("rmsprop", lr=LR, target_period=PERIOD, exchange=exchange, seed=SEED)
+    for _ in range(rounds):
+        n.step(cfg)
+    n.synchronize()
+    np.savez(out, q=n.get_flat(0), p=n.get_flat(1), opt=n.optimizer_state(),
+             grad=n.get_grads_flat())
+    dist.barrier()
+    n.close()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
