@@ -723,6 +723,9 @@ def main():
                          "step_frac_basis": "step_roofline(): MFMA kernels at their "
                                             "arithmetic's peak + algorithmic HBM bytes"},
             "kernels_us": {k: round(v, 2) for k, v in avg.items()},
+            "kernels_us_timing": "eager step, one HIP event pair per launch (ddq_profile_step): "
+                                 "5-15 % above the graph-replayed rocprofv3 averages "
+                                 "(profiles/rNN_kernel_stats_step.csv)",
             "kernel_roofline": kernel_roofline(avg, B, S, net.num_params),
             "step_ms_distribution": dist_ms,
             "final_loss": loss,
