@@ -61,6 +61,11 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #ifndef DDQ_REDUCE_HEAD_FIRST
 #define DDQ_REDUCE_HEAD_FIRST 1
 #endif
+// A/B (with DDQ_REDUCE_HEAD_FIRST): the 8 head-sum blocks dispatched before the
+// next step's draw + gather blocks
+#ifndef DDQ_REDUCE_PF_AFTER_HEAD
+#define DDQ_REDUCE_PF_AFTER_HEAD 0
+#endif
 // A/B (with DDQ_REDUCE_HEAD_FIRST): the slab units dispatched before the fused
 // fc4 apply tiles; measured: reduce 16.6 -> 22.6 us, 6254 -> 6012 updates/s (rejected)
 #ifndef DDQ_REDUCE_SLABS_FIRST

@@ -1408,11 +1408,28 @@ __global__ __launch_bounds__(256, 4) void wgrad_reduce_kernel(
     ReplayMeta* bump, int book_inc, HeadSums hs, ApplyTail fat, ApplyArgs faa, Prefetch pf,
     const float* __restrict__ fc4_x, int fc4_k) {
   __shared__ float red[4][4][64];
-  if ((int)blockIdx.x < pf.ng) {   // fused apply: the next step's draw + gather first
-    if (!(DDQ_AB_SKIP & 8)) prefetch_body(pf, blockIdx.x);
+  int bid = blockIdx.x;
+  if (DDQ_REDUCE_HEAD_FIRST && DDQ_REDUCE_PF_AFTER_HEAD) {   // head sums, then the prefetch
+    if (bid < kFc4 / 64) {
+      if (opt_init && bid == 0 && threadIdx.x == 0)
+        apply_book(iter, opt_init, book_period, bump, book_inc);
+      if (DDQ_AB_SKIP & 4) return;
+      head_sums(bid, hs.B, hs.dqbuf, hs.lpart, hs.h4q, hs.dh4, hs.loss, hs.gw5, hs.gb5, hs.gb4,
+                fat.rest != 0, fat, faa);
+      return;
+    }
+    bid -= kFc4 / 64;
+    if (bid < pf.ng) {
+      if (!(DDQ_AB_SKIP & 8)) prefetch_body(pf, bid);
+      return;
+    }
+    bid = bid - pf.ng + kFc4 / 64;   // the head-first numbering below, past its head blocks
+  } else if (bid < pf.ng) {   // fused apply: the next step's draw + gather first
+    if (!(DDQ_AB_SKIP & 8)) prefetch_body(pf, bid);
     return;
+  } else {
+    bid -= pf.ng;
   }
-  int bid = blockIdx.x - pf.ng;
   const bool rest = fat.rest != 0;
   if (DDQ_REDUCE_HEAD_FIRST) {   // the head sums' dependent latency chains next
     if (bid < kFc4 / 64) {
