@@ -71,6 +71,11 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #ifndef DDQ_REDUCE_SLABS_FIRST
 #define DDQ_REDUCE_SLABS_FIRST 0
 #endif
+// A/B: static s_setprio 1 for the second half of the waves of the split-conv
+// and weight-gradient-pair workgroups (MI355X_MICROARCH.md item 4)
+#ifndef DDQ_AB_SETPRIO
+#define DDQ_AB_SETPRIO 0
+#endif
 // conflict-free LDS stores of 32-channel weight rows and patch pixels
 // (split.h SplitWStage::row); 1 in the product build (timing-neutral:
 // conv2 forward 30.4 -> 30.2 us, within the A/B's noise)

@@ -714,6 +714,7 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
 template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, bool DGRAD>
 __global__ __launch_bounds__(64 * WM * WN * WK) void split_conv_kernel(const SplitArgs a) {
   extern __shared__ __attribute__((aligned(16))) char sm_split[];
+  if (DDQ_AB_SETPRIO && (threadIdx.x >> 6) >= WM * WN * WK / 2) __builtin_amdgcn_s_setprio(1);
   split_conv_body<CPT, CP, N, KS, TY, TX, WM, WN, WK, DGRAD>(a, sm_split, blockIdx.x, blockIdx.y,
                                                             blockIdx.z);
 }

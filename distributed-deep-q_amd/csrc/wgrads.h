@@ -435,6 +435,7 @@ template <int CIN0, int COUT0, int KS0, int PAD0, int WMAX0, int DSRC0, int CIN1
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void wgrads_pair_kernel(
     const WgradSArgs a0, const WgradSArgs a1, int n0) {
   extern __shared__ __attribute__((aligned(16))) char sm_wgp[];
+  if (DDQ_AB_SETPRIO && (threadIdx.x >> 6) >= 2) __builtin_amdgcn_s_setprio(1);
   if ((int)blockIdx.x < n0)
     wgrads_body<CIN0, COUT0, KS0, PAD0, WMAX0, DSRC0>(a0, sm_wgp, blockIdx.x);
   else
