@@ -16,8 +16,9 @@ replay filled with synthetic Snake frames.
 
 Prints ONE JSON line (rank 0).  ``value`` = minibatch updates/s summed over
 all ranks (each rank consumes its own minibatch per step: weak scaling).
-``roofline``: dominant kernel measured with HIP events on the ctx stream
-(ddq_profile_step) vs the peak of the arithmetic it runs (split-bf16 kernels:
+``roofline``: dominant kernel's in-step time inside the graph-replayed
+pipelined chain, HIP event-record nodes on the ctx stream
+(ddq_profile_graph), vs the peak of the arithmetic it runs (split-bf16 kernels:
 the bf16 dense peak over their products per f32 product).  ``cpu_baseline``: the oracle's C
 restatement of the Caffe CPU step (oracle/libddq_cpu.so) timed on the host
 cores on a bounded sample of the same workload.
@@ -89,12 +90,15 @@ def arith_peak(kernel):
 
 def pmc_traffic(label, B, S):
     """(HBM bytes per launch of `label`, source file) from the newest committed
-    PMC summary (profiles/rNN_pmc.json, tools/gpu/run_measure.sh: FETCH_SIZE x2
+    step-only PMC summary (profiles/rNN_pmc_step.json: the bench's step chain
+    alone, no exchange-path dispatches; tools/gpu/run_measure.sh: FETCH_SIZE x2
     + WRITE_SIZE, MI355X_MICROARCH.md gfx950 correction) -- a separate
     rocprofv3 --pmc run of the same bench command, NOT measured in this run;
     valid for the bench default shape only."""
     import glob
-    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc.json")))
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_step.json")))
+    if not paths:
+        paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc.json")))
     if (B, S) != (32, 64) or not paths:
         return None, None
     sym = KERNEL_SYMBOL.get(label)
@@ -129,6 +133,20 @@ def fill_replay(net, N, S, seed):
     reps = (N + pool - 1) // pool
     net.replay_import(np.tile(st, (reps, 1, 1, 1))[:N], np.tile(ac, reps)[:N],
                       np.tile(rw, reps)[:N], np.tile(nt, reps)[:N].astype(np.uint8), 0, N)
+
+
+def make_net(B, S, replay, device, rank):
+    """The bench's worker: seed-42 Gaussian fillers (identical on every rank),
+    a replay ring of `replay` synthetic Snake transitions (seed 1000 + rank)."""
+    import ddq
+    from ddq.params import init_params_flat
+    net = ddq.DeepQNet(batch=B, frame=S, device=device)
+    theta = init_params_flat(S, seed=42)
+    net.set_flat(0, theta)
+    net.set_flat(1, theta)
+    net.replay_create(replay)
+    fill_replay(net, replay, S, seed=1000 + rank)
+    return net
 
 
 def cpu_model():
@@ -434,15 +452,27 @@ EXCHANGE_PATHS = (   # (label, exchange, overlap, step mode)
     ("async-ticket", "async", False, "ticket"))    # arrival order (AsyncTicketLoop)
 
 
-def exchange_paths(net, rule, ref_value, steps=240, warmup=24, profile=5):
+def exchange_paths(net, rule, steps=240, warmup=24, profile=5):
     """The per-GPU path of BASELINE configs 4 / 5 measured on one GPU: every
     gradient exchange through a 1-rank RCCL communicator (the same kernels,
     RCCL calls, comm-stream overlap and graph capture as N > 1, without the
-    wire time), against the exchange-free step of the same run."""
+    wire time), against an exchange-free leg of the same length timed in this
+    function (before and after the paths; their mean is the reference)."""
     import ddq
     from ddq import dist as ddist
     from ddq.params import init_params_flat
     out = {}
+
+    def free_leg():
+        c0 = net.step_cfg(rule, lr=1e-4, target_period=10, exchange="none", seed=1234)
+        net.step_prepare(c0, "pipelined")
+        net.step_pipelined(c0, warmup)
+        net.synchronize()
+        t0 = time.perf_counter()
+        net.step_pipelined(c0, steps)
+        net.synchronize()
+        return steps / (time.perf_counter() - t0)
+    ref_before = free_leg()
     for label, ex, ov, mode in EXCHANGE_PATHS:
         if ex == "async":     # a fresh worker: once begun, a ctx runs async steps only
             net = ddq.DeepQNet(batch=net.batch, frame=net.frame, device=net.device)
@@ -478,8 +508,7 @@ def exchange_paths(net, rule, ref_value, steps=240, warmup=24, profile=5):
         run(steps)
         net.synchronize()
         dt = (time.perf_counter() - t0) / steps
-        e = {"updates_per_s": round(1 / dt, 2), "ms_per_step": round(dt * 1e3, 4), "mode": mode,
-             "vs_exchange_free": round((1 / dt) / ref_value, 4)}
+        e = {"updates_per_s": round(1 / dt, 2), "ms_per_step": round(dt * 1e3, 4), "mode": mode}
         if ex != "async":
             prof = {}
             for _ in range(profile):
@@ -490,9 +519,18 @@ def exchange_paths(net, rule, ref_value, steps=240, warmup=24, profile=5):
             net.close()
         out[label] = e
     out.pop("comm", None)
+    ref_after = free_leg()
+    ref = 0.5 * (ref_before + ref_after)
+    for e in out.values():
+        e["vs_exchange_free"] = round(e["updates_per_s"] / ref, 4)
     return {"note": "world-1 RCCL communicator: the N>1 per-GPU step (kernels, RCCL calls, "
                     "comm-stream overlap, graphs) without wire time; vs_exchange_free = "
-                    "this path's updates/s over the main line's", "paths": out}
+                    "this path's updates/s over an exchange-free pipelined leg of the same "
+                    "length (%d steps after %d warmup) timed before and after the paths"
+                    % (steps, warmup),
+            "exchange_free": {"updates_per_s_before": round(ref_before, 2),
+                              "updates_per_s_after": round(ref_after, 2)},
+            "paths": out}
 
 
 def frame_sweep(B=256, frames=range(16, 129, 8), steps=60, warmup=10, rule="rmsprop"):
@@ -545,7 +583,8 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--replay", type=int, default=30000)
     ap.add_argument("--rule", default="rmsprop")
-    ap.add_argument("--profile-steps", type=int, default=20)
+    ap.add_argument("--profile-steps", type=int, default=20,
+                    help="replays of the 8-step profiled graph (per-kernel in-step times)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather-stress", action="store_true",
                     help="skip the C5 1M-slot gather stress (rank 0, N=1 only)")
@@ -585,15 +624,8 @@ def main():
     dist = ddist.init_process_group(rank, world, "gloo")   # bootstrap only; data path is RCCL
     torch.cuda.set_device(local)
 
-    import ddq
     B, S = args.batch, args.frame
-    net = ddq.DeepQNet(batch=B, frame=S, device=local)
-    from ddq.params import init_params_flat
-    theta = init_params_flat(S, seed=42)            # identical on every rank
-    net.set_flat(0, theta)
-    net.set_flat(1, theta)
-    net.replay_create(args.replay)
-    fill_replay(net, args.replay, S, seed=1000 + rank)
+    net = make_net(B, S, args.replay, local, rank)
     if world > 1:
         ddist.setup_comm(net, rank, world)
     elif args.force_exchange:
@@ -662,20 +694,27 @@ def main():
                    "p90": round(float(np.percentile(per, 90)), 4),
                    "chunks": args.chunks, "steps_per_chunk": args.chunk_steps}
 
-    # per-kernel device times (HIP events on the ctx stream), averaged
-    prof = {}
-    pcfg = cfg if not (exchanged and args.exchange == "async") else \
-        net.step_cfg(args.rule, lr=1e-4, target_period=10, exchange="none", seed=1234)
-    for _ in range(args.profile_steps):
-        for name, us in net.profile_step(pcfg):
-            prof.setdefault(name, []).append(us)
-    avg = {k: float(np.median(v)) for k, v in prof.items()}
+    # per-kernel device times INSIDE the graph-replayed pipelined chain the
+    # line times: 8 captured steps with an event-record node between every two
+    # kernels (ddq_profile_graph), replayed --profile-steps times, on the ctx
+    # stream the kernels run on.  The exchange-free fused step's empty "apply"
+    # interval is the event nodes' own cost.
+    pnet = net
+    if exchanged and args.exchange == "async":   # an async ctx runs async steps only
+        pnet = make_net(B, S, args.replay, local, rank)
+    pcfg = cfg if (exchanged and args.exchange == "allreduce") else \
+        pnet.step_cfg(args.rule, lr=1e-4, target_period=10, exchange="none", seed=1234)
+    avg = dict(pnet.profile_graph(pcfg, reps=max(1, args.profile_steps)))
+    node_us = avg.pop("apply", None)
     flops = kernel_flops(B, S)
     dom = max((k for k in avg if k in flops), key=lambda k: avg[k])
-    # the roofline kernel's launch time: back-to-back launches between two
-    # HIP events (the per-kernel events above add their own overhead)
-    dom_us = net.time_layer(dom, 100) if dom.endswith("_fwd") and dom.startswith("conv") \
-        else avg[dom]
+    dom_us = avg[dom]
+    # for reference: the same layer launched 100 times back to back on the same
+    # cache-warm input (not the roofline figure)
+    iso_us = pnet.time_layer(dom, 100) if dom.endswith("_fwd") and dom.startswith("conv") \
+        else None
+    if pnet is not net:
+        pnet.close()
     achieved = flops[dom] / (dom_us * 1e-6) / 1e12
     step_flops = net.step_flops()
     step_rl = step_roofline(B, S, net.num_params)
@@ -715,17 +754,23 @@ def main():
                          "traffic": traffic, "traffic_unit": "bytes/launch",
                          "traffic_source": traffic_src,
                          "kernel_us": round(dom_us, 3),
-                         "kernel_us_timing": "100 back-to-back launches between HIP events "
-                                             "on the ctx stream",
+                         "kernel_us_timing": "in-step: mean over the graph-replayed pipelined "
+                                             "chain (8-step graphs, event-record nodes around "
+                                             "every kernel on the ctx stream, %d replays); "
+                                             "event-node pair cost %s us"
+                                             % (max(1, args.profile_steps),
+                                                None if node_us is None else round(node_us, 3)),
+                         "isolated_us": None if iso_us is None else round(iso_us, 3),
+                         "isolated_timing": "the same layer, 100 back-to-back launches on one "
+                                            "cache-warm input (not the roofline figure)",
                          "step_tflops": round(step_flops / (dt / args.steps) / 1e12, 3),
                          "step_ideal_us": step_rl["ideal_us"],
                          "step_frac": round(step_rl["ideal_us"] * 1e-3 / (dt / args.steps * 1e3), 4),
                          "step_frac_basis": "step_roofline(): MFMA kernels at their "
                                             "arithmetic's peak + algorithmic HBM bytes"},
             "kernels_us": {k: round(v, 2) for k, v in avg.items()},
-            "kernels_us_timing": "eager step, one HIP event pair per launch (ddq_profile_step): "
-                                 "5-15 % above the graph-replayed rocprofv3 averages "
-                                 "(profiles/rNN_kernel_stats_step.csv)",
+            "kernels_us_timing": "in-step, graph-replayed pipelined chain (ddq_profile_graph); "
+                                 "compare profiles/rNN_kernel_stats_step.csv (rocprofv3)",
             "kernel_roofline": kernel_roofline(avg, B, S, net.num_params),
             "step_ms_distribution": dist_ms,
             "final_loss": loss,
@@ -743,7 +788,7 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(B, S, seed=7)
         if not args.no_exchange_paths and world == 1 and not args.force_exchange:
-            out["exchange_paths"] = exchange_paths(net, args.rule, out["value"])
+            out["exchange_paths"] = exchange_paths(net, args.rule)
         print(json.dumps(out), file=json_out, flush=True)
     if world > 1:
         dist.barrier()

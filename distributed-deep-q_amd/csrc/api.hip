@@ -108,6 +108,7 @@ struct ddq_ctx {
   std::vector<std::pair<std::string, hipEvent_t>> marks;
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
+  bool mark_external = false;        // marks recorded as event nodes of a captured graph
 };
 
 static int fail(ddq_ctx* c, int code, const char* fmt, ...) {
@@ -289,7 +290,6 @@ int ddq_create(ddq_ctx** out, int device, const ddq_net_desc* desc) {
     TRY(dalloc(c, &nb.opt, (size_t)P + kShardPad));
     nb.book_inc = 1;
     TRY(dalloc(c, &nb.opt_init, 4));
-    TRY(dalloc(c, &nb.chain, 4));
     TRY(dalloc(c, &nb.iter, 1));
     // acting scratch (n <= B)
     TRY(dalloc(c, &c->act_u8, (size_t)B * 4 * S * S));
@@ -1122,7 +1122,6 @@ static int enqueue_train(ddq_ctx* c, const ddq_step_cfg* cfg, const NetBuffers& 
   NetBuffers nb = nb_in;
   nb.book_inc = step_inc(c, cfg);
   // exchange-free steps: fc4's weight update rides on the slab-reduce launch
-  // (DDQ_VARIANT bit 512: off, A/B); per-kernel profiling keeps it separate
   const int ex = has_exchange(c, cfg) ? cfg->exchange : DDQ_EXCHANGE_NONE;
   const bool ar_overlap = ex == DDQ_EXCHANGE_ALLREDUCE && cfg->overlap && c->comm;
   if ((ex == DDQ_EXCHANGE_NONE || ar_overlap) && fused_apply_ok(nb.L)) {
@@ -1490,6 +1489,22 @@ static int ensure_async_graph(ddq_ctx* c, const ddq_step_cfg* cfg, int K) {
   return DDQ_OK;
 }
 
+// After a replay of the round-robin graph: the graph's comm-stream work is a
+// branch of the launch, so the comm stream itself is not ordered behind it --
+// make it wait for the launch (the eager ticks / rounds that follow queue
+// RCCL calls, owner applies and gsl copies on it).  A graph replay re-records
+// no event either: grad_ev still marks the gradient from before the capture,
+// so record it again behind the launch (whose last round computed nb.grad),
+// and forget an earlier readiness observation.
+static int after_async_graph(ddq_ctx* c) {
+  HIP_TRY(c, hipEventRecord(c->cev[0], c->stream));
+  HIP_TRY(c, hipStreamWaitEvent(c->cs, c->cev[0], 0));
+  HIP_TRY(c, hipEventRecord(c->grad_ev, c->stream));
+  c->ready_seen = false;
+  c->grad_ev_captured = false;
+  return DDQ_OK;
+}
+
 static int async_graph_steps(ddq_ctx* c, const ddq_step_cfg* cfg, int nsteps) {
   TRY(async_prepare(c, cfg));
   const int K = async_graph_rounds(c, cfg);
@@ -1505,6 +1520,7 @@ static int async_graph_steps(ddq_ctx* c, const ddq_step_cfg* cfg, int nsteps) {
          async_phase(c, cfg) == c->agraph_phase)) {
       TRY(ensure_async_graph(c, cfg, K));
       HIP_TRY(c, hipGraphLaunch(c->agexec, c->stream));
+      TRY(after_async_graph(c));
       for (int k = 0; k < K; ++k)
         for (int w = 0; w < c->nranks; ++w) async_advance(c, w, c->applied + 1);
       c->steps += K;
@@ -1993,7 +2009,10 @@ static void mark_cb(void* arg, const char* name) {
     c->ev_pool.push_back(e);
   }
   hipEvent_t e = c->ev_pool[c->ev_used++];
-  hipEventRecord(e, c->stream);
+  if (c->mark_external)   // inside a stream capture: an event-record node of the graph
+    hipEventRecordWithFlags(e, c->stream, hipEventRecordExternal);
+  else
+    hipEventRecord(e, c->stream);
   c->marks.emplace_back(name, e);
 }
 
@@ -2021,6 +2040,80 @@ int ddq_profile_step(ddq_ctx* c, const ddq_step_cfg* cfg, char* names, float* us
     if (names) {
       memset(names + 16 * i, 0, 16);
       strncpy(names + 16 * i, c->marks[i].first.c_str(), 15);
+    }
+  }
+  return DDQ_OK;
+}
+
+// The step kernels' device times INSIDE the graph-replayed pipelined chain
+// the bench times: kGraphSteps pipelined steps (ensure_pipe's pexec_k form,
+// fused prefetch) captured with an event-record node between every two
+// kernels, replayed reps times (each replay trains: counters advance as in
+// ddq_step_pipelined_async); per kernel name the mean over the steps and
+// replays of the time between its two event nodes.  The names are the marks
+// of ddq_profile_step, in step order; an interval holding no kernel (the
+// fused step's "apply" mark) measures the event nodes' own cost.
+int ddq_profile_graph(ddq_ctx* c, const ddq_step_cfg* cfg, int32_t reps, char* names, float* usec,
+                      int32_t cap, int32_t* n) {
+  TRY(check_step(c, cfg));
+  if (!n || reps < 1) return fail(c, DDQ_EINVAL, "profile_graph: bad arguments");
+  if (is_async(c, cfg) || !fused_prefetch(c, cfg))
+    return fail(c, DDQ_EINVAL, "profile_graph: pipelined steps with the fused prefetch only "
+                               "(exchange none or allreduce, batch <= 256)");
+  TRY(set_dev(c));
+  TRY(ensure_pipe(c, cfg));   // the second minibatch set
+  ReplayMeta* bump = c->r_meta;
+  c->marks.clear();
+  c->ev_used = 0;
+  c->mark_external = true;
+  hipGraphExec_t exec = nullptr;
+  int rc = capture_exec(c, &exec, [&]() -> int {
+    for (int k = 0; k < kGraphSteps; ++k) {
+      const NetBuffers cur = mb_view(c, k & 1), nxt = mb_view(c, 1 - (k & 1));
+      TRY(enqueue_train(c, cfg, cur, &nxt, mark_cb, c, bump));
+    }
+    mark_cb(c, "end");
+    return DDQ_OK;
+  });
+  c->mark_external = false;
+  if (rc != DDQ_OK) return rc;
+  std::vector<std::string> order;
+  std::vector<double> sum;
+  std::vector<int> cnt;
+  rc = [&]() -> int {
+    if (c->steps == 0) TRY(initial_target_sync(c, cfg));
+    const NetBuffers first = mb_view(c, 0);
+    HIP_TRY(c, launch_sample_gather(first, c->r_state, c->r_action, c->r_reward, c->r_nonterm,
+                                    c->r_meta, cfg->seed, c->stream));
+    for (int r = 0; r < reps; ++r) {
+      HIP_TRY(c, hipGraphLaunch(exec, c->stream));
+      HIP_TRY(c, hipStreamSynchronize(c->stream));
+      c->steps += kGraphSteps;
+      c->applied += (int64_t)kGraphSteps * step_inc(c, cfg);
+      for (size_t i = 0; i + 1 < c->marks.size(); ++i) {
+        float ms = 0.f;
+        HIP_TRY(c, hipEventElapsedTime(&ms, c->marks[i].second, c->marks[i + 1].second));
+        size_t j = 0;
+        while (j < order.size() && order[j] != c->marks[i].first) ++j;
+        if (j == order.size()) {
+          order.push_back(c->marks[i].first);
+          sum.push_back(0.0);
+          cnt.push_back(0);
+        }
+        sum[j] += ms * 1000.0;
+        cnt[j] += 1;
+      }
+    }
+    return DDQ_OK;
+  }();
+  hipGraphExecDestroy(exec);
+  if (rc != DDQ_OK) return rc;
+  *n = (int32_t)order.size();
+  for (int i = 0; i < (int)order.size() && i < cap; ++i) {
+    if (usec) usec[i] = (float)(sum[i] / cnt[i]);
+    if (names) {
+      memset(names + 16 * i, 0, 16);
+      strncpy(names + 16 * i, order[i].c_str(), 15);
     }
   }
   return DDQ_OK;

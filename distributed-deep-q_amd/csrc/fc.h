@@ -29,12 +29,6 @@ __device__ __forceinline__ float4 fc_ld4(__amdgpu_buffer_rsrc_t r, uint32_t off)
   auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
   return *reinterpret_cast<float4*>(&v);
 }
-// sc1 (L2-served, L1 bypassed): bytes another workgroup of the same launch
-// stored sc1 and signalled for (fc4 chain, MI355X_MICROARCH.md hand-off table)
-__device__ __forceinline__ float4 fc_ld4_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 16);
-  return *reinterpret_cast<float4*>(&v);
-}
 __device__ __forceinline__ float fc_ld1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   auto v = __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
   return __builtin_bit_cast(float, v);
@@ -46,7 +40,7 @@ constexpr uint32_t kFcOOB = 0x80000000u;
 // grid (512/128, splits, nz), 4 waves; wave w owns n0 = 128*bx + 32*w, all b.
 // x = pool3 in Caffe NCHW order (B, K); W4 Caffe (512, K).  K % 32 == 0.
 // ---------------------------------------------------------------------------
-constexpr int kFc4KLen = DDQ_AB_FC4_KLEN;     // k per split (128)
+constexpr int kFc4KLen = 128;                // k per split (64: head 6.6 -> 8.4 us; 256: fc4 fwd 6.0 -> 8.7)
 
 struct Fc4FwdArgs {
   int B, K, nz;
@@ -307,14 +301,9 @@ struct Fc4DgradArgs {
 // KCW kc columns per block (32, or 16 -- the MFMA's other 16 columns read
 // nothing and are dropped): K / 16 blocks fill the 256 CUs at 64x64, where
 // K / 32 = 128 blocks streamed W4 on half of them (1.3 TB/s).
-struct NoWait {
-  __device__ void operator()() const {}
-};
-// SC1 + wait (fc4 chain): the W4 loads are issued, then wait() (dh4 is being
-// produced by other workgroups of the launch), then the dh4 loads (sc1)
-template <bool SPLIT, int KCW = 32, bool SC1 = false, class Wait = NoWait>
+template <bool SPLIT, int KCW = 32>
 __device__ __forceinline__ void fc4_dgrad_body(const Fc4DgradArgs& a, float (*red)[1024], int bx,
-                                               int by, const Wait& wait = Wait()) {
+                                               int by) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int l31 = lane & 31, h = lane >> 5;
   const int kc0 = bx * KCW, b0 = by * 32;
@@ -333,13 +322,10 @@ __device__ __forceinline__ void fc4_dgrad_body(const Fc4DgradArgs& a, float (*re
 #pragma unroll
     for (int j = 0; j < 16; ++j)
       bv[blk][j] = fc_ld1(rb, bcol ? boff + (uint32_t)((blk * 32 + j) * K) * 4 : kFcOOB);
-  wait();
 #pragma unroll
   for (int blk = 0; blk < 2; ++blk)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      av[blk][i] = SC1 ? fc_ld4_sc1(ra, aoff + (blk * 32 + 4 * i) * 4)
-                       : fc_ld4(ra, aoff + (blk * 32 + 4 * i) * 4);
+    for (int i = 0; i < 4; ++i) av[blk][i] = fc_ld4(ra, aoff + (blk * 32 + 4 * i) * 4);
   __builtin_amdgcn_sched_barrier(0);   // keep every load ahead of the first MFMA
   f32x16 acc;
 #pragma unroll

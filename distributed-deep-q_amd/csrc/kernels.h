@@ -88,12 +88,7 @@ struct NetBuffers {
   FusedApplyCfg fa;                 // on: head latches the apply flags, the slab reduce
                                     // applies (FusedApplyCfg)
   int book_inc;                     // param-server iterations per apply (1, or W: server mode)
-  int32_t* chain;                   // fc4 chain counters (4 int32, zero between launches)
 };
-
-// fc4 forward + head + fc4 data gradient as one launch (the head launch) for
-// this step (kernels.hip fc4_chain_kernel)
-bool fc4_chain_ok(const NetBuffers& nb);
 
 // fused device draw + gather for the step (B <= 256); counter advanced by the
 // step's apply bookkeeping (launch_backward's bump)

@@ -639,36 +639,8 @@ struct HeadArgs {
   int64_t wks_plane, wks2_off, wkst_off, wks3_off, wkst3_off;
 };
 
-// Intra-launch hand-off (fc4 chain): the storing workgroup's bytes are all
-// sc1 stores; every wave waits for them, then one lane adds to the counter
-// (MI355X_MICROARCH.md hand-off table, first row).  The consumer polls the
-// counter with sc1 loads (one lane), the workgroup joins at a barrier, and
-// every load of the handed-off bytes is an sc1 load.  A poll that has not
-// matched after 0.2 s gives up and raises err (wrong results, no hang).
-__device__ __forceinline__ void chain_signal(int32_t* ctr) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void chain_wait(const int32_t* ctr, int target, int32_t* err) {
-  if (threadIdx.x == 0) {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
-    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {
-        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
-  __syncthreads();
-}
-
-// One head block b (SC1: chain mode -- wait() before the partials, sc1
-// partial loads and dh4 stores, then the signal on done)
-template <bool SC1 = false, class Wait = NoWait>
-__device__ __forceinline__ void head_body(const HeadArgs& H, int b, char* smem,
-                                          const Wait& wait = Wait(), int32_t* done = nullptr) {
+// One head block b
+__device__ __forceinline__ void head_body(const HeadArgs& H, int b, char* smem) {
   const float* __restrict__ part = H.part;
   const int splits = H.splits, B = H.B;
   const float gamma = H.gamma;
@@ -729,29 +701,18 @@ __device__ __forceinline__ void head_body(const HeadArgs& H, int b, char* smem,
 #pragma unroll
   for (int a = 0; a < 4; ++a) acv[a] = action[b * 4 + a];
   const float ntb = nonterm[b], rwb = reward[b];
-  wait();
   // split-K partial sums of both towers, summed in split order
   float acc2[2] = {0.f, 0.f};
   {
     const float* p0 = part + (size_t)b * kFc4 + n;
     const float* p1 = part + ((size_t)B + b) * kFc4 + n;
-    const __amdgpu_buffer_rsrc_t rpt =
-        __builtin_amdgcn_make_buffer_rsrc((void*)part, (short)0, (int)(splits * stride * 4), 0x00020000);
-    const uint32_t o0 = (uint32_t)((size_t)b * kFc4 + n) * 4, o1 = (uint32_t)(((size_t)B + b) * kFc4 + n) * 4;
     for (int s = 0; s < splits; s += 32) {
       float v[2][32];
 #pragma unroll
       for (int u = 0; u < 32; ++u) {           // clamped, unconditional loads
         const int su = min(s + u, splits - 1);
-        if (SC1) {
-          v[0][u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                  rpt, (int)(o0 + (uint32_t)(su * stride) * 4), 0, 16));
-          v[1][u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                  rpt, (int)(o1 + (uint32_t)(su * stride) * 4), 0, 16));
-        } else {
-          v[0][u] = p0[su * stride];
-          v[1][u] = p1[su * stride];
-        }
+        v[0][u] = p0[su * stride];
+        v[1][u] = p1[su * stride];
       }
 #pragma unroll
       for (int u = 0; u < 32; ++u) {
@@ -809,12 +770,7 @@ __device__ __forceinline__ void head_body(const HeadArgs& H, int b, char* smem,
   }
   const float v = dq[0] * w5v[0][0] + dq[1] * w5v[0][1] + dq[2] * w5v[0][2] + dq[3] * w5v[0][3];
   const float dv = h[0] > 0.f ? v : 0.f;                         // ReLU backward
-  if (SC1) {
-    wt_store(wt_rsrc(dh4, (uint32_t)((size_t)B * kFc4 * 4)), (uint32_t)((size_t)b * kFc4 + n) * 4, dv);
-    chain_signal(done);
-  } else {
-    dh4[(size_t)b * kFc4 + n] = dv;
-  }
+  dh4[(size_t)b * kFc4 + n] = dv;
 }
 
 __global__ __launch_bounds__(512) void fc4_head_kernel(const HeadArgs H) {
@@ -1014,77 +970,6 @@ static HeadArgs head_args(const NetBuffers& nb, ReplayMeta* bump) {
                   L.wks_off[2], L.wkst3_off};
 }
 
-// ---------------------------------------------------------------------------
-// fc4 chain: fc4 forward -> head -> fc4 data gradient as ONE launch
-// (train_val.prototxt:159-483 forward + backward to dpool3).  Three block
-// ranges, each waiting for the one before through a counter (chain_signal /
-// chain_wait); a range only waits for lower block indices, which every XCD
-// dispatches first, so the chain cannot deadlock whatever fits at once.  What
-// it buys: the data gradient's W4 stream (8.4 MB) is issued at dispatch, under
-// the forward's (16.8 MB) and the head's latency chain, and two launch
-// boundaries go.  The last data-gradient block zeroes the counters for the
-// next launch (every wait of this launch has then matched).  Training steps
-// with the fused apply (nw = 0) and B <= 32 only (fc4_chain_ok).
-// ---------------------------------------------------------------------------
-#if DDQ_FC4_CHAIN
-struct Fc4ChainArgs {
-  Fc4FwdArgs f;
-  int nF;                 // forward blocks [0, nF): 8 waves x 32 n, split-K partials
-  HeadArgs h;
-  int nH;                 // head blocks: B samples (they signal) + 34 weight transposes
-  Fc4DgradArgs d;
-  int ndx, nD;            // data-gradient blocks
-  int32_t* ctr;           // [0] forward blocks done, [1] head samples done,
-                          // [2] data-gradient blocks done, [3] timeout flag (sticky)
-};
-constexpr int kChainFwdN = 256;   // n per forward block (8 waves)
-constexpr int kChainSmemB = 32 * 1024;
-static_assert(kChainSmemB >= fc4_fwd_smem_bytes<1>() && kChainSmemB >= kWkstSmemB &&
-                  kChainSmemB >= 8 * 1024 * 4,
-              "chain LDS");
-
-template <int KCW>
-__global__ __launch_bounds__(512) void fc4_chain_kernel(const Fc4ChainArgs c) {
-  extern __shared__ __attribute__((aligned(16))) char sm_ch[];
-  int bid = blockIdx.x;
-  if (bid < c.nF) {
-    const int nxb = kFc4 / kChainFwdN, spl = (c.f.K + kFc4KLen - 1) / kFc4KLen;
-    fc4_fwd_split_body<1, kChainFwdN / 32>(c.f, sm_ch, bid % nxb, (bid / nxb) % spl,
-                                           bid / (nxb * spl));
-    chain_signal(c.ctr + 0);
-    return;
-  }
-  bid -= c.nF;
-  if (bid < c.nH) {
-    int32_t* err = c.ctr + 3;
-    const int32_t* fdone = c.ctr;
-    const int nF = c.nF;
-    head_body<true>(c.h, bid, sm_ch, [=]() { chain_wait(fdone, nF, err); }, c.ctr + 1);
-    return;
-  }
-  bid -= c.nH;
-  {
-    int32_t* err = c.ctr + 3;
-    const int32_t* hdone = c.ctr + 1;
-    const int B = c.h.B;
-    fc4_dgrad_body<true, KCW, true>(c.d, reinterpret_cast<float (*)[1024]>(sm_ch), bid % c.ndx,
-                                    bid / c.ndx, [=]() { chain_wait(hdone, B, err); });
-  }
-  __syncthreads();
-  if (threadIdx.x == 0 &&
-      __hip_atomic_fetch_add(c.ctr + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == c.nD - 1) {
-    __hip_atomic_store(c.ctr + 0, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(c.ctr + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(c.ctr + 2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-#endif
-
-bool fc4_chain_ok(const NetBuffers& nb) {
-  return DDQ_FC4_CHAIN && nb.chain && nb.B <= 32 && nb.fa.on && !nb.fa.ext && !nb.fwd_only;
-}
-
 static Fc4DgradArgs fc4_dgrad_args(const NetBuffers& nb, bool& narrow, int& ndx, int& nd) {
   const int s4 = nb.S / 8, B = nb.B;
   Fc4DgradArgs f;
@@ -1100,23 +985,6 @@ static Fc4DgradArgs fc4_dgrad_args(const NetBuffers& nb, bool& narrow, int& ndx,
 }
 
 hipError_t launch_head(const NetBuffers& nb, hipStream_t s, ReplayMeta* bump) {
-#if DDQ_FC4_CHAIN
-  if (fc4_chain_ok(nb)) {
-    Fc4ChainArgs c;
-    const int s4 = nb.S / 8;
-    c.f.B = nb.B; c.f.K = 64 * s4 * s4; c.f.nz = 2; c.f.part = nb.fc4_part;
-    for (int z = 0; z < 2; ++z) { c.f.x[z] = nb.pool3[z]; c.f.w[z] = nb.theta[z] + nb.L.w[3]; }
-    c.nF = (kFc4 / kChainFwdN) * fc4_fwd_splits(c.f.K) * 2;
-    c.h = head_args(nb, bump);
-    c.nH = nb.B + 25 + 9;
-    bool narrow;
-    c.d = fc4_dgrad_args(nb, narrow, c.ndx, c.nD);
-    c.ctr = nb.chain;
-    auto kern = narrow ? fc4_chain_kernel<16> : fc4_chain_kernel<32>;
-    hipLaunchKernelGGL(kern, dim3(c.nF + c.nH + c.nD), dim3(512), kChainSmemB, s, c);
-    return hipGetLastError();
-  }
-#endif
   hipLaunchKernelGGL(fc4_head_kernel, dim3(nb.B + 25 + 9), dim3(kFc4), 0, s, head_args(nb, bump));
   return hipGetLastError();
 }
@@ -1409,71 +1277,30 @@ __global__ __launch_bounds__(256, 4) void wgrad_reduce_kernel(
     const float* __restrict__ fc4_x, int fc4_k) {
   __shared__ float red[4][4][64];
   int bid = blockIdx.x;
-  if (DDQ_REDUCE_HEAD_FIRST && DDQ_REDUCE_PF_AFTER_HEAD) {   // head sums, then the prefetch
-    if (bid < kFc4 / 64) {
-      if (opt_init && bid == 0 && threadIdx.x == 0)
-        apply_book(iter, opt_init, book_period, bump, book_inc);
-      if (DDQ_AB_SKIP & 4) return;
-      head_sums(bid, hs.B, hs.dqbuf, hs.lpart, hs.h4q, hs.dh4, hs.loss, hs.gw5, hs.gb5, hs.gb4,
-                fat.rest != 0, fat, faa);
-      return;
-    }
-    bid -= kFc4 / 64;
-    if (bid < pf.ng) {
-      if (!(DDQ_AB_SKIP & 8)) prefetch_body(pf, bid);
-      return;
-    }
-    bid = bid - pf.ng + kFc4 / 64;   // the head-first numbering below, past its head blocks
-  } else if (bid < pf.ng) {   // fused apply: the next step's draw + gather first
-    if (!(DDQ_AB_SKIP & 8)) prefetch_body(pf, bid);
+  // block order: the next step's draw + gather (fused apply), then the head
+  // sums' dependent latency chains (behind 800+ HBM-streaming blocks they
+  // cost 3 us: reduce 19.4 -> 16.4), then the fused fc4-weight apply tiles
+  // (the longest HBM streams start before the slab units: the other order
+  // measured 16.6 -> 22.6 us), then the slab units
+  if (bid < pf.ng) {
+    prefetch_body(pf, bid);
     return;
-  } else {
-    bid -= pf.ng;
   }
+  bid -= pf.ng;
   const bool rest = fat.rest != 0;
-  if (DDQ_REDUCE_HEAD_FIRST) {   // the head sums' dependent latency chains next
-    if (bid < kFc4 / 64) {
-      if (opt_init && bid == 0 && threadIdx.x == 0)
-        apply_book(iter, opt_init, book_period, bump, book_inc);
-      if (DDQ_AB_SKIP & 4) return;
-      head_sums(bid, hs.B, hs.dqbuf, hs.lpart, hs.h4q, hs.dh4, hs.loss, hs.gw5, hs.gb5, hs.gb4,
-                rest, fat, faa);
-      return;
-    }
-    bid -= kFc4 / 64;
-  }
-  if (DDQ_REDUCE_HEAD_FIRST && DDQ_REDUCE_SLABS_FIRST && fat.nfa > 0) {
-    // the slab units' latency chains ahead of the fc4 apply tiles' HBM streams
-    if (bid < nub) {
-      if (DDQ_AB_SKIP & 2) return;
-      const WredDims& d = bid >= d1.blk0 ? d1 : (bid >= d2.blk0 ? d2 : d0);
-      if (d.G == 1)
-        wred_block<1>(part, grad, d, bid - d.blk0, red, rest, fat, faa);
-      else if (d.G == 2)
-        wred_block<2>(part, grad, d, bid - d.blk0, red, rest, fat, faa);
-      else
-        wred_block<4>(part, grad, d, bid - d.blk0, red, rest, fat, faa);
-      return;
-    }
-    if (!(DDQ_AB_SKIP & 1)) fc4_apply_tile(fat, faa, hs.B, fc4_k, hs.dh4, fc4_x, bid - nub);
+  if (bid < kFc4 / 64) {
+    if (opt_init && bid == 0 && threadIdx.x == 0)
+      apply_book(iter, opt_init, book_period, bump, book_inc);
+    head_sums(bid, hs.B, hs.dqbuf, hs.lpart, hs.h4q, hs.dh4, hs.loss, hs.gw5, hs.gb5, hs.gb4,
+              rest, fat, faa);
     return;
   }
-  if (fat.nfa > 0) {   // fused fc4-weight gradient + apply blocks come first: the
-                       // longest HBM streams start before the reduce blocks
-    if (bid < fat.nfa) {
-      if (!(DDQ_AB_SKIP & 1)) fc4_apply_tile(fat, faa, hs.B, fc4_k, hs.dh4, fc4_x, bid);
-      return;
-    }
-    bid -= fat.nfa;
-  }
-  if (!DDQ_REDUCE_HEAD_FIRST && opt_init && bid == 0 && threadIdx.x == 0)
-    apply_book(iter, opt_init, book_period, bump, book_inc);
-  if (DDQ_AB_SKIP & (bid >= nub ? 4 : 2)) return;
-  if (bid >= nub) {
-    head_sums(bid - nub, hs.B, hs.dqbuf, hs.lpart, hs.h4q, hs.dh4, hs.loss, hs.gw5, hs.gb5,
-              hs.gb4, rest, fat, faa);
+  bid -= kFc4 / 64;
+  if (bid < fat.nfa) {
+    fc4_apply_tile(fat, faa, hs.B, fc4_k, hs.dh4, fc4_x, bid);
     return;
   }
+  bid -= fat.nfa;
   const WredDims& d = bid >= d1.blk0 ? d1 : (bid >= d2.blk0 ? d2 : d0);
   if (d.G == 1)
     wred_block<1>(part, grad, d, bid - d.blk0, red, rest, fat, faa);
@@ -1605,73 +1432,6 @@ static ApplyTail apply_tail(const NetBuffers& nb) {
   return t;
 }
 
-#if DDQ_FA_IN_PAIR
-// conv2 + conv3 weight gradients (wgrads_pair_kernel) with the fused fc4-weight
-// apply blocks (fc4_apply_tile) interleaved in chunks of 8 blocks: the
-// HBM-bound apply streams (42 MB at 64x64) run under the MFMA-bound weight
-// gradients instead of in the slab-reduce launch.  Chunk c is an apply chunk
-// when c is odd and apply chunks remain; every wgrad chunk keeps its block
-// index mod 8 (the XCD-aware decode of wgrads_body).  Legal here: fc4's
-// weight gradient needs dh4 (head) and pool3 (forward) only, nothing later in
-// the step reads W4, and the apply flags were latched by the head.
-template <int CIN0, int COUT0, int KS0, int PAD0, int WMAX0, int DSRC0, int CIN1, int COUT1,
-          int KS1, int PAD1, int WMAX1, int DSRC1>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void wgrads_pair_fa_kernel(
-    const WgradSArgs a0, const WgradSArgs a1, int n0, int nfa, ApplyTail fat, ApplyArgs faa,
-    int B, int K, const float* dh4, const float* x) {
-  extern __shared__ __attribute__((aligned(16))) char sm_wgpa[];
-  const int c = blockIdx.x >> 3, nac = nfa >> 3;
-  if ((c & 1) && (c >> 1) < nac) {
-    fc4_apply_tile(fat, faa, B, K, dh4, x, (c >> 1) * 8 + (blockIdx.x & 7));
-    return;
-  }
-  const int L = (c - min((c + 1) >> 1, nac)) * 8 + (blockIdx.x & 7);
-  if (L < n0)
-    wgrads_body<CIN0, COUT0, KS0, PAD0, WMAX0, DSRC0>(a0, sm_wgpa, L);
-  else
-    wgrads_body<CIN1, COUT1, KS1, PAD1, WMAX1, DSRC1>(a1, sm_wgpa, L - n0);
-}
-
-template <int CIN0, int COUT0, int KS0, int PAD0, int WMAX0, int DSRC0, int CIN1, int COUT1,
-          int KS1, int PAD1, int WMAX1, int DSRC1>
-static hipError_t launch_wgrads_pair_fa_w(const WgradSArgs& a0, const WgradSArgs& a1, int nfa,
-                                          const ApplyTail& fat, const ApplyArgs& faa, int B, int K,
-                                          const float* dh4, const float* x, hipStream_t st) {
-  const size_t s0 = wgrads_smem_bytes<CIN0, PAD0>(a0.W), s1 = wgrads_smem_bytes<CIN1, PAD1>(a1.W);
-  const size_t shm = s0 > s1 ? s0 : s1;
-  if (shm > 160 * 1024 || nfa % 8) return hipErrorInvalidValue;
-  auto kern = wgrads_pair_fa_kernel<CIN0, COUT0, KS0, PAD0, WMAX0, DSRC0, CIN1, COUT1, KS1, PAD1,
-                                    WMAX1, DSRC1>;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
-  const int n0 = (a0.G + 7) / 8 * 8 * (COUT0 / 32) * KS0;
-  const int n1 = (a1.G + 7) / 8 * 8 * (COUT1 / 32) * KS1;
-  hipLaunchKernelGGL(kern, dim3(n0 + n1 + nfa), dim3(256), shm, st, a0, a1, n0, nfa, fat, faa, B, K,
-                     dh4, x);
-  return hipGetLastError();
-}
-
-static hipError_t launch_wgrads_conv23_fa(const WgradSArgs& a2, const WgradSArgs& a3, int nfa,
-                                          const ApplyTail& fat, const ApplyArgs& faa, int B, int K,
-                                          const float* dh4, const float* x, hipStream_t st) {
-  if (a2.W <= 16)
-    return launch_wgrads_pair_fa_w<32, 64, 5, 2, 16, 0, 64, 64, 3, 1, 16, 2>(a2, a3, nfa, fat, faa, B,
-                                                                             K, dh4, x, st);
-  if (a2.W <= 32)
-    return launch_wgrads_pair_fa_w<32, 64, 5, 2, 32, 0, 64, 64, 3, 1, 16, 2>(a2, a3, nfa, fat, faa, B,
-                                                                             K, dh4, x, st);
-  if (a2.W <= 64)
-    return launch_wgrads_pair_fa_w<32, 64, 5, 2, 64, 0, 64, 64, 3, 1, 32, 2>(a2, a3, nfa, fat, faa, B,
-                                                                             K, dh4, x, st);
-  return hipErrorInvalidValue;
-}
-#endif
-
 // The fused fc4-weight apply (NetBuffers::fa): fc4's weight gradient is final
 // after the fc4 backward, so its update runs as extra blocks of the slab-
 // reduce launch and the apply launch keeps the rest of the parameters.
@@ -1767,8 +1527,7 @@ template <int TY, int TX, int WM>
 constexpr TileOpt conv1_tile() { return {TY, TX, WM * Conv1Cfg<TY, TX, WM>::TM * 32}; }
 
 template <class T, int n>
-static const T& pick_tile(const T (&menu)[n], int H, int W, int force = -1) {
-  if (force >= 0 && force < n) return menu[force];   // A/B: DDQ_AB_TILE_*
+static const T& pick_tile(const T (&menu)[n], int H, int W) {
   auto cost = [&](const TileOpt& o) {
     return (int64_t)((H + o.ty - 1) / o.ty) * ((W + o.tx - 1) / o.tx) * (o.rows + 32);
   };
@@ -1830,10 +1589,10 @@ static const Conv1Menu kConv1Fwd[] = {DDQ_CONV1_TILE(32, 32, 16), DDQ_CONV1_TILE
                                       DDQ_CONV1_TILE(16, 16, 8), DDQ_CONV1_TILE(24, 24, 9)};
 #undef DDQ_CONV1_TILE
 
-// conv1 weight-gradient band height: the largest power of two <= DDQ_AB_W1BAND (8) dividing
+// conv1 weight-gradient band height: the largest power of two <= 8 dividing
 // S (one slab per band)
 static int wgrad1_band(int S) {
-  int R = DDQ_AB_W1BAND;
+  int R = 8;
   while (R > 1 && S % R != 0) R >>= 1;
   return R;
 }
@@ -1847,7 +1606,9 @@ int wgrad_splits_for(int layer, int B, int S, int* np) {
   *np = ((KC[layer] + 1 + 63) / 64) * 64;
   if (layer == 0) return B * (S / wgrad1_band(S));
   const int nts[3] = {0, 2 * 5, 2 * 3};
-  const int target[3] = {0, DDQ_AB_WG_TARGET2, DDQ_AB_WG_TARGET3};
+  // about 256 workgroups each (24 / 40 slabs at 64x64 B=32: fewer, larger
+  // slabs than at 512 -- pair 30.0 -> 27.7 us, reduce 21.9 -> 19.2)
+  const int target[3] = {0, 256, 256};
   int G, RPG;
   wgrads_groups(B * H, nts[layer], &G, &RPG, target[layer]);
   return G;
@@ -1864,7 +1625,7 @@ __global__ __launch_bounds__(512) void fc4_bwd_kernel(const Fc4DgradArgs d, cons
   const int bid = blockIdx.x;
   if (bid < nd) {
     int lb = bid;
-    if (DDQ_FC4BWD_XCD && KCW == 16 && nd % 16 == 0) {
+    if (KCW == 16 && nd % 16 == 0) {
       // 16-column blocks 2m and 2m+1 read the two halves of the same 128-byte
       // W4 lines: dispatch them to one XCD (workgroup i runs on XCD i % 8), so
       // that XCD's L2 fetches each line once
@@ -1908,12 +1669,7 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     c1.out_elems = (int64_t)B * (S / 2) * (S / 2) * 32;
     c1.mask[0] = nb.mask1; c1.mask[1] = nullptr;
     M("conv1_fwd");
-#if DDQ_CONV1_PIPE
-    if (S % 16 == 0)
-      CHECK_LAUNCH((launch_split_conv1_pipe<16, 16, 8>(c1, nz, s, L.wks_total)));
-    else
-#endif
-      CHECK_LAUNCH(pick_tile(kConv1Fwd, S, S, DDQ_AB_TILE_C1F).launch(c1, nz, s, L.wks_total));
+    CHECK_LAUNCH(pick_tile(kConv1Fwd, S, S).launch(c1, nz, s, L.wks_total));
   }
   if (!nb.fwd_only || nb.fwd_only == 2) {
     // conv2 (train_val.prototxt:79-118): split bf16, 16x16 tiles, 16 waves of
@@ -1933,12 +1689,7 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     a2.out_elems = (int64_t)B * (H / 2) * (H / 2) * 64;
     a2.mask[0] = nb.mask2; a2.mask[1] = nullptr;
     M("conv2_fwd");
-#if DDQ_CONV2_PIPE
-    if (H % 16 == 0)
-      CHECK_LAUNCH((launch_split_conv_pipe<32, 32, 64, 5, 8, 16, 4, 2, 1, false>(a2, nz, s)));
-    else
-#endif
-      CHECK_LAUNCH(pick_tile(kConv2Fwd, H, H, DDQ_AB_TILE_C2F).launch(a2, nz, s));
+    CHECK_LAUNCH(pick_tile(kConv2Fwd, H, H).launch(a2, nz, s));
   }
   if (!nb.fwd_only || nb.fwd_only == 3) {
     // conv3 (train_val.prototxt:119-158): split bf16, 8x8 tiles (kConv3Fwd), two k groups
@@ -1958,14 +1709,9 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     a3.nchw = 1;
     a3.mask[0] = nb.mask3; a3.mask[1] = nullptr;
     M("conv3_fwd");
-#if DDQ_AB_C3F_WIDE   // A/B: 8 x 16 tiles, 16 waves (half the workgroups, half the weight streaming)
-    CHECK_LAUNCH((launch_split_conv<64, 64, 64, 3, 8, 16, 4, 2, 2, false>(a3, nz, s)));
-#else
-    CHECK_LAUNCH(pick_tile(kConv3Fwd, H, H, DDQ_AB_TILE_C3F).launch(a3, nz, s));
-#endif
+    CHECK_LAUNCH(pick_tile(kConv3Fwd, H, H).launch(a3, nz, s));
   }
   if (nb.fwd_only) return hipSuccess;   // ddq_time_layer: one conv layer
-  if (!out && fc4_chain_ok(nb)) return hipSuccess;   // the head launch runs fc4 (fc4 chain)
   // fc4 (train_val.prototxt:159-185): split bf16 MFMA register-direct, split-K
   // partials (reduced by the head kernel, or by fc4_reduce_out below)
   const int s4 = S / 8;
@@ -1992,9 +1738,8 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
   const int B = nb.B, S = nb.S;
   const int s4 = S / 8;
   auto M = [&](const char* n) { if (mark) mark(marg, n); };
-  if (!fc4_chain_ok(nb)) {  // fc4 (train_val.prototxt:159-185): data gradient -> pooled
-     // dpool3, and the weight gradient unless the fused apply computes it itself
-     // (the fc4 chain ran the data gradient in the head launch)
+  {  // fc4 (train_val.prototxt:159-185): data gradient -> pooled dpool3, and
+     // the weight gradient unless the fused apply computes it itself
     bool narrow;
     int ndx, nd;
     Fc4DgradArgs f = fc4_dgrad_args(nb, narrow, ndx, nd);
@@ -2020,13 +1765,8 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     a.pd_split = nb.dconv2s; a.pd_elems = (int64_t)B * H * H * 64;
     a.xsplit = nb.dconv3s; a.x_elems = (int64_t)B * H * H * 64;
     M("conv3_dgrad");
-    CHECK_LAUNCH(pick_tile(kConv3Dgrad, H, H, DDQ_AB_TILE_C3D).launch(a, 1, s));
+    CHECK_LAUNCH(pick_tile(kConv3Dgrad, H, H).launch(a, 1, s));
   }
-  // exchange-free fused steps: the fc4-weight apply rides on the weight-gradient
-  // pair launch (DDQ_FA_IN_PAIR) instead of the slab-reduce launch
-  const bool fa_in_pair = DDQ_FA_IN_PAIR && nb.fa.on && !nb.fa.ext &&
-                          fc4_wgrad_blocks<kFc4ApplyR>(64 * s4 * s4) % 8 == 0;
-  [[maybe_unused]] const int nfa_pair = fa_in_pair ? fc4_wgrad_blocks<kFc4ApplyR>(64 * s4 * s4) : 0;
   {  // conv3 weight gradient (split bf16, wgrads.h): rows of the expanded split
      // dconv3 (pure copies) against the split pool2; conv2's on the split
      // pooled dpool2 and the split pool1
@@ -2045,23 +1785,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     // one launch (wgrads_pair_kernel, conv2's blocks first): 35.2 -> 30.2 us
     // against the two launches, same-box kernel trace
     M("conv23_wgrad");
-#if DDQ_FA_IN_PAIR
-    if (fa_in_pair) {   // + the fused fc4-weight apply blocks (wgrads_pair_fa_kernel)
-      ApplyTail fat = apply_tail(nb);
-      ApplyArgs faa = apply_args(nb, nb.fa.rule, nb.fa.lr, nb.fa.decay, nb.fa.eps, nb.fa.momentum,
-                                 nb.fa.wd, nb.fa.period);
-      faa.lo = L.w[3];
-      faa.hi = L.b[3];
-      fat.nfa = nfa_pair;
-      fat.ext = 0;
-      fat.rest = 1;
-      CHECK_LAUNCH(launch_wgrads_conv23_fa(w2, w3, nfa_pair, fat, faa, B, 64 * s4 * s4, nb.dh4,
-                                           nb.pool3[0], s));
-    } else
-#endif
-    {
-      CHECK_LAUNCH(launch_wgrads_conv23(w2, w3, s));
-    }
+    CHECK_LAUNCH(launch_wgrads_conv23(w2, w3, s));
   }
   {  // conv2 data gradient -> split pooled dpool1 (split bf16, DGRAD): the
      // split pooled dpool2 expanded through mask2 while staged, the transposed
@@ -2075,12 +1799,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     a.in_route = nb.mask2;
     a.pd_split = nb.dconv1s; a.pd_elems = (int64_t)B * H * H * 32;
     M("conv2_dgrad");
-#if DDQ_C2D_PIPE
-    if (H % 16 == 0)   // two 32-channel chunks, pipelined
-      CHECK_LAUNCH((launch_split_conv_pipe<64, 32, 32, 5, 8, 16, 4, 1, 2, true>(a, 1, s)));
-    else
-#endif
-      CHECK_LAUNCH(pick_tile(kConv2Dgrad, H, H, DDQ_AB_TILE_C2D).launch(a, 1, s));
+    CHECK_LAUNCH(pick_tile(kConv2Dgrad, H, H).launch(a, 1, s));
   }
   // slab-reduce geometry: layer l's blocks start at d[l].blk0
   WredDims d[3];
@@ -2117,7 +1836,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     if (nb.fa.on) {   // fc4 weights [w4, b4): its gradient is final since fc4_bwd
       faa.lo = L.w[3];
       faa.hi = L.b[3];
-      nfa = fa_in_pair ? 0 : fc4_wgrad_blocks<kFc4ApplyR>(64 * s4 * s4);
+      nfa = fc4_wgrad_blocks<kFc4ApplyR>(64 * s4 * s4);
       fat.nfa = nfa;
       fat.ext = nb.fa.ext;
       // and everything else where its gradient is reduced -- unless the rest

@@ -146,10 +146,10 @@ struct SplitWStage {
   // lanes 4-7 hit the banks of lanes 0-3 when they write row n + 1; writing
   // rows n and n + 4 instead (80 dwords apart: the other 16 banks) is
   // conflict-free -- a permutation of the rows within blocks of 8, the same
-  // for the load and the store of a lane (DDQ_LDS_ROWPERM)
+  // for the load and the store of a lane
   static __device__ __forceinline__ int row(int q) {
     const int n0 = q / (CP / 8);
-    if (!DDQ_LDS_ROWPERM || CP != 32) return n0;
+    if (CP != 32) return n0;
     return (n0 & ~7) | ((n0 & 7) >> 1) | ((n0 & 1) << 2);
   }
 
@@ -171,7 +171,7 @@ struct SplitWStage {
       const int f0 = tid + S * C::kGroup;
       // lanes past the vectors store nothing (whole waves at these sizes:
       // a uniform branch); they used to rewrite the last vector
-      if (DDQ_LDS_ROWPERM && (3 * WV) % C::kGroup != 0 && f0 >= 3 * WV) continue;
+      if ((3 * WV) % C::kGroup != 0 && f0 >= 3 * WV) continue;
       const int f = (3 * WV) % C::kGroup == 0 || f0 < 3 * WV ? f0 : 3 * WV - 1;
       const int p = f / WV, q = f - p * WV;
       const int n = row(q), c8 = q % (CP / 8);
@@ -249,7 +249,6 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, const f32x16 
           const size_t onhwc = (((size_t)b * Hp + pyy) * Wp + pxx) * N + n;
           // (plain stores: write-through measured no faster here, and slower
           // for the scattered NCHW pool3 and the routing bytes)
-          if ((DDQ_AB_SKIP & 128) && a.B > 0) continue;   // A/B: no stores
           if (outz) outz[a.nchw ? (((size_t)b * N + n) * Hp + pyy) * Wp + pxx : onhwc] = o;
           if (osplit) store_split(osplit, a.out_elems, onhwc, o);
           if (maskz) maskz[onhwc] = (uint8_t)(pos ? arg : 4);
@@ -333,7 +332,6 @@ __device__ __forceinline__ void split_epilogue_fwd_lds(const SplitArgs& a,
     }
   }
   __syncthreads();
-  if ((DDQ_AB_SKIP & 128) && a.B > 0) return;   // A/B: no stores
   const int Hp = a.H >> 1, Wp = a.W >> 1;
   auto pix = [&](int win, int& off) {           // pooled NHWC pixel of window win
     const int pyy = y0 / 2 + win / (TX / 2), pxx = x0 / 2 + win % (TX / 2);
@@ -437,7 +435,7 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
       // 32-channel pixels (20 dwords apart): pixels q and q + 4 share an
       // 8-lane store group instead of q and q + 1 (SplitWStage::row)
       constexpr int NPX = C::PH * C::PW;
-      const int pix = (DDQ_LDS_ROWPERM && CP == 32 && pix0 < (NPX & ~7))
+      const int pix = (CP == 32 && pix0 < (NPX & ~7))
                           ? (pix0 & ~7) | ((pix0 & 7) >> 1) | ((pix0 & 1) << 2)
                           : pix0;
       const int py = pix / C::PW, px = pix % C::PW;
@@ -559,8 +557,7 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
     const int sc = st < NSTEP ? st : NSTEP - 1;
     w.load(wk, a.wk_elems, sc / T, sc % T, tid);
   };
-  constexpr bool kAbC2f = !DGRAD && CPT == 32;   // A/B: conv2 forward only
-  if (!(kAbC2f && (DDQ_AB_SKIP & 64))) stage_patch(0);
+  stage_patch(0);
   wload(ws0, 0);
   ws0.store(wbuf, tid);
   if (NSTEP > 1) wload(ws1, 1);
@@ -657,7 +654,7 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
     w.store(wbuf + ((s + 1) & 1) * 3 * C::kWSlot, tid);
     __syncthreads();
   };
-  for (int s = 0; s < ((kAbC2f && (DDQ_AB_SKIP & 16)) ? 0 : NSTEP); s += 2) {
+  for (int s = 0; s < NSTEP; s += 2) {
     if (s + 2 < NSTEP) {
       wload(ws0, s + 2);
       __builtin_amdgcn_sched_barrier(0);
@@ -701,7 +698,6 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
         }
       }
   }
-  if (kAbC2f && (DDQ_AB_SKIP & 32) && a.B > 0) return;   // (kept MFMAs: B unknown)
   if constexpr (!DGRAD && C::NWIN * N * 7 <= C::kSmemB) {
     split_epilogue_fwd_lds<TM, TN, TX, N, WK, C::NWIN, C::kThreads>(a, acc, bpre, smem, b, z, y0,
                                                                     x0, wmi, wni, l31, h, wkg, tid);
@@ -714,7 +710,6 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
 template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, bool DGRAD>
 __global__ __launch_bounds__(64 * WM * WN * WK) void split_conv_kernel(const SplitArgs a) {
   extern __shared__ __attribute__((aligned(16))) char sm_split[];
-  if (DDQ_AB_SETPRIO && (threadIdx.x >> 6) >= WM * WN * WK / 2) __builtin_amdgcn_s_setprio(1);
   split_conv_body<CPT, CP, N, KS, TY, TX, WM, WN, WK, DGRAD>(a, sm_split, blockIdx.x, blockIdx.y,
                                                             blockIdx.z);
 }
@@ -723,13 +718,9 @@ template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK
 inline hipError_t launch_split_conv(SplitArgs a, int nz, hipStream_t st) {
   using C = SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK>;
   auto kern = split_conv_kernel<CPT, CP, N, KS, TY, TX, WM, WN, WK, DGRAD>;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, C::kSmemB);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  static std::atomic<uint64_t> attr{0};
+  if (hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(kern), attr, (int)(C::kSmemB)))
+    return e;
   // the forward epilogue writes one of the fp32 / split outputs (see
   // split_epilogue_fwd_lds)
   if (!DGRAD && ((a.out[0] && a.out_split[0]) || (a.out[1] && a.out_split[1])))
@@ -738,331 +729,6 @@ inline hipError_t launch_split_conv(SplitArgs a, int nz, hipStream_t st) {
   const int tiles_y = (a.H + TY - 1) / TY;
   hipLaunchKernelGGL(kern, dim3(tiles_y * a.tiles_x, a.B, nz), dim3(C::kThreads), C::kSmemB, st,
                      a);
-  return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
-// Persistent, software-pipelined direct convolution.  The one-round launch
-// above stages its halo patch with nothing to overlap it (every CU loads at
-// once, then computes) and stores its outputs at the end (every CU stores at
-// once).  Here a workgroup per CU slot loops over units u = (tile, channel
-// chunk) of its tiles t = blockIdx.x, +gridDim.x, ... with two patch buffers:
-//  * unit u + 1's patch is loaded into registers when unit u starts (DGRAD:
-//    the pooled source and its routing bytes) and committed to the other
-//    buffer at tap kCommit of unit u (expanded through the routing bytes
-//    there); that buffer's last reader, unit u - 1 (or its epilogue),
-//    finished before unit u's first barrier;
-//  * a tile's epilogue runs after its last unit: the k groups meet in that
-//    unit's (now free) patch buffer, the forward gathers its pooled outputs
-//    there too, and the stores drain while the next tile's first taps run;
-//  * the weight ring runs on the global step g = (unit g / T, tap g % T):
-//    slot g & 1, chunk and tower of that unit, so unit boundaries cost no
-//    ring refill.
-// Tiles are numbered tower-major ((z, b, ty, tx)), so the tower of local tile
-// li is just blockIdx.x + li * gridDim.x >= tiles per tower.  Per output
-// element the accumulation order (chunk, tap, k-step, the six products, the k
-// groups in order) is that of split_conv_body with the same CP / WK: the
-// outputs are bit-identical to that configuration's.
-// ---------------------------------------------------------------------------
-template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, bool DGRAD>
-struct SplitPipeCfg {
-  using C = SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK>;
-  static constexpr int kSmemB = 2 * C::kPatchB + C::kWB;
-  static constexpr int kCommit = C::T / 2;   // tap at which the next patch is stored
-  static_assert(kSmemB <= 160 * 1024, "LDS budget (two patch buffers + ring)");
-  static_assert(DGRAD || C::NWIN * N * 7 <= C::kPatchB, "epilogue gather fits a patch buffer");
-  static_assert(WK == 1 || WK * WM * WN * 16 * 64 * 4 <= C::kPatchB, "k groups meet in a buffer");
-};
-
-template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, bool DGRAD>
-__device__ __forceinline__ void split_conv_pipe_body(const SplitArgs& a, char* smem, int ntiles,
-                                                     int tpi, int tpt) {
-  using P = SplitPipeCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK, DGRAD>;
-  using C = typename P::C;
-  constexpr int TM = C::TM, TN = C::TN, T = C::T, NCH = C::NCH;
-  constexpr int kPB = C::kPatchB / 2;                     // bf16 per patch buffer
-  __bf16* const patch0 = reinterpret_cast<__bf16*>(smem);
-  __bf16* const wbuf = reinterpret_cast<__bf16*>(smem + 2 * C::kPatchB);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int l31 = lane & 31, h = lane >> 5;
-  const int G = gridDim.x, bx = blockIdx.x;
-  const int nmine = bx < ntiles ? (ntiles - 1 - bx) / G + 1 : 0;
-  if (nmine == 0) return;
-  const int nunit = nmine * NCH;
-  const int nstep = nunit * T;
-  auto tower = [&](int li) { return bx + li * G >= tpt ? 1 : 0; };
-  // (b, y0, x0) of local tile li (runtime divisions: once per unit)
-  auto coords = [&](int li, int& b, int& y0, int& x0) {
-    int t = bx + li * G;
-    if (t >= tpt) t -= tpt;
-    b = t / tpi;
-    const int r = t - b * tpi;
-    const int ty = r / a.tiles_x;
-    y0 = ty * TY;
-    x0 = (r - ty * a.tiles_x) * TX;
-  };
-
-  // ---- halo patch of a unit: bounds-checked buffer loads into registers ----
-  constexpr uint32_t kOOB = 0x80000000u;
-  // plane extent of the split source: (B, H, W, CPT), pooled (B, H/2, W/2, CPT) for DGRAD
-  const uint32_t src_elems = DGRAD ? (uint32_t)(a.B * (a.H >> 1) * (a.W >> 1) * CPT)
-                                   : (uint32_t)(a.B * a.H * a.W * CPT);
-  constexpr int NV = C::PH * C::PW * (CP / 8);            // 16-byte vectors per plane
-  constexpr int NIT = (NV + C::kThreads - 1) / C::kThreads;
-  u32x4 pv[3][NIT];
-  u32x2 pm[DGRAD ? NIT : 1];                              // DGRAD: routing bytes
-  int pdst[NIT];
-  uint32_t pq[DGRAD ? NIT : 1];                           // DGRAD: quadrant of the pixel
-  auto patch_issue = [&](int u) {
-    const bool live = u < nunit;
-    const int li = live ? u / NCH : 0, ch = live ? u - li * NCH : 0;
-    int b = 0, y0 = 0, x0 = 0;
-    if (live) coords(li, b, y0, x0);
-    const __bf16* in = (live && tower(li)) ? a.in[1] : a.in[0];
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int f0 = tid + it * C::kThreads;
-      const bool ok = live && f0 < NV;
-      const int f = ok ? f0 : 0;
-      const int pix = f / (CP / 8), c8 = f % (CP / 8);
-      const int py = pix / C::PW, px = pix % C::PW;
-      const int gy = y0 - a.pad + py, gx = x0 - a.pad + px;
-      const bool in_img = ok && (unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W;
-      pdst[it] = ok ? py * C::RS + px * C::CS + 8 * c8 : -1;
-      const uint32_t o = DGRAD ? (uint32_t)(((b * (a.H >> 1) + (gy >> 1)) * (a.W >> 1) + (gx >> 1)) *
-                                                CPT + ch * CP + 8 * c8)
-                               : (uint32_t)(((b * a.H + gy) * a.W + gx) * CPT + ch * CP + 8 * c8);
-#pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(in + p * a.in_elems), (short)0, (int)(src_elems * 2), 0x00020000);
-        pv[p][it] = __builtin_bit_cast(
-            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(in_img ? o * 2 : kOOB), 0, 0));
-      }
-      if constexpr (DGRAD) {
-        const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)a.in_route, (short)0, (int)src_elems, 0x00020000);
-        pm[it] = __builtin_bit_cast(
-            u32x2, __builtin_amdgcn_raw_buffer_load_b64(rr, (int)(in_img ? o : kOOB), 0, 0));
-        pq[it] = ((gy & 1) << 1) | (gx & 1);
-      }
-    }
-  };
-  auto patch_commit = [&](int u) {
-    __bf16* buf = patch0 + (u & 1) * kPB;
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      if (pdst[it] < 0) continue;
-#pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        u32x4 v = pv[p][it];
-        if constexpr (DGRAD) {   // expand: the value at its routed quadrant, 0 elsewhere
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const uint32_t mw = pm[it][e >> 1];
-            const uint32_t r0 = (mw >> (16 * (e & 1))) & 0xff;
-            const uint32_t r1 = (mw >> (16 * (e & 1) + 8)) & 0xff;
-            v[e] = (r0 == pq[it] ? (v[e] & 0xffffu) : 0u) | (r1 == pq[it] ? (v[e] & 0xffff0000u) : 0u);
-          }
-        }
-        *reinterpret_cast<u32x4*>(buf + p * C::kPlane + pdst[it]) = v;
-      }
-    }
-  };
-
-  // ---- weights of global step g (unit g / T, tap g % T), clamped ----
-  SplitWStage<C, CPT, CP, N> ws0, ws1;
-  auto wload = [&](SplitWStage<C, CPT, CP, N>& w, int g) {
-    const int gc = g < nstep ? g : nstep - 1;
-    const int u = gc / T, li = u / NCH;
-    w.load(tower(li) ? a.wk[1] : a.wk[0], a.wk_elems, u - li * NCH, gc - u * T, tid);
-  };
-
-  // ---- per-lane operand offsets (split_conv_body) ----
-  const int wkg = wid / (WM * WN), wmn = wid % (WM * WN);
-  const int wmi = wmn / WN, wni = wmn % WN;
-  int abase[TM];
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int m = wmi * TM * 32 + 32 * i + l31;
-    const int win = (m >> 2) < C::NWIN ? m >> 2 : 0, dy = (m >> 1) & 1, dx = m & 1;
-    const int wy = win / (TX / 2), wx = win % (TX / 2);
-    abase[i] = (2 * wy + dy) * C::RS + (2 * wx + dx) * C::CS + h * 8 + 16 * C::KSW * wkg;
-  }
-  int bbase[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j)
-    bbase[j] = (wni * TN * 32 + 32 * j + l31) * C::CW + h * 8 + 16 * C::KSW * wkg;
-  float bpre[TN];
-  auto bias_load = [&](int li) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) bpre[j] = 0.f;
-    if (DGRAD) return;
-    const float* bz = tower(li < nmine ? li : 0) ? a.bias[1] : a.bias[0];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) bpre[j] = bz[wni * TN * 32 + 32 * j + l31];
-  };
-
-  f32x16 acc[TM][TN], cor[TM][TN];
-  auto zero_acc = [&]() {
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; cor[i][j][r] = 0.f; }
-  };
-  auto tap_step = [&](int t, const __bf16* patch, int slot) {
-    const __bf16* wb = wbuf + slot * 3 * C::kWSlot;
-    const int ky = t / KS, kx = t % KS;
-    const __bf16* pa = patch + ky * C::RS + kx * C::CS;
-#pragma unroll
-    for (int g = 0; g < C::KSW; ++g) {
-      bf16x8 av[3][TM], bv[3][TN];
-#pragma unroll
-      for (int p = 0; p < 3; ++p) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-          av[p][i] = *reinterpret_cast<const bf16x8*>(pa + p * C::kPlane + abase[i] + 16 * g);
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          bv[p][j] = *reinterpret_cast<const bf16x8*>(wb + p * C::kWSlot + bbase[j] + 16 * g);
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2][i], bv[0][j], cor[i][j], 0, 0, 0);
-          cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[1][j], cor[i][j], 0, 0, 0);
-          cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[2][j], cor[i][j], 0, 0, 0);
-          cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[0][j], cor[i][j], 0, 0, 0);
-          cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[1][j], cor[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[0][j], acc[i][j], 0, 0, 0);
-        }
-    }
-  };
-  // the end of a tile (after its last unit's last tap): k groups meet, epilogue
-  auto tile_end = [&](int li, __bf16* freebuf) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] += cor[i][j];
-    if (WK > 1) {   // as split_conv_body, in the finished unit's patch buffer
-      float* red = reinterpret_cast<float*>(freebuf);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          __syncthreads();
-#pragma unroll
-          for (int r = 0; r < 16; ++r) red[((wkg * WM * WN + wmn) * 16 + r) * 64 + lane] = acc[i][j][r];
-          __syncthreads();
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            if ((r >> 2) % WK != wkg) continue;
-            float v = 0.f;
-#pragma unroll
-            for (int k = 0; k < WK; ++k) v += red[((k * WM * WN + wmn) * 16 + r) * 64 + lane];
-            acc[i][j][r] = v;
-          }
-        }
-    }
-    int b, y0, x0;
-    coords(li, b, y0, x0);
-    if constexpr (DGRAD)
-      split_epilogue<TM, TN, TX, N, true, WK, C::NWIN>(a, acc, bpre, b, 0, y0, x0, wmi, wni, l31,
-                                                       h, wkg);
-    else
-      split_epilogue_fwd_lds<TM, TN, TX, N, WK, C::NWIN, C::kThreads>(
-          a, acc, bpre, reinterpret_cast<char*>(freebuf), b, tower(li), y0, x0, wmi, wni, l31, h,
-          wkg, tid);
-  };
-  // one global step: the MFMAs of (unit u, tap t) from ring slot g & 1; at
-  // tap kCommit the next unit's patch goes to the other buffer; at the last
-  // tap the next-next unit's patch loads (and at a tile's last unit its
-  // epilogue and the next tile's bias); then the ring slot of step g + 1 and
-  // the step's barrier.
-  auto step = [&](int g, SplitWStage<C, CPT, CP, N>& wnext) {
-    const int u = g / T, t = g - u * T;
-    __bf16* const patch = patch0 + (u & 1) * kPB;
-    tap_step(t, patch, g & 1);
-    __builtin_amdgcn_sched_barrier(0);
-    if (t == P::kCommit && u + 1 < nunit) patch_commit(u + 1);
-    if (t == T - 1) {
-      const int li = u / NCH;
-      if (u - li * NCH == NCH - 1) {
-        tile_end(li, patch);
-        zero_acc();
-        bias_load(li + 1);
-      }
-      if (u + 2 < nunit) patch_issue(u + 2);
-    }
-    if (g + 1 < nstep) {
-      wnext.store(wbuf + ((g + 1) & 1) * 3 * C::kWSlot, tid);
-      __syncthreads();
-    }
-  };
-
-  // prologue: unit 0's patch, tile 0's bias, ring slot 0, step 1's weights,
-  // unit 1's patch loads
-  patch_issue(0);
-  patch_commit(0);
-  bias_load(0);
-  wload(ws0, 0);
-  ws0.store(wbuf, tid);
-  if (nstep > 1) wload(ws1, 1);
-  patch_issue(1);
-  zero_acc();
-  __syncthreads();
-  for (int g = 0; g < nstep; g += 2) {
-    if (g + 2 < nstep) {
-      wload(ws0, g + 2);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    step(g, ws1);
-    if (g + 1 >= nstep) break;
-    if (g + 3 < nstep) {
-      wload(ws1, g + 3);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    step(g + 1, ws0);
-  }
-}
-
-template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, bool DGRAD>
-__global__ __launch_bounds__(64 * WM * WN * WK) void split_conv_pipe_kernel(const SplitArgs a,
-                                                                            int ntiles, int tpi,
-                                                                            int tpt) {
-  extern __shared__ __attribute__((aligned(16))) char sm_pipe[];
-  split_conv_pipe_body<CPT, CP, N, KS, TY, TX, WM, WN, WK, DGRAD>(a, sm_pipe, ntiles, tpi, tpt);
-}
-
-// grid: one workgroup per CU (the two patch buffers take the LDS), at most
-// one per tile
-template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, bool DGRAD>
-inline hipError_t launch_split_conv_pipe(SplitArgs a, int nz, hipStream_t st) {
-  using P = SplitPipeCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK, DGRAD>;
-  auto kern = split_conv_pipe_kernel<CPT, CP, N, KS, TY, TX, WM, WN, WK, DGRAD>;
-  static int ncu = 0;
-  if (!ncu) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, P::kSmemB);
-    if (e != hipSuccess) return e;
-    int dev = 0;
-    if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
-    int n = 0;
-    if ((e = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
-      return e;
-    ncu = n > 0 ? n : 256;
-  }
-  if (!DGRAD && ((a.out[0] && a.out_split[0]) || (a.out[1] && a.out_split[1])))
-    return hipErrorInvalidValue;
-  if (DGRAD && (a.in_f32 || a.xsplit)) return hipErrorInvalidValue;   // split_conv_body only
-  a.tiles_x = (a.W + TX - 1) / TX;
-  const int tiles_y = (a.H + TY - 1) / TY;
-  const int tpi = tiles_y * a.tiles_x, tpt = tpi * a.B, ntiles = tpt * nz;
-  const int grid = ntiles < ncu ? ntiles : ncu;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(P::C::kThreads), P::kSmemB, st, a, ntiles, tpi, tpt);
   return hipGetLastError();
 }
 
@@ -1227,217 +893,15 @@ __global__ __launch_bounds__(64 * WM) void split_conv1_kernel(const Conv1Args a)
     split_epilogue<TM, 1, TX, 32, false, 1, C::NWIN>(e, acc, bpre, b, z, y0, x0, wid, 0, l31, h);
 }
 
-// Persistent pipelined conv1 (split_conv_pipe_body's scheme): a workgroup
-// keeps the split weights of its tower resident, owns a contiguous run of
-// tiles (tower-major numbering: at most one weight restage per workgroup),
-// loads the next tile's frames into registers while a tile computes, commits
-// them to the other patch buffer after tap row 3, and gathers / stores its
-// pooled outputs from a buffer of their own while the next tile computes.
-template <int TY, int TX, int WM>
-struct Conv1PipeCfg {
-  using C = Conv1Cfg<TY, TX, WM>;
-  static constexpr int kGatherB = C::NWIN * 32 * 7;
-  static constexpr int kSmemB = C::kWB + 2 * C::kPatchB + kGatherB;
-  static_assert(kSmemB <= 160 * 1024, "LDS");
-};
-
-template <int TY, int TX, int WM>
-__global__ __launch_bounds__(64 * WM) __attribute__((amdgpu_waves_per_eu(4))) void split_conv1_pipe_kernel(const Conv1Args a, int ntiles,
-                                                                   int per, int tpi, int tpt) {
-  using P = Conv1PipeCfg<TY, TX, WM>;
-  using C = typename P::C;
-  constexpr int TM = C::TM;
-  constexpr int kThreads = 64 * WM;
-  extern __shared__ __attribute__((aligned(16))) char sm_c1p[];
-  __bf16* const wbuf = reinterpret_cast<__bf16*>(sm_c1p);
-  __bf16* const patch0 = reinterpret_cast<__bf16*>(sm_c1p + C::kWB);
-  char* const gather = sm_c1p + C::kWB + 2 * C::kPatchB;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int l31 = lane & 31, h = lane >> 5;
-  const int t0 = blockIdx.x * per;
-  const int nmine = ntiles - t0 < per ? ntiles - t0 : per;
-  if (nmine <= 0) return;
-  auto coords = [&](int li, int& z, int& b, int& y0, int& x0) {
-    int t = t0 + li;
-    z = t >= tpt ? 1 : 0;
-    if (z) t -= tpt;
-    b = t / tpi;
-    const int r = t - b * tpi;
-    const int ty = r / a.tiles_x;
-    y0 = ty * TY;
-    x0 = (r - ty * a.tiles_x) * TX;
-  };
-  // frames of a tile: one pixel (4 channels, fp32 -> exact bf16) per item
-  constexpr int NP = C::PH * C::PW;
-  constexpr int NIT = (NP + kThreads - 1) / kThreads;
-  float4 pv[NIT];
-  auto patch_issue = [&](int li) {
-    const bool live = li < nmine;
-    int z = 0, b = 0, y0 = 0, x0 = 0;
-    if (live) coords(li, z, b, y0, x0);
-    const float* __restrict__ in = z ? a.in[1] : a.in[0];
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int f = tid + it * kThreads;
-      const int py = f / C::PW, px = f % C::PW;
-      const int gy = y0 - 3 + py, gx = x0 - 3 + px;
-      pv[it] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (live && f < NP && px < TX + 6 && (unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W)
-        pv[it] = *reinterpret_cast<const float4*>(in + (((size_t)b * a.H + gy) * a.W + gx) * 4);
-    }
-  };
-  auto patch_commit = [&](int li) {
-    __bf16* const patch = patch0 + (li & 1) * (C::kPatchB / 2);
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int f = tid + it * kThreads;
-      if (f < NP) {
-        const int py = f / C::PW, px = f % C::PW;
-        __bf16 q[4] = {(__bf16)pv[it].x, (__bf16)pv[it].y, (__bf16)pv[it].z, (__bf16)pv[it].w};
-        *reinterpret_cast<uint2*>(patch + py * C::RS + px * 4) = *reinterpret_cast<uint2*>(q);
-      }
-    }
-  };
-  auto stage_weights = [&](int z) {
-    const __bf16* __restrict__ wk = z ? a.wk[1] : a.wk[0];
-    constexpr int NW = 3 * kConv1WPlane / 8;
-    constexpr int WIT = (NW + kThreads - 1) / kThreads;
-    u32x4 w[WIT];
-#pragma unroll
-    for (int it = 0; it < WIT; ++it) {
-      const int f0 = tid + it * kThreads;
-      const int f = f0 < NW ? f0 : NW - 1;
-      const int p = f / (kConv1WPlane / 8), r = f % (kConv1WPlane / 8);
-      w[it] = *reinterpret_cast<const u32x4*>(wk + p * a.wk_elems + 8 * (size_t)r);
-    }
-#pragma unroll
-    for (int it = 0; it < WIT; ++it) {
-      const int f0 = tid + it * kThreads;
-      const int f = f0 < NW ? f0 : NW - 1;
-      const int p = f / (kConv1WPlane / 8), r = f % (kConv1WPlane / 8);
-      const int n = r / 28, q8 = r % 28;
-      *reinterpret_cast<u32x4*>(wbuf + (p * 32 + n) * C::CW + 8 * q8) = w[it];
-    }
-  };
-  int abase[TM];
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int m = wid * TM * 32 + 32 * i + l31;
-    const int win = (m >> 2) < C::NWIN ? m >> 2 : 0, dy = (m >> 1) & 1, dx = m & 1;
-    const int wy = win / (TX / 2), wx = win % (TX / 2);
-    abase[i] = (2 * wy + dy) * C::RS + (2 * wx + dx + 2 * h) * 4;
-  }
-  const int bbase = l31 * C::CW + h * 8;
-  SplitArgs e{};
-  e.B = a.B; e.H = a.H; e.W = a.W;
-  e.out[0] = a.out[0]; e.out[1] = a.out[1];
-  e.out_split[0] = a.out_split[0]; e.out_split[1] = a.out_split[1];
-  e.out_elems = a.out_elems;
-  e.mask[0] = a.mask[0]; e.mask[1] = a.mask[1];
-
-  int zc, bq, yq, xq;
-  coords(0, zc, bq, yq, xq);
-  patch_issue(0);
-  stage_weights(zc);
-  patch_commit(0);
-  patch_issue(1);
-  __syncthreads();
-  for (int li = 0; li < nmine; ++li) {
-    int z, b, y0, x0;
-    coords(li, z, b, y0, x0);
-    if (z != zc) {   // tower change (once at most): the epilogue's barriers fenced every reader
-      stage_weights(z);
-      __syncthreads();
-      zc = z;
-    }
-    const float bpre[1] = {(z ? a.bias[1] : a.bias[0])[l31]};
-    const __bf16* const patch = patch0 + (li & 1) * (C::kPatchB / 2);
-    f32x16 acc[TM][1], cor[TM];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) { acc[i][0][r] = 0.f; cor[i][r] = 0.f; }
-#pragma unroll
-    for (int ky = 0; ky < 7; ++ky) {
-      if (ky == 4 && li + 1 < nmine) {   // the next tile's frames (their loads have landed)
-        __builtin_amdgcn_sched_barrier(0);
-        patch_commit(li + 1);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-#pragma unroll
-      for (int g = 0; g < 2; ++g) {
-        bf16x8 bv[3];
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-          bv[p] = *reinterpret_cast<const bf16x8*>(wbuf + p * 32 * C::CW + bbase + ky * 32 + 16 * g);
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const __bf16* pa = patch + abase[i] + ky * C::RS + 16 * g;
-          typedef __attribute__((address_space(3))) const u32x2 lds_u2;
-          typedef __attribute__((address_space(3))) const char lds_c;
-          lds_u2* la = (lds_u2*)pa;
-          uint32_t hi_off = 8;                       // separate ds_read_b64 (split_conv1_kernel)
-          asm volatile("" : "+v"(hi_off));
-          const u32x2 lo = *la;
-          const u32x2 hi = *(lds_u2*)((lds_c*)la + hi_off);
-          u32x4 av4 = {lo[0], lo[1], hi[0], hi[1]};
-          const bf16x8 av = *reinterpret_cast<bf16x8*>(&av4);
-          cor[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv[2], cor[i], 0, 0, 0);
-          cor[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv[1], cor[i], 0, 0, 0);
-          acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv[0], acc[i][0], 0, 0, 0);
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i) acc[i][0] += cor[i];
-    // gather buffer: its previous readers (the last tile's stores) read it
-    // before that epilogue's end; the barrier at the top of this one fences
-    // every wave's patch reads of this tile as well
-    split_epilogue_fwd_lds<TM, 1, TX, 32, 1, C::NWIN, kThreads>(e, acc, bpre, gather, b, z, y0, x0,
-                                                                wid, 0, l31, h, 0, tid);
-    if (li + 2 < nmine) patch_issue(li + 2);
-  }
-}
-
-template <int TY, int TX, int WM>
-inline hipError_t launch_split_conv1_pipe(Conv1Args a, int nz, hipStream_t st, int64_t wk_elems) {
-  using P = Conv1PipeCfg<TY, TX, WM>;
-  a.wk_elems = wk_elems;
-  if ((a.out[0] && a.out_split[0]) || (a.out[1] && a.out_split[1])) return hipErrorInvalidValue;
-  auto kern = split_conv1_pipe_kernel<TY, TX, WM>;
-  static int slots = 0;
-  if (!slots) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, P::kSmemB);
-    if (e != hipSuccess) return e;
-    int dev = 0, n = 0;
-    if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
-    if ((e = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
-      return e;
-    slots = (n > 0 ? n : 256) * ((160 * 1024) / P::kSmemB);   // workgroups resident at once
-  }
-  a.tiles_x = (a.W + TX - 1) / TX;
-  const int tiles_y = (a.H + TY - 1) / TY;
-  const int tpi = tiles_y * a.tiles_x, tpt = tpi * a.B, ntiles = tpt * nz;
-  const int per = (ntiles + slots - 1) / slots;
-  const int grid = (ntiles + per - 1) / per;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WM), P::kSmemB, st, a, ntiles, per, tpi, tpt);
-  return hipGetLastError();
-}
-
 template <int TY, int TX, int WM>
 inline hipError_t launch_split_conv1(Conv1Args a, int nz, hipStream_t st, int64_t wk_elems) {
   a.wk_elems = wk_elems;
   if ((a.out[0] && a.out_split[0]) || (a.out[1] && a.out_split[1])) return hipErrorInvalidValue;
   using C = Conv1Cfg<TY, TX, WM>;
   auto kern = split_conv1_kernel<TY, TX, WM>;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, C::kSmemB);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  static std::atomic<uint64_t> attr{0};
+  if (hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(kern), attr, (int)(C::kSmemB)))
+    return e;
   a.tiles_x = (a.W + TX - 1) / TX;
   const int tiles_y = (a.H + TY - 1) / TY;
   hipLaunchKernelGGL(kern, dim3(tiles_y * a.tiles_x, a.B, nz), dim3(64 * WM), C::kSmemB, st, a);

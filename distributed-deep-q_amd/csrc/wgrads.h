@@ -435,7 +435,6 @@ template <int CIN0, int COUT0, int KS0, int PAD0, int WMAX0, int DSRC0, int CIN1
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void wgrads_pair_kernel(
     const WgradSArgs a0, const WgradSArgs a1, int n0) {
   extern __shared__ __attribute__((aligned(16))) char sm_wgp[];
-  if (DDQ_AB_SETPRIO && (threadIdx.x >> 6) >= 2) __builtin_amdgcn_s_setprio(1);
   if ((int)blockIdx.x < n0)
     wgrads_body<CIN0, COUT0, KS0, PAD0, WMAX0, DSRC0>(a0, sm_wgp, blockIdx.x);
   else
@@ -450,13 +449,9 @@ inline hipError_t launch_wgrads_pair_w(const WgradSArgs& a0, const WgradSArgs& a
   if (shm > 160 * 1024) return hipErrorInvalidValue;
   auto kern = wgrads_pair_kernel<CIN0, COUT0, KS0, PAD0, WMAX0, DSRC0, CIN1, COUT1, KS1, PAD1,
                                  WMAX1, DSRC1>;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  static std::atomic<uint64_t> attr{0};
+  if (hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(kern), attr, (int)(160 * 1024)))
+    return e;
   const int n0 = (a0.G + 7) / 8 * 8 * (COUT0 / 32) * KS0;
   const int n1 = (a1.G + 7) / 8 * 8 * (COUT1 / 32) * KS1;
   hipLaunchKernelGGL(kern, dim3(n0 + n1), dim3(256), shm, st, a0, a1, n0);
@@ -506,9 +501,8 @@ struct Wgrad1SGeom {
   static __host__ __device__ int d_plane(int W) { return ((W + 15) & ~15) * PSD; }
   // the halo patch + the NW waves' dconv row pairs; at least the image of the
   // final cross-wave sums (NW x 16 x 64 floats)
-  // dconv rows staged per wave: both conv rows of a pooled row (6 planes), or
-  // one at a time (3 planes, DDQ_AB_W1SEQ: half the LDS, two workgroups per CU)
-  static constexpr int kRowPlanes = DDQ_AB_W1SEQ ? 3 : 6;
+  // dconv rows staged per wave: both conv rows of a pooled row (6 planes)
+  static constexpr int kRowPlanes = 6;
   static __host__ __device__ size_t bytes(int W, int R) {
     const size_t a = ((size_t)(R + 6) * in_row(W) + NW * kRowPlanes * d_plane(W)) * 2;
     return a > (size_t)NW * 16 * 64 * 4 ? a : (size_t)NW * 16 * 64 * 4;
@@ -720,18 +714,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) vo
 // the kernel is VALU-bound on the routing expansion, not latency-bound)
 template <int WMAX>
 inline hipError_t launch_wgrad1s_w(const Wgrad1SArgs& a, hipStream_t st) {
-  constexpr int NW = WMAX <= 64 ? DDQ_AB_W1NW : 2;   // two staged rows per wave: LDS
+  constexpr int NW = WMAX <= 64 ? 4 : 2;   // two staged rows per wave: LDS
   using Geo = Wgrad1SGeom<WMAX, NW>;
   const size_t shm = Geo::bytes(a.W, a.R);
   if (shm > 160 * 1024) return hipErrorInvalidValue;
   auto kern = wgrad1s_kernel<WMAX, NW>;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  static std::atomic<uint64_t> attr{0};
+  if (hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(kern), attr, (int)(160 * 1024)))
+    return e;
   hipLaunchKernelGGL(kern, dim3(a.B * (a.H / a.R)), dim3(64 * NW), shm, st, a);
   return hipGetLastError();
 }

@@ -126,11 +126,22 @@ class AsyncTicketLoop:
     several tickets while a slow one takes one.  No device ever waits for a
     ticket: the order is decided on the host, the ticks are enqueued
     asynchronously and the gradient of the next tick computes meanwhile.
+
+    Ticket state lives in the loop: a ticket this rank took that lies past the
+    end of a ``run`` (it became ready while the last ticks were executed) is
+    executed by the next ``run`` of the same loop, on every rank.  Each loop
+    instance keys its tickets under an instance number of its own (the n-th
+    loop a rank creates on ``store`` is instance n -- every rank creates its
+    loops in the same order), so a new loop never replays an older loop's
+    tickets; tickets still held when a loop is dropped are dropped with it.
     """
 
     def __init__(self, net, cfg, store, rank, world):
-        self.net, self.cfg, self.store = net, cfg, store
+        import torch.distributed as dist
+        self.net, self.cfg = net, cfg
         self.rank, self.world = int(rank), int(world)
+        self.instance = store.add("instances/%d" % self.rank, 1) - 1
+        self.store = dist.PrefixStore("i%d" % self.instance, store)
         self.next = 0            # next ticket to execute
         self.holding = False     # this rank holds a ticket not yet executed
 

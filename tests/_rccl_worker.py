@@ -5,6 +5,10 @@ gradient saved for the parent to compare with an in-process group.
 
 usage: RANK=r WORLD_SIZE=W MASTER_ADDR=127.0.0.1 MASTER_PORT=p \
        python tests/_rccl_worker.py EXCHANGE ROUNDS OUT.npz
+
+EXCHANGE "async-graph": the async exchange stepped as graph replays mixed with
+eager rounds (ddq_step_graph_async: one eager round, one K-round graph, then
+eager rounds after the replay -- the comm-stream ordering of ADVICE r03).
 """
 import os
 import sys
@@ -41,8 +45,15 @@ def main():
     n.replay_create(N)
     n.replay_import(*member_data(rank), 0, N)
     ddist.setup_comm(n, rank, world)
-    cfg = n.step_cfg("rmsprop", lr=LR, target_period=PERIOD, exchange=exchange, seed=SEED)
-    for _ in range(rounds):
+    graph = exchange == "async-graph"
+    cfg = n.step_cfg("rmsprop", lr=LR, target_period=PERIOD,
+                     exchange="async" if graph else exchange, seed=SEED)
+    done = 0
+    if graph:   # K = PERIOD / gcd(W, PERIOD) rounds per graph, after one eager round
+        k = 1 + PERIOD // np.gcd(world, PERIOD)
+        n.step_graph(cfg, min(k, rounds))
+        done = min(k, rounds)
+    for _ in range(rounds - done):
         n.step(cfg)
     n.synchronize()
     np.savez(out, q=n.get_flat(0), p=n.get_flat(1), opt=n.optimizer_state(),

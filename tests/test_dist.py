@@ -374,7 +374,12 @@ def _ticket_worker(rank, world, port, npush, out):
     net = _FakeAsyncNet(rank, 0.002 if rank == 0 else 0.012)
     loop = ddist.AsyncTicketLoop(net, None, ddist.ticket_store(world, rank), rank, world)
     order = loop.run(npush // 2) + loop.run(npush - npush // 2)   # two calls: state carries
-    out.put((rank, order, net.ticks))
+    # a second loop on the same store keys its own tickets (no replay of the
+    # first loop's): its ticket counter starts at 0
+    loop2 = ddist.AsyncTicketLoop(net, None, ddist.ticket_store(world, rank), rank, world)
+    order2 = loop2.run(6)
+    taken2 = int(loop2.store.add("ticket", 0))
+    out.put((rank, order, net.ticks[:npush], (loop2.instance, order2, taken2)))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -403,3 +408,7 @@ def test_gloo_async_ticket_order(world):
     assert len(orders[0]) == npush
     counts = np.bincount(orders[0], minlength=world)
     assert counts[0] > max(counts[1:]) and min(counts) >= 1, counts
+    second = [r[3] for r in res]
+    assert all(inst == 1 for inst, _, _ in second)
+    assert all(o2 == second[0][1] and len(o2) == 6 for _, o2, _ in second)
+    assert all(6 <= taken <= 6 + world for _, _, taken in second), second

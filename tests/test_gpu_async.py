@@ -174,3 +174,44 @@ def test_rccl_world1_async_ticks_and_graph_equal_plain_steps(ddq, period):
     finally:
         for n in nets:
             n.close()
+
+
+def test_rccl_world1_async_graph_mixed_with_eager_ticks_and_tickets(ddq):
+    """W = 1, period 3 (K = 3 rounds per graph): graph replays followed by an
+    eager remainder round, ticket ticks (ddq_async_tick after ddq_async_ready)
+    and an AsyncTicketLoop run, then graphs again -- the comm stream must wait
+    for a replay before the next eager tick's RCCL calls / owner apply, and
+    the ready event must mark the gradient the replay computed.
+    Bit-exact against plain exchange-free steps."""
+    from ddq import dist as ddist
+    nets = _world1_nets(ddq, 2, seed=11)
+    try:
+        nets[0].comm_init(ddq.DeepQNet.comm_unique_id(), 1, 0)
+        acfg = nets[0].step_cfg("rmsprop", lr=1e-4, target_period=3, exchange="async", seed=4)
+        total = 0
+        nets[0].step_graph(acfg, 5)          # 1 eager round, one 3-round graph, 1 eager
+        total += 5
+        for _ in range(2):
+            while not nets[0].async_ready():
+                pass
+            nets[0].async_tick(acfg, 0)
+        total += 2
+        nets[0].step_graph(acfg, 3)          # a replay right after eager ticks
+        total += 3
+        loop = ddist.AsyncTicketLoop(nets[0], acfg, ddist.ticket_store(1), 0, 1)
+        assert loop.run(4) == [0] * 4        # ticket ticks right after a replay
+        total += 4
+        nets[0].step_graph(acfg, 7)
+        total += 7
+        plain = nets[1].step_cfg("rmsprop", lr=1e-4, target_period=3, exchange="none", seed=4)
+        for _ in range(total):
+            nets[1].step(plain)
+        for n in nets:
+            n.synchronize()
+        for z in (0, 1):
+            np.testing.assert_array_equal(nets[0].get_flat(z), nets[1].get_flat(z))
+        np.testing.assert_array_equal(nets[0].optimizer_state(), nets[1].optimizer_state())
+        np.testing.assert_array_equal(nets[0].get_grads_flat(), nets[1].get_grads_flat())
+    finally:
+        for n in nets:
+            n.close()

@@ -78,7 +78,8 @@ def _group(ddq, exchange, world, rounds):
         n.replay_import(*W_.member_data(r), 0, W_.N)
         nets.append(n)
     arr = ddq.DeepQNet.group_init(nets)
-    cfg = nets[0].step_cfg("rmsprop", lr=W_.LR, target_period=W_.PERIOD, exchange=exchange,
+    cfg = nets[0].step_cfg("rmsprop", lr=W_.LR, target_period=W_.PERIOD,
+                           exchange="async" if exchange == "async-graph" else exchange,
                            seed=W_.SEED)
     for _ in range(rounds):
         ddq.DeepQNet.group_step(nets, cfg, arr)
@@ -90,7 +91,7 @@ def _group(ddq, exchange, world, rounds):
 
 
 @pytest.mark.skipif("_ngpu() < 2")
-@pytest.mark.parametrize("exchange", ["async", "server", "sharded", "allreduce"])
+@pytest.mark.parametrize("exchange", ["async", "async-graph", "server", "sharded", "allreduce"])
 def test_rccl_two_ranks_equal_in_process_group(exchange, tmp_path):
     import ddq
     world, rounds = 2, 5            # 10 async ticks: special updates at iterations 4 and 8
