@@ -275,7 +275,6 @@ int ddq_create(ddq_ctx** out, int device, const ddq_net_desc* desc) {
     TRY(dalloc(c, &nb.dconv3, (size_t)B * S3 * S3 * 64));
     TRY(dalloc(c, &nb.dconv2s, (size_t)3 * B * S3 * S3 * 64));
     TRY(dalloc(c, &nb.dconv3s, (size_t)3 * B * S3 * S3 * 64));
-    TRY(dalloc(c, &nb.dconv1s, (size_t)3 * B * S2 * S2 * 32));
     int64_t off = 0;
     const int cout[3] = {32, 64, 64};
     for (int l = 0; l < 3; ++l) {

@@ -63,7 +63,7 @@ struct NetBuffers {
   float *q_out, *p_out, *q_sa, *p_sa, *target, *loss;
   // backward scratch
   float *dh4, *dconv3;               // dh4 (B,512); dconv3: fp32 pooled dpool3 (fc4 dgrad)
-  __bf16 *dconv2s, *dconv1s;        // split pooled dpool2 / dpool1 (conv3 / conv2 data gradients)
+  __bf16* dconv2s;                  // split pooled dpool2 (conv3's data gradient)
   __bf16* dconv3s;                  // split expanded dconv3 (B,S/4,S/4,64): conv3's weight gradient
   float* wpart;                     // conv wgrad slabs (3 layers, disjoint)
   int64_t wpart_off[3];

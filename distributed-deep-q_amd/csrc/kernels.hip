@@ -1589,22 +1589,18 @@ static const Conv1Menu kConv1Fwd[] = {DDQ_CONV1_TILE(32, 32, 16), DDQ_CONV1_TILE
                                       DDQ_CONV1_TILE(16, 16, 8), DDQ_CONV1_TILE(24, 24, 9)};
 #undef DDQ_CONV1_TILE
 
-// conv1 weight-gradient band height: the largest power of two <= 8 dividing
-// S (one slab per band)
-static int wgrad1_band(int S) {
-  int R = 8;
-  while (R > 1 && S % R != 0) R >>= 1;
-  return R;
-}
-
 // Slabs of the conv weight gradients and their pitch np (>= KC + 1: the bias
-// column, padded to 64 for the reduce's units).  conv1: one per band;
-// conv2 / conv3: one per row group (wgrads_groups).
+// column, padded to 64 for the reduce's units).  conv1: one per tile of
+// conv2's data gradient (the fused conv1 weight gradient, split.h
+// w1_tile_wgrad); conv2 / conv3: one per row group (wgrads_groups).
 int wgrad_splits_for(int layer, int B, int S, int* np) {
   const int H = S >> layer;
   const int KC[3] = {196, 800, 576};
   *np = ((KC[layer] + 1 + 63) / 64) * 64;
-  if (layer == 0) return B * (S / wgrad1_band(S));
+  if (layer == 0) {
+    const TileOpt& t = pick_tile(kConv2Dgrad, S / 2, S / 2).opt;
+    return B * ((S / 2 + t.ty - 1) / t.ty) * ((S / 2 + t.tx - 1) / t.tx);
+  }
   const int nts[3] = {0, 2 * 5, 2 * 3};
   // about 256 workgroups each (24 / 40 slabs at 64x64 B=32: fewer, larger
   // slabs than at 512 -- pair 30.0 -> 27.7 us, reduce 21.9 -> 19.2)
@@ -1787,17 +1783,22 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     M("conv23_wgrad");
     CHECK_LAUNCH(launch_wgrads_conv23(w2, w3, s));
   }
-  {  // conv2 data gradient -> split pooled dpool1 (split bf16, DGRAD): the
-     // split pooled dpool2 expanded through mask2 while staged, the transposed
-     // split weights the head kernel rebuilt, one 64-channel chunk, 8x16-pixel (kConv2Dgrad)
-     // tiles, four k groups (their sums meet in LDS in fixed order)
+  {  // conv2 data gradient -> dpool1 (split bf16, DGRAD): the split pooled
+     // dpool2 expanded through mask2 while staged, the transposed split
+     // weights the head kernel rebuilt, one 64-channel chunk, 8x16-pixel
+     // (kConv2Dgrad) tiles, four k groups (their sums meet in LDS in fixed
+     // order) -- and conv1's weight gradient of the tile's conv1 pixels in the
+     // same workgroup (split.h w1_tile_wgrad): dpool1 routed through mask1
+     // into LDS, the frames' halo, one fp32 slab per tile (train_val.prototxt
+     // :39-61; conv1 has no bottom diff)
     const int H = S / 2;
     SplitArgs a{};
     a.B = B; a.H = H; a.W = H; a.pad = 2;
     a.in[0] = nb.dconv2s; a.in_elems = (int64_t)B * (H / 2) * (H / 2) * 64;
     a.wk[0] = nb.wks[0] + L.wkst_off; a.wk_elems = L.wks_total;
     a.in_route = nb.mask2;
-    a.pd_split = nb.dconv1s; a.pd_elems = (int64_t)B * H * H * 32;
+    a.w1_route = nb.mask1; a.w1_in = nb.state;
+    a.w1_part = nb.wpart + nb.wpart_off[0]; a.w1_np = nb.wnp[0];
     M("conv2_dgrad");
     CHECK_LAUNCH(pick_tile(kConv2Dgrad, H, H).launch(a, 1, s));
   }
@@ -1812,15 +1813,6 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     d[l] = {L.w[l], L.b[l], nb.wpart_off[l], cout[l], cin[l], ks[l], sp, nb.wnp[l],
             blk, L.wks_off[l], G};
     blk += cout[l] * (nb.wnp[l] / 64) * G / 4;   // units per layer: a multiple of 32
-  }
-  {  // conv1 weight gradient (split3, wgrads.h): the split pooled dpool1
-     // (conv2 dgrad) against the frames, three MFMAs per (tap row, 16 pixels)
-    Wgrad1SArgs w{};
-    w.B = B; w.H = S; w.W = S; w.R = wgrad1_band(S); w.NP = nb.wnp[0];
-    w.dpool = nb.dconv1s; w.d_elems = (int64_t)B * (S / 2) * (S / 2) * 32;
-    w.droute = nb.mask1; w.in = nb.state; w.part = nb.wpart + nb.wpart_off[0];
-    M("conv1_wgrad");
-    CHECK_LAUNCH(launch_wgrad1s(w, s));
   }
   {  // slab reduce -> grads (Caffe layout) [+ the fused apply + next draw]
     if (nb.fc4_wait) CHECK_LAUNCH(hipStreamWaitEvent(s, nb.fc4_wait, 0));

@@ -87,6 +87,20 @@ __device__ __forceinline__ void store_split(__bf16* t, int64_t E, int64_t e, flo
   t[2 * E + e] = l;
 }
 
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+
+// ds_read_b64_tr_b16 pair: lane 4q+p of a 16-lane group addresses row q,
+// columns 4p..4p+3 of a 4-row block and receives column i of the four rows;
+// two blocks (p0, p1) make one 8-element MFMA operand
+__device__ __forceinline__ bf16x8 tr_pair(const __bf16* p0, const __bf16* p1) {
+  typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+  const i16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(p0));
+  const i16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(p1));
+  typedef short i16x8 __attribute__((ext_vector_type(8)));
+  const i16x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
 // bank-conflict-free strides for the 32x32x16 operand reads (tools/lds_banks.py):
 // pixel stride CP + 8 bf16 (an odd number of 16-byte units), patch row stride
 // == 128 (mod 256) bytes: the four 16-lane groups of a ds_read_b128 then hit
@@ -203,6 +217,12 @@ struct SplitArgs {
   __bf16* xsplit;            // dgrad, one channel chunk: the staged source expanded and
   int64_t x_elems;           // split, NHWC (B,H,W,CPT), written once (nullable) -- the
                              // layer's weight gradient then copies rows (wgrads DSRC 2)
+  // conv2's data gradient only (N = 32): conv1's weight gradient fused in
+  // (w1_tile_wgrad) -- w1_part non-null turns it on
+  const uint8_t* w1_route;   // pool1's routing bytes, NHWC (B,H,W,32): the dgrad's grid
+  const float* w1_in;        // conv1's input frames, fp32 NHWC (B,2H,2W,4)
+  float* w1_part;            // slabs [B * tiles][32][w1_np], bias at column 196
+  int w1_np;
 };
 
 // Epilogue of a direct conv tile (accumulator rows window-major: a lane's 4
@@ -382,6 +402,225 @@ __device__ __forceinline__ void split_epilogue_fwd_lds(const SplitArgs& a,
       __builtin_amdgcn_raw_buffer_store_b128(
           *reinterpret_cast<const u32x4*>(sm + win * N + 16 * c), rm, off * N + 16 * c, 0, 16);
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// conv1's weight gradient fused into conv2's data gradient (backward of
+// train_val.prototxt:39-61; conv1 has no bottom diff).  A data-gradient tile
+// ends with dpool1 at its TY x TX pool1 pixels; through pool1's routing bytes
+// that is dconv1 at the 2TY x 2TX conv1 pixels under them, and those pixels'
+// share of
+//   dW1[co][ky][kx][ci] = sum_p dconv1[p][co] frame[p + (ky-3, kx-3)][ci]
+//   db1[co]             = sum_p dconv1[p][co]
+// needs nothing else but the frames' halo.  So the workgroup scatters its
+// dpool1 values (split, split.h split3) into an LDS image of the expanded
+// dconv1 rows, stages the halo (frames are integers: exact in bf16, ONE
+// plane), runs conv1's MFMAs over its own pixels and writes its fp32 slab for
+// the slab reduce (fixed order: deterministic, no atomics).  dpool1 never
+// leaves the workgroup: round 3 wrote it split (6.3 MB at 64x64 B = 32) for a
+// separate 14 us launch that re-read and re-expanded it.
+//
+// MFMA form (as round 3's standalone kernel): A = dconv1 (32 co x 16 pixels of
+// a row), B = frames (16 pixels x n = 4 kx + ci, kx 0..7: column 28..31 is a
+// zero tap, dropped), both read with ds_read_b64_tr_b16 out of pixel-major
+// rows; the halo row is stored with pixel stride 4 bf16, so tap row ky's B is
+// one transposed read of halo row y + ky at offset 4x + n.  Work unit = (tap
+// row ky, 16-pixel column segment): 3 MFMAs (the three dconv1 planes x the
+// exact frame) per conv1 row of the tile; a unit's sums over the segments
+// meet in LDS in fixed order.
+// ---------------------------------------------------------------------------
+template <int TY, int TX, int NT>
+struct W1Fuse {
+  static constexpr int R = 2 * TY;                  // conv1 rows of the tile
+  static constexpr int XW = (2 * TX + 15) & ~15;    // conv1 pixels per row, whole k-steps
+  static constexpr int NSEG = XW / 16;
+  static constexpr int PSD = 32;                    // bf16 per pixel (32 channels, 64 B:
+                                                    // conflict-free transposed reads)
+  static constexpr int XPL = R * XW * PSD;          // bf16 per dconv1 plane
+  static constexpr int HR = R + 6;                  // halo rows
+  static constexpr int HW = XW + 6;                 // halo pixels per row
+  static constexpr int IROW = 4 * HW + 64;          // bf16 per halo row (+ the read tail)
+  static constexpr int kXB = 3 * XPL * 2;
+  static constexpr int kHaloB = HR * IROW * 2;
+  static constexpr int NU = 7 * NSEG;               // MFMA units (ky, seg)
+  static constexpr int NWV = NT / 64;
+  static constexpr int UPW = (NU + NWV - 1) / NWV;  // units per wave
+  static constexpr int kRedB = NU * 16 * 64 * 4;
+  static constexpr int kBiasB = NT * 4;
+  static constexpr int kSmemB = (kXB + kHaloB > kRedB ? kXB + kHaloB : kRedB) + kBiasB;
+  static constexpr int NH = (HR * HW + NT - 1) / NT;   // halo pixels per thread
+  static_assert(kSmemB <= 160 * 1024, "fused conv1 weight gradient: LDS");
+  static_assert(UPW <= 4, "fused conv1 weight gradient: accumulators");
+};
+
+// The frames' halo of the tile, loaded to registers before the data
+// gradient's k-group sums (its latency hides under them): pixel (hy, hx) of
+// the halo is frame pixel (2 y0 - 3 + hy, 2 x0 - 3 + hx), zero outside.
+template <class F>
+__device__ __forceinline__ void w1_halo_load(const SplitArgs& a, int b, int y0, int x0, int tid,
+                                             float4 (&hv)[F::NH]) {
+  const int H1 = 2 * a.H, W1 = 2 * a.W;
+#pragma unroll
+  for (int k = 0; k < F::NH; ++k) {
+    const int f = tid + k * (F::NWV * 64);
+    const int hy = f / F::HW, hx = f - hy * F::HW;
+    const int gy = 2 * y0 - 3 + hy, gx = 2 * x0 - 3 + hx;
+    hv[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (f < F::HR * F::HW && (unsigned)gy < (unsigned)H1 && (unsigned)gx < (unsigned)W1)
+      hv[k] = *reinterpret_cast<const float4*>(a.w1_in + (((size_t)b * H1 + gy) * W1 + gx) * 4);
+  }
+}
+
+// The routing bytes of the lane's epilogue elements (split_epilogue's DGRAD
+// enumeration; 4 = nothing routed, also outside the image / tile).
+template <int TM, int TN, int TX, int WK, int NWIN>
+__device__ __forceinline__ void w1_route_load(const SplitArgs& a, int b, int y0, int x0, int wmi,
+                                              int l31, int h, int wkg, uint8_t (&rt)[TM][16]) {
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int mb = wmi * TM * 32 + 32 * i;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      rt[i][r] = 4;
+      if ((r >> 2) % WK != wkg) continue;
+      const int m = mb + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int win = m >> 2;
+      if (win >= NWIN) continue;
+      const int y = y0 + 2 * (win / (TX / 2)) + ((m >> 1) & 1);
+      const int x = x0 + 2 * (win % (TX / 2)) + (m & 1);
+      if (y >= a.H || x >= a.W) continue;
+      rt[i][r] = a.w1_route[(((size_t)b * a.H + y) * a.W + x) * 32 + l31];
+    }
+  }
+}
+
+// The fused conv1 weight gradient of one data-gradient tile (TN = 1, N = 32:
+// channel l31).  acc: the lane's dpool1 values (split_epilogue's rows); every
+// wave of the workgroup calls it (barriers inside).
+template <int TY, int TX, int NT, int TM, int WK, int NWIN>
+__device__ __forceinline__ void w1_tile_wgrad(const SplitArgs& a, char* smem,
+                                              const f32x16 (&acc)[TM][1],
+                                              const uint8_t (&rt)[TM][16],
+                                              const float4 (&hv)[W1Fuse<TY, TX, NT>::NH], int b,
+                                              int tile, int wmi, int l31, int h, int wkg,
+                                              int tid) {
+  using F = W1Fuse<TY, TX, NT>;
+  const int lane = tid & 63, wid = tid >> 6;
+  __bf16* X = reinterpret_cast<__bf16*>(smem);                       // [3][R][XW][32]
+  __bf16* halo = reinterpret_cast<__bf16*>(smem + F::kXB);           // [HR][IROW]
+  float* bsm = reinterpret_cast<float*>(smem + (F::kXB + F::kHaloB > F::kRedB
+                                                    ? F::kXB + F::kHaloB : F::kRedB));
+  __syncthreads();   // every wave's reads of the k-group sums (smem) are done
+  // ---- scatter: each element's value to its routed quadrant, 0 to the others ----
+  float bsum = 0.f;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int mb = wmi * TM * 32 + 32 * i;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if ((r >> 2) % WK != wkg) continue;
+      const int m = mb + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int win = m >> 2;
+      if (win >= NWIN) continue;                  // padding rows: no pixel
+      const int ty = 2 * (win / (TX / 2)) + ((m >> 1) & 1);
+      const int tx = 2 * (win % (TX / 2)) + (m & 1);
+      const int q = rt[i][r];
+      const float v = q < 4 ? acc[i][0][r] : 0.f;   // 4: ReLU'd window / outside the image
+      bsum += v;
+      __bf16 s0, s1, s2;
+      split3(v, s0, s1, s2);
+      const __bf16 zero = (__bf16)0.f;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int e = ((2 * ty + (qq >> 1)) * F::XW + 2 * tx + (qq & 1)) * F::PSD + l31;
+        const bool on = q == qq;
+        X[e] = on ? s0 : zero;
+        X[F::XPL + e] = on ? s1 : zero;
+        X[2 * F::XPL + e] = on ? s2 : zero;
+      }
+    }
+  }
+  // the rows' padding pixels (2 TX .. XW) stay zero
+  if constexpr (F::XW > 2 * TX) {
+    constexpr int PADV = (F::XW - 2 * TX) * (F::PSD / 8);   // 16-byte vectors per row and plane
+    for (int f = tid; f < 3 * F::R * PADV; f += NT) {
+      const int pr = f / PADV, c = f - pr * PADV;            // (plane, row), vector
+      const int p = pr / F::R, row = pr - p * F::R;
+      *reinterpret_cast<u32x4*>(X + p * F::XPL + (row * F::XW + 2 * TX) * F::PSD + 8 * c) =
+          u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+  // ---- the frames' halo: fp32 -> bf16 (exact), pixel stride 4 ----
+#pragma unroll
+  for (int k = 0; k < F::NH; ++k) {
+    const int f = tid + k * NT;
+    if (f < F::HR * F::HW) {
+      const int hy = f / F::HW, hx = f - hy * F::HW;
+      __bf16 q4[4] = {(__bf16)hv[k].x, (__bf16)hv[k].y, (__bf16)hv[k].z, (__bf16)hv[k].w};
+      *reinterpret_cast<uint2*>(halo + hy * F::IROW + 4 * hx) = *reinterpret_cast<uint2*>(q4);
+    }
+  }
+  bsm[tid] = bsum;
+  __syncthreads();
+  // ---- MFMAs: unit u = (ky, seg) of wave u % NWV ----
+  const int gq = lane >> 4, iq = (lane & 15) >> 2, ip = lane & 3;
+  const int pix0 = 8 * (gq >> 1) + iq;
+  const int chn = 16 * (gq & 1) + 4 * ip;
+  f32x16 wacc[F::UPW];
+#pragma unroll
+  for (int k = 0; k < F::UPW; ++k)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) wacc[k][e] = 0.f;
+#pragma unroll
+  for (int k = 0; k < F::UPW; ++k) {
+    const int u = wid + F::NWV * k;
+    if (u >= F::NU) break;                        // wave-uniform
+    const int ky = u / F::NSEG, seg = u - ky * F::NSEG;
+    const __bf16* pa0 = X + (16 * seg + pix0) * F::PSD + chn;
+    const __bf16* pb0 = halo + ky * F::IROW + 4 * (16 * seg + pix0) + chn;
+#pragma unroll 4
+    for (int row = 0; row < F::R; ++row) {
+      bf16x8 av[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const __bf16* pa = pa0 + p * F::XPL + row * F::XW * F::PSD;
+        av[p] = tr_pair(pa, pa + 4 * F::PSD);
+      }
+      const __bf16* pb = pb0 + row * F::IROW;
+      const bf16x8 bv = tr_pair(pb, pb + 16);
+      wacc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2], bv, wacc[k], 0, 0, 0);
+      wacc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], bv, wacc[k], 0, 0, 0);
+      wacc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv, wacc[k], 0, 0, 0);
+    }
+  }
+  __syncthreads();   // X / halo reads done: the units' tiles go where X was
+  float* red = reinterpret_cast<float*>(smem);    // [NU][16][64]
+#pragma unroll
+  for (int k = 0; k < F::UPW; ++k) {
+    const int u = wid + F::NWV * k;
+    if (u >= F::NU) break;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) red[(u * 16 + e) * 64 + lane] = wacc[k][e];
+  }
+  __syncthreads();
+  // ---- the tile's slab: sums over the segments in order, write-through ----
+  const uint32_t slab = (uint32_t)tile * 32u * (uint32_t)a.w1_np;
+  const __amdgpu_buffer_rsrc_t rs =
+      wt_rsrc(a.w1_part, (uint32_t)((size_t)(slab + 32u * (uint32_t)a.w1_np) * 4));
+  for (int f = tid; f < 7 * 1024; f += NT) {
+    const int ky = f >> 10, e = f & 1023;
+    const int r = e >> 6, l = e & 63;
+    float v = red[((ky * F::NSEG) * 16) * 64 + e];
+#pragma unroll
+    for (int sg = 1; sg < F::NSEG; ++sg) v += red[((ky * F::NSEG + sg) * 16) * 64 + e];
+    const int co = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), n = l & 31;
+    if (n < 28) wt_store(rs, (slab + (uint32_t)(co * a.w1_np + ky * 28 + n)) * 4, v);
+  }
+  if (tid < 32) {   // bias: the lanes of channel tid, waves in order
+    float v = 0.f;
+    for (int w = 0; w < F::NWV; ++w) v += bsm[w * 64 + tid] + bsm[w * 64 + 32 + tid];
+    wt_store(rs, (slab + (uint32_t)(tid * a.w1_np + 196)) * 4, v);
   }
 }
 
@@ -674,6 +913,19 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] += cor[i][j];
+  // conv2's data gradient with conv1's weight gradient fused: the frames'
+  // halo and the routing bytes are loaded now, under the k-group sums
+  constexpr bool kW1 = DGRAD && N == 32 && CPT == 64 && TN == 1;
+  using F1 = W1Fuse<kW1 ? TY : 2, kW1 ? TX : 2, C::kThreads>;   // (no instantiation otherwise)
+  float4 w1h[F1::NH];
+  uint8_t w1r[TM][16];
+  const bool w1 = kW1 && a.w1_part != nullptr;
+  if constexpr (kW1) {
+    if (w1) {
+      w1_halo_load<F1>(a, b, y0, x0, tid, w1h);
+      w1_route_load<TM, 1, TX, WK, C::NWIN>(a, b, y0, x0, wmi, l31, h, wkg, w1r);
+    }
+  }
   if (WK > 1) {
     // every k group parks its sums in LDS; group k then finishes the pooling
     // windows gi (4 accumulator rows each) with gi % WK == k, summing the
@@ -703,6 +955,15 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
                                                                     x0, wmi, wni, l31, h, wkg, tid);
     return;
   }
+  if constexpr (kW1) {
+    if (w1) {
+      const f32x16(&acc1)[TM][1] = reinterpret_cast<const f32x16(&)[TM][1]>(acc);
+      w1_tile_wgrad<TY, TX, C::kThreads, TM, WK, C::NWIN>(a, smem, acc1, w1r, w1h, b,
+                                                          by * gridDim.x + bx, wmi, l31, h, wkg,
+                                                          tid);
+      return;
+    }
+  }
   split_epilogue<TM, TN, TX, N, DGRAD, WK, C::NWIN>(a, acc, bpre, b, z, y0, x0, wmi, wni, l31, h,
                                                     wkg);
 }
@@ -718,8 +979,12 @@ template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK
 inline hipError_t launch_split_conv(SplitArgs a, int nz, hipStream_t st) {
   using C = SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK>;
   auto kern = split_conv_kernel<CPT, CP, N, KS, TY, TX, WM, WN, WK, DGRAD>;
+  // conv2's data gradient: room for the fused conv1 weight gradient too
+  constexpr bool kW1 = DGRAD && N == 32 && CPT == 64 && C::TN == 1;
+  constexpr int kW1B = kW1 ? W1Fuse<kW1 ? TY : 2, kW1 ? TX : 2, C::kThreads>::kSmemB : 0;
+  constexpr int smem = C::kSmemB > kW1B ? C::kSmemB : kW1B;
   static std::atomic<uint64_t> attr{0};
-  if (hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(kern), attr, (int)(C::kSmemB)))
+  if (hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(kern), attr, smem))
     return e;
   // the forward epilogue writes one of the fp32 / split outputs (see
   // split_epilogue_fwd_lds)
@@ -727,8 +992,7 @@ inline hipError_t launch_split_conv(SplitArgs a, int nz, hipStream_t st) {
     return hipErrorInvalidValue;
   a.tiles_x = (a.W + TX - 1) / TX;
   const int tiles_y = (a.H + TY - 1) / TY;
-  hipLaunchKernelGGL(kern, dim3(tiles_y * a.tiles_x, a.B, nz), dim3(C::kThreads), C::kSmemB, st,
-                     a);
+  hipLaunchKernelGGL(kern, dim3(tiles_y * a.tiles_x, a.B, nz), dim3(C::kThreads), smem, st, a);
   return hipGetLastError();
 }
 

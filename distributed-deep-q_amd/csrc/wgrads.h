@@ -37,8 +37,6 @@ inline void wgrads_groups(int rows, int nts, int* G, int* RPG, int target = 512)
   *G = (rows + rpg - 1) / rpg;
 }
 
-typedef short i16x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 struct WgradSArgs {
   int B, H, W;              // layer grid (input and dconv share H x W)
@@ -73,14 +71,6 @@ struct WgradSGeom {
 };
 
 
-__device__ __forceinline__ bf16x8 tr_pair(const __bf16* p0, const __bf16* p1) {
-  typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
-  const i16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(p0));
-  const i16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(p1));
-  typedef short i16x8 __attribute__((ext_vector_type(8)));
-  const i16x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-  return __builtin_bit_cast(bf16x8, v);
-}
 
 // DSRC: the dconv rows' source -- 0: pooled split + routing bytes (conv2's),
 // 1: pooled fp32 + routing bytes, split while staged, 2: expanded split
@@ -469,269 +459,4 @@ inline hipError_t launch_wgrads_conv23(const WgradSArgs& a2, const WgradSArgs& a
 
 }  // namespace ddq
 
-namespace ddq {
 
-// ---------------------------------------------------------------------------
-// conv1 weight gradient on the bf16 matrix cores.  The input is the replay
-// frames (exact in bf16: ONE plane), so a (tile, k-step) needs three MFMAs
-// (dconv planes x frame).  One workgroup = one image band of R rows, 4 waves;
-// the band's input halo (R+6 rows, single bf16 plane, pixel stride 4: a row
-// read at offset 4x + n is input pixel x + kx - 3, channel ci for
-// n = 4 kx + ci, so the B operand of tap row ky is a plain transposed read
-// of the halo row y + ky, columns n = 0..31) is staged once; every wave
-// streams its own dconv rows (3 planes, expanded from the pooled split
-// gradient through pool1's routing bytes) and accumulates all 7 tap rows.
-// Output: one fp32 slab per band, [band][co][NP], n = ky*28 + kx*4 + ci
-// (columns 28..31 of a tap row are dropped), bias at n = 196.
-// ---------------------------------------------------------------------------
-struct Wgrad1SArgs {
-  int B, H, W, R;              // conv1 grid (H = W = S), band height
-  int NP;                      // slab pitch (>= 197)
-  const __bf16* dpool;         // split pooled gradient (B,H/2,W/2,32), plane stride d_elems
-  int64_t d_elems;
-  const uint8_t* droute;       // pool1's NHWC routing bytes
-  const float* in;             // fp32 NHWC (B,H,W,4) frames (exact in bf16)
-  float* part;                 // [B * H / R][32][NP]
-};
-
-template <int WMAX, int NW>
-struct Wgrad1SGeom {
-  static constexpr int PSD = 32;                           // dconv pixel stride (64 B)
-  static __host__ __device__ int in_row(int W) { return 4 * (W + 6) + 64; }   // + read tail
-  static __host__ __device__ int d_plane(int W) { return ((W + 15) & ~15) * PSD; }
-  // the halo patch + the NW waves' dconv row pairs; at least the image of the
-  // final cross-wave sums (NW x 16 x 64 floats)
-  // dconv rows staged per wave: both conv rows of a pooled row (6 planes)
-  static constexpr int kRowPlanes = 6;
-  static __host__ __device__ size_t bytes(int W, int R) {
-    const size_t a = ((size_t)(R + 6) * in_row(W) + NW * kRowPlanes * d_plane(W)) * 2;
-    return a > (size_t)NW * 16 * 64 * 4 ? a : (size_t)NW * 16 * 64 * 4;
-  }
-};
-
-template <int WMAX, int NW>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) void wgrad1s_kernel(
-    const Wgrad1SArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char sm_w1[];
-  using Geo = Wgrad1SGeom<WMAX, NW>;
-  const int W = a.W, H = a.H, R = a.R;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int l31 = lane & 31, h = lane >> 5;
-  const int irow = Geo::in_row(W), dpl = Geo::d_plane(W);
-  __bf16* patch = reinterpret_cast<__bf16*>(sm_w1);                 // [R+6][irow]
-  __bf16* rd = patch + (R + 6) * irow + w * Geo::kRowPlanes * dpl;  // this wave's [2 or 1][3][W16][32]
-  const int bands = H / R;
-  const int band = blockIdx.x;
-  const int b = band / bands, y0 = (band % bands) * R;
-
-  // ---- input halo: fp32 -> bf16 (exact), zero outside the image ----
-  for (int f = threadIdx.x; f < (R + 6) * (irow / 4); f += 64 * NW) {
-    const int py = f / (irow / 4), px = f % (irow / 4);
-    const int gy = y0 - 3 + py, gx = px - 3;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if ((unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
-      v = *reinterpret_cast<const float4*>(a.in + (((size_t)b * H + gy) * W + gx) * 4);
-    __bf16 q[4] = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
-    *reinterpret_cast<uint2*>(patch + py * irow + 4 * px) = *reinterpret_cast<uint2*>(q);
-  }
-  // dconv tail pixels (W..W16) stay zero
-  for (int i = lane; i < Geo::kRowPlanes * (((W + 15) & ~15) - W) * 4; i += 64) {
-    const int per = (((W + 15) & ~15) - W) * 4;
-    const int p = i / per, r = i - p * per;
-    reinterpret_cast<u32x4*>(rd + p * dpl + W * Geo::PSD)[r] = u32x4{0u, 0u, 0u, 0u};
-  }
-
-  f32x16 acc[7];
-#pragma unroll
-  for (int t = 0; t < 7; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-  float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-
-  // A wave owns pooled dconv rows k (conv rows 2k and 2k+1 of the band): the
-  // pooled row is loaded once and expanded into both conv rows (the four
-  // quadrants of every pooling window) with one routing-byte extraction; the
-  // bias sums every routed value once (route != 4).  Lane keeps chunk dc8
-  // (8 of the 32 channels) and walks pooled pixels dpx, dpx + 16, ...
-  constexpr int NPD = (WMAX / 2 + 15) / 16;
-  const int dc8 = lane & 3, dpx = lane >> 2;
-  struct Regs {
-    u32x4 d[3][NPD];
-    u32x2 m[NPD];
-  };
-  // bounds-checked buffer loads (wgrads_body): out-of-range chunks read 0 --
-  // routing bytes 0 with values 0, which route and sum nothing
-  constexpr uint32_t kOOB = 0x80000000u;
-  const uint32_t db = (uint32_t)(a.B * (H >> 1) * (W >> 1) * 32);
-  const __amdgpu_buffer_rsrc_t rd_g[3] = {
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.dpool, (short)0, (int)(db * 2), 0x00020000),
-      __builtin_amdgcn_make_buffer_rsrc((void*)(a.dpool + a.d_elems), (short)0, (int)(db * 2),
-                                        0x00020000),
-      __builtin_amdgcn_make_buffer_rsrc((void*)(a.dpool + 2 * a.d_elems), (short)0, (int)(db * 2),
-                                        0x00020000)};
-  const __amdgpu_buffer_rsrc_t rm_g =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.droute, (short)0, (int)db, 0x00020000);
-  auto load = [&](Regs& G, int k) {
-    const bool live = 2 * k < R;
-    const int yp = (y0 >> 1) + k;
-    const uint32_t o0 = (uint32_t)(((b * (H >> 1) + yp) * (W >> 1) + dpx) * 32 + 8 * dc8);
-#pragma unroll
-    for (int u = 0; u < NPD; ++u) {
-      const bool ok = live && dpx + 16 * u < (W >> 1);
-      const uint32_t o = o0 + (uint32_t)(u * 16 * 32);
-      G.m[u] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rm_g, (int)(ok ? o : kOOB), 0, 0));
-#pragma unroll
-      for (int p = 0; p < 3; ++p)
-        G.d[p][u] = __builtin_bit_cast(
-            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rd_g[p], (int)(ok ? o * 2 : kOOB), 0, 0));
-    }
-  };
-  // dys: the conv rows (dy bits) whose quadrants are stored now; bias with dy 0
-  auto store = [&](const Regs& G, int dys) {
-#pragma unroll
-    for (int u = 0; u < NPD; ++u) {
-      const int px = dpx + 16 * u;
-      if (px >= (W >> 1)) continue;
-      uint32_t ra[4], rb[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {   // routing bytes of channels 2e, 2e+1
-        const uint32_t mw = G.m[u][e >> 1];
-        ra[e] = (mw >> (16 * (e & 1))) & 0xff;
-        rb[e] = (mw >> (16 * (e & 1) + 8)) & 0xff;
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {   // quadrant q = 2 dy + dx
-        if (!((dys >> (q >> 1)) & 1)) continue;
-        uint32_t keep[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          keep[e] = (ra[e] == (uint32_t)q ? 0xffffu : 0u) | (rb[e] == (uint32_t)q ? 0xffff0000u : 0u);
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          u32x4 o;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = G.d[p][u][e] & keep[e];
-          *reinterpret_cast<u32x4*>(rd + ((Geo::kRowPlanes == 6 ? (q >> 1) : 0) * 3 + p) * dpl +
-                                    (2 * px + (q & 1)) * Geo::PSD + 8 * dc8) = o;
-        }
-      }
-      if (!(dys & 1)) continue;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {   // bias: every routed value once
-        const uint32_t any = (ra[e] != 4u ? 0xffffu : 0u) | (rb[e] != 4u ? 0xffff0000u : 0u);
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          const uint32_t o = G.d[p][u][e] & any;
-          bsum[2 * e] += __builtin_bit_cast(float, o << 16);
-          bsum[2 * e + 1] += __builtin_bit_cast(float, o & 0xffff0000u);
-        }
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  };
-  // transposed-read lane offsets (as wgrads_body)
-  const int gq = lane >> 4, iq = (lane & 15) >> 2, ip = lane & 3;
-  const int pix0 = 8 * (gq >> 1) + iq;
-  const int chn = 16 * (gq & 1) + 4 * ip;
-  __syncthreads();   // the halo patch
-  Regs g;
-  if (2 * w < R) load(g, w);
-  for (int k = w; 2 * k < R; k += NW) {
-    Regs cur = g;
-    if (Geo::kRowPlanes == 6) store(cur, 3);
-    load(g, k + NW);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int dy = 0; dy < 2; ++dy) {
-      if (Geo::kRowPlanes == 3) {   // this conv row's quadrants into the wave's 3 planes
-        if (dy) __builtin_amdgcn_wave_barrier();   // row 0's reads done (wave-private region)
-        store(cur, 1 << dy);
-      }
-      const int r = 2 * k + dy;
-      const __bf16* rdr = rd + (Geo::kRowPlanes == 6 ? dy : 0) * 3 * dpl;
-#pragma unroll
-      for (int s = 0; s < WMAX / 16; ++s) {
-        if (16 * s >= W) break;
-        // B fragments one tap row ahead of their three MFMAs (all seven live
-        // at once would spill at W = 84)
-        bf16x8 av[3], bv[2];
-        const __bf16* pb = patch + r * irow + 4 * (16 * s + pix0) + chn;
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          const __bf16* pa = rdr + p * dpl + (16 * s + pix0) * Geo::PSD + chn;
-          av[p] = tr_pair(pa, pa + 4 * Geo::PSD);
-        }
-        bv[0] = tr_pair(pb, pb + 16);
-#pragma unroll
-        for (int ky = 0; ky < 7; ++ky) {
-          if (ky < 6) bv[(ky + 1) & 1] = tr_pair(pb + (ky + 1) * irow, pb + (ky + 1) * irow + 16);
-          acc[ky] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2], bv[ky & 1], acc[ky], 0, 0, 0);
-          acc[ky] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], bv[ky & 1], acc[ky], 0, 0, 0);
-          acc[ky] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[ky & 1], acc[ky], 0, 0, 0);
-        }
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-  // ---- the NW waves' tiles in fixed order -> the band's slab ----
-  float* red = reinterpret_cast<float*>(sm_w1);
-  const __amdgpu_buffer_rsrc_t srs =
-      wt_rsrc(a.part, (uint32_t)((size_t)a.B * (a.H / a.R) * 32 * a.NP * 4));
-  const uint32_t sbase = (uint32_t)((size_t)band * 32 * a.NP * 4);
-#pragma unroll
-  for (int t = 0; t < 7; ++t) {
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 16; ++r) red[(w * 16 + r) * 64 + lane] = acc[t][r];
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 16 / NW; ++j) {
-      const int r = w + NW * j;
-      const int e = r * 64 + lane;
-      float v = red[e];
-#pragma unroll
-      for (int ww = 1; ww < NW; ++ww) v += red[ww * 1024 + e];
-      const int co = (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (l31 < 28) wt_store(srs, sbase + (uint32_t)((co * a.NP + t * 28 + l31) * 4), v);
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < 8; ++j) red[(w * 64 + lane) * 8 + j] = bsum[j];
-  __syncthreads();
-  if (threadIdx.x < 32) {
-    const int co = threadIdx.x, c8 = co >> 3, j = co & 7;
-    float v = 0.f;
-    for (int ww = 0; ww < NW; ++ww)
-      for (int l = c8; l < 64; l += 4) v += red[(ww * 64 + l) * 8 + j];
-    wt_store(srs, sbase + (uint32_t)((co * a.NP + 196) * 4), v);
-  }
-}
-
-// NW = 4 waves (8 waves, one per band row: 16.3 us against 14.3 at 64x64 --
-// the kernel is VALU-bound on the routing expansion, not latency-bound)
-template <int WMAX>
-inline hipError_t launch_wgrad1s_w(const Wgrad1SArgs& a, hipStream_t st) {
-  constexpr int NW = WMAX <= 64 ? 4 : 2;   // two staged rows per wave: LDS
-  using Geo = Wgrad1SGeom<WMAX, NW>;
-  const size_t shm = Geo::bytes(a.W, a.R);
-  if (shm > 160 * 1024) return hipErrorInvalidValue;
-  auto kern = wgrad1s_kernel<WMAX, NW>;
-  static std::atomic<uint64_t> attr{0};
-  if (hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(kern), attr, (int)(160 * 1024)))
-    return e;
-  hipLaunchKernelGGL(kern, dim3(a.B * (a.H / a.R)), dim3(64 * NW), shm, st, a);
-  return hipGetLastError();
-}
-
-inline hipError_t launch_wgrad1s(const Wgrad1SArgs& a, hipStream_t st) {
-  if (a.W <= 32) return launch_wgrad1s_w<32>(a, st);
-  if (a.W <= 64) return launch_wgrad1s_w<64>(a, st);
-  if (a.W <= 96) return launch_wgrad1s_w<96>(a, st);
-  if (a.W <= 128) return launch_wgrad1s_w<128>(a, st);
-  return hipErrorInvalidValue;
-}
-
-}  // namespace ddq
