@@ -533,6 +533,109 @@ def exchange_paths(net, rule, steps=240, warmup=24, profile=5):
             "paths": out}
 
 
+PUBLISHED_MESSAGING = {   # results/cost-vs-image-size.txt:2-5 (Caffe CPU worker, 2015)
+    16: {"message_MB": 0.91, "generate_ms": 1.97, "load_ms": 0.93, "server_latency_ms": 5},
+    32: {"message_MB": 2.49, "generate_ms": 4.18, "load_ms": 2.05, "server_latency_ms": 15},
+    64: {"message_MB": 8.78, "generate_ms": 8.55, "load_ms": 5.11, "server_latency_ms": 40},
+    128: {"message_MB": 33.94, "generate_ms": 27.47, "load_ms": 18.99, "server_latency_ms": 116}}
+
+
+def messaging_costs(frames=(16, 32, 64, 128), B=32, trials=7):
+    """The push/pull half the reference publishes (results/cost-vs-image-size
+    .txt, results/server-latency.txt; harness barista/messaging.py:168-230 and
+    the HTTP round trip of baristanet.py:105-123): per frame side, the gradient
+    message through ddq/barista/messaging.py -- size, generate (device ->
+    host copy of the gradient + framing) and load times, uncompressed and
+    zlib -- and the HTTP round trips to a ddq.param_server.ParamServer (its
+    model and apply on this GPU) on 127.0.0.1: POST /api/v1/update_model of
+    that message (the reference's 'server latency') and GET
+    /api/v1/latest_model.  Medians over `trials`."""
+    import http.client
+    import socket
+    import threading
+    import ddq
+    from ddq.barista import messaging as M
+    from ddq.param_server import ParamServer
+    from ddq.params import init_params_flat
+
+    def med(fn):
+        ts = []
+        for _ in range(trials):
+            t0 = time.perf_counter()
+            r = fn()
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts)) * 1e3, r
+
+    out = []
+    for S in frames:
+        net = ddq.DeepQNet(batch=B, frame=S)
+        theta = init_params_flat(S, seed=42)
+        net.set_flat(0, theta)
+        net.set_flat(1, theta)
+        net.replay_create(2048)
+        fill_replay(net, 2048, S, seed=5)
+        cfg = net.step_cfg("rmsprop", lr=1e-4, target_period=10, seed=1234)
+        net.step(cfg)
+        net.synchronize()
+        e = {"frame": S, "params": int(net.num_params)}
+        for comp in (False, True):
+            gen_ms, msg = med(lambda: M.create_gradient_message(net, compress=comp))
+            load_ms, _ = med(lambda: M.load_gradient_message(msg, compressed=comp))
+            key = "zlib" if comp else "raw"
+            e[key] = {"message_MB": round(len(msg) / 1e6, 4), "generate_ms": round(gen_ms, 3),
+                      "load_ms": round(load_ms, 3)}
+        raw = M.create_gradient_message(net)
+        net.close()
+        ps = ParamServer(frame=S, batch=B)
+        ps.init_params(seed=42)
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        th = threading.Thread(target=ps.serve, kwargs={"port": port}, daemon=True)
+        th.start()
+        conn = None
+        for _ in range(200):
+            try:
+                conn = http.client.HTTPConnection("127.0.0.1", port, timeout=30)
+                conn.request("GET", "/")
+                conn.getresponse().read()
+                break
+            except OSError:
+                conn = None
+                time.sleep(0.01)
+
+        def post():
+            conn.request("POST", "/api/v1/update_model", body=raw,
+                         headers={"Content-Type": "application/deepQ"})
+            return conn.getresponse().read()
+
+        def get():
+            conn.request("GET", "/api/v1/latest_model",
+                         headers={"Content-Type": "application/deepQ"})
+            return conn.getresponse().read()
+        post_ms, reply = med(post)
+        get_ms, model = med(get)
+        assert reply == b"Updated", reply
+        e["server"] = {"update_roundtrip_ms": round(post_ms, 3),
+                       "latest_model_roundtrip_ms": round(get_ms, 3),
+                       "model_message_MB": round(len(model) / 1e6, 4)}
+        conn.close()
+        ps.shutdown()
+        th.join(timeout=10)
+        ps.net.close()
+        if S in PUBLISHED_MESSAGING:
+            e["reference_published"] = PUBLISHED_MESSAGING[S]
+        out.append(e)
+    return {"batch": B, "trials": trials,
+            "note": "gradient message = the reference's framing + fp32 Q* payload "
+                    "(ddq/barista/messaging.py); generate includes the device -> host copy "
+                    "of the flat gradient; server round trips over HTTP/1.1 keep-alive on "
+                    "127.0.0.1 to ParamServer (model + rmsprop apply on this GPU); "
+                    "reference_published: results/cost-vs-image-size.txt (sys.getsizeof of "
+                    "the message, Caffe CPU worker, 2015 hardware)",
+            "frames": out}
+
+
 def frame_sweep(B=256, frames=range(16, 129, 8), steps=60, warmup=10, rule="rmsprop"):
     """batch 256, frame side 16..128 (results/cost-vs-image-size)."""
     import ddq
@@ -594,6 +697,8 @@ def main():
     ap.add_argument("--acting", action="store_true",
                     help="also time updates including acting (select_action + add_experience)")
     ap.add_argument("--no-sweep", action="store_true", help="skip the C3 frame sweep")
+    ap.add_argument("--no-messaging", action="store_true",
+                    help="skip the gradient-message / param-server round-trip costs (N=1)")
     ap.add_argument("--sweep", action="store_true",
                     help="C3: also run the batch-256 frame-size sweep 16..128 (slow)")
     ap.add_argument("--eager", action="store_true", help="no hipGraph (debug)")
@@ -785,6 +890,8 @@ def main():
             # the reduced sweep 16 / 64 / 128, --sweep the reference's 16..128/8
             out["frame_sweep"] = frame_sweep(frames=range(16, 129, 8) if args.sweep
                                              else (16, 64, 128))
+        if not args.no_messaging and world == 1:
+            out["messaging"] = messaging_costs()
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(B, S, seed=7)
         if not args.no_exchange_paths and world == 1 and not args.force_exchange:

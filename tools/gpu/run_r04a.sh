@@ -14,3 +14,7 @@ cd $R
 python3 tools/trace_summary.py gpurun_out/prof_step step
 python3 tools/bench_summary.py gpurun_out/bench_driver.json
 python3 tools/bench_summary.py gpurun_out/bench.json
+timeout -k 10 240 python -c "import json, bench; print(json.dumps(bench.messaging_costs()))" > gpurun_out/messaging.json 2> gpurun_out/messaging.err || { echo MESSAGING_FAILED; tail -20 gpurun_out/messaging.err; exit 1; }
+python -c "
+import json; d=json.load(open('gpurun_out/messaging.json'))
+for f in d['frames']: print(f['frame'], f['raw'], f['server'])"
