@@ -65,8 +65,9 @@ def ring():
             np.tile(nt, reps)[:N])
 
 
-def oracle_chain(ref, theta, ring_arrays, log, rule, lr, period):
+def oracle_chain(ref, theta, ring_arrays, log, rule, lr, period, S=S):
     st, ac, rw, nt = ring_arrays
+    N = len(st)
     r = ref.ReplayRef((4, S, S), N)
     r.state, r.action, r.reward, r.non_terminal = st, ac, rw, nt.astype(bool)
     r.head, r.valid = 0, N
@@ -93,7 +94,8 @@ def oracle_chain(ref, theta, ring_arrays, log, rule, lr, period):
     return thq, thp, state, loss
 
 
-def make_net(ddq, theta, ring, log=64):
+def make_net(ddq, theta, ring, log=64, S=S):
+    N = len(ring[0])
     net = ddq.DeepQNet(batch=B, frame=S)
     net.set_flat(0, theta)
     net.set_flat(1, theta)
@@ -193,3 +195,33 @@ def test_shipped_chain_free_running(ref_mod, ring, rule, lr, calls):
     if state is not None:
         close(net.optimizer_state(), state, what="%s cache after %d" % (rule, T))
     close(float(net.blob("loss")), loss, what="%s loss of step %d" % (rule, T))
+
+
+def test_deepq16_chain_free_running_48_sgd(ref_mod):
+    """48 free-running sgd steps of the shipped pipelined chain at the
+    reference's committed shape (deepq16: 16x16, B = 32; train_val.prototxt
+    :8-11), four P <- Q syncs, against the oracle replaying the reference's
+    loop on the logged minibatches: theta_Q, theta_P and the loss at rtol 1e-4
+    after the whole chain (calls of 20 + 5 + 23 steps: 8-step graphs, tail
+    graphs, single steps)."""
+    import ddq
+    from ddq.expgain import synthetic_transitions
+    from ddq.params import init_params_flat
+    S16, N16 = 16, 4096
+    ring16 = synthetic_transitions(N16, S16, seed=77)
+    theta = init_params_flat(S16, seed=42)
+    net = make_net(ddq, theta, ring16, log=64, S=S16)
+    calls = (20, 5, 23)
+    T = sum(calls)
+    cfg = net.step_cfg("sgd", lr=1e-2, target_period=10, seed=4321)
+    for k in calls:
+        net.step_pipelined(cfg, k)
+    net.synchronize()
+    log = net.index_log(0, T)
+    thq, thp, _, loss = oracle_chain(ref_mod, theta, ring16, log, "sgd", 1e-2, 10, S=S16)
+    gq, gp = net.get_flat(0), net.get_flat(1)
+    assert not np.array_equal(gq, theta)
+    close(gq, thq, what="sgd theta_Q after %d" % T)
+    close(gp, thp, what="sgd theta_P after %d" % T)
+    close(float(net.blob("loss")), loss, what="sgd loss of step %d" % T)
+    net.close()

@@ -171,6 +171,8 @@ FULL_PASS_CASES = [
     # C3: batch 256 across the frame sweep (results/cost-vs-image-size-trials.txt)
     (24, 256, "snake", "x3"), (64, 256, "bench", "bench"), (128, 256, "snake", "x3"),
     (104, 256, "snake", "x3"),
+    # C3 B = 256 at the frames whose tiles leave partial edge tiles
+    (40, 256, "snake", "x3"), (72, 256, "uniform", "x3"), (120, 256, "snake", "x3"),
     # the rest of the sweep's frames 16..128 / 8 (conv tilings incl. the
     # partial edge tiles of 40, 72, 104 and 120)
     (32, 4, "uniform", "x3"), (48, 4, "snake", "x3"), (56, 4, "uniform", "x3"),
