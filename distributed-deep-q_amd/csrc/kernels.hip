@@ -1519,9 +1519,9 @@ int fc4_splits_for(int S) { return fc4_fwd_splits(64 * (S / 8) * (S / 8)); }
 struct TileOpt {
   int ty, tx, rows;
 };
-template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK>
+template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, int MF = 0>
 constexpr TileOpt split_tile() {
-  return {TY, TX, WM * SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK>::TM * 32};
+  return {TY, TX, WM * SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK, MF>::TM * 32};
 }
 template <int TY, int TX, int WM>
 constexpr TileOpt conv1_tile() { return {TY, TX, WM * Conv1Cfg<TY, TX, WM>::TM * 32}; }
@@ -1541,42 +1541,50 @@ static const T& pick_tile(const T (&menu)[n], int H, int W) {
   return menu[best];
 }
 
+// A/B (make variant DEFS=-DDDQ_MF_FWD=1): the forward convolutions on
+// v_mfma_f32_16x16x32_bf16 (split.h SplitCfg MF)
+#ifndef DDQ_MF_FWD
+#define DDQ_MF_FWD 0
+#endif
+#ifndef DDQ_MF_C3F
+#define DDQ_MF_C3F 0
+#endif
 struct SplitMenu {
   TileOpt opt;
   hipError_t (*launch)(SplitArgs, int, hipStream_t);
 };
-#define DDQ_SPLIT_TILE(CPT, CP, N, KS, TY, TX, WM, WN, WK, DG)              \
+#define DDQ_SPLIT_TILE(CPT, CP, N, KS, TY, TX, WM, WN, WK, DG, MF)          \
   SplitMenu {                                                              \
-    split_tile<CPT, CP, N, KS, TY, TX, WM, WN, WK>(),                      \
-        &launch_split_conv<CPT, CP, N, KS, TY, TX, WM, WN, WK, DG>          \
+    split_tile<CPT, CP, N, KS, TY, TX, WM, WN, WK, MF>(),                  \
+        &launch_split_conv<CPT, CP, N, KS, TY, TX, WM, WN, WK, DG, MF>      \
   }
 // conv2 forward (32 -> 64, 5x5): 16 waves of one 32x32 block on 16 x 16
 static const SplitMenu kConv2Fwd[] = {
-    DDQ_SPLIT_TILE(32, 32, 64, 5, 16, 16, 8, 2, 1, false),
-    DDQ_SPLIT_TILE(32, 32, 64, 5, 10, 20, 7, 2, 1, false),
-    DDQ_SPLIT_TILE(32, 32, 64, 5, 12, 12, 5, 2, 1, false),
-    DDQ_SPLIT_TILE(32, 32, 64, 5, 8, 8, 2, 2, 1, false),
-    DDQ_SPLIT_TILE(32, 32, 64, 5, 8, 26, 7, 2, 1, false),
-    DDQ_SPLIT_TILE(32, 32, 64, 5, 14, 14, 7, 2, 1, false)};
+    DDQ_SPLIT_TILE(32, 32, 64, 5, 16, 16, 8, 2, 1, false, DDQ_MF_FWD),
+    DDQ_SPLIT_TILE(32, 32, 64, 5, 10, 20, 7, 2, 1, false, DDQ_MF_FWD),
+    DDQ_SPLIT_TILE(32, 32, 64, 5, 12, 12, 5, 2, 1, false, DDQ_MF_FWD),
+    DDQ_SPLIT_TILE(32, 32, 64, 5, 8, 8, 2, 2, 1, false, DDQ_MF_FWD),
+    DDQ_SPLIT_TILE(32, 32, 64, 5, 8, 26, 7, 2, 1, false, DDQ_MF_FWD),
+    DDQ_SPLIT_TILE(32, 32, 64, 5, 14, 14, 7, 2, 1, false, DDQ_MF_FWD)};
 // conv3 forward (64 -> 64, 3x3): two k groups on 8 x 8
 static const SplitMenu kConv3Fwd[] = {
-    DDQ_SPLIT_TILE(64, 64, 64, 3, 8, 8, 2, 2, 2, false),
-    DDQ_SPLIT_TILE(64, 64, 64, 3, 10, 10, 4, 2, 2, false),
-    DDQ_SPLIT_TILE(64, 64, 64, 3, 12, 12, 5, 2, 1, false),
-    DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 18, 4, 2, 2, false),
-    DDQ_SPLIT_TILE(64, 64, 64, 3, 4, 4, 1, 2, 2, false),
-    DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 26, 5, 2, 1, false)};
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 8, 8, 2, 2, 2, false, DDQ_MF_C3F),
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 10, 10, 4, 2, 2, false, 0),
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 12, 12, 5, 2, 1, false, 0),
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 18, 4, 2, 2, false, 0),
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 4, 4, 1, 2, 2, false, 0),
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 26, 5, 2, 1, false, 0)};
 // conv3 data gradient: four k groups on 4 x 8
 static const SplitMenu kConv3Dgrad[] = {
-    DDQ_SPLIT_TILE(64, 64, 64, 3, 4, 8, 1, 2, 4, true),
-    DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 10, 2, 2, 4, true),
-    DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 26, 5, 2, 1, true)};
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 4, 8, 1, 2, 4, true, 0),
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 10, 2, 2, 4, true, 0),
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 26, 5, 2, 1, true, 0)};
 // conv2 data gradient (64 -> 32): four k groups on 8 x 16
 static const SplitMenu kConv2Dgrad[] = {
-    DDQ_SPLIT_TILE(64, 64, 32, 5, 8, 16, 4, 1, 4, true),
-    DDQ_SPLIT_TILE(64, 64, 32, 5, 8, 20, 5, 1, 2, true),
-    DDQ_SPLIT_TILE(64, 64, 32, 5, 12, 12, 5, 1, 2, true),
-    DDQ_SPLIT_TILE(64, 64, 32, 5, 8, 8, 2, 1, 4, true)};
+    DDQ_SPLIT_TILE(64, 64, 32, 5, 8, 16, 4, 1, 4, true, 0),
+    DDQ_SPLIT_TILE(64, 64, 32, 5, 8, 20, 5, 1, 2, true, 0),
+    DDQ_SPLIT_TILE(64, 64, 32, 5, 12, 12, 5, 1, 2, true, 0),
+    DDQ_SPLIT_TILE(64, 64, 32, 5, 8, 8, 2, 1, 4, true, 0)};
 #undef DDQ_SPLIT_TILE
 
 struct Conv1Menu {

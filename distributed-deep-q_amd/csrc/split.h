@@ -109,16 +109,22 @@ __device__ __forceinline__ bf16x8 tr_pair(const __bf16* p0, const __bf16* p1) {
 // CPT input channels are processed in NCH = CPT / CP chunks of CP (the patch
 // of one chunk is resident at a time: conv2 dgrad's 64-channel patch of a
 // 16 x 16 tile would not fit LDS with its 3 planes).
-template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK = 1>
+// MF: the MFMA shape -- 0: v_mfma_f32_32x32x16_bf16 (32x32 blocks, k-steps of
+// 16 channels), 1: v_mfma_f32_16x16x32_bf16 (a wave's 32x32 sub-tile as four
+// 16x16 blocks, k-steps of 32 channels; the same operand bytes and MFMA
+// cycles per FLOP).  MF = 1 reads lane l's 8 channels [8 (l / 16), +8) of row
+// l % 16: pixel and weight-row strides CP + 16 bf16 (6 16-byte units) are
+// conflict-free for it (a bank model of the four 16-lane groups).
+template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK = 1, int MF = 0>
 struct SplitCfg {
   static constexpr int NCH = CPT / CP;
   static constexpr int PH = TY + KS - 1, PW = TX + KS - 1;
-  static constexpr int CS = CP + 8;                                   // bf16 per pixel
+  static constexpr int CS = CP + (MF ? 16 : 8);                       // bf16 per pixel
   static constexpr int RS0 = PW * CS;
   static constexpr int RS = RS0 + ((64 - (RS0 % 128)) + 128) % 128;   // == 64 (mod 128) bf16
-  static constexpr int CW = CP + 8;                                   // bf16 per weight row
+  static constexpr int CW = CP + (MF ? 16 : 8);                       // bf16 per weight row
   static constexpr int T = KS * KS;
-  static constexpr int KSTEP = CP / 16;
+  static constexpr int KSTEP = CP / (MF ? 32 : 16);
   static constexpr int kGroup = 64 * WM * WN * WK;                     // all waves stage
   static constexpr int kThreads = kGroup;
   static constexpr int KSW = KSTEP / WK;                              // k-steps per wave
@@ -142,6 +148,7 @@ struct SplitCfg {
   // every k group's accumulators for the fixed-order sums of the epilogue
   static_assert(WK == 1 || WK * WM * WN * 16 * 64 * 4 <= kSmemB, "k-split reduction");
   static_assert(4 % WK == 0, "epilogue windows per k group");
+  static_assert(MF == 0 || CP % 32 == 0, "16x16x32: whole 32-channel k-steps");
 };
 
 // Weight staging of one (chunk, tap) (3 planes of N x CP bf16): a global ->
@@ -163,7 +170,7 @@ struct SplitWStage {
   // for the load and the store of a lane
   static __device__ __forceinline__ int row(int q) {
     const int n0 = q / (CP / 8);
-    if (CP != 32) return n0;
+    if (CP != 32 || C::CW != 40) return n0;
     return (n0 & ~7) | ((n0 & 7) >> 1) | ((n0 & 1) << 2);
   }
 
@@ -303,10 +310,11 @@ __device__ __forceinline__ void split_epilogue(const SplitArgs& a, const f32x16 
 // finished reading the patch / ring (the barrier at the top).  LDS: NWIN * N *
 // 7 bytes.  One of out / out_split per launch (the forward passes never ask
 // for both).
-template <int TM, int TN, int TX, int N, int WK, int NWIN, int NT>
+template <int TM, int TN, int TX, int N, int WK, int NWIN, int NT, int MF = 0>
 __device__ __forceinline__ void split_epilogue_fwd_lds(const SplitArgs& a,
                                                        const f32x16 (&acc)[TM][TN],
-                                                       const float (&bpre)[TN], char* smem, int b,
+                                                       const float (&bpre)[TN * (MF ? 2 : 1)],
+                                                       char* smem, int b,
                                                        int z, int y0, int x0, int wmi, int wni,
                                                        int l31, int h, int wkg, int tid) {
   float* __restrict__ outz = z ? a.out[1] : a.out[0];
@@ -317,17 +325,22 @@ __device__ __forceinline__ void split_epilogue_fwd_lds(const SplitArgs& a,
   uint8_t* sm = reinterpret_cast<uint8_t*>(smem) + NWIN * N * 6;  // [NWIN][N]
   const bool split = osplit != nullptr;
   __syncthreads();
+  const int lane = l31 + 32 * h;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int mb = wmi * TM * 32 + 32 * i;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int n = wni * TN * 32 + 32 * j + l31;
-      const float bvv = bpre[j];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         if (g % WK != wkg) continue;
-        const int win = (mb + 8 * g + 4 * h) >> 2;
+        // element group g of the lane's accumulator: one pooling window x one
+        // output channel (MF 0: 32x32 rows 8g + 4h + 0..3, column l31; MF 1:
+        // 16x16 block (g >> 1, g & 1), rows 4 (lane >> 4) + 0..3, column lane & 15)
+        const int win = MF ? (mb + 16 * (g >> 1) + 4 * (lane >> 4)) >> 2 : (mb + 8 * g + 4 * h) >> 2;
+        const int n = MF ? wni * TN * 32 + 32 * j + 16 * (g & 1) + (lane & 15)
+                         : wni * TN * 32 + 32 * j + l31;
+        const float bvv = MF ? bpre[2 * j + (g & 1)] : bpre[j];
         if (win >= NWIN) continue;                // padding rows
         const float v0 = acc[i][j][4 * g + 0] + bvv, v1 = acc[i][j][4 * g + 1] + bvv;
         const float v2 = acc[i][j][4 * g + 2] + bvv, v3 = acc[i][j][4 * g + 3] + bvv;
@@ -624,10 +637,12 @@ __device__ __forceinline__ void w1_tile_wgrad(const SplitArgs& a, char* smem,
   }
 }
 
-template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, bool DGRAD>
+template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, bool DGRAD,
+          int MF = 0>
 __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, int bx, int by,
                                                 int bz) {
-  using C = SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK>;
+  using C = SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK, MF>;
+  static_assert(MF == 0 || !DGRAD, "16x16x32: forward convolutions only");
   constexpr int TM = C::TM, TN = C::TN, T = C::T, NCH = C::NCH;
   __bf16* patch = reinterpret_cast<__bf16*>(smem);
   __bf16* wbuf = reinterpret_cast<__bf16*>(smem + C::kPatchB);
@@ -639,12 +654,12 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
   const __bf16* __restrict__ wk = z ? a.wk[1] : a.wk[0];
   // the bias of the lane's output channels (fwd), loaded now: at the epilogue
   // its latency was exposed once per workgroup after the last MFMA
-  float bpre[C::TN];
+  float bpre[C::TN * (MF ? 2 : 1)];
 #pragma unroll
-  for (int j = 0; j < C::TN; ++j)
+  for (int j = 0; j < C::TN * (MF ? 2 : 1); ++j)
     bpre[j] = DGRAD ? 0.f
-                    : (z ? a.bias[1] : a.bias[0])[((wid % (WM * WN)) % WN) * C::TN * 32 + 32 * j +
-                                                  (lane & 31)];
+                    : (z ? a.bias[1] : a.bias[0])[((wid % (WM * WN)) % WN) * C::TN * 32 +
+                                                  (MF ? 16 * j + (lane & 15) : 32 * j + (lane & 31))];
 
   // ---- stage the halo patch of channel chunk ch (3 planes, zero outside) ----
   // Batches of 8 vectors per thread: every load of a batch is issued before
@@ -674,7 +689,7 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
       // 32-channel pixels (20 dwords apart): pixels q and q + 4 share an
       // 8-lane store group instead of q and q + 1 (SplitWStage::row)
       constexpr int NPX = C::PH * C::PW;
-      const int pix = (CP == 32 && pix0 < (NPX & ~7))
+      const int pix = (CP == 32 && C::CS == 40 && pix0 < (NPX & ~7))
                           ? (pix0 & ~7) | ((pix0 & 7) >> 1) | ((pix0 & 1) << 2)
                           : pix0;
       const int py = pix / C::PW, px = pix % C::PW;
@@ -826,18 +841,23 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
   // [wkg * KSW, +KSW) of every tap: WK x the waves on the same LDS images
   const int wkg = wid / (WM * WN), wmn = wid % (WM * WN);
   const int wmi = wmn / WN, wni = wmn % WN;
-  int abase[TM];
+  // MF 0: row l31 of 32-row block i, channels [8 h, +8) of a 16-channel k-step;
+  // MF 1: row lane & 15 of 16-row block 2 i + (half), channels [8 (lane >> 4), +8)
+  // of a 32-channel k-step
+  constexpr int NA = MF ? 2 * TM : TM, NB = MF ? 2 * TN : TN, KW = MF ? 32 : 16;
+  const int arow = MF ? (lane & 15) : l31, koff = MF ? 8 * (lane >> 4) : 8 * h;
+  int abase[NA];
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int m = wmi * TM * 32 + 32 * i + l31;
+  for (int i = 0; i < NA; ++i) {
+    const int m = wmi * TM * 32 + (MF ? 16 : 32) * i + arow;
     const int win = (m >> 2) < C::NWIN ? m >> 2 : 0, dy = (m >> 1) & 1, dx = m & 1;
     const int wy = win / (TX / 2), wx = win % (TX / 2);
-    abase[i] = (2 * wy + dy) * C::RS + (2 * wx + dx) * C::CS + h * 8 + 16 * C::KSW * wkg;
+    abase[i] = (2 * wy + dy) * C::RS + (2 * wx + dx) * C::CS + koff + KW * C::KSW * wkg;
   }
-  int bbase[TN];
+  int bbase[NB];
 #pragma unroll
-  for (int j = 0; j < TN; ++j)
-    bbase[j] = (wni * TN * 32 + 32 * j + l31) * C::CW + h * 8 + 16 * C::KSW * wkg;
+  for (int j = 0; j < NB; ++j)
+    bbase[j] = (wni * TN * 32 + (MF ? 16 : 32) * j + arow) * C::CW + koff + KW * C::KSW * wkg;
 
   f32x16 acc[TM][TN], cor[TM][TN];
 #pragma unroll
@@ -846,6 +866,18 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) { acc[i][j][r] = 0.f; cor[i][j][r] = 0.f; }
+  // MF 1: the four 16x16 blocks (bi, bj) of sub-tile (i, j), elements
+  // 4 (2 bi + bj) + 0..3 of acc[i][j] (f32x4 views)
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  f32x4 acc4[MF ? 2 * TM : 1][MF ? 2 * TN : 1], cor4[MF ? 2 * TM : 1][MF ? 2 * TN : 1];
+  if constexpr (MF) {
+#pragma unroll
+    for (int i = 0; i < 2 * TM; ++i)
+#pragma unroll
+      for (int j = 0; j < 2 * TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { acc4[i][j][r] = 0.f; cor4[i][j][r] = 0.f; }
+  }
 
   // one step: the MFMAs of tap t of the resident chunk on ring slot `slot`
   auto tap_step = [&](int s, int slot) {
@@ -855,27 +887,41 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
     const __bf16* pa = patch + ky * C::RS + kx * C::CS;
 #pragma unroll
     for (int g = 0; g < C::KSW; ++g) {
-      bf16x8 av[3][TM], bv[3][TN];
+      bf16x8 av[3][NA], bv[3][NB];
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
-          av[p][i] = *reinterpret_cast<const bf16x8*>(pa + p * C::kPlane + abase[i] + 16 * g);
+        for (int i = 0; i < NA; ++i)
+          av[p][i] = *reinterpret_cast<const bf16x8*>(pa + p * C::kPlane + abase[i] + KW * g);
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-          bv[p][j] = *reinterpret_cast<const bf16x8*>(wb + p * C::kWSlot + bbase[j] + 16 * g);
+        for (int j = 0; j < NB; ++j)
+          bv[p][j] = *reinterpret_cast<const bf16x8*>(wb + p * C::kWSlot + bbase[j] + KW * g);
       }
+      if constexpr (MF) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < NA; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2][i], bv[0][j], cor[i][j], 0, 0, 0);
-          cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[1][j], cor[i][j], 0, 0, 0);
-          cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[2][j], cor[i][j], 0, 0, 0);
-          cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[0][j], cor[i][j], 0, 0, 0);
-          cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[1][j], cor[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[0][j], acc[i][j], 0, 0, 0);
-        }
+          for (int j = 0; j < NB; ++j) {
+            cor4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[2][i], bv[0][j], cor4[i][j], 0, 0, 0);
+            cor4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][i], bv[1][j], cor4[i][j], 0, 0, 0);
+            cor4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[2][j], cor4[i][j], 0, 0, 0);
+            cor4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[1][i], bv[0][j], cor4[i][j], 0, 0, 0);
+            cor4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[1][j], cor4[i][j], 0, 0, 0);
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[0][i], bv[0][j], acc4[i][j], 0, 0, 0);
+          }
+      } else {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2][i], bv[0][j], cor[i][j], 0, 0, 0);
+            cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[1][j], cor[i][j], 0, 0, 0);
+            cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[2][j], cor[i][j], 0, 0, 0);
+            cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1][i], bv[0][j], cor[i][j], 0, 0, 0);
+            cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[1][j], cor[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0][i], bv[0][j], acc[i][j], 0, 0, 0);
+          }
+      }
     }
   };
   // end of step s: store step s+1's weights, restage the patch at a chunk
@@ -909,10 +955,23 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
     if (s + 2 >= NSTEP) break;
     step_end(ws0, s + 1);
   }
+  if constexpr (MF) {   // the 16x16 blocks into the f32x16 layout described above
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] += cor[i][j];
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 v = acc4[2 * i + (g >> 1)][2 * j + (g & 1)] + cor4[2 * i + (g >> 1)][2 * j + (g & 1)];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][4 * g + r] = v[r];
+        }
+  } else {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] += cor[i][j];
+  }
   // conv2's data gradient with conv1's weight gradient fused: the frames'
   // halo and the routing bytes are loaded now, under the k-group sums
   constexpr bool kW1 = DGRAD && N == 32 && CPT == 64 && TN == 1;
@@ -950,11 +1009,12 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
         }
       }
   }
+  static_assert(MF == 0 || C::NWIN * N * 7 <= C::kSmemB, "16x16x32: the LDS epilogue");
   if constexpr (!DGRAD && C::NWIN * N * 7 <= C::kSmemB) {
-    split_epilogue_fwd_lds<TM, TN, TX, N, WK, C::NWIN, C::kThreads>(a, acc, bpre, smem, b, z, y0,
-                                                                    x0, wmi, wni, l31, h, wkg, tid);
+    split_epilogue_fwd_lds<TM, TN, TX, N, WK, C::NWIN, C::kThreads, MF>(
+        a, acc, bpre, smem, b, z, y0, x0, wmi, wni, l31, h, wkg, tid);
     return;
-  }
+  } else {
   if constexpr (kW1) {
     if (w1) {
       const f32x16(&acc1)[TM][1] = reinterpret_cast<const f32x16(&)[TM][1]>(acc);
@@ -966,19 +1026,22 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
   }
   split_epilogue<TM, TN, TX, N, DGRAD, WK, C::NWIN>(a, acc, bpre, b, z, y0, x0, wmi, wni, l31, h,
                                                     wkg);
+  }
 }
 
-template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, bool DGRAD>
+template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, bool DGRAD,
+          int MF>
 __global__ __launch_bounds__(64 * WM * WN * WK) void split_conv_kernel(const SplitArgs a) {
   extern __shared__ __attribute__((aligned(16))) char sm_split[];
-  split_conv_body<CPT, CP, N, KS, TY, TX, WM, WN, WK, DGRAD>(a, sm_split, blockIdx.x, blockIdx.y,
-                                                            blockIdx.z);
+  split_conv_body<CPT, CP, N, KS, TY, TX, WM, WN, WK, DGRAD, MF>(a, sm_split, blockIdx.x,
+                                                                blockIdx.y, blockIdx.z);
 }
 
-template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, bool DGRAD>
+template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, bool DGRAD,
+          int MF = 0>
 inline hipError_t launch_split_conv(SplitArgs a, int nz, hipStream_t st) {
-  using C = SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK>;
-  auto kern = split_conv_kernel<CPT, CP, N, KS, TY, TX, WM, WN, WK, DGRAD>;
+  using C = SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK, MF>;
+  auto kern = split_conv_kernel<CPT, CP, N, KS, TY, TX, WM, WN, WK, DGRAD, MF>;
   // conv2's data gradient: room for the fused conv1 weight gradient too
   constexpr bool kW1 = DGRAD && N == 32 && CPT == 64 && C::TN == 1;
   constexpr int kW1B = kW1 ? W1Fuse<kW1 ? TY : 2, kW1 ? TX : 2, C::kThreads>::kSmemB : 0;

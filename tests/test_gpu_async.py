@@ -211,7 +211,8 @@ def test_rccl_world1_async_graph_mixed_with_eager_ticks_and_tickets(ddq):
         for z in (0, 1):
             np.testing.assert_array_equal(nets[0].get_flat(z), nets[1].get_flat(z))
         np.testing.assert_array_equal(nets[0].optimizer_state(), nets[1].optimizer_state())
-        np.testing.assert_array_equal(nets[0].get_grads_flat(), nets[1].get_grads_flat())
+        # (no gradient comparison: after its last pull an async worker has
+        # already computed its NEXT gradient, at the new parameters)
     finally:
         for n in nets:
             n.close()
