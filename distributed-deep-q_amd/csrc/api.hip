@@ -109,6 +109,7 @@ struct ddq_ctx {
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
   bool mark_external = false;        // marks recorded as event nodes of a captured graph
+  hipError_t mark_err = hipSuccess;  // the first failure of such a mark
 };
 
 static int fail(ddq_ctx* c, int code, const char* fmt, ...) {
@@ -2008,10 +2009,23 @@ static void mark_cb(void* arg, const char* name) {
     c->ev_pool.push_back(e);
   }
   hipEvent_t e = c->ev_pool[c->ev_used++];
-  if (c->mark_external)   // inside a stream capture: an event-record node of the graph
-    hipEventRecordWithFlags(e, c->stream, hipEventRecordExternal);
-  else
+  if (c->mark_external) {
+    // inside a stream capture: an event-record node appended to the captured
+    // graph behind the stream's current leaf nodes, which it then replaces
+    hipStreamCaptureStatus cs;
+    unsigned long long id = 0;
+    hipGraph_t g = nullptr;
+    const hipGraphNode_t* deps = nullptr;
+    size_t nd = 0;
+    hipGraphNode_t node = nullptr;
+    hipError_t r = hipStreamGetCaptureInfo_v2(c->stream, &cs, &id, &g, &deps, &nd);
+    if (r == hipSuccess) r = hipGraphAddEventRecordNode(&node, g, deps, nd, e);
+    if (r == hipSuccess)
+      r = hipStreamUpdateCaptureDependencies(c->stream, &node, 1, hipStreamSetCaptureDependencies);
+    if (r != hipSuccess && c->mark_err == hipSuccess) c->mark_err = r;
+  } else {
     hipEventRecord(e, c->stream);
+  }
   c->marks.emplace_back(name, e);
 }
 
@@ -2065,6 +2079,7 @@ int ddq_profile_graph(ddq_ctx* c, const ddq_step_cfg* cfg, int32_t reps, char* n
   c->marks.clear();
   c->ev_used = 0;
   c->mark_external = true;
+  c->mark_err = hipSuccess;
   hipGraphExec_t exec = nullptr;
   int rc = capture_exec(c, &exec, [&]() -> int {
     for (int k = 0; k < kGraphSteps; ++k) {
@@ -2076,6 +2091,10 @@ int ddq_profile_graph(ddq_ctx* c, const ddq_step_cfg* cfg, int32_t reps, char* n
   });
   c->mark_external = false;
   if (rc != DDQ_OK) return rc;
+  if (c->mark_err != hipSuccess) {
+    hipGraphExecDestroy(exec);
+    return fail(c, DDQ_EHIP, "profile_graph: event-record node: %s", hipGetErrorString(c->mark_err));
+  }
   std::vector<std::string> order;
   std::vector<double> sum;
   std::vector<int> cnt;

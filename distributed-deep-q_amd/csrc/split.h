@@ -78,6 +78,18 @@ __device__ __forceinline__ void wt_store_split(__amdgpu_buffer_rsrc_t r, uint32_
   wt_store_b16(r, (2 * E + e) * 2, l);
 }
 
+// Keep-masks of 4 channels whose max-pool routing bytes (mw, values 0..4) name
+// quadrant q (q4 = q * 0x01010101): 0xFFFF halves for the bf16 pairs (0,1)
+// and (2,3).  Byte arithmetic instead of a compare + select per channel.
+__device__ __forceinline__ void route_keep(uint32_t mw, uint32_t q4, uint32_t& k01,
+                                           uint32_t& k23) {
+  const uint32_t x = mw ^ q4;                                     // byte 0 iff routed to q
+  const uint32_t nz = (x | (x >> 1) | (x >> 2)) & 0x01010101u;    // bytes <= 7: 1 iff not
+  const uint32_t kb = (nz ^ 0x01010101u) * 0xFFu;                 // 0xFF iff routed to q
+  k01 = __builtin_amdgcn_perm(kb, kb, 0x01010000u);
+  k23 = __builtin_amdgcn_perm(kb, kb, 0x03030202u);
+}
+
 // Store the split of v at element e of a split tensor of E elements.
 __device__ __forceinline__ void store_split(__bf16* t, int64_t E, int64_t e, float v) {
   __bf16 h, m, l;
@@ -706,14 +718,12 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
             u32x4, __builtin_amdgcn_raw_buffer_load_b128(rin[p], (int)(in_img ? o * 2 : kOOB), 0, 0));
         const u32x2 m = __builtin_bit_cast(
             u32x2, __builtin_amdgcn_raw_buffer_load_b64(rroute, (int)(in_img ? o : kOOB), 0, 0));
-        const uint32_t q = ((gy & 1) << 1) | (gx & 1);
+        const uint32_t q4 = ((((gy & 1) << 1) | (gx & 1))) * 0x01010101u;
+        uint32_t k[4];   // bf16 pair e = channels 2e, 2e+1 (zeros route nothing)
+        route_keep(m[0], q4, k[0], k[1]);
+        route_keep(m[1], q4, k[2], k[3]);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {   // bf16 pair e = channels 2e, 2e+1 (zeros route nothing)
-          const uint32_t mw = m[e >> 1];
-          const uint32_t r0 = (mw >> (16 * (e & 1))) & 0xff;
-          const uint32_t r1 = (mw >> (16 * (e & 1) + 8)) & 0xff;
-          v[u][e] = (r0 == q ? (uw[e] & 0xffffu) : 0u) | (r1 == q ? (uw[e] & 0xffff0000u) : 0u);
-        }
+        for (int e = 0; e < 4; ++e) v[u][e] = uw[e] & k[e];
       } else {
         const uint32_t o = (uint32_t)(((b * a.H + gy) * a.W + gx) * CPT + ch * CP + 8 * c8);
         v[u] = __builtin_bit_cast(

@@ -283,13 +283,8 @@ __device__ __forceinline__ void wgrads_body(const WgradSArgs& a, char* smem, int
         const uint32_t qd = qy | dx;
         // per bf16 pair e (channels 2e, 2e+1): keep-masks from the routing bytes
         uint32_t keep[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const uint32_t mw = R.m[u][e >> 1];
-          const uint32_t ra = (mw >> (16 * (e & 1))) & 0xff;
-          const uint32_t rb = (mw >> (16 * (e & 1) + 8)) & 0xff;
-          keep[e] = (ra == qd ? 0xffffu : 0u) | (rb == qd ? 0xffff0000u : 0u);
-        }
+        route_keep(R.m[u][0], qd * 0x01010101u, keep[0], keep[1]);
+        route_keep(R.m[u][1], qd * 0x01010101u, keep[2], keep[3]);
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
           u32x4 o;

@@ -18,4 +18,3 @@ timeout -k 10 240 python -c "import json, bench; print(json.dumps(bench.messagin
 python -c "
 import json; d=json.load(open('gpurun_out/messaging.json'))
 for f in d['frames']: print(f['frame'], f['raw'], f['server'])"
-bash tools/gpu/run_ab.sh mf1
