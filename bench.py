@@ -445,8 +445,8 @@ def gather_stress(S=64, N=1_000_000, sizes=(256, 4096, 32768), seed=3):
 EXCHANGE_PATHS = (   # (label, exchange, overlap, step mode)
     ("allreduce+overlap", "allreduce", True, "pipelined"),
     ("allreduce", "allreduce", False, "pipelined"),
-    ("sharded", "sharded", False, "graph"),
-    ("server", "server", False, "graph"),
+    ("sharded", "sharded", False, "pipelined"),
+    ("server", "server", False, "pipelined"),
     ("async", "async", False, "eager"),            # round-robin rounds, eager
     ("async-graph", "async", False, "graph"),      # round-robin rounds as hipGraphs
     ("async-ticket", "async", False, "ticket"))    # arrival order (AsyncTicketLoop)

@@ -1095,7 +1095,7 @@ static int enqueue_exchange_apply(ddq_ctx* c, const ddq_step_cfg* cfg, const Net
   if (mark) mark(marg, "apply_shard");
   HIP_TRY(c, launch_apply_shard(nb, u.rule, u.lr, u.decay, u.eps, u.momentum, u.weight_decay,
                                 c->gsl, (int64_t)c->rank * len, (int64_t)len, (int64_t)len,
-                                ex == DDQ_EXCHANGE_SHARDED ? 1 : W, c->stream));
+                                ex == DDQ_EXCHANGE_SHARDED ? 1 : W, c->stream, nullptr, -1, pf));
   if (mark) mark(marg, "all_gather");
   NCCL_TRY(c, ncclAllGather(nb.theta[0] + (size_t)c->rank * len, nb.theta[0], len, ncclFloat,
                             c->comm, c->stream));
@@ -1111,9 +1111,11 @@ static int enqueue_exchange_apply(ddq_ctx* c, const ddq_step_cfg* cfg, const Net
 // the index stream equals the sequential one).
 // Pipelined steps whose next draw + gather ride on the apply launch (no side
 // stream): exchanges that end in the plain apply kernel, B <= 256.
+// (sharded / server: on the owner-apply launch, after the slab reduce's
+// bookkeeping advanced the draw counter)
 static bool fused_prefetch(const ddq_ctx* c, const ddq_step_cfg* cfg) {
   const int ex = has_exchange(c, cfg) ? cfg->exchange : DDQ_EXCHANGE_NONE;
-  return (ex == DDQ_EXCHANGE_NONE || ex == DDQ_EXCHANGE_ALLREDUCE) && c->nb.B <= 256;
+  return ex != DDQ_EXCHANGE_ASYNC && c->nb.B <= 256;
 }
 
 static int enqueue_train(ddq_ctx* c, const ddq_step_cfg* cfg, const NetBuffers& nb_in,

@@ -43,6 +43,8 @@ struct FusedApplyCfg {
   float lr, decay, eps, momentum, wd;
 };
 
+struct Prefetch;
+
 struct NetBuffers {
   int B, S;
   // minibatch (NHWC frames; action one-hot (B,4); reward / non_terminal (B))
@@ -105,7 +107,6 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s, void (*ma
 // slab-reduce launch can carry the next step's draw + gather
 hipError_t launch_head(const NetBuffers& nb, hipStream_t s, ReplayMeta* bump = nullptr);
 bool fused_apply_ok(const ParamLayout& L);
-struct Prefetch;
 // book: the slab reduce also does the apply bookkeeping (target period
 // book_period); fc4_done: called right after the fc4 weight gradient is
 // enqueued (the overlapped all-reduce starts there); pf (fused apply only):
@@ -142,10 +143,12 @@ hipError_t launch_relayout(const NetBuffers& nb, int z, hipStream_t s);
 // owner copy otherwise).  first >= 0: the rules' first-call flag from the host
 // and the apply's bookkeeping (iteration += 1) done by the launch itself
 // (async owner applies); -1: the flags latched by a prior launch_book.
+// pre: the next step's draw + gather as extra blocks (pipelined steps)
 hipError_t launch_apply_shard(const NetBuffers& nb, int rule, float lr, float decay, float eps,
                               float momentum, float wd, const float* gsl, int64_t off,
                               int64_t len, int64_t slice, int W, hipStream_t s,
-                              float* theta = nullptr, int first = -1);
+                              float* theta = nullptr, int first = -1,
+                              const Prefetch* pre = nullptr);
 // force_sync >= 0: P <- Q decided by the host instead of the latched flag
 hipError_t launch_refresh(const NetBuffers& nb, hipStream_t s, int force_sync = -1);
 // one apply's bookkeeping (first-call / sync latches, iteration += 1)

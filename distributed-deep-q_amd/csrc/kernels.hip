@@ -1079,6 +1079,10 @@ __device__ __forceinline__ void apply_at(const ApplyTail& t, const ApplyArgs& a,
 // element's sum runs n = 0 .. B-1 in order with fmaf, whatever R, so every
 // caller (the gradient launches and the fused apply) produces the same bits.
 constexpr int kFc4WTileK = 256;
+// A/B: batch rows per round of the fc4 weight-gradient sums' loads
+#ifndef DDQ_FC4W_UNROLL
+#define DDQ_FC4W_UNROLL 4
+#endif
 template <int R>
 __host__ __device__ inline int fc4_wgrad_blocks(int K) {
   return (512 / (4 * R)) * ((K + kFc4WTileK - 1) / kFc4WTileK);
@@ -1103,7 +1107,7 @@ __device__ __forceinline__ void fc4_wgrad_sum(int B, int K, const float* __restr
     for (int e = 0; e < 4; ++e) g[r][e] = 0.f;
   const float* xp = x + k;
   const float* dp = dh4 + o0;
-#pragma unroll 4
+#pragma unroll DDQ_FC4W_UNROLL
   for (int n = 0; n < B; ++n) {
     const float4 xv = *reinterpret_cast<const float4*>(xp + (size_t)n * K);
 #pragma unroll
@@ -1343,16 +1347,24 @@ __global__ void apply_book_kernel(int64_t* iter, int32_t* opt_init, int period) 
 // first >= 0: the rules' first-call flag given by the host (async owner
 // applies, whose bookkeeping is this kernel's: block 0 advances the iteration
 // and marks the state initialised -- nothing in the launch reads either)
+// Blocks [0, pf.ng): the next step's draw + gather (pipelined sharded /
+// server steps: the step's bookkeeping in the slab reduce advanced the draw
+// counter already).
 __global__ __launch_bounds__(256) void apply_shard_kernel(
     float* __restrict__ theta, const float* __restrict__ gsl, float* __restrict__ opt,
     int32_t* __restrict__ opt_init, int64_t off, int64_t len, int64_t slice, int W,
-    ApplyArgs a, int first_host, int64_t* iter) {
+    ApplyArgs a, int first_host, int64_t* iter, Prefetch pf) {
+  if ((int)blockIdx.x < pf.ng) {
+    prefetch_body(pf, blockIdx.x);
+    return;
+  }
+  const int bid = (int)blockIdx.x - pf.ng;
   const bool first = first_host >= 0 ? first_host != 0 : opt_init[2] != 0;
-  if (first_host >= 0 && blockIdx.x == 0 && threadIdx.x == 0) {
+  if (first_host >= 0 && bid == 0 && threadIdx.x == 0) {
     *iter += 1;
     opt_init[0] = 1;
   }
-  const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const int64_t j = ((int64_t)bid * blockDim.x + threadIdx.x) * 4;
   if (j >= len) return;
   const int64_t i = off + j;
   const float4 t4 = *reinterpret_cast<const float4*>(theta + i);
@@ -1442,13 +1454,15 @@ bool fused_apply_ok(const ParamLayout& L) {
 hipError_t launch_apply_shard(const NetBuffers& nb, int rule, float lr, float decay, float eps,
                               float momentum, float wd, const float* gsl, int64_t off,
                               int64_t len, int64_t slice, int W, hipStream_t s, float* theta,
-                              int first) {
+                              int first, const Prefetch* pre) {
   const ApplyArgs a = apply_args(nb, rule, lr, decay, eps, momentum, wd, 0);
+  Prefetch pf{};
+  if (pre) pf = *pre;
   const int64_t blocks = (len / 4 + 255) / 256;
-  if (blocks > 0)
-    hipLaunchKernelGGL(apply_shard_kernel, dim3((uint32_t)blocks), dim3(256), 0, s,
+  if (blocks + pf.ng > 0)
+    hipLaunchKernelGGL(apply_shard_kernel, dim3((uint32_t)(blocks + pf.ng)), dim3(256), 0, s,
                        theta ? theta : nb.theta[0], gsl, nb.opt, nb.opt_init, off, len, slice, W,
-                       a, first, nb.iter);
+                       a, first, nb.iter, pf);
   return hipGetLastError();
 }
 

@@ -157,6 +157,10 @@ def test_rccl_world1_exchange_equals_plain_step(ddq, ref, exchange, overlap):
                          exchange=exchange if i == 0 else "none", overlap=overlap, seed=9)
         n.step_graph(cfg, 5)
         n.step(cfg)
+        # pipelined chains: the next draw + gather on the apply (allreduce:
+        # fused slab-reduce launch; sharded / server: the owner-apply launch)
+        n.step_pipelined(cfg, 11)
+        n.step(cfg)
         n.synchronize()
     for z in (0, 1):
         np.testing.assert_array_equal(nets[0].get_flat(z), nets[1].get_flat(z))
