@@ -16,9 +16,9 @@ replay filled with synthetic Snake frames.
 
 Prints ONE JSON line (rank 0).  ``value`` = minibatch updates/s summed over
 all ranks (each rank consumes its own minibatch per step: weak scaling).
-``roofline``: dominant kernel's in-step time inside the graph-replayed
-pipelined chain, HIP event-record nodes on the ctx stream
-(ddq_profile_graph), vs the peak of the arithmetic it runs (split-bf16 kernels:
+``roofline``: dominant kernel's in-step time (its own dispatch start / stop
+events, hipExtLaunchKernel, in eager steps: ddq_profile_step) vs the peak of
+the arithmetic it runs (split-bf16 kernels:
 the bf16 dense peak over their products per f32 product).  ``cpu_baseline``: the oracle's C
 restatement of the Caffe CPU step (oracle/libddq_cpu.so) timed on the host
 cores on a bounded sample of the same workload.
@@ -462,29 +462,32 @@ def exchange_paths(net, rule, steps=240, warmup=24, profile=5):
     from ddq import dist as ddist
     from ddq.params import init_params_flat
     out = {}
+    base = net
 
     def free_leg():
-        c0 = net.step_cfg(rule, lr=1e-4, target_period=10, exchange="none", seed=1234)
-        net.step_prepare(c0, "pipelined")
-        net.step_pipelined(c0, warmup)
-        net.synchronize()
+        c0 = base.step_cfg(rule, lr=1e-4, target_period=10, exchange="none", seed=1234)
+        base.step_prepare(c0, "pipelined")
+        base.step_pipelined(c0, warmup)
+        base.synchronize()
         t0 = time.perf_counter()
-        net.step_pipelined(c0, steps)
-        net.synchronize()
+        base.step_pipelined(c0, steps)
+        base.synchronize()
         return steps / (time.perf_counter() - t0)
     ref_before = free_leg()
     for label, ex, ov, mode in EXCHANGE_PATHS:
         if ex == "async":     # a fresh worker: once begun, a ctx runs async steps only
-            net = ddq.DeepQNet(batch=net.batch, frame=net.frame, device=net.device)
-            theta = init_params_flat(net.frame, seed=42)
+            net = ddq.DeepQNet(batch=base.batch, frame=base.frame, device=base.device)
+            theta = init_params_flat(base.frame, seed=42)
             net.set_flat(0, theta)
             net.set_flat(1, theta)
             net.replay_create(30000)
-            fill_replay(net, 30000, net.frame, seed=1000)
+            fill_replay(net, 30000, base.frame, seed=1000)
             ddist.setup_comm(net, 0, 1)
-        elif "comm" not in out:
-            ddist.setup_comm(net, 0, 1)
-            out["comm"] = True
+        else:
+            net = base
+            if "comm" not in out:
+                ddist.setup_comm(net, 0, 1)
+                out["comm"] = True
         cfg = net.step_cfg(rule, lr=1e-4, target_period=10, exchange=ex, overlap=ov, seed=1234)
         if mode != "ticket":
             net.step_prepare(cfg, mode)
@@ -799,29 +802,21 @@ def main():
                    "p90": round(float(np.percentile(per, 90)), 4),
                    "chunks": args.chunks, "steps_per_chunk": args.chunk_steps}
 
-    # per-kernel device times INSIDE the graph-replayed pipelined chain the
-    # line times: 8 captured steps with an event-record node between every two
-    # kernels (ddq_profile_graph), replayed --profile-steps times, on the ctx
-    # stream the kernels run on.  The exchange-free fused step's empty "apply"
-    # interval is the event nodes' own cost.
+    # per-kernel device times: eager steps whose every kernel carries start /
+    # stop events of its own (hipExtLaunchKernel: the dispatch packet's
+    # timestamps -- what rocprofv3's kernel trace reads -- with no marker
+    # packets between the kernels), on the ctx stream the kernels run on;
+    # median over --profile-steps steps
     pnet = net
     if exchanged and args.exchange == "async":   # an async ctx runs async steps only
         pnet = make_net(B, S, args.replay, local, rank)
-    pcfg = cfg if (exchanged and args.exchange == "allreduce") else \
+    pcfg = cfg if not (exchanged and args.exchange == "async") else \
         pnet.step_cfg(args.rule, lr=1e-4, target_period=10, exchange="none", seed=1234)
-    in_graph = True
-    try:
-        avg = dict(pnet.profile_graph(pcfg, reps=max(1, args.profile_steps)))
-    except Exception as e:   # no event-record nodes: the eager per-kernel events
-        print("bench: profile_graph failed (%s); eager per-kernel events instead" % e,
-              file=sys.stderr)
-        in_graph = False
-        prof = {}
-        for _ in range(max(1, args.profile_steps)):
-            for name, us in pnet.profile_step(pcfg):
-                prof.setdefault(name, []).append(us)
-        avg = {k: float(np.median(v)) for k, v in prof.items()}
-    node_us = avg.pop("apply", None)
+    prof = {}
+    for _ in range(max(1, args.profile_steps)):
+        for name, us in pnet.profile_step(pcfg):
+            prof.setdefault(name, []).append(us)
+    avg = {k: float(np.median(v)) for k, v in prof.items()}
     flops = kernel_flops(B, S)
     dom = max((k for k in avg if k in flops), key=lambda k: avg[k])
     dom_us = avg[dom]
@@ -870,15 +865,10 @@ def main():
                          "traffic": traffic, "traffic_unit": "bytes/launch",
                          "traffic_source": traffic_src,
                          "kernel_us": round(dom_us, 3),
-                         "kernel_us_timing": ("in-step: mean over the graph-replayed pipelined "
-                                              "chain (8-step graphs, event-record nodes around "
-                                              "every kernel on the ctx stream, %d replays); "
-                                              "event-node pair cost %s us"
-                                              % (max(1, args.profile_steps),
-                                                 None if node_us is None else round(node_us, 3)))
-                                             if in_graph else
-                                             "eager step, one HIP event pair per launch "
-                                             "(profile_graph unavailable)",
+                         "kernel_us_timing": "in-step: median over %d eager steps of the "
+                                             "kernel's own dispatch start / stop "
+                                             "(hipExtLaunchKernel events on the ctx stream)"
+                                             % max(1, args.profile_steps),
                          "isolated_us": None if iso_us is None else round(iso_us, 3),
                          "isolated_timing": "the same layer, 100 back-to-back launches on one "
                                             "cache-warm input (not the roofline figure)",
@@ -888,8 +878,9 @@ def main():
                          "step_frac_basis": "step_roofline(): MFMA kernels at their "
                                             "arithmetic's peak + algorithmic HBM bytes"},
             "kernels_us": {k: round(v, 2) for k, v in avg.items()},
-            "kernels_us_timing": "in-step, graph-replayed pipelined chain (ddq_profile_graph); "
-                                 "compare profiles/rNN_kernel_stats_step.csv (rocprofv3)",
+            "kernels_us_timing": "each kernel's own dispatch start / stop in eager steps "
+                                 "(ddq_profile_step, hipExtLaunchKernel events); compare "
+                                 "profiles/rNN_kernel_stats_step.csv (rocprofv3, graph replay)",
             "kernel_roofline": kernel_roofline(avg, B, S, net.num_params),
             "step_ms_distribution": dist_ms,
             "final_loss": loss,

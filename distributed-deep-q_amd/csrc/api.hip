@@ -104,12 +104,14 @@ struct ddq_ctx {
   bool have_pipe = false;
   int64_t steps = 0;
   int64_t applied = 0;               // host mirror of the device iteration counter
-  // profiling marks
-  std::vector<std::pair<std::string, hipEvent_t>> marks;
+  // profiling marks: a kernel's own dispatch start / stop events
+  struct Mark {
+    std::string name;
+    hipEvent_t start, stop;
+  };
+  std::vector<Mark> marks;
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
-  bool mark_external = false;        // marks recorded as event nodes of a captured graph
-  hipError_t mark_err = hipSuccess;  // the first failure of such a mark
 };
 
 static int fail(ddq_ctx* c, int code, const char* fmt, ...) {
@@ -2003,32 +2005,25 @@ int ddq_group_step(ddq_ctx** ctxs, int32_t W, const ddq_step_cfg* cfg) {
 int64_t ddq_step_count(const ddq_ctx* c) { return c ? c->steps : -1; }
 
 // ---------------- measurement ----------------
+// A mark names the kernel launched next: arm that launch's own start / stop
+// events (common.h ddq_launch).  A mark no kernel follows (an RCCL call, the
+// fused step's empty "apply") is still armed at the next mark: dropped.
+static void mark_settle(ddq_ctx* c) {
+  if (g_ext_timing.start && !c->marks.empty()) c->marks.pop_back();   // not launched
+  g_ext_timing = ExtTiming{};
+}
+
 static void mark_cb(void* arg, const char* name) {
   ddq_ctx* c = reinterpret_cast<ddq_ctx*>(arg);
-  if (c->ev_used == c->ev_pool.size()) {
+  mark_settle(c);
+  while (c->ev_used + 2 > c->ev_pool.size()) {
     hipEvent_t e;
     hipEventCreate(&e);
     c->ev_pool.push_back(e);
   }
-  hipEvent_t e = c->ev_pool[c->ev_used++];
-  if (c->mark_external) {
-    // inside a stream capture: an event-record node appended to the captured
-    // graph behind the stream's current leaf nodes, which it then replaces
-    hipStreamCaptureStatus cs;
-    unsigned long long id = 0;
-    hipGraph_t g = nullptr;
-    const hipGraphNode_t* deps = nullptr;
-    size_t nd = 0;
-    hipGraphNode_t node = nullptr;
-    hipError_t r = hipStreamGetCaptureInfo_v2(c->stream, &cs, &id, &g, &deps, &nd);
-    if (r == hipSuccess) r = hipGraphAddEventRecordNode(&node, g, deps, nd, e);
-    if (r == hipSuccess)
-      r = hipStreamUpdateCaptureDependencies(c->stream, &node, 1, hipStreamSetCaptureDependencies);
-    if (r != hipSuccess && c->mark_err == hipSuccess) c->mark_err = r;
-  } else {
-    hipEventRecord(e, c->stream);
-  }
-  c->marks.emplace_back(name, e);
+  hipEvent_t e0 = c->ev_pool[c->ev_used++], e1 = c->ev_pool[c->ev_used++];
+  g_ext_timing = ExtTiming{e0, e1};
+  c->marks.push_back({name, e0, e1});
 }
 
 int ddq_profile_step(ddq_ctx* c, const ddq_step_cfg* cfg, char* names, float* usec, int32_t cap,
@@ -2041,99 +2036,21 @@ int ddq_profile_step(ddq_ctx* c, const ddq_step_cfg* cfg, char* names, float* us
   c->marks.clear();
   c->ev_used = 0;
   if (c->steps == 0) TRY(initial_target_sync(c, cfg));
-  TRY(enqueue_step(c, cfg, mark_cb, c));
-  mark_cb(c, "end");
+  const int rc = enqueue_step(c, cfg, mark_cb, c);
+  mark_settle(c);
+  TRY(rc);
   c->steps++;
   c->applied += step_inc(c, cfg);
   HIP_TRY(c, hipStreamSynchronize(c->stream));
-  const int k = (int)c->marks.size() - 1;
+  const int k = (int)c->marks.size();
   *n = k;
   for (int i = 0; i < k && i < cap; ++i) {
     float ms = 0.f;
-    HIP_TRY(c, hipEventElapsedTime(&ms, c->marks[i].second, c->marks[i + 1].second));
+    HIP_TRY(c, hipEventElapsedTime(&ms, c->marks[i].start, c->marks[i].stop));
     if (usec) usec[i] = ms * 1000.f;
     if (names) {
       memset(names + 16 * i, 0, 16);
-      strncpy(names + 16 * i, c->marks[i].first.c_str(), 15);
-    }
-  }
-  return DDQ_OK;
-}
-
-// The step kernels' device times INSIDE the graph-replayed pipelined chain
-// the bench times: kGraphSteps pipelined steps (ensure_pipe's pexec_k form,
-// fused prefetch) captured with an event-record node between every two
-// kernels, replayed reps times (each replay trains: counters advance as in
-// ddq_step_pipelined_async); per kernel name the mean over the steps and
-// replays of the time between its two event nodes.  The names are the marks
-// of ddq_profile_step, in step order; an interval holding no kernel (the
-// fused step's "apply" mark) measures the event nodes' own cost.
-int ddq_profile_graph(ddq_ctx* c, const ddq_step_cfg* cfg, int32_t reps, char* names, float* usec,
-                      int32_t cap, int32_t* n) {
-  TRY(check_step(c, cfg));
-  if (!n || reps < 1) return fail(c, DDQ_EINVAL, "profile_graph: bad arguments");
-  if (is_async(c, cfg) || !fused_prefetch(c, cfg))
-    return fail(c, DDQ_EINVAL, "profile_graph: pipelined steps with the fused prefetch only "
-                               "(exchange none or allreduce, batch <= 256)");
-  TRY(set_dev(c));
-  TRY(ensure_pipe(c, cfg));   // the second minibatch set
-  ReplayMeta* bump = c->r_meta;
-  c->marks.clear();
-  c->ev_used = 0;
-  c->mark_external = true;
-  c->mark_err = hipSuccess;
-  hipGraphExec_t exec = nullptr;
-  int rc = capture_exec(c, &exec, [&]() -> int {
-    for (int k = 0; k < kGraphSteps; ++k) {
-      const NetBuffers cur = mb_view(c, k & 1), nxt = mb_view(c, 1 - (k & 1));
-      TRY(enqueue_train(c, cfg, cur, &nxt, mark_cb, c, bump));
-    }
-    mark_cb(c, "end");
-    return DDQ_OK;
-  });
-  c->mark_external = false;
-  if (rc != DDQ_OK) return rc;
-  if (c->mark_err != hipSuccess) {
-    hipGraphExecDestroy(exec);
-    return fail(c, DDQ_EHIP, "profile_graph: event-record node: %s", hipGetErrorString(c->mark_err));
-  }
-  std::vector<std::string> order;
-  std::vector<double> sum;
-  std::vector<int> cnt;
-  rc = [&]() -> int {
-    if (c->steps == 0) TRY(initial_target_sync(c, cfg));
-    const NetBuffers first = mb_view(c, 0);
-    HIP_TRY(c, launch_sample_gather(first, c->r_state, c->r_action, c->r_reward, c->r_nonterm,
-                                    c->r_meta, cfg->seed, c->stream));
-    for (int r = 0; r < reps; ++r) {
-      HIP_TRY(c, hipGraphLaunch(exec, c->stream));
-      HIP_TRY(c, hipStreamSynchronize(c->stream));
-      c->steps += kGraphSteps;
-      c->applied += (int64_t)kGraphSteps * step_inc(c, cfg);
-      for (size_t i = 0; i + 1 < c->marks.size(); ++i) {
-        float ms = 0.f;
-        HIP_TRY(c, hipEventElapsedTime(&ms, c->marks[i].second, c->marks[i + 1].second));
-        size_t j = 0;
-        while (j < order.size() && order[j] != c->marks[i].first) ++j;
-        if (j == order.size()) {
-          order.push_back(c->marks[i].first);
-          sum.push_back(0.0);
-          cnt.push_back(0);
-        }
-        sum[j] += ms * 1000.0;
-        cnt[j] += 1;
-      }
-    }
-    return DDQ_OK;
-  }();
-  hipGraphExecDestroy(exec);
-  if (rc != DDQ_OK) return rc;
-  *n = (int32_t)order.size();
-  for (int i = 0; i < (int)order.size() && i < cap; ++i) {
-    if (usec) usec[i] = (float)(sum[i] / cnt[i]);
-    if (names) {
-      memset(names + 16 * i, 0, 16);
-      strncpy(names + 16 * i, order[i].c_str(), 15);
+      strncpy(names + 16 * i, c->marks[i].name.c_str(), 15);
     }
   }
   return DDQ_OK;

@@ -7,7 +7,31 @@
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+#include <hip/hip_ext.h>
+
 namespace ddq {
+
+// Kernel timing (ddq_profile_step): when armed, the next launch through
+// ddq_launch records these events at the dispatch's own start and end
+// (hipExtLaunchKernel: the dispatch packet's timestamps, no marker packets
+// around it), then disarms.  Thread-local: every ctx call runs on the
+// caller's thread.
+struct ExtTiming {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+extern thread_local ExtTiming g_ext_timing;
+
+template <class F, class... Args>
+inline void ddq_launch(F kern, const dim3& grid, const dim3& block, uint32_t smem, hipStream_t s,
+                       Args... args) {
+  if (g_ext_timing.start) {
+    const ExtTiming t = g_ext_timing;
+    g_ext_timing = ExtTiming{};
+    hipExtLaunchKernelGGL(kern, grid, block, smem, s, t.start, t.stop, 0, args...);
+  } else {
+    hipLaunchKernelGGL(kern, grid, block, smem, s, args...);
+  }
+}
 
 constexpr int kWave = 64;          // CDNA wavefront
 constexpr int kActions = 4;        // barista/constants.py:8

@@ -263,11 +263,11 @@ inline int fc4_fwd_splits(int K) { return (K + kFc4KLen - 1) / kFc4KLen; }
 
 inline hipError_t launch_fc4_fwd_direct(const Fc4FwdArgs& a, hipStream_t st) {
   if (a.B <= 32) {
-    hipLaunchKernelGGL(fc4_fwd_split_kernel<1>, dim3(512 / 128, fc4_fwd_splits(a.K), a.nz),
+    ddq_launch(fc4_fwd_split_kernel<1>, dim3(512 / 128, fc4_fwd_splits(a.K), a.nz),
                        dim3(256), 0, st, a);
   } else {
     const int nbt = (a.B + 63) / 64;
-    hipLaunchKernelGGL(fc4_fwd_split_kernel<2>, dim3(512 / 128, fc4_fwd_splits(a.K), a.nz * nbt),
+    ddq_launch(fc4_fwd_split_kernel<2>, dim3(512 / 128, fc4_fwd_splits(a.K), a.nz * nbt),
                        dim3(256), 0, st, a);
   }
   return hipGetLastError();

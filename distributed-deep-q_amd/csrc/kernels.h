@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "common.h"   // ddq_launch / ExtTiming (kernel timing)
+
 namespace ddq {
 
 // Flat parameter layout of one tower (pycaffe order), element offsets.

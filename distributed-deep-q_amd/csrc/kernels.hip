@@ -10,6 +10,7 @@ namespace ddq {
 // first failing launch site of the last failed launch sequence (api.hip
 // appends it to the error message)
 thread_local const char* g_launch_where = "";
+thread_local ExtTiming g_ext_timing;
 #define DDQ_STR2(x) #x
 #define DDQ_STR(x) DDQ_STR2(x)
 #define CHECK_LAUNCH(x)                                             \
@@ -248,7 +249,7 @@ __global__ __launch_bounds__(256) void sample_gather_kernel(
 hipError_t launch_sample(const NetBuffers& nb, ReplayMeta* meta, uint64_t seed, hipStream_t s) {
   int threads = 64;                 // one wave for B <= 64: cheap barriers
   while (threads < nb.B) threads <<= 1;
-  hipLaunchKernelGGL(sample_kernel, dim3(1), dim3(threads), 0, s, meta, nb.B, seed, nb.idx,
+  ddq_launch(sample_kernel, dim3(1), dim3(threads), 0, s, meta, nb.B, seed, nb.idx,
                      nb.idx_log, nb.log_cap);
   return hipGetLastError();
 }
@@ -258,7 +259,7 @@ hipError_t launch_sample_gather(const NetBuffers& nb, const uint8_t* st, const u
                                 uint64_t seed, hipStream_t s) {
   const int SS = nb.S * nb.S;
   dim3 grid((SS / 4 + 255) / 256, nb.B, 2);
-  hipLaunchKernelGGL(sample_gather_kernel, grid, dim3(256), 0, s, st, act, rew, nt, meta, nb.B,
+  ddq_launch(sample_gather_kernel, grid, dim3(256), 0, s, st, act, rew, nt, meta, nb.B,
                      seed, nb.idx, nb.S, nb.state, nb.next_state, nb.action, nb.reward,
                      nb.nonterm, nb.idx_log, nb.log_cap);
   return hipGetLastError();
@@ -269,7 +270,7 @@ hipError_t launch_gather(const NetBuffers& nb, const uint8_t* st, const uint8_t*
                          hipStream_t s) {
   const int SS = nb.S * nb.S;
   dim3 grid((SS / 4 + 255) / 256, nb.B, 2);
-  hipLaunchKernelGGL(gather_kernel, grid, dim3(256), 0, s, st, act, rew, nt, meta, nb.idx, nb.S,
+  ddq_launch(gather_kernel, grid, dim3(256), 0, s, st, act, rew, nt, meta, nb.idx, nb.S,
                      nb.state, nb.next_state, nb.action, nb.reward, nb.nonterm);
   return hipGetLastError();
 }
@@ -441,10 +442,10 @@ hipError_t launch_sample_batch(ReplayMeta* meta, int64_t valid, int n, uint64_t 
   const int64_t nwords = (valid + 31) / 32;
   const int nblk = (int)((nwords + 1023) / 1024);
   CHECK_LAUNCH(hipMemsetAsync(bm, 0, (size_t)nblk * 1024 * 4, s));
-  hipLaunchKernelGGL(claim_kernel, dim3((n + 255) / 256), dim3(256), 0, s, meta, n, seed, ctr, bm);
-  hipLaunchKernelGGL(bm_count_kernel, dim3(nblk), dim3(256), 0, s, bm, nwords, blk);
-  hipLaunchKernelGGL(bm_scan_kernel, dim3(1), dim3(256), 0, s, blk, nblk);
-  hipLaunchKernelGGL(bm_emit_kernel, dim3(nblk), dim3(256), 0, s, bm, nwords, blk, idx, n);
+  ddq_launch(claim_kernel, dim3((n + 255) / 256), dim3(256), 0, s, meta, n, seed, ctr, bm);
+  ddq_launch(bm_count_kernel, dim3(nblk), dim3(256), 0, s, bm, nwords, blk);
+  ddq_launch(bm_scan_kernel, dim3(1), dim3(256), 0, s, blk, nblk);
+  ddq_launch(bm_emit_kernel, dim3(nblk), dim3(256), 0, s, bm, nwords, blk, idx, n);
   return hipGetLastError();
 }
 
@@ -455,7 +456,7 @@ hipError_t launch_gather_nchw(const uint8_t* st, const uint8_t* act, const int16
   const uint32_t wps = (uint32_t)(S * S);          // 4-byte words per slot
   const uint64_t tot = (uint64_t)n * wps;           // < 2^31 (n <= 2^31 / S^2 checked)
   const uint64_t blocks = std::max<uint64_t>((tot + 1023) / 1024, (uint64_t)(n + 255) / 256);
-  hipLaunchKernelGGL(gather_nchw_kernel, dim3((uint32_t)blocks, 2), dim3(256), 0, s, st, act,
+  ddq_launch(gather_nchw_kernel, dim3((uint32_t)blocks, 2), dim3(256), 0, s, st, act,
                      rew, nt, meta, idx, n, FastDiv(wps), s0, s1, action, reward, nonterm);
   return hipGetLastError();
 }
@@ -473,7 +474,7 @@ __global__ __launch_bounds__(256) void tile_kernel(uint8_t* __restrict__ dst,
 
 hipError_t launch_tile(uint8_t* dst, const uint8_t* src, uint64_t pool_bytes, uint64_t total,
                        hipStream_t s) {
-  hipLaunchKernelGGL(tile_kernel, dim3(4096), dim3(256), 0, s, dst, src, pool_bytes, total);
+  ddq_launch(tile_kernel, dim3(4096), dim3(256), 0, s, dst, src, pool_bytes, total);
   return hipGetLastError();
 }
 
@@ -489,7 +490,7 @@ __global__ void u8_to_nhwc_kernel(const uint8_t* src, int n, int S, float* dst) 
 
 hipError_t launch_u8_to_nhwc(const uint8_t* src, int n, int S, float* dst, hipStream_t s) {
   const int tot = n * S * S;
-  hipLaunchKernelGGL(u8_to_nhwc_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, src, n, S, dst);
+  ddq_launch(u8_to_nhwc_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, src, n, S, dst);
   return hipGetLastError();
 }
 
@@ -536,7 +537,7 @@ static void conv_dims(const ParamLayout& L, ConvDims* d) {
 hipError_t launch_relayout(const NetBuffers& nb, int z, hipStream_t s) {
   ConvDims d[3];
   conv_dims(nb.L, d);
-  hipLaunchKernelGGL(relayout_kernel, dim3(64, 3), dim3(256), 0, s, nb.theta[z], nb.wks[z],
+  ddq_launch(relayout_kernel, dim3(64, 3), dim3(256), 0, s, nb.theta[z], nb.wks[z],
                      nb.L.wks_total, d[0], d[1], d[2]);
   return hipGetLastError();
 }
@@ -985,7 +986,7 @@ static Fc4DgradArgs fc4_dgrad_args(const NetBuffers& nb, bool& narrow, int& ndx,
 }
 
 hipError_t launch_head(const NetBuffers& nb, hipStream_t s, ReplayMeta* bump) {
-  hipLaunchKernelGGL(fc4_head_kernel, dim3(nb.B + 25 + 9), dim3(kFc4), 0, s, head_args(nb, bump));
+  ddq_launch(fc4_head_kernel, dim3(nb.B + 25 + 9), dim3(kFc4), 0, s, head_args(nb, bump));
   return hipGetLastError();
 }
 
@@ -1460,7 +1461,7 @@ hipError_t launch_apply_shard(const NetBuffers& nb, int rule, float lr, float de
   if (pre) pf = *pre;
   const int64_t blocks = (len / 4 + 255) / 256;
   if (blocks + pf.ng > 0)
-    hipLaunchKernelGGL(apply_shard_kernel, dim3((uint32_t)(blocks + pf.ng)), dim3(256), 0, s,
+    ddq_launch(apply_shard_kernel, dim3((uint32_t)(blocks + pf.ng)), dim3(256), 0, s,
                        theta ? theta : nb.theta[0], gsl, nb.opt, nb.opt_init, off, len, slice, W,
                        a, first, nb.iter, pf);
   return hipGetLastError();
@@ -1469,20 +1470,20 @@ hipError_t launch_apply_shard(const NetBuffers& nb, int rule, float lr, float de
 
 hipError_t launch_refresh(const NetBuffers& nb, hipStream_t s, int force_sync) {
   const ApplyArgs a = apply_args(nb, 0, 0.f, 0.f, 0.f, 0.f, 0.f, 0);
-  hipLaunchKernelGGL(refresh_kernel, dim3((uint32_t)((a.n / 4 + 255) / 256)), dim3(256), 0, s,
+  ddq_launch(refresh_kernel, dim3((uint32_t)((a.n / 4 + 255) / 256)), dim3(256), 0, s,
                      nb.theta[0], nb.opt_init, nb.theta[1], nb.wks[0], nb.wks[1],
                      nb.L.wks_total, a, force_sync);
   return hipGetLastError();
 }
 
 hipError_t launch_book(const NetBuffers& nb, int period, hipStream_t s) {
-  hipLaunchKernelGGL(apply_book_kernel, dim3(1), dim3(1), 0, s, nb.iter, nb.opt_init, period);
+  ddq_launch(apply_book_kernel, dim3(1), dim3(1), 0, s, nb.iter, nb.opt_init, period);
   return hipGetLastError();
 }
 
 hipError_t launch_sum_slices(float* out, const float* in, int W, int64_t len, int64_t slice,
                              hipStream_t s) {
-  hipLaunchKernelGGL(sum_slices_kernel, dim3((uint32_t)((len + 255) / 256)), dim3(256), 0, s, out,
+  ddq_launch(sum_slices_kernel, dim3((uint32_t)((len + 255) / 256)), dim3(256), 0, s, out,
                      in, W, len, slice);
   return hipGetLastError();
 }
@@ -1506,14 +1507,14 @@ hipError_t launch_apply(const NetBuffers& nb, int rule, float lr, float decay, f
   Prefetch pf{};
   if (pre) pf = *pre;
   ApplyArgs a = apply_args(nb, rule, lr, decay, eps, momentum, wd, period);
-  if (!booked) hipLaunchKernelGGL(apply_book_kernel, dim3(1), dim3(1), 0, s, nb.iter, nb.opt_init, period);
+  if (!booked) ddq_launch(apply_book_kernel, dim3(1), dim3(1), 0, s, nb.iter, nb.opt_init, period);
   // fused steps: the slab-reduce launch already updated every parameter --
   // or, with its fc4 gradient summed over the ranks under the conv backward
   // (fa.ext), fc4's weights: the rest (summed after the reduce) here
   if (nb.fa.on && nb.fa.ext) { a.skip_lo = nb.L.w[3]; a.skip_len = nb.L.wn[3]; }
   const int blocks = (nb.fa.on && !nb.fa.ext) ? 0 : (int)(((a.n - a.skip_len) / 4 + 255) / 256);
   if (blocks + pf.ng == 0) return hipSuccess;
-  hipLaunchKernelGGL(apply_kernel, dim3(blocks + pf.ng), dim3(256), 0, s, apply_tail(nb), a, pf);
+  ddq_launch(apply_kernel, dim3(blocks + pf.ng), dim3(256), 0, s, apply_tail(nb), a, pf);
   return hipGetLastError();
 }
 
@@ -1740,7 +1741,7 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
   CHECK_LAUNCH(launch_fc4_fwd_direct(f, s));
   if (!out) return hipSuccess;   // training: reduce + Q_out fused into the head kernel
   M("fc4_reduce_out");
-  hipLaunchKernelGGL(fc4_reduce_out_kernel, dim3(B, nz), dim3(kFc4), 0, s, nb.fc4_part,
+  ddq_launch(fc4_reduce_out_kernel, dim3(B, nz), dim3(kFc4), 0, s, nb.fc4_part,
                      fc4_fwd_splits(f.K), nz, B, nb.theta[0] + L.b[3], nb.theta[1] + L.b[3],
                      nb.theta[0] + L.w[4], nb.theta[0] + L.b[4], nb.theta[1] + L.w[4],
                      nb.theta[1] + L.b[4], nb.h4[0], nb.h4[1], nb.q_out, nb.p_out);
@@ -1763,7 +1764,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     Fc4DgradArgs f = fc4_dgrad_args(nb, narrow, ndx, nd);
     const int nw = (nb.fa.on && !nb.fa.ext) ? 0 : fc4_wgrad_blocks<8>(f.K);
     M("fc4_bwd");
-    hipLaunchKernelGGL((narrow ? fc4_bwd_kernel<true, 16> : fc4_bwd_kernel<true, 32>),
+    ddq_launch((narrow ? fc4_bwd_kernel<true, 16> : fc4_bwd_kernel<true, 32>),
                        dim3(nd + nw), dim3(512), 0, s, f, nb.pool3[0], nb.grad + L.w[3], nd, ndx);
     CHECK_LAUNCH(hipGetLastError());
   }
@@ -1859,7 +1860,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     }
     Prefetch pf{};
     if (pre && nb.fa.on) pf = *pre;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(pf.ng + nub + kFc4 / 64 + nfa), dim3(256), 0, s,
+    ddq_launch(wgrad_reduce_kernel, dim3(pf.ng + nub + kFc4 / 64 + nfa), dim3(256), 0, s,
                        nb.wpart, nb.grad, d[0], d[1], d[2], nub, nb.iter,
                        book ? nb.opt_init : nullptr, book_period,
                        book && !nb.fa.on ? bump : nullptr, nb.book_inc, hs, fat, faa, pf,
@@ -1897,7 +1898,7 @@ hipError_t launch_act(const NetBuffers& nb, const float* in, int n, float* pool3
   a.q_out = qout; a.p_out = qout;
   CHECK_LAUNCH(launch_forward(a, 1, s, nullptr, nullptr));
   if (actions) {
-    hipLaunchKernelGGL(argmax_kernel, dim3((n + 63) / 64), dim3(64), 0, s, n, qout, actions);
+    ddq_launch(argmax_kernel, dim3((n + 63) / 64), dim3(64), 0, s, n, qout, actions);
     CHECK_LAUNCH(hipGetLastError());
   }
   return hipSuccess;

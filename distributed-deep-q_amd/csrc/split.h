@@ -1065,7 +1065,7 @@ inline hipError_t launch_split_conv(SplitArgs a, int nz, hipStream_t st) {
     return hipErrorInvalidValue;
   a.tiles_x = (a.W + TX - 1) / TX;
   const int tiles_y = (a.H + TY - 1) / TY;
-  hipLaunchKernelGGL(kern, dim3(tiles_y * a.tiles_x, a.B, nz), dim3(C::kThreads), smem, st, a);
+  ddq_launch(kern, dim3(tiles_y * a.tiles_x, a.B, nz), dim3(C::kThreads), smem, st, a);
   return hipGetLastError();
 }
 
@@ -1241,7 +1241,7 @@ inline hipError_t launch_split_conv1(Conv1Args a, int nz, hipStream_t st, int64_
     return e;
   a.tiles_x = (a.W + TX - 1) / TX;
   const int tiles_y = (a.H + TY - 1) / TY;
-  hipLaunchKernelGGL(kern, dim3(tiles_y * a.tiles_x, a.B, nz), dim3(64 * WM), C::kSmemB, st, a);
+  ddq_launch(kern, dim3(tiles_y * a.tiles_x, a.B, nz), dim3(64 * WM), C::kSmemB, st, a);
   return hipGetLastError();
 }
 

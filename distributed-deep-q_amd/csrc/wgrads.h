@@ -439,7 +439,7 @@ inline hipError_t launch_wgrads_pair_w(const WgradSArgs& a0, const WgradSArgs& a
     return e;
   const int n0 = (a0.G + 7) / 8 * 8 * (COUT0 / 32) * KS0;
   const int n1 = (a1.G + 7) / 8 * 8 * (COUT1 / 32) * KS1;
-  hipLaunchKernelGGL(kern, dim3(n0 + n1), dim3(256), shm, st, a0, a1, n0);
+  ddq_launch(kern, dim3(n0 + n1), dim3(256), shm, st, a0, a1, n0);
   return hipGetLastError();
 }
 

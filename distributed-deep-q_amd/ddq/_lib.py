@@ -124,8 +124,6 @@ _SIGS = {
     "ddq_set_straggle": (ctypes.c_int, [_P, _i64]),
     "ddq_profile_step": (ctypes.c_int, [_P, ctypes.POINTER(StepCfg), _P, _fp, _i32,
                                         ctypes.POINTER(_i32)]),
-    "ddq_profile_graph": (ctypes.c_int, [_P, ctypes.POINTER(StepCfg), _i32, _P, _fp, _i32,
-                                         ctypes.POINTER(_i32)]),
     "ddq_time_layer": (ctypes.c_int, [_P, ctypes.c_char_p, _i32, _fp]),
     "ddq_step_flops": (ctypes.c_double, [_P]),
 }

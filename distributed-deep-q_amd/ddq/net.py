@@ -366,19 +366,6 @@ class DeepQNet:
         return [(raw[16 * i:16 * i + 16].split(b"\0")[0].decode(), float(us[i]))
                 for i in range(min(n.value, cap))]
 
-    def profile_graph(self, cfg, reps=20, cap=32):
-        """Per-kernel mean device microseconds inside the graph-replayed
-        pipelined chain (event-record nodes between the kernels of 8 captured
-        steps, reps replays); [(name, us)] in step order."""
-        names = ctypes.create_string_buffer(16 * cap)
-        us = (ctypes.c_float * cap)()
-        n = _lib._i32()
-        self._check(self.lib.ddq_profile_graph(self.ctx, ctypes.byref(cfg), int(reps), names, us,
-                                               cap, ctypes.byref(n)))
-        raw = names.raw
-        return [(raw[16 * i:16 * i + 16].split(b"\0")[0].decode(), float(us[i]))
-                for i in range(min(n.value, cap))]
-
     def time_layer(self, name, reps=100):
         """Average device microseconds of one launch of a forward conv layer
         ("conv1_fwd" / "conv2_fwd" / "conv3_fwd"), reps launches back to back."""

@@ -317,18 +317,12 @@ int ddq_set_straggle(ddq_ctx* ctx, int64_t usec);
 /* ---------------- measurement ------------------------------------------ */
 /* Kernel ids for ddq_profile_step. */
 #define DDQ_MAX_KERNELS 32
-/* Run one eager step with HIP events around every kernel on the ctx stream;
- * fills names (16 chars each, NUL padded) and device-time microseconds. */
+/* Run one eager step; every kernel is launched with start / stop events of
+ * its own (hipExtLaunchKernel: the dispatch's timestamps, no marker packets
+ * between the kernels); fills names (16 chars each, NUL padded) and each
+ * kernel's device microseconds, in step order (RCCL calls are not timed). */
 int ddq_profile_step(ddq_ctx* ctx, const ddq_step_cfg* cfg, char* names, float* usec,
                      int32_t cap, int32_t* n);
-/* The same kernels' device times inside the graph-replayed pipelined chain
- * (ddq_step_pipelined_async's 8-step graphs): 8 steps captured with an
- * event-record node between every two kernels, replayed reps times (training
- * steps: the ctx's counters advance by 8 per replay); per kernel name the
- * mean microseconds over steps and replays, in step order.  Exchange none or
- * allreduce, batch <= 256. */
-int ddq_profile_graph(ddq_ctx* ctx, const ddq_step_cfg* cfg, int32_t reps, char* names,
-                      float* usec, int32_t cap, int32_t* n);
 /* Launch one forward conv layer ("conv1_fwd", "conv2_fwd" or "conv3_fwd",
  * both towers, the step's own kernel and arguments) reps times back to back
  * between two HIP events on the ctx stream; *usec = average device time per
