@@ -1110,7 +1110,10 @@ struct Conv1Cfg {
   static_assert(kSmemB <= 160 * 1024, "LDS");
 };
 
-template <int TY, int TX, int WM>
+// MF 1: v_mfma_f32_16x16x32_bf16 -- one k-step per tap row (kx 0..7 x 4
+// channels: lane k-group g reads taps 2g, 2g + 1), the wave's 32-row blocks as
+// 16 x 16 blocks (split_conv_body's MF 1 element layout)
+template <int TY, int TX, int WM, int MF>
 __global__ __launch_bounds__(64 * WM) void split_conv1_kernel(const Conv1Args a) {
   using C = Conv1Cfg<TY, TX, WM>;
   constexpr int TM = C::TM;
@@ -1124,7 +1127,9 @@ __global__ __launch_bounds__(64 * WM) void split_conv1_kernel(const Conv1Args a)
   const float* __restrict__ in = z ? a.in[1] : a.in[0];
   const __bf16* __restrict__ wk = z ? a.wk[1] : a.wk[0];
   constexpr int kThreads = 64 * WM;
-  const float bias_pre = (z ? a.bias[1] : a.bias[0])[lane & 31];   // the epilogue's, early
+  const float* bz_ = z ? a.bias[1] : a.bias[0];   // the epilogue's biases, early
+  const float bias_pre = bz_[MF ? (lane & 15) : (lane & 31)];
+  const float bias_pre2 = MF ? bz_[16 + (lane & 15)] : 0.f;
   // patch: one pixel (4 channels) per item, fp32 -> bf16 (exact), loads first
   {
     constexpr int NP = C::PH * C::PW;
@@ -1170,6 +1175,65 @@ __global__ __launch_bounds__(64 * WM) void split_conv1_kernel(const Conv1Args a)
   }
   __syncthreads();
   const int l31 = lane & 31, h = lane >> 5;
+  f32x16 acc[TM][1];
+  if constexpr (MF) {
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    const int kg = lane >> 4;
+    int abase[2 * TM];
+#pragma unroll
+    for (int q = 0; q < 2 * TM; ++q) {
+      const int m = wid * TM * 32 + 16 * q + (lane & 15);
+      const int win = (m >> 2) < C::NWIN ? m >> 2 : 0, dy = (m >> 1) & 1, dx = m & 1;
+      const int wy = win / (TX / 2), wx = win % (TX / 2);
+      abase[q] = (2 * wy + dy) * C::RS + (2 * wx + dx + 2 * kg) * 4;
+    }
+    int bbase[2];
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj) bbase[bj] = (16 * bj + (lane & 15)) * C::CW + 8 * kg;
+    f32x4 a4[2 * TM][2], c4[2 * TM][2];
+#pragma unroll
+    for (int q = 0; q < 2 * TM; ++q)
+#pragma unroll
+      for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { a4[q][bj][r] = 0.f; c4[q][bj][r] = 0.f; }
+#pragma unroll
+    for (int ky = 0; ky < 7; ++ky) {
+      bf16x8 bv[2][3];
+#pragma unroll
+      for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          bv[bj][p] = *reinterpret_cast<const bf16x8*>(wbuf + p * 32 * C::CW + bbase[bj] + ky * 32);
+#pragma unroll
+      for (int q = 0; q < 2 * TM; ++q) {
+        const __bf16* pa = patch + abase[q] + ky * C::RS;
+        typedef __attribute__((address_space(3))) const u32x2 lds_u2;
+        typedef __attribute__((address_space(3))) const char lds_c;
+        lds_u2* la = (lds_u2*)pa;
+        uint32_t hi_off = 8;                       // separate ds_read_b64 (8-byte aligned pixels)
+        asm volatile("" : "+v"(hi_off));
+        const u32x2 lo = *la;
+        const u32x2 hi = *(lds_u2*)((lds_c*)la + hi_off);
+        u32x4 av4 = {lo[0], lo[1], hi[0], hi[1]};
+        const bf16x8 av = *reinterpret_cast<bf16x8*>(&av4);
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj) {
+          c4[q][bj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv[bj][2], c4[q][bj], 0, 0, 0);
+          c4[q][bj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv[bj][1], c4[q][bj], 0, 0, 0);
+          a4[q][bj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv[bj][0], a4[q][bj], 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 v = a4[2 * i + (g >> 1)][g & 1] + c4[2 * i + (g >> 1)][g & 1];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][0][4 * g + r] = v[r];
+      }
+  } else {
   int abase[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -1179,8 +1243,7 @@ __global__ __launch_bounds__(64 * WM) void split_conv1_kernel(const Conv1Args a)
     abase[i] = (2 * wy + dy) * C::RS + (2 * wx + dx + 2 * h) * 4;
   }
   const int bbase = l31 * C::CW + h * 8;
-  const float bpre[1] = {bias_pre};
-  f32x16 acc[TM][1], cor[TM];
+  f32x16 cor[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1217,6 +1280,10 @@ __global__ __launch_bounds__(64 * WM) void split_conv1_kernel(const Conv1Args a)
   }
 #pragma unroll
   for (int i = 0; i < TM; ++i) acc[i][0] += cor[i];
+  }
+  float bpre[MF ? 2 : 1];
+  bpre[0] = bias_pre;
+  if constexpr (MF) bpre[MF] = bias_pre2;
   SplitArgs e{};
   e.B = a.B; e.H = a.H; e.W = a.W;
   e.out[0] = a.out[0]; e.out[1] = a.out[1];
@@ -1224,18 +1291,19 @@ __global__ __launch_bounds__(64 * WM) void split_conv1_kernel(const Conv1Args a)
   e.out_elems = a.out_elems;
   e.mask[0] = a.mask[0]; e.mask[1] = a.mask[1];
   if constexpr (C::NWIN * 32 * 7 <= C::kSmemB)
-    split_epilogue_fwd_lds<TM, 1, TX, 32, 1, C::NWIN, 64 * WM>(e, acc, bpre, sm_c1, b, z, y0, x0,
-                                                               wid, 0, l31, h, 0, tid);
-  else
+    split_epilogue_fwd_lds<TM, 1, TX, 32, 1, C::NWIN, 64 * WM, MF>(e, acc, bpre, sm_c1, b, z, y0,
+                                                                   x0, wid, 0, l31, h, 0, tid);
+  else if constexpr (!MF)
     split_epilogue<TM, 1, TX, 32, false, 1, C::NWIN>(e, acc, bpre, b, z, y0, x0, wid, 0, l31, h);
+  static_assert(!MF || C::NWIN * 32 * 7 <= C::kSmemB, "16x16x32: the LDS epilogue");
 }
 
-template <int TY, int TX, int WM>
+template <int TY, int TX, int WM, int MF>
 inline hipError_t launch_split_conv1(Conv1Args a, int nz, hipStream_t st, int64_t wk_elems) {
   a.wk_elems = wk_elems;
   if ((a.out[0] && a.out_split[0]) || (a.out[1] && a.out_split[1])) return hipErrorInvalidValue;
   using C = Conv1Cfg<TY, TX, WM>;
-  auto kern = split_conv1_kernel<TY, TX, WM>;
+  auto kern = split_conv1_kernel<TY, TX, WM, MF>;
   static std::atomic<uint64_t> attr{0};
   if (hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(kern), attr, (int)(C::kSmemB)))
     return e;
