@@ -1234,11 +1234,18 @@ static int check_step(ddq_ctx* c, const ddq_step_cfg* cfg) {
 // model this worker last pulled (no apply bookkeeping: the owners keep the
 // iteration), into nb.grad, on the ctx stream; grad_ev marks it ready.
 static int async_compute(ddq_ctx* c, const ddq_step_cfg* cfg) {
-  const NetBuffers& nb = c->nb;
-  HIP_TRY(c, launch_sample(nb, c->r_meta, cfg->seed, c->stream));
-  HIP_TRY(c, launch_gather(nb, c->r_state, c->r_action, c->r_reward, c->r_nonterm, c->r_meta,
-                           c->stream));
-  TRY(enqueue_fwd_bwd_x(c, nb, nullptr, nullptr, -1, nullptr, false));
+  NetBuffers nb = c->nb;
+  if (nb.B <= 256) {   // one draw + gather launch; the head advances the counter
+    nb.head_bump = 1;
+    HIP_TRY(c, launch_sample_gather(nb, c->r_state, c->r_action, c->r_reward, c->r_nonterm,
+                                    c->r_meta, cfg->seed, c->stream));
+    TRY(enqueue_fwd_bwd_x(c, nb, nullptr, nullptr, -1, c->r_meta, false));
+  } else {
+    HIP_TRY(c, launch_sample(nb, c->r_meta, cfg->seed, c->stream));
+    HIP_TRY(c, launch_gather(nb, c->r_state, c->r_action, c->r_reward, c->r_nonterm, c->r_meta,
+                             c->stream));
+    TRY(enqueue_fwd_bwd_x(c, nb, nullptr, nullptr, -1, nullptr, false));
+  }
   HIP_TRY(c, hipEventRecord(c->grad_ev, c->stream));
   c->ready_seen = false;
   c->grad_ev_captured = c->acapture;

@@ -92,6 +92,8 @@ struct NetBuffers {
   FusedApplyCfg fa;                 // on: head latches the apply flags, the slab reduce
                                     // applies (FusedApplyCfg)
   int book_inc;                     // param-server iterations per apply (1, or W: server mode)
+  int head_bump;                    // the head kernel advances the draw counter without a
+                                    // fused apply (async gradients: sample_gather draws)
 };
 
 // fused device draw + gather for the step (B <= 256); counter advanced by the

@@ -680,8 +680,10 @@ __device__ __forceinline__ void head_body(const HeadArgs& H, int b, char* smem) 
   if (latch && b == 0 && n == 0) {
     latch[2] = (latch[0] == 0);
     latch[3] = period > 0 && ((*iter + inc) % period) == 0;
-    if (bump) bump->counter += 1;   // the step's draw (apply_book's bump, moved here)
   }
+  // the step's draw-counter advance (apply_book's bump, moved here): fused
+  // apply steps, and async gradients (no apply on the worker)
+  if (bump && b == 0 && n == 0) bump->counter += 1;
   const size_t stride = (size_t)2 * B * kFc4;
   float h[2];
   float q[8];
@@ -967,7 +969,8 @@ static HeadArgs head_args(const NetBuffers& nb, ReplayMeta* bump) {
                   L.w[4], L.b[4], nb.action, nb.reward, nb.nonterm, nb.h4[0], nb.h4[1], nb.q_out,
                   nb.p_out, nb.q_sa, nb.p_sa, nb.target, nb.dqbuf, nb.lpart, nb.dh4,
                   nb.fa.on ? nb.opt_init : nullptr, nb.iter, nb.fa.period, nb.book_inc,
-                  nb.fa.on ? bump : nullptr, nb.wks[0], L.wks_total, L.wks_off[1], L.wkst_off,
+                  (nb.fa.on || nb.head_bump) ? bump : nullptr, nb.wks[0], L.wks_total,
+                  L.wks_off[1], L.wkst_off,
                   L.wks_off[2], L.wkst3_off};
 }
 
@@ -1560,6 +1563,11 @@ static const T& pick_tile(const T (&menu)[n], int H, int W) {
 #ifndef DDQ_C2F_WN
 #define DDQ_C2F_WN 2
 #endif
+// conv2 data-gradient launches below this many workgroups run on a second
+// graph branch beside the weight gradients (launch_backward)
+#ifndef DDQ_FORK_WGS
+#define DDQ_FORK_WGS 128
+#endif
 struct SplitMenu {
   TileOpt opt;
   hipError_t (*launch)(SplitArgs, int, hipStream_t);
@@ -1789,6 +1797,17 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     M("conv3_dgrad");
     CHECK_LAUNCH(pick_tile(kConv3Dgrad, H, H).launch(a, 1, s));
   }
+  // Small maps: conv2's data gradient (+ conv1's weight gradient) runs on a
+  // second graph branch beside the conv2 / conv3 weight gradients -- both need
+  // only conv3's data gradient, and at these sizes each underfills the GPU
+  // (deepq16: 32 workgroups beside ~300).  Eager profiling keeps one stream.
+  const TileOpt& c2dt = pick_tile(kConv2Dgrad, S / 2, S / 2).opt;
+  const int c2d_wgs = ((S / 2 + c2dt.ty - 1) / c2dt.ty) * ((S / 2 + c2dt.tx - 1) / c2dt.tx) * B;
+  const bool fork = nb.side && !mark && c2d_wgs < DDQ_FORK_WGS;
+  if (fork) {
+    CHECK_LAUNCH(hipEventRecord(nb.ev[0], s));
+    CHECK_LAUNCH(hipStreamWaitEvent(nb.side, nb.ev[0], 0));
+  }
   {  // conv3 weight gradient (split bf16, wgrads.h): rows of the expanded split
      // dconv3 (pure copies) against the split pool2; conv2's on the split
      // pooled dpool2 and the split pool1
@@ -1826,7 +1845,11 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     a.w1_route = nb.mask1; a.w1_in = nb.state;
     a.w1_part = nb.wpart + nb.wpart_off[0]; a.w1_np = nb.wnp[0];
     M("conv2_dgrad");
-    CHECK_LAUNCH(pick_tile(kConv2Dgrad, H, H).launch(a, 1, s));
+    CHECK_LAUNCH(pick_tile(kConv2Dgrad, H, H).launch(a, 1, fork ? nb.side : s));
+  }
+  if (fork) {
+    CHECK_LAUNCH(hipEventRecord(nb.ev[1], nb.side));
+    CHECK_LAUNCH(hipStreamWaitEvent(s, nb.ev[1], 0));
   }
   // slab-reduce geometry: layer l's blocks start at d[l].blk0
   WredDims d[3];
