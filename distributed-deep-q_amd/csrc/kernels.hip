@@ -1537,9 +1537,10 @@ int fc4_splits_for(int S) { return fc4_fwd_splits(64 * (S / 8) * (S / 8)); }
 struct TileOpt {
   int ty, tx, rows;
 };
-template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, int MF = 0>
+template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, int MF = 0,
+          int TPS = 1>
 constexpr TileOpt split_tile() {
-  return {TY, TX, WM * SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK, MF>::TM * 32};
+  return {TY, TX, WM * SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK, MF, TPS>::TM * 32};
 }
 template <int TY, int TX, int WM>
 constexpr TileOpt conv1_tile() { return {TY, TX, WM * Conv1Cfg<TY, TX, WM>::TM * 32}; }
@@ -1559,6 +1560,11 @@ static const T& pick_tile(const T (&menu)[n], int H, int W) {
   return menu[best];
 }
 
+// A/B: the small-map tiles (8 x 8, 4 x 4, 4 x 8) stage 2-3 taps per weight-ring
+// step (SplitCfg TPS: a barrier per 2-3 taps instead of per tap)
+#ifndef DDQ_TPS_SMALL
+#define DDQ_TPS_SMALL 0
+#endif
 // A/B: conv2 forward's 16 x 16 tile as 8 waves of 32 x 64 (1) instead of 16 of 32 x 32 (2)
 #ifndef DDQ_C2F_WN
 #define DDQ_C2F_WN 2
@@ -1572,41 +1578,41 @@ struct SplitMenu {
   TileOpt opt;
   hipError_t (*launch)(SplitArgs, int, hipStream_t);
 };
-#define DDQ_SPLIT_TILE(CPT, CP, N, KS, TY, TX, WM, WN, WK, DG, MF)          \
+#define DDQ_SPLIT_TILE(CPT, CP, N, KS, TY, TX, WM, WN, WK, DG, MF, TPS)     \
   SplitMenu {                                                              \
-    split_tile<CPT, CP, N, KS, TY, TX, WM, WN, WK, MF>(),                  \
-        &launch_split_conv<CPT, CP, N, KS, TY, TX, WM, WN, WK, DG, MF>      \
+    split_tile<CPT, CP, N, KS, TY, TX, WM, WN, WK, MF, TPS>(),             \
+        &launch_split_conv<CPT, CP, N, KS, TY, TX, WM, WN, WK, DG, MF, TPS> \
   }
 // conv2 forward (32 -> 64, 5x5): 16 waves of one 32x32 block on 16 x 16, on
 // v_mfma_f32_16x16x32_bf16 (MF 1; split.h SplitCfg): 30.1 -> 26.3 us against
 // the 32x32x16 form at 64x64, same-box A/B (the chip holds a higher clock on
 // the 16x16 shape, MI355X_MICROARCH.md DVFS item 7)
 static const SplitMenu kConv2Fwd[] = {
-    DDQ_SPLIT_TILE(32, 32, 64, 5, 16, 16, 8, DDQ_C2F_WN, 1, false, 1),
-    DDQ_SPLIT_TILE(32, 32, 64, 5, 10, 20, 7, 2, 1, false, 1),
-    DDQ_SPLIT_TILE(32, 32, 64, 5, 12, 12, 5, 2, 1, false, 1),
-    DDQ_SPLIT_TILE(32, 32, 64, 5, 8, 8, 2, 2, 1, false, 1),
-    DDQ_SPLIT_TILE(32, 32, 64, 5, 8, 26, 7, 2, 1, false, 1),
-    DDQ_SPLIT_TILE(32, 32, 64, 5, 14, 14, 7, 2, 1, false, 1)};
+    DDQ_SPLIT_TILE(32, 32, 64, 5, 16, 16, 8, DDQ_C2F_WN, 1, false, 1, 1),
+    DDQ_SPLIT_TILE(32, 32, 64, 5, 10, 20, 7, 2, 1, false, 1, 1),
+    DDQ_SPLIT_TILE(32, 32, 64, 5, 12, 12, 5, 2, 1, false, 1, 1),
+    DDQ_SPLIT_TILE(32, 32, 64, 5, 8, 8, 2, 2, 1, false, 1, DDQ_TPS_SMALL ? 3 : 1),
+    DDQ_SPLIT_TILE(32, 32, 64, 5, 8, 26, 7, 2, 1, false, 1, 1),
+    DDQ_SPLIT_TILE(32, 32, 64, 5, 14, 14, 7, 2, 1, false, 1, 1)};
 // conv3 forward (64 -> 64, 3x3): two k groups on 8 x 8
 static const SplitMenu kConv3Fwd[] = {
-    DDQ_SPLIT_TILE(64, 64, 64, 3, 8, 8, 2, 2, 2, false, 1),
-    DDQ_SPLIT_TILE(64, 64, 64, 3, 10, 10, 4, 2, 2, false, 1),
-    DDQ_SPLIT_TILE(64, 64, 64, 3, 12, 12, 5, 2, 1, false, 1),
-    DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 18, 4, 2, 2, false, 1),
-    DDQ_SPLIT_TILE(64, 64, 64, 3, 4, 4, 1, 2, 2, false, 1),
-    DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 26, 5, 2, 1, false, 0)};   // (MF 1 exceeds LDS)
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 8, 8, 2, 2, 2, false, 1, 1),
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 10, 10, 4, 2, 2, false, 1, 1),
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 12, 12, 5, 2, 1, false, 1, 1),
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 18, 4, 2, 2, false, 1, 1),
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 4, 4, 1, 2, 2, false, 1, DDQ_TPS_SMALL ? 2 : 1),
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 26, 5, 2, 1, false, 0, 1)};   // (MF 1 exceeds LDS)
 // conv3 data gradient: four k groups on 4 x 8
 static const SplitMenu kConv3Dgrad[] = {
-    DDQ_SPLIT_TILE(64, 64, 64, 3, 4, 8, 1, 2, 4, true, 0),
-    DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 10, 2, 2, 4, true, 0),
-    DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 26, 5, 2, 1, true, 0)};
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 4, 8, 1, 2, 4, true, 0, DDQ_TPS_SMALL ? 2 : 1),
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 10, 2, 2, 4, true, 0, 1),
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 26, 5, 2, 1, true, 0, 1)};
 // conv2 data gradient (64 -> 32): four k groups on 8 x 16
 static const SplitMenu kConv2Dgrad[] = {
-    DDQ_SPLIT_TILE(64, 64, 32, 5, 8, 16, 4, 1, 4, true, 0),
-    DDQ_SPLIT_TILE(64, 64, 32, 5, 8, 20, 5, 1, 2, true, 0),
-    DDQ_SPLIT_TILE(64, 64, 32, 5, 12, 12, 5, 1, 2, true, 0),
-    DDQ_SPLIT_TILE(64, 64, 32, 5, 8, 8, 2, 1, 4, true, 0)};
+    DDQ_SPLIT_TILE(64, 64, 32, 5, 8, 16, 4, 1, 4, true, 0, 1),
+    DDQ_SPLIT_TILE(64, 64, 32, 5, 8, 20, 5, 1, 2, true, 0, 1),
+    DDQ_SPLIT_TILE(64, 64, 32, 5, 12, 12, 5, 1, 2, true, 0, 1),
+    DDQ_SPLIT_TILE(64, 64, 32, 5, 8, 8, 2, 1, 4, true, 0, DDQ_TPS_SMALL ? 3 : 1)};
 #undef DDQ_SPLIT_TILE
 
 struct Conv1Menu {

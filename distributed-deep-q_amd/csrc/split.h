@@ -127,7 +127,10 @@ __device__ __forceinline__ bf16x8 tr_pair(const __bf16* p0, const __bf16* p1) {
 // cycles per FLOP).  MF = 1 reads lane l's 8 channels [8 (l / 16), +8) of row
 // l % 16: pixel and weight-row strides CP + 16 bf16 (6 16-byte units) are
 // conflict-free for it (a bank model of the four 16-lane groups).
-template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK = 1, int MF = 0>
+// TPS: taps per weight-ring step (one barrier per TPS taps; small maps, where a
+// step's MFMAs are few and the per-step barrier / latency dominates).
+template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK = 1, int MF = 0,
+          int TPS = 1>
 struct SplitCfg {
   static constexpr int NCH = CPT / CP;
   static constexpr int PH = TY + KS - 1, PW = TX + KS - 1;
@@ -136,6 +139,8 @@ struct SplitCfg {
   static constexpr int RS = RS0 + ((64 - (RS0 % 128)) + 128) % 128;   // == 64 (mod 128) bf16
   static constexpr int CW = CP + (MF ? 16 : 8);                       // bf16 per weight row
   static constexpr int T = KS * KS;
+  static constexpr int kTPS = TPS;
+  static constexpr int TS = (T + TPS - 1) / TPS;                      // ring steps per chunk
   static constexpr int KSTEP = CP / (MF ? 32 : 16);
   static constexpr int kGroup = 64 * WM * WN * WK;                     // all waves stage
   static constexpr int kThreads = kGroup;
@@ -150,7 +155,7 @@ struct SplitCfg {
   static constexpr int kPlane = PH * RS;                              // bf16 per patch plane
   static constexpr int kWSlot = N * CW;                               // bf16 per weight plane
   static constexpr int kPatchB = 3 * kPlane * 2;
-  static constexpr int kWB = 2 * 3 * kWSlot * 2;                      // two-slot ring
+  static constexpr int kWB = 2 * TPS * 3 * kWSlot * 2;                // two-slot ring
   static constexpr int kSmemB = kPatchB + kWB;
   static_assert(CPT % CP == 0 && CP % 16 == 0 && TY % 2 == 0 && TX % 2 == 0, "shape");
   static_assert(TM >= 1 && TN >= 1 && (WM * TM - 1) * 8 < NWIN && N == WN * TN * 32, "wave tile");
@@ -171,7 +176,8 @@ struct SplitCfg {
 template <class C, int CPT, int CP, int N>
 struct SplitWStage {
   static constexpr int WV = N * CP / 8;                         // 16-byte vectors per plane
-  static constexpr int kPer = (3 * WV + C::kGroup - 1) / C::kGroup;
+  static constexpr int NVS = 3 * WV * C::kTPS;                   // vectors per ring step
+  static constexpr int kPer = (NVS + C::kGroup - 1) / C::kGroup;
   static_assert(kPer <= 12, "weight staging registers");
   u32x4 r[kPer];
   // ds_write_b128 serves 8 contiguous lanes per LDS cycle on banks (a/4) mod
@@ -186,12 +192,15 @@ struct SplitWStage {
     return (n0 & ~7) | ((n0 & 7) >> 1) | ((n0 & 1) << 2);
   }
 
-  __device__ __forceinline__ void load(const __bf16* __restrict__ wk, int64_t E, int ch, int t,
+  // the TPS taps tg * TPS + i of chunk ch (taps past T read tap T - 1: unused)
+  __device__ __forceinline__ void load(const __bf16* __restrict__ wk, int64_t E, int ch, int tg,
                                        int tid) {
 #pragma unroll
     for (int S = 0; S < kPer; ++S) {   // clamped, unconditional: the store drops extra lanes
       const int f0 = tid + S * C::kGroup;
-      const int f = (3 * WV) % C::kGroup == 0 || f0 < 3 * WV ? f0 : 3 * WV - 1;
+      const int f1 = NVS % C::kGroup == 0 || f0 < NVS ? f0 : NVS - 1;
+      const int ti = f1 / (3 * WV), f = f1 - ti * (3 * WV);
+      const int t0 = tg * C::kTPS + ti, t = t0 < C::T ? t0 : C::T - 1;
       const int p = f / WV, q = f - p * WV;
       const int n = row(q), c8 = q % (CP / 8);
       r[S] = *reinterpret_cast<const u32x4*>(wk + p * E + ((size_t)n * C::T + t) * CPT + ch * CP +
@@ -204,11 +213,12 @@ struct SplitWStage {
       const int f0 = tid + S * C::kGroup;
       // lanes past the vectors store nothing (whole waves at these sizes:
       // a uniform branch); they used to rewrite the last vector
-      if ((3 * WV) % C::kGroup != 0 && f0 >= 3 * WV) continue;
-      const int f = (3 * WV) % C::kGroup == 0 || f0 < 3 * WV ? f0 : 3 * WV - 1;
+      if (NVS % C::kGroup != 0 && f0 >= NVS) continue;
+      const int f1 = NVS % C::kGroup == 0 || f0 < NVS ? f0 : NVS - 1;
+      const int ti = f1 / (3 * WV), f = f1 - ti * (3 * WV);
       const int p = f / WV, q = f - p * WV;
       const int n = row(q), c8 = q % (CP / 8);
-      *reinterpret_cast<u32x4*>(dst + p * C::kWSlot + n * C::CW + 8 * c8) = r[S];
+      *reinterpret_cast<u32x4*>(dst + (ti * 3 + p) * C::kWSlot + n * C::CW + 8 * c8) = r[S];
     }
   }
 };
@@ -650,10 +660,10 @@ __device__ __forceinline__ void w1_tile_wgrad(const SplitArgs& a, char* smem,
 }
 
 template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, bool DGRAD,
-          int MF = 0>
+          int MF = 0, int TPS = 1>
 __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, int bx, int by,
                                                 int bz) {
-  using C = SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK, MF>;
+  using C = SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK, MF, TPS>;
   static_assert(MF == 0 || !DGRAD, "16x16x32: forward convolutions only");
   constexpr int TM = C::TM, TN = C::TN, T = C::T, NCH = C::NCH;
   __bf16* patch = reinterpret_cast<__bf16*>(smem);
@@ -815,11 +825,12 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
   // ---- weights: step s = (chunk s / T, tap s % T) -> ring slot s & 1 ----
   // Two register sets: the loads of step s+2 are issued at the start of step
   // s and stored at the end of step s+1 (two steps of MFMAs to land in).
-  constexpr int NSTEP = NCH * T;
+  constexpr int TS = C::TS;
+  constexpr int NSTEP = NCH * TS;
   SplitWStage<C, CPT, CP, N> ws0, ws1;
   auto wload = [&](SplitWStage<C, CPT, CP, N>& w, int st) {
     const int sc = st < NSTEP ? st : NSTEP - 1;
-    w.load(wk, a.wk_elems, sc / T, sc % T, tid);
+    w.load(wk, a.wk_elems, sc / TS, sc % TS, tid);
   };
   stage_patch(0);
   wload(ws0, 0);
@@ -891,8 +902,11 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
 
   // one step: the MFMAs of tap t of the resident chunk on ring slot `slot`
   auto tap_step = [&](int s, int slot) {
-    const __bf16* wb = wbuf + slot * 3 * C::kWSlot;
-    const int t = s % T;
+#pragma unroll
+    for (int ti = 0; ti < TPS; ++ti) {
+    const int t = (s % TS) * TPS + ti;
+    if (TPS > 1 && t >= T) break;                   // (wave-uniform)
+    const __bf16* wb = wbuf + (slot * TPS + ti) * 3 * C::kWSlot;
     const int ky = t / KS, kx = t % KS;
     const __bf16* pa = patch + ky * C::RS + kx * C::CS;
 #pragma unroll
@@ -933,6 +947,7 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
           }
       }
     }
+    }
   };
   // end of step s: store step s+1's weights, restage the patch at a chunk
   // boundary (the barrier before fences every wave's reads of the old chunk)
@@ -941,12 +956,12 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
     // hoists them above: every wave then waited for all its LDS reads and the
     // barrier before its first MFMA of the step)
     __builtin_amdgcn_sched_barrier(0);
-    const bool chunk_edge = NCH > 1 && (s + 1) % T == 0;
+    const bool chunk_edge = NCH > 1 && (s + 1) % TS == 0;
     if (chunk_edge) {
       __syncthreads();
-      stage_patch((s + 1) / T);
+      stage_patch((s + 1) / TS);
     }
-    w.store(wbuf + ((s + 1) & 1) * 3 * C::kWSlot, tid);
+    w.store(wbuf + ((s + 1) & 1) * TPS * 3 * C::kWSlot, tid);
     __syncthreads();
   };
   for (int s = 0; s < NSTEP; s += 2) {
@@ -1040,18 +1055,18 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
 }
 
 template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, bool DGRAD,
-          int MF>
+          int MF, int TPS>
 __global__ __launch_bounds__(64 * WM * WN * WK) void split_conv_kernel(const SplitArgs a) {
   extern __shared__ __attribute__((aligned(16))) char sm_split[];
-  split_conv_body<CPT, CP, N, KS, TY, TX, WM, WN, WK, DGRAD, MF>(a, sm_split, blockIdx.x,
-                                                                blockIdx.y, blockIdx.z);
+  split_conv_body<CPT, CP, N, KS, TY, TX, WM, WN, WK, DGRAD, MF, TPS>(a, sm_split, blockIdx.x,
+                                                                     blockIdx.y, blockIdx.z);
 }
 
 template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, bool DGRAD,
-          int MF = 0>
+          int MF = 0, int TPS = 1>
 inline hipError_t launch_split_conv(SplitArgs a, int nz, hipStream_t st) {
-  using C = SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK, MF>;
-  auto kern = split_conv_kernel<CPT, CP, N, KS, TY, TX, WM, WN, WK, DGRAD, MF>;
+  using C = SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK, MF, TPS>;
+  auto kern = split_conv_kernel<CPT, CP, N, KS, TY, TX, WM, WN, WK, DGRAD, MF, TPS>;
   // conv2's data gradient: room for the fused conv1 weight gradient too
   constexpr bool kW1 = DGRAD && N == 32 && CPT == 64 && C::TN == 1;
   constexpr int kW1B = kW1 ? W1Fuse<kW1 ? TY : 2, kW1 ? TX : 2, C::kThreads>::kSmemB : 0;
