@@ -48,9 +48,23 @@ def kernel_flops(B, S):
     c2 = 2.0 * B * s2 * s2 * 64 * 800
     c3 = 2.0 * B * s3 * s3 * 64 * 576
     fc = 2.0 * B * 512 * k4
+    # conv2_dgrad: conv2's data gradient with conv1's weight gradient fused
+    # into its tiles (split.h w1_tile_wgrad): c2 split + c1 split3 FLOPs
     return {"conv1_fwd": 2 * c1, "conv2_fwd": 2 * c2, "conv3_fwd": 2 * c3, "fc4_fwd": 2 * fc,
-            "fc4_bwd": fc, "conv3_dgrad": c3, "conv23_wgrad": c2 + c3, "conv2_dgrad": c2,
-            "conv1_wgrad": c1}
+            "fc4_bwd": fc, "conv3_dgrad": c3, "conv23_wgrad": c2 + c3, "conv2_dgrad": c2 + c1}
+
+
+def kernel_parts(B, S):
+    """(FLOPs, arithmetic) parts of each MFMA kernel: a fused kernel's ideal
+    time is the sum of its parts at their arithmetic's peak."""
+    s2, s3 = S // 2, S // 4
+    c1 = 2.0 * B * S * S * 32 * 196
+    c2 = 2.0 * B * s2 * s2 * 64 * 800
+    c3 = 2.0 * B * s3 * s3 * 64 * 576
+    return {"conv1_fwd": [(2 * c1, "split3")], "conv2_fwd": [(2 * c2, "split")],
+            "conv3_fwd": [(2 * c3, "split")], "conv3_dgrad": [(c3, "split")],
+            "conv23_wgrad": [(c2 + c3, "split")],
+            "conv2_dgrad": [(c2, "split"), (c1, "split3")]}
 
 
 # rocprof kernel symbol (prefix) of each profiled step kernel
@@ -65,7 +79,6 @@ KERNEL_SYMBOL = {
     "conv3_dgrad": "void ddq::split_conv_kernel<64, 64, 64, 3, 4, 8,",
     "conv23_wgrad": "void ddq::wgrads_pair_kernel",
     "conv2_dgrad": "void ddq::split_conv_kernel<64, 64, 32, 5,",
-    "conv1_wgrad": "void ddq::wgrad1s_kernel",
     "wgrad_reduce": "ddq::wgrad_reduce_kernel",
     "apply": "ddq::apply_kernel",
 }
@@ -76,16 +89,20 @@ KERNEL_SYMBOL = {
 # "f32" = v_mfma_f32_32x32x2_f32 / f32 VALU.  Its roofline peak is the bf16
 # dense peak over the products per f32 product (the f32 MFMA peak for "f32").
 KERNEL_ARITH = {
-    "conv1_fwd": "split3", "conv2_fwd": "split", "conv3_fwd": "split",
-    "conv1_wgrad": "split3", "conv23_wgrad": "split",
-    "conv2_dgrad": "split", "conv3_dgrad": "split", "fc4_fwd": "split", "fc4_bwd": "split",
+    "conv1_fwd": "split3", "conv2_fwd": "split", "conv3_fwd": "split", "conv23_wgrad": "split",
+    "conv2_dgrad": "split+split3", "conv3_dgrad": "split", "fc4_fwd": "split", "fc4_bwd": "split",
 }
 BF16_MFMA_PEAK = 2.5e15       # MI355X_MICROARCH.md: dense bf16
 
 
-def arith_peak(kernel):
-    kind = KERNEL_ARITH.get(kernel, "f32")
+def arith_peak(kernel, kind=None):
+    kind = kind or KERNEL_ARITH.get(kernel, "f32")
     return {"split": BF16_MFMA_PEAK / 6, "split3": BF16_MFMA_PEAK / 3}.get(kind, F32_MFMA_PEAK)
+
+
+def ideal_s(kernel, B, S):
+    """Seconds of a kernel's FLOPs at the peaks of the arithmetic each part runs."""
+    return sum(f / arith_peak(kernel, kind) for f, kind in kernel_parts(B, S)[kernel])
 
 
 def pmc_traffic(label, B, S):
@@ -115,8 +132,8 @@ def step_roofline(B, S, P):
     f32 minibatch write, fc4 weights read by the two forwards and the data
     gradient, rmsprop apply 20 P).  The fraction measured / ideal is the
     step's roofline fraction (SURVEY 8(d) composite, split-aware)."""
-    fl = kernel_flops(B, S)
-    mfma_s = sum(v / arith_peak(k) for k, v in fl.items() if k in KERNEL_ARITH)
+    mfma_s = sum(ideal_s(k, B, S) for k in kernel_parts(B, S)) + \
+        sum(kernel_flops(B, S)[k] / arith_peak(k) for k in ("fc4_fwd", "fc4_bwd"))
     K4 = 64 * (S // 8) ** 2
     gather = 2 * B * 4 * S * S + 2 * B * 4 * S * S * 4 + B * 24
     fc4 = 3 * 512 * K4 * 4
@@ -312,8 +329,10 @@ def kernel_roofline(avg_us, B, S, P):
         elif k in fl:
             tf = fl[k] / (us * 1e-6) / 1e12
             out[k] = {"TFLOPs": round(tf, 2), "arith": KERNEL_ARITH.get(k, "f32"),
-                      "peak": round(arith_peak(k) / 1e12, 1),
-                      "frac": round(tf * 1e12 / arith_peak(k), 3)}
+                      "ideal_us": round(ideal_s(k, B, S) * 1e6, 3),
+                      "frac": round(ideal_s(k, B, S) / (us * 1e-6), 3)}
+            if "+" not in out[k]["arith"]:
+                out[k]["peak"] = round(arith_peak(k) / 1e12, 1)
         elif k == "sample_gather":
             by = 2 * B * 4 * S * S * 5 + B * 24
             out[k] = {"GBps": round(by / (us * 1e-6) / 1e9, 1),
@@ -700,6 +719,8 @@ def main():
     ap.add_argument("--acting", action="store_true",
                     help="also time updates including acting (select_action + add_experience)")
     ap.add_argument("--no-sweep", action="store_true", help="skip the C3 frame sweep")
+    ap.add_argument("--no-isolated", action="store_true",
+                    help="skip the dominant layer's isolated back-to-back timing (profiling runs)")
     ap.add_argument("--no-messaging", action="store_true",
                     help="skip the gradient-message / param-server round-trip costs (N=1)")
     ap.add_argument("--sweep", action="store_true",
@@ -823,10 +844,13 @@ def main():
     # for reference: the same layer launched 100 times back to back on the same
     # cache-warm input (not the roofline figure)
     iso_us = pnet.time_layer(dom, 100) if dom.endswith("_fwd") and dom.startswith("conv") \
-        else None
+        and not args.no_isolated else None
     if pnet is not net:
         pnet.close()
     achieved = flops[dom] / (dom_us * 1e-6) / 1e12
+    # peak of the arithmetic the kernel runs (a fused kernel: its FLOPs over
+    # the ideal time of its parts)
+    dom_peak = flops[dom] / ideal_s(dom, B, S)
     step_flops = net.step_flops()
     step_rl = step_roofline(B, S, net.num_params)
     traffic, traffic_src = pmc_traffic(dom, B, S)
@@ -855,8 +879,8 @@ def main():
                                                      else "+overlap")) if exchanged else "none",
                        "pipelined": bool(args.pipeline and not args.eager)},
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3),
-                         "peak": round(arith_peak(dom) / 1e12, 1), "unit": "TFLOP/s",
-                         "frac": round(achieved * 1e12 / arith_peak(dom), 4),
+                         "peak": round(dom_peak / 1e12, 1), "unit": "TFLOP/s",
+                         "frac": round(achieved * 1e12 / dom_peak, 4),
                          "arith": KERNEL_ARITH.get(dom, "f32"),
                          "peak_basis": "algorithmic f32 FLOPs; peak = bf16 dense 2.5 PF/s over "
                                        "the bf16 products per f32 product (split: 6, split3: "

@@ -1569,10 +1569,9 @@ static const T& pick_tile(const T (&menu)[n], int H, int W) {
 #ifndef DDQ_C2F_WN
 #define DDQ_C2F_WN 2
 #endif
-// conv2 data-gradient launches below this many workgroups run on a second
-// graph branch beside the weight gradients (launch_backward)
-#ifndef DDQ_FORK_WGS
-#define DDQ_FORK_WGS 128
+// A/B: taps per weight-ring step of conv2's 8 x 16 data-gradient tile
+#ifndef DDQ_C2D_TPS
+#define DDQ_C2D_TPS 1
 #endif
 struct SplitMenu {
   TileOpt opt;
@@ -1609,7 +1608,7 @@ static const SplitMenu kConv3Dgrad[] = {
     DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 26, 5, 2, 1, true, 0, 1)};
 // conv2 data gradient (64 -> 32): four k groups on 8 x 16
 static const SplitMenu kConv2Dgrad[] = {
-    DDQ_SPLIT_TILE(64, 64, 32, 5, 8, 16, 4, 1, 4, true, 0, 1),
+    DDQ_SPLIT_TILE(64, 64, 32, 5, 8, 16, 4, 1, 4, true, 0, DDQ_C2D_TPS),
     DDQ_SPLIT_TILE(64, 64, 32, 5, 8, 20, 5, 1, 2, true, 0, 1),
     DDQ_SPLIT_TILE(64, 64, 32, 5, 12, 12, 5, 1, 2, true, 0, 1),
     DDQ_SPLIT_TILE(64, 64, 32, 5, 8, 8, 2, 1, 4, true, 0, DDQ_TPS_SMALL ? 3 : 1)};
@@ -1803,17 +1802,6 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     M("conv3_dgrad");
     CHECK_LAUNCH(pick_tile(kConv3Dgrad, H, H).launch(a, 1, s));
   }
-  // Small maps: conv2's data gradient (+ conv1's weight gradient) runs on a
-  // second graph branch beside the conv2 / conv3 weight gradients -- both need
-  // only conv3's data gradient, and at these sizes each underfills the GPU
-  // (deepq16: 32 workgroups beside ~300).  Eager profiling keeps one stream.
-  const TileOpt& c2dt = pick_tile(kConv2Dgrad, S / 2, S / 2).opt;
-  const int c2d_wgs = ((S / 2 + c2dt.ty - 1) / c2dt.ty) * ((S / 2 + c2dt.tx - 1) / c2dt.tx) * B;
-  const bool fork = nb.side && !mark && c2d_wgs < DDQ_FORK_WGS;
-  if (fork) {
-    CHECK_LAUNCH(hipEventRecord(nb.ev[0], s));
-    CHECK_LAUNCH(hipStreamWaitEvent(nb.side, nb.ev[0], 0));
-  }
   {  // conv3 weight gradient (split bf16, wgrads.h): rows of the expanded split
      // dconv3 (pure copies) against the split pool2; conv2's on the split
      // pooled dpool2 and the split pool1
@@ -1851,11 +1839,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     a.w1_route = nb.mask1; a.w1_in = nb.state;
     a.w1_part = nb.wpart + nb.wpart_off[0]; a.w1_np = nb.wnp[0];
     M("conv2_dgrad");
-    CHECK_LAUNCH(pick_tile(kConv2Dgrad, H, H).launch(a, 1, fork ? nb.side : s));
-  }
-  if (fork) {
-    CHECK_LAUNCH(hipEventRecord(nb.ev[1], nb.side));
-    CHECK_LAUNCH(hipStreamWaitEvent(s, nb.ev[1], 0));
+    CHECK_LAUNCH(pick_tile(kConv2Dgrad, H, H).launch(a, 1, s));
   }
   // slab-reduce geometry: layer l's blocks start at d[l].blk0
   WredDims d[3];

@@ -643,19 +643,78 @@ __device__ __forceinline__ void w1_tile_wgrad(const SplitArgs& a, char* smem,
   const uint32_t slab = (uint32_t)tile * 32u * (uint32_t)a.w1_np;
   const __amdgpu_buffer_rsrc_t rs =
       wt_rsrc(a.w1_part, (uint32_t)((size_t)(slab + 32u * (uint32_t)a.w1_np) * 4));
-  for (int f = tid; f < 7 * 1024; f += NT) {
-    const int ky = f >> 10, e = f & 1023;
-    const int r = e >> 6, l = e & 63;
-    float v = red[((ky * F::NSEG) * 16) * 64 + e];
+  // 16-byte stores of 4 consecutive columns (4-byte write-through stores
+  // cost ~6x the time per byte, MI355X_MICROARCH.md): item = (ky, row r,
+  // half h, columns 4q..4q+3 < 28)
+  for (int f = tid; f < 7 * 16 * 14; f += NT) {
+    const int ky = f / 224, rem = f - ky * 224;
+    const int r = rem / 14, g = rem - r * 14, h2 = g / 7, q = g - h2 * 7;
+    const int e = r * 64 + 32 * h2 + 4 * q;
+    float4 v = *reinterpret_cast<const float4*>(red + ((ky * F::NSEG) * 16) * 64 + e);
 #pragma unroll
-    for (int sg = 1; sg < F::NSEG; ++sg) v += red[((ky * F::NSEG + sg) * 16) * 64 + e];
-    const int co = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), n = l & 31;
-    if (n < 28) wt_store(rs, (slab + (uint32_t)(co * a.w1_np + ky * 28 + n)) * 4, v);
+    for (int sg = 1; sg < F::NSEG; ++sg) {
+      const float4 w = *reinterpret_cast<const float4*>(red + ((ky * F::NSEG + sg) * 16) * 64 + e);
+      v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+    }
+    const int co = (r & 3) + 8 * (r >> 2) + 4 * h2;
+    wt_store4(rs, (slab + (uint32_t)(co * a.w1_np + ky * 28 + 4 * q)) * 4, v);
   }
   if (tid < 32) {   // bias: the lanes of channel tid, waves in order
     float v = 0.f;
     for (int w = 0; w < F::NWV; ++w) v += bsm[w * 64 + tid] + bsm[w * 64 + 32 + tid];
     wt_store(rs, (slab + (uint32_t)(tid * a.w1_np + 196)) * 4, v);
+  }
+}
+
+// Data-gradient epilogue through LDS: the tile's split output (the previous
+// pool output's gradient, NHWC) gathered in LDS in the output's order, then
+// copied out as 16-byte vectors (the accumulator layout gives 2-byte stores,
+// 3 per element, scattered over the planes).  Every wave must have finished
+// reading the patch / ring (the barrier at the top).  LDS: 6 TY TX N bytes.
+template <int TM, int TN, int TX, int TY, int N, int WK, int NWIN, int NT>
+__device__ __forceinline__ void split_epilogue_dgrad_lds(const SplitArgs& a,
+                                                         const f32x16 (&acc)[TM][TN], char* smem,
+                                                         int b, int y0, int x0, int wmi, int wni,
+                                                         int l31, int h, int wkg, int tid) {
+  constexpr int NPX = TY * TX;
+  __bf16* sv = reinterpret_cast<__bf16*>(smem);   // [3][NPX][N]
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int mb = wmi * TM * 32 + 32 * i;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = wni * TN * 32 + 32 * j + l31;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if ((r >> 2) % WK != wkg) continue;
+        const int m = mb + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int win = m >> 2;
+        if (win >= NWIN) continue;                // padding rows
+        const int ty = 2 * (win / (TX / 2)) + ((m >> 1) & 1);
+        const int tx = 2 * (win % (TX / 2)) + (m & 1);
+        __bf16 hh, mm, ll;
+        split3(acc[i][j][r], hh, mm, ll);
+        const int e = (ty * TX + tx) * N + n;
+        sv[e] = hh;
+        sv[NPX * N + e] = mm;
+        sv[2 * NPX * N + e] = ll;
+      }
+    }
+  }
+  __syncthreads();
+  constexpr int VPP = N / 8;                      // 16-byte vectors per pixel and plane
+#pragma unroll
+  for (int p = 0; p < 3; ++p) {
+    __bf16* dst = a.pd_split + p * a.pd_elems;
+    for (int f = tid; f < NPX * VPP; f += NT) {
+      const int px = f / VPP, c = f - px * VPP;
+      const int ty = px / TX, tx = px - ty * TX;
+      const int y = y0 + ty, x = x0 + tx;
+      if (y >= a.H || x >= a.W) continue;
+      *reinterpret_cast<u32x4*>(dst + (((size_t)b * a.H + y) * a.W + x) * N + 8 * c) =
+          *reinterpret_cast<const u32x4*>(sv + (p * NPX + px) * N + 8 * c);
+    }
   }
 }
 
@@ -1046,6 +1105,13 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
       w1_tile_wgrad<TY, TX, C::kThreads, TM, WK, C::NWIN>(a, smem, acc1, w1r, w1h, b,
                                                           by * gridDim.x + bx, wmi, l31, h, wkg,
                                                           tid);
+      return;
+    }
+  }
+  if constexpr (DGRAD && 6 * TY * TX * N <= C::kSmemB) {
+    if (a.pd_split && !a.pd) {
+      split_epilogue_dgrad_lds<TM, TN, TX, TY, N, WK, C::NWIN, C::kThreads>(
+          a, acc, smem, b, y0, x0, wmi, wni, l31, h, wkg, tid);
       return;
     }
   }

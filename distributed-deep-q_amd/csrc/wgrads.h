@@ -84,7 +84,6 @@ __device__ __forceinline__ void wgrads_body(const WgradSArgs& a, char* smem, int
   using Geo = WgradSGeom<CIN, PAD>;
   const int W = a.W, H = a.H;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int l31 = lane & 31, h = lane >> 5;
   const int ipl = Geo::in_plane(W), dpl = Geo::d_plane(W);
   __bf16* rin = reinterpret_cast<__bf16*>(smem) + w * Geo::region(W);   // [3][W+2P+8][PSI]
   __bf16* rd = rin + 3 * ipl;                                            // [3][W][PSD]
@@ -378,13 +377,18 @@ __device__ __forceinline__ void wgrads_body(const WgradSArgs& a, char* smem, int
     for (int r = 0; r < 16; ++r) red[(w * 16 + r) * 64 + lane] = acc[t][r];
     __syncthreads();
     const int nbase = (ky * KS + t / NCB) * CIN + (t % NCB) * 32;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int r = w + 4 * j;                       // element (r, lane) of the tile
-      const int e = r * 64 + lane;
-      const float v = (red[e] + red[1024 + e]) + (red[2048 + e] + red[3072 + e]);
-      const int co = (r & 3) + 8 * (r >> 2) + 4 * h;
-      wt_store(srs, sbase + (uint32_t)((co * a.NP + nbase + l31) * 4), v);
+    {   // thread = (tile row r, lanes 4q..4q+3): 4 consecutive columns, one
+        // 16-byte write-through store (4-byte ones cost ~6x per byte)
+      const int tt = threadIdx.x, r = tt >> 4, l0 = 4 * (tt & 15);
+      const int e = r * 64 + l0;
+      const float4 a0 = *reinterpret_cast<const float4*>(red + e);
+      const float4 a1 = *reinterpret_cast<const float4*>(red + 1024 + e);
+      const float4 a2 = *reinterpret_cast<const float4*>(red + 2048 + e);
+      const float4 a3 = *reinterpret_cast<const float4*>(red + 3072 + e);
+      const float4 v = make_float4((a0.x + a1.x) + (a2.x + a3.x), (a0.y + a1.y) + (a2.y + a3.y),
+                                   (a0.z + a1.z) + (a2.z + a3.z), (a0.w + a1.w) + (a2.w + a3.w));
+      const int co = (r & 3) + 8 * (r >> 2) + 4 * (l0 >> 5);
+      wt_store4(srs, sbase + (uint32_t)((co * a.NP + nbase + (l0 & 31)) * 4), v);
     }
   }
   if (ky == 0) {   // bias column n = KC: lanes with equal lane & 3 share 8 channels
