@@ -1083,10 +1083,6 @@ __device__ __forceinline__ void apply_at(const ApplyTail& t, const ApplyArgs& a,
 // element's sum runs n = 0 .. B-1 in order with fmaf, whatever R, so every
 // caller (the gradient launches and the fused apply) produces the same bits.
 constexpr int kFc4WTileK = 256;
-// A/B: batch rows per round of the fc4 weight-gradient sums' loads
-#ifndef DDQ_FC4W_UNROLL
-#define DDQ_FC4W_UNROLL 4
-#endif
 template <int R>
 __host__ __device__ inline int fc4_wgrad_blocks(int K) {
   return (512 / (4 * R)) * ((K + kFc4WTileK - 1) / kFc4WTileK);
@@ -1111,7 +1107,7 @@ __device__ __forceinline__ void fc4_wgrad_sum(int B, int K, const float* __restr
     for (int e = 0; e < 4; ++e) g[r][e] = 0.f;
   const float* xp = x + k;
   const float* dp = dh4 + o0;
-#pragma unroll DDQ_FC4W_UNROLL
+#pragma unroll 4   // batch rows per round of loads (8 / 16 measured slower)
   for (int n = 0; n < B; ++n) {
     const float4 xv = *reinterpret_cast<const float4*>(xp + (size_t)n * K);
 #pragma unroll
@@ -1537,10 +1533,9 @@ int fc4_splits_for(int S) { return fc4_fwd_splits(64 * (S / 8) * (S / 8)); }
 struct TileOpt {
   int ty, tx, rows;
 };
-template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, int MF = 0,
-          int TPS = 1>
+template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, int MF = 0>
 constexpr TileOpt split_tile() {
-  return {TY, TX, WM * SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK, MF, TPS>::TM * 32};
+  return {TY, TX, WM * SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK, MF>::TM * 32};
 }
 template <int TY, int TX, int WM>
 constexpr TileOpt conv1_tile() { return {TY, TX, WM * Conv1Cfg<TY, TX, WM>::TM * 32}; }
@@ -1560,70 +1555,53 @@ static const T& pick_tile(const T (&menu)[n], int H, int W) {
   return menu[best];
 }
 
-// A/B: the small-map tiles (8 x 8, 4 x 4, 4 x 8) stage 2-3 taps per weight-ring
-// step (SplitCfg TPS: a barrier per 2-3 taps instead of per tap)
-#ifndef DDQ_TPS_SMALL
-#define DDQ_TPS_SMALL 0
-#endif
-// A/B: conv2 forward's 16 x 16 tile as 8 waves of 32 x 64 (1) instead of 16 of 32 x 32 (2)
-#ifndef DDQ_C2F_WN
-#define DDQ_C2F_WN 2
-#endif
-// A/B: taps per weight-ring step of conv2's 8 x 16 data-gradient tile
-#ifndef DDQ_C2D_TPS
-#define DDQ_C2D_TPS 1
-#endif
 struct SplitMenu {
   TileOpt opt;
   hipError_t (*launch)(SplitArgs, int, hipStream_t);
 };
-#define DDQ_SPLIT_TILE(CPT, CP, N, KS, TY, TX, WM, WN, WK, DG, MF, TPS)     \
-  SplitMenu {                                                              \
-    split_tile<CPT, CP, N, KS, TY, TX, WM, WN, WK, MF, TPS>(),             \
-        &launch_split_conv<CPT, CP, N, KS, TY, TX, WM, WN, WK, DG, MF, TPS> \
+#define DDQ_SPLIT_TILE(CPT, CP, N, KS, TY, TX, WM, WN, WK, DG, MF)     \
+  SplitMenu {                                                         \
+    split_tile<CPT, CP, N, KS, TY, TX, WM, WN, WK, MF>(),             \
+        &launch_split_conv<CPT, CP, N, KS, TY, TX, WM, WN, WK, DG, MF> \
   }
 // conv2 forward (32 -> 64, 5x5): 16 waves of one 32x32 block on 16 x 16, on
 // v_mfma_f32_16x16x32_bf16 (MF 1; split.h SplitCfg): 30.1 -> 26.3 us against
 // the 32x32x16 form at 64x64, same-box A/B (the chip holds a higher clock on
 // the 16x16 shape, MI355X_MICROARCH.md DVFS item 7)
 static const SplitMenu kConv2Fwd[] = {
-    DDQ_SPLIT_TILE(32, 32, 64, 5, 16, 16, 8, DDQ_C2F_WN, 1, false, 1, 1),
-    DDQ_SPLIT_TILE(32, 32, 64, 5, 10, 20, 7, 2, 1, false, 1, 1),
-    DDQ_SPLIT_TILE(32, 32, 64, 5, 12, 12, 5, 2, 1, false, 1, 1),
-    DDQ_SPLIT_TILE(32, 32, 64, 5, 8, 8, 2, 2, 1, false, 1, DDQ_TPS_SMALL ? 3 : 1),
-    DDQ_SPLIT_TILE(32, 32, 64, 5, 8, 26, 7, 2, 1, false, 1, 1),
-    DDQ_SPLIT_TILE(32, 32, 64, 5, 14, 14, 7, 2, 1, false, 1, 1)};
+    DDQ_SPLIT_TILE(32, 32, 64, 5, 16, 16, 8, 2, 1, false, 1),
+    DDQ_SPLIT_TILE(32, 32, 64, 5, 10, 20, 7, 2, 1, false, 1),
+    DDQ_SPLIT_TILE(32, 32, 64, 5, 12, 12, 5, 2, 1, false, 1),
+    DDQ_SPLIT_TILE(32, 32, 64, 5, 8, 8, 2, 2, 1, false, 1),
+    DDQ_SPLIT_TILE(32, 32, 64, 5, 8, 26, 7, 2, 1, false, 1),
+    DDQ_SPLIT_TILE(32, 32, 64, 5, 14, 14, 7, 2, 1, false, 1)};
 // conv3 forward (64 -> 64, 3x3): two k groups on 8 x 8
 static const SplitMenu kConv3Fwd[] = {
-    DDQ_SPLIT_TILE(64, 64, 64, 3, 8, 8, 2, 2, 2, false, 1, 1),
-    DDQ_SPLIT_TILE(64, 64, 64, 3, 10, 10, 4, 2, 2, false, 1, 1),
-    DDQ_SPLIT_TILE(64, 64, 64, 3, 12, 12, 5, 2, 1, false, 1, 1),
-    DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 18, 4, 2, 2, false, 1, 1),
-    DDQ_SPLIT_TILE(64, 64, 64, 3, 4, 4, 1, 2, 2, false, 1, DDQ_TPS_SMALL ? 2 : 1),
-    DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 26, 5, 2, 1, false, 0, 1)};   // (MF 1 exceeds LDS)
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 8, 8, 2, 2, 2, false, 1),
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 10, 10, 4, 2, 2, false, 1),
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 12, 12, 5, 2, 1, false, 1),
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 18, 4, 2, 2, false, 1),
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 4, 4, 1, 2, 2, false, 1),
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 26, 5, 2, 1, false, 0)};   // (MF 1 exceeds LDS)
 // conv3 data gradient: four k groups on 4 x 8
 static const SplitMenu kConv3Dgrad[] = {
-    DDQ_SPLIT_TILE(64, 64, 64, 3, 4, 8, 1, 2, 4, true, 0, DDQ_TPS_SMALL ? 2 : 1),
-    DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 10, 2, 2, 4, true, 0, 1),
-    DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 26, 5, 2, 1, true, 0, 1)};
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 4, 8, 1, 2, 4, true, 0),
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 10, 2, 2, 4, true, 0),
+    DDQ_SPLIT_TILE(64, 64, 64, 3, 6, 26, 5, 2, 1, true, 0)};
 // conv2 data gradient (64 -> 32): four k groups on 8 x 16
 static const SplitMenu kConv2Dgrad[] = {
-    DDQ_SPLIT_TILE(64, 64, 32, 5, 8, 16, 4, 1, 4, true, 0, DDQ_C2D_TPS),
-    DDQ_SPLIT_TILE(64, 64, 32, 5, 8, 20, 5, 1, 2, true, 0, 1),
-    DDQ_SPLIT_TILE(64, 64, 32, 5, 12, 12, 5, 1, 2, true, 0, 1),
-    DDQ_SPLIT_TILE(64, 64, 32, 5, 8, 8, 2, 1, 4, true, 0, DDQ_TPS_SMALL ? 3 : 1)};
+    DDQ_SPLIT_TILE(64, 64, 32, 5, 8, 16, 4, 1, 4, true, 0),
+    DDQ_SPLIT_TILE(64, 64, 32, 5, 8, 20, 5, 1, 2, true, 0),
+    DDQ_SPLIT_TILE(64, 64, 32, 5, 12, 12, 5, 1, 2, true, 0),
+    DDQ_SPLIT_TILE(64, 64, 32, 5, 8, 8, 2, 1, 4, true, 0)};
 #undef DDQ_SPLIT_TILE
 
 struct Conv1Menu {
   TileOpt opt;
   hipError_t (*launch)(Conv1Args, int, hipStream_t, int64_t);
 };
-// A/B: conv1 forward on v_mfma_f32_16x16x32_bf16 (split.h split_conv1_kernel MF)
-#ifndef DDQ_C1F_MF
-#define DDQ_C1F_MF 0
-#endif
 #define DDQ_CONV1_TILE(TY, TX, WM) \
-  Conv1Menu { conv1_tile<TY, TX, WM>(), &launch_split_conv1<TY, TX, WM, DDQ_C1F_MF> }
+  Conv1Menu { conv1_tile<TY, TX, WM>(), &launch_split_conv1<TY, TX, WM> }
 static const Conv1Menu kConv1Fwd[] = {DDQ_CONV1_TILE(32, 32, 16), DDQ_CONV1_TILE(20, 20, 13),
                                       DDQ_CONV1_TILE(16, 16, 8), DDQ_CONV1_TILE(24, 24, 9)};
 #undef DDQ_CONV1_TILE

@@ -127,10 +127,7 @@ __device__ __forceinline__ bf16x8 tr_pair(const __bf16* p0, const __bf16* p1) {
 // cycles per FLOP).  MF = 1 reads lane l's 8 channels [8 (l / 16), +8) of row
 // l % 16: pixel and weight-row strides CP + 16 bf16 (6 16-byte units) are
 // conflict-free for it (a bank model of the four 16-lane groups).
-// TPS: taps per weight-ring step (one barrier per TPS taps; small maps, where a
-// step's MFMAs are few and the per-step barrier / latency dominates).
-template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK = 1, int MF = 0,
-          int TPS = 1>
+template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK = 1, int MF = 0>
 struct SplitCfg {
   static constexpr int NCH = CPT / CP;
   static constexpr int PH = TY + KS - 1, PW = TX + KS - 1;
@@ -139,8 +136,6 @@ struct SplitCfg {
   static constexpr int RS = RS0 + ((64 - (RS0 % 128)) + 128) % 128;   // == 64 (mod 128) bf16
   static constexpr int CW = CP + (MF ? 16 : 8);                       // bf16 per weight row
   static constexpr int T = KS * KS;
-  static constexpr int kTPS = TPS;
-  static constexpr int TS = (T + TPS - 1) / TPS;                      // ring steps per chunk
   static constexpr int KSTEP = CP / (MF ? 32 : 16);
   static constexpr int kGroup = 64 * WM * WN * WK;                     // all waves stage
   static constexpr int kThreads = kGroup;
@@ -155,7 +150,7 @@ struct SplitCfg {
   static constexpr int kPlane = PH * RS;                              // bf16 per patch plane
   static constexpr int kWSlot = N * CW;                               // bf16 per weight plane
   static constexpr int kPatchB = 3 * kPlane * 2;
-  static constexpr int kWB = 2 * TPS * 3 * kWSlot * 2;                // two-slot ring
+  static constexpr int kWB = 2 * 3 * kWSlot * 2;                      // two-slot ring
   static constexpr int kSmemB = kPatchB + kWB;
   static_assert(CPT % CP == 0 && CP % 16 == 0 && TY % 2 == 0 && TX % 2 == 0, "shape");
   static_assert(TM >= 1 && TN >= 1 && (WM * TM - 1) * 8 < NWIN && N == WN * TN * 32, "wave tile");
@@ -176,7 +171,7 @@ struct SplitCfg {
 template <class C, int CPT, int CP, int N>
 struct SplitWStage {
   static constexpr int WV = N * CP / 8;                         // 16-byte vectors per plane
-  static constexpr int NVS = 3 * WV * C::kTPS;                   // vectors per ring step
+  static constexpr int NVS = 3 * WV;                             // vectors per ring step
   static constexpr int kPer = (NVS + C::kGroup - 1) / C::kGroup;
   static_assert(kPer <= 12, "weight staging registers");
   u32x4 r[kPer];
@@ -192,15 +187,13 @@ struct SplitWStage {
     return (n0 & ~7) | ((n0 & 7) >> 1) | ((n0 & 1) << 2);
   }
 
-  // the TPS taps tg * TPS + i of chunk ch (taps past T read tap T - 1: unused)
-  __device__ __forceinline__ void load(const __bf16* __restrict__ wk, int64_t E, int ch, int tg,
+  // tap t of chunk ch
+  __device__ __forceinline__ void load(const __bf16* __restrict__ wk, int64_t E, int ch, int t,
                                        int tid) {
 #pragma unroll
     for (int S = 0; S < kPer; ++S) {   // clamped, unconditional: the store drops extra lanes
       const int f0 = tid + S * C::kGroup;
-      const int f1 = NVS % C::kGroup == 0 || f0 < NVS ? f0 : NVS - 1;
-      const int ti = f1 / (3 * WV), f = f1 - ti * (3 * WV);
-      const int t0 = tg * C::kTPS + ti, t = t0 < C::T ? t0 : C::T - 1;
+      const int f = NVS % C::kGroup == 0 || f0 < NVS ? f0 : NVS - 1;
       const int p = f / WV, q = f - p * WV;
       const int n = row(q), c8 = q % (CP / 8);
       r[S] = *reinterpret_cast<const u32x4*>(wk + p * E + ((size_t)n * C::T + t) * CPT + ch * CP +
@@ -214,11 +207,10 @@ struct SplitWStage {
       // lanes past the vectors store nothing (whole waves at these sizes:
       // a uniform branch); they used to rewrite the last vector
       if (NVS % C::kGroup != 0 && f0 >= NVS) continue;
-      const int f1 = NVS % C::kGroup == 0 || f0 < NVS ? f0 : NVS - 1;
-      const int ti = f1 / (3 * WV), f = f1 - ti * (3 * WV);
+      const int f = NVS % C::kGroup == 0 || f0 < NVS ? f0 : NVS - 1;
       const int p = f / WV, q = f - p * WV;
       const int n = row(q), c8 = q % (CP / 8);
-      *reinterpret_cast<u32x4*>(dst + (ti * 3 + p) * C::kWSlot + n * C::CW + 8 * c8) = r[S];
+      *reinterpret_cast<u32x4*>(dst + p * C::kWSlot + n * C::CW + 8 * c8) = r[S];
     }
   }
 };
@@ -719,10 +711,10 @@ __device__ __forceinline__ void split_epilogue_dgrad_lds(const SplitArgs& a,
 }
 
 template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, bool DGRAD,
-          int MF = 0, int TPS = 1>
+          int MF = 0>
 __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, int bx, int by,
                                                 int bz) {
-  using C = SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK, MF, TPS>;
+  using C = SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK, MF>;
   static_assert(MF == 0 || !DGRAD, "16x16x32: forward convolutions only");
   constexpr int TM = C::TM, TN = C::TN, T = C::T, NCH = C::NCH;
   __bf16* patch = reinterpret_cast<__bf16*>(smem);
@@ -884,12 +876,11 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
   // ---- weights: step s = (chunk s / T, tap s % T) -> ring slot s & 1 ----
   // Two register sets: the loads of step s+2 are issued at the start of step
   // s and stored at the end of step s+1 (two steps of MFMAs to land in).
-  constexpr int TS = C::TS;
-  constexpr int NSTEP = NCH * TS;
+  constexpr int NSTEP = NCH * T;
   SplitWStage<C, CPT, CP, N> ws0, ws1;
   auto wload = [&](SplitWStage<C, CPT, CP, N>& w, int st) {
     const int sc = st < NSTEP ? st : NSTEP - 1;
-    w.load(wk, a.wk_elems, sc / TS, sc % TS, tid);
+    w.load(wk, a.wk_elems, sc / T, sc % T, tid);
   };
   stage_patch(0);
   wload(ws0, 0);
@@ -961,11 +952,8 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
 
   // one step: the MFMAs of tap t of the resident chunk on ring slot `slot`
   auto tap_step = [&](int s, int slot) {
-#pragma unroll
-    for (int ti = 0; ti < TPS; ++ti) {
-    const int t = (s % TS) * TPS + ti;
-    if (TPS > 1 && t >= T) break;                   // (wave-uniform)
-    const __bf16* wb = wbuf + (slot * TPS + ti) * 3 * C::kWSlot;
+    const int t = s % T;
+    const __bf16* wb = wbuf + slot * 3 * C::kWSlot;
     const int ky = t / KS, kx = t % KS;
     const __bf16* pa = patch + ky * C::RS + kx * C::CS;
 #pragma unroll
@@ -1006,7 +994,6 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
           }
       }
     }
-    }
   };
   // end of step s: store step s+1's weights, restage the patch at a chunk
   // boundary (the barrier before fences every wave's reads of the old chunk)
@@ -1015,12 +1002,12 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
     // hoists them above: every wave then waited for all its LDS reads and the
     // barrier before its first MFMA of the step)
     __builtin_amdgcn_sched_barrier(0);
-    const bool chunk_edge = NCH > 1 && (s + 1) % TS == 0;
+    const bool chunk_edge = NCH > 1 && (s + 1) % T == 0;
     if (chunk_edge) {
       __syncthreads();
-      stage_patch((s + 1) / TS);
+      stage_patch((s + 1) / T);
     }
-    w.store(wbuf + ((s + 1) & 1) * TPS * 3 * C::kWSlot, tid);
+    w.store(wbuf + ((s + 1) & 1) * 3 * C::kWSlot, tid);
     __syncthreads();
   };
   for (int s = 0; s < NSTEP; s += 2) {
@@ -1121,18 +1108,18 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
 }
 
 template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, bool DGRAD,
-          int MF, int TPS>
+          int MF>
 __global__ __launch_bounds__(64 * WM * WN * WK) void split_conv_kernel(const SplitArgs a) {
   extern __shared__ __attribute__((aligned(16))) char sm_split[];
-  split_conv_body<CPT, CP, N, KS, TY, TX, WM, WN, WK, DGRAD, MF, TPS>(a, sm_split, blockIdx.x,
+  split_conv_body<CPT, CP, N, KS, TY, TX, WM, WN, WK, DGRAD, MF>(a, sm_split, blockIdx.x,
                                                                      blockIdx.y, blockIdx.z);
 }
 
 template <int CPT, int CP, int N, int KS, int TY, int TX, int WM, int WN, int WK, bool DGRAD,
-          int MF = 0, int TPS = 1>
+          int MF = 0>
 inline hipError_t launch_split_conv(SplitArgs a, int nz, hipStream_t st) {
-  using C = SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK, MF, TPS>;
-  auto kern = split_conv_kernel<CPT, CP, N, KS, TY, TX, WM, WN, WK, DGRAD, MF, TPS>;
+  using C = SplitCfg<CPT, CP, N, KS, TY, TX, WM, WN, WK, MF>;
+  auto kern = split_conv_kernel<CPT, CP, N, KS, TY, TX, WM, WN, WK, DGRAD, MF>;
   // conv2's data gradient: room for the fused conv1 weight gradient too
   constexpr bool kW1 = DGRAD && N == 32 && CPT == 64 && C::TN == 1;
   constexpr int kW1B = kW1 ? W1Fuse<kW1 ? TY : 2, kW1 ? TX : 2, C::kThreads>::kSmemB : 0;
@@ -1191,10 +1178,9 @@ struct Conv1Cfg {
   static_assert(kSmemB <= 160 * 1024, "LDS");
 };
 
-// MF 1: v_mfma_f32_16x16x32_bf16 -- one k-step per tap row (kx 0..7 x 4
-// channels: lane k-group g reads taps 2g, 2g + 1), the wave's 32-row blocks as
-// 16 x 16 blocks (split_conv_body's MF 1 element layout)
-template <int TY, int TX, int WM, int MF>
+// (A v_mfma_f32_16x16x32_bf16 form -- one k-step per tap row -- measured no
+// faster here: conv1's MFMAs are 3 per tap row, not what bounds it.)
+template <int TY, int TX, int WM>
 __global__ __launch_bounds__(64 * WM) void split_conv1_kernel(const Conv1Args a) {
   using C = Conv1Cfg<TY, TX, WM>;
   constexpr int TM = C::TM;
@@ -1209,8 +1195,7 @@ __global__ __launch_bounds__(64 * WM) void split_conv1_kernel(const Conv1Args a)
   const __bf16* __restrict__ wk = z ? a.wk[1] : a.wk[0];
   constexpr int kThreads = 64 * WM;
   const float* bz_ = z ? a.bias[1] : a.bias[0];   // the epilogue's biases, early
-  const float bias_pre = bz_[MF ? (lane & 15) : (lane & 31)];
-  const float bias_pre2 = MF ? bz_[16 + (lane & 15)] : 0.f;
+  const float bias_pre = bz_[lane & 31];
   // patch: one pixel (4 channels) per item, fp32 -> bf16 (exact), loads first
   {
     constexpr int NP = C::PH * C::PW;
@@ -1257,64 +1242,6 @@ __global__ __launch_bounds__(64 * WM) void split_conv1_kernel(const Conv1Args a)
   __syncthreads();
   const int l31 = lane & 31, h = lane >> 5;
   f32x16 acc[TM][1];
-  if constexpr (MF) {
-    typedef float f32x4 __attribute__((ext_vector_type(4)));
-    const int kg = lane >> 4;
-    int abase[2 * TM];
-#pragma unroll
-    for (int q = 0; q < 2 * TM; ++q) {
-      const int m = wid * TM * 32 + 16 * q + (lane & 15);
-      const int win = (m >> 2) < C::NWIN ? m >> 2 : 0, dy = (m >> 1) & 1, dx = m & 1;
-      const int wy = win / (TX / 2), wx = win % (TX / 2);
-      abase[q] = (2 * wy + dy) * C::RS + (2 * wx + dx + 2 * kg) * 4;
-    }
-    int bbase[2];
-#pragma unroll
-    for (int bj = 0; bj < 2; ++bj) bbase[bj] = (16 * bj + (lane & 15)) * C::CW + 8 * kg;
-    f32x4 a4[2 * TM][2], c4[2 * TM][2];
-#pragma unroll
-    for (int q = 0; q < 2 * TM; ++q)
-#pragma unroll
-      for (int bj = 0; bj < 2; ++bj)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) { a4[q][bj][r] = 0.f; c4[q][bj][r] = 0.f; }
-#pragma unroll
-    for (int ky = 0; ky < 7; ++ky) {
-      bf16x8 bv[2][3];
-#pragma unroll
-      for (int bj = 0; bj < 2; ++bj)
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-          bv[bj][p] = *reinterpret_cast<const bf16x8*>(wbuf + p * 32 * C::CW + bbase[bj] + ky * 32);
-#pragma unroll
-      for (int q = 0; q < 2 * TM; ++q) {
-        const __bf16* pa = patch + abase[q] + ky * C::RS;
-        typedef __attribute__((address_space(3))) const u32x2 lds_u2;
-        typedef __attribute__((address_space(3))) const char lds_c;
-        lds_u2* la = (lds_u2*)pa;
-        uint32_t hi_off = 8;                       // separate ds_read_b64 (8-byte aligned pixels)
-        asm volatile("" : "+v"(hi_off));
-        const u32x2 lo = *la;
-        const u32x2 hi = *(lds_u2*)((lds_c*)la + hi_off);
-        u32x4 av4 = {lo[0], lo[1], hi[0], hi[1]};
-        const bf16x8 av = *reinterpret_cast<bf16x8*>(&av4);
-#pragma unroll
-        for (int bj = 0; bj < 2; ++bj) {
-          c4[q][bj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv[bj][2], c4[q][bj], 0, 0, 0);
-          c4[q][bj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv[bj][1], c4[q][bj], 0, 0, 0);
-          a4[q][bj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv[bj][0], a4[q][bj], 0, 0, 0);
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x4 v = a4[2 * i + (g >> 1)][g & 1] + c4[2 * i + (g >> 1)][g & 1];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][0][4 * g + r] = v[r];
-      }
-  } else {
   int abase[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -1361,10 +1288,7 @@ __global__ __launch_bounds__(64 * WM) void split_conv1_kernel(const Conv1Args a)
   }
 #pragma unroll
   for (int i = 0; i < TM; ++i) acc[i][0] += cor[i];
-  }
-  float bpre[MF ? 2 : 1];
-  bpre[0] = bias_pre;
-  if constexpr (MF) bpre[MF] = bias_pre2;
+  const float bpre[1] = {bias_pre};
   SplitArgs e{};
   e.B = a.B; e.H = a.H; e.W = a.W;
   e.out[0] = a.out[0]; e.out[1] = a.out[1];
@@ -1372,19 +1296,18 @@ __global__ __launch_bounds__(64 * WM) void split_conv1_kernel(const Conv1Args a)
   e.out_elems = a.out_elems;
   e.mask[0] = a.mask[0]; e.mask[1] = a.mask[1];
   if constexpr (C::NWIN * 32 * 7 <= C::kSmemB)
-    split_epilogue_fwd_lds<TM, 1, TX, 32, 1, C::NWIN, 64 * WM, MF>(e, acc, bpre, sm_c1, b, z, y0,
-                                                                   x0, wid, 0, l31, h, 0, tid);
-  else if constexpr (!MF)
+    split_epilogue_fwd_lds<TM, 1, TX, 32, 1, C::NWIN, 64 * WM>(e, acc, bpre, sm_c1, b, z, y0, x0,
+                                                               wid, 0, l31, h, 0, tid);
+  else
     split_epilogue<TM, 1, TX, 32, false, 1, C::NWIN>(e, acc, bpre, b, z, y0, x0, wid, 0, l31, h);
-  static_assert(!MF || C::NWIN * 32 * 7 <= C::kSmemB, "16x16x32: the LDS epilogue");
 }
 
-template <int TY, int TX, int WM, int MF>
+template <int TY, int TX, int WM>
 inline hipError_t launch_split_conv1(Conv1Args a, int nz, hipStream_t st, int64_t wk_elems) {
   a.wk_elems = wk_elems;
   if ((a.out[0] && a.out_split[0]) || (a.out[1] && a.out_split[1])) return hipErrorInvalidValue;
   using C = Conv1Cfg<TY, TX, WM>;
-  auto kern = split_conv1_kernel<TY, TX, WM, MF>;
+  auto kern = split_conv1_kernel<TY, TX, WM>;
   static std::atomic<uint64_t> attr{0};
   if (hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(kern), attr, (int)(C::kSmemB)))
     return e;

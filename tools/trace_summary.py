@@ -30,7 +30,7 @@ def main():
     per = collections.defaultdict(list)
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
-        m = re.search(r"split_conv_kernel<(\d+), \d+, (\d+), (\d+),.*(true|false)(, \d+)?>", name)
+        m = re.search(r"split_conv_kernel<(\d+), \d+, (\d+), (\d+),.*(true|false)(, \d+)*>", name)
         if m:
             short = SPLIT.get((int(m.group(1)), int(m.group(2)), int(m.group(3)), m.group(4)))
             if short:
