@@ -1,11 +1,12 @@
 # A/B of variant libraries (distributed-deep-q_amd/ab/<name>/libddq_hip.so,
 # make variant): a parity subset on each variant first, then the bench main
 # line and a rocprofv3 kernel trace of the step for the product and each
-# variant.  Usage: [FRAME=16] bash tools/gpu/run_ab.sh name1 [name2 ...]
+# variant.  Usage: [FRAME=16] [STEPS=n] [NOPARITY=1] bash tools/gpu/run_ab.sh name1 [name2 ...]
 set -e
 mkdir -p gpurun_out/ab
 R=$GRAFT_REPO_ROOT
 for V in "$@"; do
+  [ -n "$NOPARITY" ] && break   # (a variant already tested: e.g. the previous product)
   LIBV=$R/distributed-deep-q_amd/ab/$V/libddq_hip.so
   DDQ_LIB_PATH=$LIBV timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "full_pass_parity and (64-32 or 16-32 or 40-4 or 24-8 or 72-4 or 96-4 or 128-2)" > gpurun_out/ab/parity_$V.log 2>&1 || { echo VARIANT_PARITY_FAILED $V; tail -30 gpurun_out/ab/parity_$V.log; exit 1; }
   echo "[$V] $(tail -1 gpurun_out/ab/parity_$V.log)"
