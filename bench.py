@@ -726,6 +726,9 @@ def main():
     ap.add_argument("--sweep", action="store_true",
                     help="C3: also run the batch-256 frame-size sweep 16..128 (slow)")
     ap.add_argument("--eager", action="store_true", help="no hipGraph (debug)")
+    ap.add_argument("--no-grad-store", action="store_true",
+                    help="exchange-free steps do not store fc4's weight gradient "
+                         "(DDQ_STEP_NO_GRAD_STORE; the update is unchanged)")
     ap.add_argument("--exchange", default="allreduce",
                     choices=["allreduce", "sharded", "server", "async"],
                     help="N>1 gradient exchange (include/ddq_hip.h enum ddq_exchange)")
@@ -761,9 +764,13 @@ def main():
         ddist.setup_comm(net, 0, 1)
         args.exchange = args.force_exchange
     exchanged = world > 1 or bool(args.force_exchange)
+    # --no-grad-store: exchange-free steps do not store fc4's weight gradient
+    # (include/ddq_hip.h DDQ_STEP_NO_GRAD_STORE: the update is the same, bit
+    # for bit, tests/test_gpu_parity.py)
     cfg = net.step_cfg(args.rule, lr=1e-4, target_period=10,
                        exchange=args.exchange if exchanged else "none",
-                       overlap=not args.no_overlap, seed=ddist.index_seed(1234, rank))
+                       overlap=not args.no_overlap, seed=ddist.index_seed(1234, rank),
+                       store_grads=not args.no_grad_store)
 
     ticket = None
     if exchanged and args.exchange == "async" and args.async_order == "ticket":
@@ -832,7 +839,8 @@ def main():
     if exchanged and args.exchange == "async":   # an async ctx runs async steps only
         pnet = make_net(B, S, args.replay, local, rank)
     pcfg = cfg if not (exchanged and args.exchange == "async") else \
-        pnet.step_cfg(args.rule, lr=1e-4, target_period=10, exchange="none", seed=1234)
+        pnet.step_cfg(args.rule, lr=1e-4, target_period=10, exchange="none", seed=1234,
+                      store_grads=not args.no_grad_store)
     prof = {}
     for _ in range(max(1, args.profile_steps)):
         for name, us in pnet.profile_step(pcfg):
@@ -877,7 +885,10 @@ def main():
                        "exchange": (args.exchange + ("" if args.no_overlap or
                                                      args.exchange != "allreduce"
                                                      else "+overlap")) if exchanged else "none",
-                       "pipelined": bool(args.pipeline and not args.eager)},
+                       "pipelined": bool(args.pipeline and not args.eager),
+                       "grad_store": "fc4 weight gradient stored" if not args.no_grad_store or exchanged
+                                     else "fc4 weight gradient applied, not stored "
+                                          "(DDQ_STEP_NO_GRAD_STORE)"},
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3),
                          "peak": round(dom_peak / 1e12, 1), "unit": "TFLOP/s",
                          "frac": round(achieved * 1e12 / dom_peak, 4),

@@ -1132,6 +1132,7 @@ static int enqueue_train(ddq_ctx* c, const ddq_step_cfg* cfg, const NetBuffers& 
     const ddq_update_cfg& u = cfg->update;
     nb.fa.on = 1;
     nb.fa.ext = ar_overlap ? 1 : 0;
+    nb.fa.store_grad = ar_overlap || !(cfg->flags & DDQ_STEP_NO_GRAD_STORE);
     nb.fc4_wait = ar_overlap ? c->cev[2] : nullptr;
     nb.fa.rule = u.rule;
     nb.fa.period = cfg->target_period > 0 ? cfg->target_period : 0;
@@ -1211,6 +1212,8 @@ static int check_step(ddq_ctx* c, const ddq_step_cfg* cfg) {
                 c->nb.B, (long long)c->valid);
   if (cfg->exchange < DDQ_EXCHANGE_NONE || cfg->exchange > DDQ_EXCHANGE_ASYNC)
     return fail(c, DDQ_EINVAL, "unknown exchange %d", cfg->exchange);
+  if (cfg->flags & ~DDQ_STEP_NO_GRAD_STORE)
+    return fail(c, DDQ_EINVAL, "unknown step flags 0x%x", (unsigned)cfg->flags);
   if (cfg->exchange != DDQ_EXCHANGE_NONE && c->nranks > 1 && !c->comm && !c->local)
     return fail(c, DDQ_ESTATE, "no communicator");
   return DDQ_OK;

@@ -41,6 +41,7 @@ struct ReplayMeta {
 // after their (small) all-reduce.
 struct FusedApplyCfg {
   int on, ext;
+  int store_grad;             // fc4's weight gradient also to the gradient buffer
   int rule, period;
   float lr, decay, eps, momentum, wd;
 };

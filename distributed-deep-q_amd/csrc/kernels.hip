@@ -857,6 +857,7 @@ struct ApplyTail {
   int ext;                   // slab reduce: fc4's weight gradient is in grad already
                              // (computed by fc4_bwd, summed over the ranks under the
                              // conv backward): apply from it instead of computing it
+  int store_grad;            // fused apply: also store fc4's computed weight gradient
   int64_t w5_off, b5_off, b4_off;
 };
 
@@ -1161,7 +1162,7 @@ __device__ __forceinline__ void fc4_apply_tile(const ApplyTail& t, const ApplyAr
   for (int r = 0; r < R; ++r) {
     const int64_t i = i0 + (int64_t)r * K;
     const uint32_t ib = (uint32_t)(i * 4);
-    if (!t.ext) wt_store4(rg, ib, make_float4(g[r][0], g[r][1], g[r][2], g[r][3]));
+    if (!t.ext && t.store_grad) wt_store4(rg, ib, make_float4(g[r][0], g[r][1], g[r][2], g[r][3]));
     float th[4] = {t4[r].x, t4[r].y, t4[r].z, t4[r].w};
     float st[4] = {s4[r].x, s4[r].y, s4[r].z, s4[r].w};
 #pragma unroll
@@ -1441,6 +1442,7 @@ static ApplyTail apply_tail(const NetBuffers& nb) {
   t.theta = nb.theta[0]; t.grad = nb.grad; t.opt = nb.opt; t.opt_init = nb.opt_init;
   t.thetaP = nb.theta[1]; t.wks = nb.wks[0]; t.wksP = nb.wks[1]; t.wks_plane = nb.L.wks_total;
   t.w5_off = nb.L.w[4]; t.b5_off = nb.L.b[4]; t.b4_off = nb.L.b[3];
+  t.store_grad = 1;
   return t;
 }
 
@@ -1572,7 +1574,11 @@ static const SplitMenu kConv2Fwd[] = {
     DDQ_SPLIT_TILE(32, 32, 64, 5, 16, 16, 8, 2, 1, false, 1),
     DDQ_SPLIT_TILE(32, 32, 64, 5, 10, 20, 7, 2, 1, false, 1),
     DDQ_SPLIT_TILE(32, 32, 64, 5, 12, 12, 5, 2, 1, false, 1),
+#ifdef DDQ_C2F_SMALL_WK2
+    DDQ_SPLIT_TILE(32, 32, 64, 5, 8, 8, 2, 2, 2, false, 0),
+#else
     DDQ_SPLIT_TILE(32, 32, 64, 5, 8, 8, 2, 2, 1, false, 1),
+#endif
     DDQ_SPLIT_TILE(32, 32, 64, 5, 8, 26, 7, 2, 1, false, 1),
     DDQ_SPLIT_TILE(32, 32, 64, 5, 14, 14, 7, 2, 1, false, 1)};
 // conv3 forward (64 -> 64, 3x3): two k groups on 8 x 8
@@ -1682,7 +1688,11 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     c1.out_elems = (int64_t)B * (S / 2) * (S / 2) * 32;
     c1.mask[0] = nb.mask1; c1.mask[1] = nullptr;
     M("conv1_fwd");
-    CHECK_LAUNCH(pick_tile(kConv1Fwd, S, S).launch(c1, nz, s, L.wks_total));
+#ifndef DDQ_C1_FORCE
+#define DDQ_C1_FORCE -1
+#endif
+    CHECK_LAUNCH((DDQ_C1_FORCE >= 0 ? kConv1Fwd[DDQ_C1_FORCE] : pick_tile(kConv1Fwd, S, S))
+                     .launch(c1, nz, s, L.wks_total));
   }
   if (!nb.fwd_only || nb.fwd_only == 2) {
     // conv2 (train_val.prototxt:79-118): split bf16, 16x16 tiles, 16 waves of
@@ -1816,6 +1826,9 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     a.in_route = nb.mask2;
     a.w1_route = nb.mask1; a.w1_in = nb.state;
     a.w1_part = nb.wpart + nb.wpart_off[0]; a.w1_np = nb.wnp[0];
+#ifdef DDQ_TIMING_NOW1
+    a.w1_part = nullptr;   // timing-only A/B: conv2's data gradient without conv1's (wrong results)
+#endif
     M("conv2_dgrad");
     CHECK_LAUNCH(pick_tile(kConv2Dgrad, H, H).launch(a, 1, s));
   }
@@ -1848,6 +1861,7 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
       nfa = fc4_wgrad_blocks<kFc4ApplyR>(64 * s4 * s4);
       fat.nfa = nfa;
       fat.ext = nb.fa.ext;
+      fat.store_grad = nb.fa.store_grad;
       // and everything else where its gradient is reduced -- unless the rest
       // must be summed over the ranks first (ext: apply launch after that)
       fat.rest = !nb.fa.ext;

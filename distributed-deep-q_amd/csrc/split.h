@@ -457,6 +457,11 @@ __device__ __forceinline__ void split_epilogue_fwd_lds(const SplitArgs& a,
 // exact frame) per conv1 row of the tile; a unit's sums over the segments
 // meet in LDS in fixed order.
 // ---------------------------------------------------------------------------
+#ifdef DDQ_W1_ZF
+constexpr bool kW1ZF = true;
+#else
+constexpr bool kW1ZF = false;
+#endif
 template <int TY, int TX, int NT>
 struct W1Fuse {
   static constexpr int R = 2 * TY;                  // conv1 rows of the tile
@@ -501,23 +506,29 @@ __device__ __forceinline__ void w1_halo_load(const SplitArgs& a, int b, int y0, 
 
 // The routing bytes of the lane's epilogue elements (split_epilogue's DGRAD
 // enumeration; 4 = nothing routed, also outside the image / tile).
+// Bounds-checked byte buffer loads, all issued before the first use: an
+// element outside the tile / image gets an out-of-range offset (reads 0) and
+// its byte is replaced by 4 after the load -- no branch per element.
 template <int TM, int TN, int TX, int WK, int NWIN>
 __device__ __forceinline__ void w1_route_load(const SplitArgs& a, int b, int y0, int x0, int wmi,
                                               int l31, int h, int wkg, uint8_t (&rt)[TM][16]) {
+  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.w1_route, (short)0, (int)(a.B * a.H * a.W * 32), 0x00020000);
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int mb = wmi * TM * 32 + 32 * i;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       rt[i][r] = 4;
-      if ((r >> 2) % WK != wkg) continue;
+      if ((r >> 2) % WK != wkg) continue;           // (wave-uniform)
       const int m = mb + (r & 3) + 8 * (r >> 2) + 4 * h;
       const int win = m >> 2;
-      if (win >= NWIN) continue;
       const int y = y0 + 2 * (win / (TX / 2)) + ((m >> 1) & 1);
       const int x = x0 + 2 * (win % (TX / 2)) + (m & 1);
-      if (y >= a.H || x >= a.W) continue;
-      rt[i][r] = a.w1_route[(((size_t)b * a.H + y) * a.W + x) * 32 + l31];
+      const bool ok = win < NWIN && y < a.H && x < a.W;
+      const uint32_t off = ok ? (uint32_t)(((b * a.H + y) * a.W + x) * 32 + l31) : 0x80000000u;
+      const uint8_t v = __builtin_amdgcn_raw_buffer_load_b8(rr, (int)off, 0, 0);
+      rt[i][r] = ok ? v : (uint8_t)4;
     }
   }
 }
@@ -539,6 +550,12 @@ __device__ __forceinline__ void w1_tile_wgrad(const SplitArgs& a, char* smem,
   float* bsm = reinterpret_cast<float*>(smem + (F::kXB + F::kHaloB > F::kRedB
                                                     ? F::kXB + F::kHaloB : F::kRedB));
   __syncthreads();   // every wave's reads of the k-group sums (smem) are done
+#ifdef DDQ_W1_ZF
+  // zero the expanded image with 16-byte stores, then each element to its
+  // routed quadrant only
+  for (int f = tid; f < 3 * F::XPL / 8; f += NT) reinterpret_cast<u32x4*>(X)[f] = u32x4{0u, 0u, 0u, 0u};
+  __syncthreads();
+#endif
   // ---- scatter: each element's value to its routed quadrant, 0 to the others ----
   float bsum = 0.f;
 #pragma unroll
@@ -557,6 +574,14 @@ __device__ __forceinline__ void w1_tile_wgrad(const SplitArgs& a, char* smem,
       bsum += v;
       __bf16 s0, s1, s2;
       split3(v, s0, s1, s2);
+#ifdef DDQ_W1_ZF
+      if (q < 4) {
+        const int e = ((2 * ty + (q >> 1)) * F::XW + 2 * tx + (q & 1)) * F::PSD + l31;
+        X[e] = s0;
+        X[F::XPL + e] = s1;
+        X[2 * F::XPL + e] = s2;
+      }
+#else
       const __bf16 zero = (__bf16)0.f;
 #pragma unroll
       for (int qq = 0; qq < 4; ++qq) {
@@ -566,10 +591,11 @@ __device__ __forceinline__ void w1_tile_wgrad(const SplitArgs& a, char* smem,
         X[F::XPL + e] = on ? s1 : zero;
         X[2 * F::XPL + e] = on ? s2 : zero;
       }
+#endif
     }
   }
   // the rows' padding pixels (2 TX .. XW) stay zero
-  if constexpr (F::XW > 2 * TX) {
+  if constexpr (F::XW > 2 * TX && !kW1ZF) {
     constexpr int PADV = (F::XW - 2 * TX) * (F::PSD / 8);   // 16-byte vectors per row and plane
     for (int f = tid; f < 3 * F::R * PADV; f += NT) {
       const int pr = f / PADV, c = f - pr * PADV;            // (plane, row), vector

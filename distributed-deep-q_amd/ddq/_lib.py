@@ -48,8 +48,10 @@ class UpdateCfg(ctypes.Structure):
 class StepCfg(ctypes.Structure):
     _fields_ = [("update", UpdateCfg), ("target_period", ctypes.c_int32),
                 ("exchange", ctypes.c_int32), ("seed", ctypes.c_uint64),
-                ("overlap", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("overlap", ctypes.c_int32), ("flags", ctypes.c_int32)]
 
+
+STEP_NO_GRAD_STORE = 1     # include/ddq_hip.h DDQ_STEP_NO_GRAD_STORE
 
 ABI_VERSION = 4
 EXCHANGES = {"none": 0, "allreduce": 1, "sharded": 2, "server": 3, "async": 4}

@@ -331,14 +331,17 @@ class DeepQNet:
 
     # -------------------------------------------------------------------- step
     def step_cfg(self, rule="rmsprop", lr=1e-4, target_period=10, allreduce=False, seed=0,
-                 exchange=None, overlap=False, **kw):
+                 exchange=None, overlap=False, store_grads=True, **kw):
         """exchange: "none" | "allreduce" | "sharded" | "server" | "async" (include/ddq_hip.h
-        enum ddq_exchange); allreduce=True is shorthand for "allreduce"."""
+        enum ddq_exchange); allreduce=True is shorthand for "allreduce".
+        store_grads=False: exchange-free steps do not store fc4's weight gradient
+        (DDQ_STEP_NO_GRAD_STORE; the update is the same, bit for bit)."""
         if exchange is None:
             exchange = "allreduce" if allreduce else "none"
         ex = _lib.EXCHANGES[exchange] if isinstance(exchange, str) else int(exchange)
+        flags = 0 if store_grads else _lib.STEP_NO_GRAD_STORE
         return _lib.StepCfg(_lib.update_cfg(rule, lr, **kw), int(target_period), ex, int(seed),
-                            int(bool(overlap)), 0)
+                            int(bool(overlap)), flags)
 
     def step(self, cfg):
         self._check(self.lib.ddq_step_async(self.ctx, ctypes.byref(cfg)))

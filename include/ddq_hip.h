@@ -132,8 +132,16 @@ typedef struct ddq_step_cfg {
   uint64_t seed;           /* device index-stream seed (per rank)            */
   int32_t overlap;         /* ALLREDUCE over RCCL: reduce the fc4 weight
                               bucket on a comm stream under the conv backward */
-  int32_t reserved;        /* 0 */
+  int32_t flags;           /* DDQ_STEP_* bits, 0 = none                      */
 } ddq_step_cfg;
+
+/* Exchange-free steps: fc4's weight gradient (96 % of the parameters) is
+ * computed and applied tile by tile inside the slab-reduce launch and NOT
+ * stored to the gradient buffer (8.4 MB of writes per step at 64x64), so
+ * ddq_get_grads after such a step returns that block of an earlier step.
+ * The update is unchanged, bit for bit.  No effect on exchanged steps (their
+ * gradient is what is exchanged). */
+#define DDQ_STEP_NO_GRAD_STORE 1
 
 /* ---------------- context ---------------------------------------------- */
 /* caffe.Net(prototxt, model) + set_mode_gpu + set_phase_test

@@ -208,10 +208,32 @@ def test_partial_gradient_message_is_refused(param_server):
 
 
 def test_barista_tcp_loop_with_dummy_client(param_server, tmp_path, monkeypatch):
-    """Config 1 plumbing: dummy client -> Barista TCP 'G' -> param server."""
+    """Config 1: dummy client -> Barista TCP 'G' -> param server, checked by
+    value: every gradient the worker pushes against the oracle's full pass on
+    the parameters and minibatch the worker held (GPU routing at proven
+    near-ties, tests/_parity.py), and the server's model after the three
+    pushes against the oracle's rmsprop chain over the pushed gradients
+    (server.py:86-105, first call c = g^2, then the lagged cache)."""
+    from _parity import check_full_pass
     from ddq.barista import main as bmain
+    from ddq.barista.baristanet import BaristaNet
     from ddq.barista.dummy_client import DummyClient
     ps, driver = param_server
+    theta0 = ps.net.get_flat(0)
+    pushes, errors = [], []
+    orig = BaristaNet.send_gradient_update
+
+    def checked_push(self):
+        try:
+            dq, S = self.dqn, self.dqn.frame
+            pQ, pP = dq.get_flat(0), dq.get_flat(1)
+            check_full_pass(ref, dq, ref.unflatten(pQ, S, "Q"), ref.unflatten(pP, S, "P"),
+                            dq.read_minibatch(), quiet=True, what="push%d " % len(pushes))
+            pushes.append(dq.get_grads_flat())
+        except Exception as e:                     # raised again in the test's thread
+            errors.append(e)
+        return orig(self)
+    monkeypatch.setattr(BaristaNet, "send_gradient_update", checked_push)
     monkeypatch.chdir(tmp_path)
     port = free_port()
     args = ["%s" % os.path.join(GOLD, "deepq16.prototxt"), "none", "--port", str(port),
@@ -232,6 +254,13 @@ def test_barista_tcp_loop_with_dummy_client(param_server, tmp_path, monkeypatch)
         c.close()
     th.join(timeout=60)
     assert ps.iteration == 3
+    if errors:
+        raise errors[0]
+    assert len(pushes) == 3
+    theta, cache = theta0, None
+    for g in pushes:
+        theta, cache = ref.rmsprop_update(theta, g, cache, 1e-3)
+    np.testing.assert_allclose(ps.net.get_flat(0), theta, rtol=1e-5, atol=1e-8)
 
 
 def test_time_layer_times_the_step_kernels_without_side_effects():

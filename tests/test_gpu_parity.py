@@ -382,3 +382,46 @@ def test_fused_apply_matches_separate_apply(ddq, ref, rule):
     np.testing.assert_array_equal(a.optimizer_state(), b.optimizer_state())
     np.testing.assert_array_equal(a.get_grads_flat(), b.get_grads_flat())
     assert not np.array_equal(a.get_flat(0), theta)
+
+
+@pytest.mark.parametrize("S", [16])
+def test_no_grad_store_keeps_the_update(ddq, ref, S):
+    """DDQ_STEP_NO_GRAD_STORE (exchange-free steps do not store fc4's weight
+    gradient; the bench's main line) against the default: identical indices,
+    parameters of both towers and optimizer state, bit for bit, over eager,
+    pipelined and graph chains across P<-Q syncs; the gradient buffer's conv,
+    bias and Q_out blocks equal too, only fc4's weight block is left stale."""
+    from ddq.params import init_params_flat
+    B, N = 32, 300
+    rng = np.random.default_rng(41)
+    theta = init_params_flat(S, seed=42)          # the bench's initialisation: live ReLUs
+    st = rng.integers(0, 256, (N, 4, S, S)).astype(np.uint8)
+    acts = rng.integers(0, 4, N).astype(np.uint8)
+    rws = rng.integers(-1, 2, N).astype(np.int16)
+    nts = (rng.random(N) > 0.1).astype(np.uint8)
+    nets = []
+    for _ in range(2):
+        n = ddq.DeepQNet(batch=B, frame=S)
+        n.set_flat(0, theta)
+        n.set_flat(1, theta)
+        n.replay_create(N)
+        n.replay_import(st, acts, rws, nts, 0, N)
+        nets.append(n)
+    for n, store in zip(nets, (True, False)):
+        cfg = n.step_cfg("rmsprop", lr=1e-4, target_period=3, seed=4, store_grads=store)
+        n.step(cfg)
+        n.step_pipelined(cfg, 9)
+        n.step_graph(cfg, 5)
+        n.synchronize()
+    a, b = nets
+    np.testing.assert_array_equal(a.read_indices(), b.read_indices())
+    np.testing.assert_array_equal(a.get_flat(0), b.get_flat(0))
+    np.testing.assert_array_equal(a.get_flat(1), b.get_flat(1))
+    np.testing.assert_array_equal(a.optimizer_state(), b.optimizer_state())
+    _, off, cnt = a.layout["Qfc4"][0]
+    ga, gb = a.get_grads_flat(), b.get_grads_flat()
+    keep = np.ones(ga.size, bool)
+    keep[off:off + cnt] = False
+    np.testing.assert_array_equal(ga[keep], gb[keep])
+    assert np.count_nonzero(ga[~keep]) > cnt // 100     # a's last fc4 gradient, stored
+    assert not np.array_equal(ga[~keep], gb[~keep])

@@ -1,0 +1,14 @@
+# DDQ_STEP_NO_GRAD_STORE: its bit-exactness test + the fused-apply tests, then
+# the main line with and without it, alternating (same box).
+set -e
+mkdir -p gpurun_out/j
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q -m gpu -k "no_grad_store or fused_apply" --timeout 300 --timeout-method thread > gpurun_out/j/tests.log 2>&1 || { echo TESTS_FAILED; tail -30 gpurun_out/j/tests.log; exit 1; }
+tail -1 gpurun_out/j/tests.log
+for i in 1 2; do
+  for m in store nostore; do
+    F=""; [ $m = store ] && F="--store-grads"
+    timeout -k 10 200 python bench.py --steps 400 --warmup 40 $F --no-cpu-baseline --no-gather-stress --no-sweep --no-exchange-paths --no-messaging > gpurun_out/j/$m$i.json 2> gpurun_out/j/$m$i.err || { echo BENCH_FAILED; tail -5 gpurun_out/j/$m$i.err; exit 1; }
+    python3 tools/bench_summary.py gpurun_out/j/$m$i.json | sed "s/^/[$m$i] /" | head -3
+  done
+done
+echo done
