@@ -1574,11 +1574,7 @@ static const SplitMenu kConv2Fwd[] = {
     DDQ_SPLIT_TILE(32, 32, 64, 5, 16, 16, 8, 2, 1, false, 1),
     DDQ_SPLIT_TILE(32, 32, 64, 5, 10, 20, 7, 2, 1, false, 1),
     DDQ_SPLIT_TILE(32, 32, 64, 5, 12, 12, 5, 2, 1, false, 1),
-#ifdef DDQ_C2F_SMALL_WK2
-    DDQ_SPLIT_TILE(32, 32, 64, 5, 8, 8, 2, 2, 2, false, 0),
-#else
     DDQ_SPLIT_TILE(32, 32, 64, 5, 8, 8, 2, 2, 1, false, 1),
-#endif
     DDQ_SPLIT_TILE(32, 32, 64, 5, 8, 26, 7, 2, 1, false, 1),
     DDQ_SPLIT_TILE(32, 32, 64, 5, 14, 14, 7, 2, 1, false, 1)};
 // conv3 forward (64 -> 64, 3x3): two k groups on 8 x 8
@@ -1688,11 +1684,7 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     c1.out_elems = (int64_t)B * (S / 2) * (S / 2) * 32;
     c1.mask[0] = nb.mask1; c1.mask[1] = nullptr;
     M("conv1_fwd");
-#ifndef DDQ_C1_FORCE
-#define DDQ_C1_FORCE -1
-#endif
-    CHECK_LAUNCH((DDQ_C1_FORCE >= 0 ? kConv1Fwd[DDQ_C1_FORCE] : pick_tile(kConv1Fwd, S, S))
-                     .launch(c1, nz, s, L.wks_total));
+    CHECK_LAUNCH(pick_tile(kConv1Fwd, S, S).launch(c1, nz, s, L.wks_total));
   }
   if (!nb.fwd_only || nb.fwd_only == 2) {
     // conv2 (train_val.prototxt:79-118): split bf16, 16x16 tiles, 16 waves of
@@ -1826,9 +1818,6 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
     a.in_route = nb.mask2;
     a.w1_route = nb.mask1; a.w1_in = nb.state;
     a.w1_part = nb.wpart + nb.wpart_off[0]; a.w1_np = nb.wnp[0];
-#ifdef DDQ_TIMING_NOW1
-    a.w1_part = nullptr;   // timing-only A/B: conv2's data gradient without conv1's (wrong results)
-#endif
     M("conv2_dgrad");
     CHECK_LAUNCH(pick_tile(kConv2Dgrad, H, H).launch(a, 1, s));
   }

@@ -457,11 +457,6 @@ __device__ __forceinline__ void split_epilogue_fwd_lds(const SplitArgs& a,
 // exact frame) per conv1 row of the tile; a unit's sums over the segments
 // meet in LDS in fixed order.
 // ---------------------------------------------------------------------------
-#ifdef DDQ_W1_ZF
-constexpr bool kW1ZF = true;
-#else
-constexpr bool kW1ZF = false;
-#endif
 template <int TY, int TX, int NT>
 struct W1Fuse {
   static constexpr int R = 2 * TY;                  // conv1 rows of the tile
@@ -550,12 +545,6 @@ __device__ __forceinline__ void w1_tile_wgrad(const SplitArgs& a, char* smem,
   float* bsm = reinterpret_cast<float*>(smem + (F::kXB + F::kHaloB > F::kRedB
                                                     ? F::kXB + F::kHaloB : F::kRedB));
   __syncthreads();   // every wave's reads of the k-group sums (smem) are done
-#ifdef DDQ_W1_ZF
-  // zero the expanded image with 16-byte stores, then each element to its
-  // routed quadrant only
-  for (int f = tid; f < 3 * F::XPL / 8; f += NT) reinterpret_cast<u32x4*>(X)[f] = u32x4{0u, 0u, 0u, 0u};
-  __syncthreads();
-#endif
   // ---- scatter: each element's value to its routed quadrant, 0 to the others ----
   float bsum = 0.f;
 #pragma unroll
@@ -574,14 +563,6 @@ __device__ __forceinline__ void w1_tile_wgrad(const SplitArgs& a, char* smem,
       bsum += v;
       __bf16 s0, s1, s2;
       split3(v, s0, s1, s2);
-#ifdef DDQ_W1_ZF
-      if (q < 4) {
-        const int e = ((2 * ty + (q >> 1)) * F::XW + 2 * tx + (q & 1)) * F::PSD + l31;
-        X[e] = s0;
-        X[F::XPL + e] = s1;
-        X[2 * F::XPL + e] = s2;
-      }
-#else
       const __bf16 zero = (__bf16)0.f;
 #pragma unroll
       for (int qq = 0; qq < 4; ++qq) {
@@ -591,11 +572,10 @@ __device__ __forceinline__ void w1_tile_wgrad(const SplitArgs& a, char* smem,
         X[F::XPL + e] = on ? s1 : zero;
         X[2 * F::XPL + e] = on ? s2 : zero;
       }
-#endif
     }
   }
   // the rows' padding pixels (2 TX .. XW) stay zero
-  if constexpr (F::XW > 2 * TX && !kW1ZF) {
+  if constexpr (F::XW > 2 * TX) {
     constexpr int PADV = (F::XW - 2 * TX) * (F::PSD / 8);   // 16-byte vectors per row and plane
     for (int f = tid; f < 3 * F::R * PADV; f += NT) {
       const int pr = f / PADV, c = f - pr * PADV;            // (plane, row), vector
