@@ -1,4 +1,7 @@
 """Debug: fc4 gradient block after exchange-free steps at S = 16 / 64."""
+import os
+import sys
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "distributed-deep-q_amd"))
 import numpy as np
 import ddq
 from ddq.params import init_params_flat
