@@ -384,10 +384,10 @@ def test_fused_apply_matches_separate_apply(ddq, ref, rule):
     assert not np.array_equal(a.get_flat(0), theta)
 
 
-@pytest.mark.parametrize("S", [16])
-def test_no_grad_store_keeps_the_update(ddq, ref, S):
+@pytest.mark.parametrize("S,rule,lr", [(16, "rmsprop", 1e-4), (64, "sgd", 1e-5)])
+def test_no_grad_store_keeps_the_update(ddq, ref, S, rule, lr):
     """DDQ_STEP_NO_GRAD_STORE (exchange-free steps do not store fc4's weight
-    gradient; the bench's main line) against the default: identical indices,
+    gradient; bench --no-grad-store) against the default: identical indices,
     parameters of both towers and optimizer state, bit for bit, over eager,
     pipelined and graph chains across P<-Q syncs; the gradient buffer's conv,
     bias and Q_out blocks equal too, only fc4's weight block is left stale."""
@@ -407,13 +407,17 @@ def test_no_grad_store_keeps_the_update(ddq, ref, S):
         n.replay_create(N)
         n.replay_import(st, acts, rws, nts, 0, N)
         nets.append(n)
+    # (64x64 on this small random ring: sgd at a small rate -- lagged rmsprop
+    # from c = g^2 diverges there within a few steps, as the reference's rule
+    # does, and dead ReLUs would leave nothing to compare)
     for n, store in zip(nets, (True, False)):
-        cfg = n.step_cfg("rmsprop", lr=1e-4, target_period=3, seed=4, store_grads=store)
+        cfg = n.step_cfg(rule, lr=lr, target_period=3, seed=4, store_grads=store)
         n.step(cfg)
         n.step_pipelined(cfg, 9)
         n.step_graph(cfg, 5)
         n.synchronize()
     a, b = nets
+    assert np.isfinite(float(a.blob("loss")))
     np.testing.assert_array_equal(a.read_indices(), b.read_indices())
     np.testing.assert_array_equal(a.get_flat(0), b.get_flat(0))
     np.testing.assert_array_equal(a.get_flat(1), b.get_flat(1))
