@@ -545,7 +545,12 @@ __device__ __forceinline__ void w1_tile_wgrad(const SplitArgs& a, char* smem,
   float* bsm = reinterpret_cast<float*>(smem + (F::kXB + F::kHaloB > F::kRedB
                                                     ? F::kXB + F::kHaloB : F::kRedB));
   __syncthreads();   // every wave's reads of the k-group sums (smem) are done
-  // ---- scatter: each element's value to its routed quadrant, 0 to the others ----
+  // ---- the expanded image zeroed with 16-byte stores (row padding included),
+  // then each element written to its routed quadrant only: 3 two-byte stores
+  // an element instead of 12 with selects (conv2 data gradient 24.9 -> 24.4
+  // us, same-box A/B) ----
+  for (int f = tid; f < 3 * F::XPL / 8; f += NT) reinterpret_cast<u32x4*>(X)[f] = u32x4{0u, 0u, 0u, 0u};
+  __syncthreads();
   float bsum = 0.f;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -563,25 +568,12 @@ __device__ __forceinline__ void w1_tile_wgrad(const SplitArgs& a, char* smem,
       bsum += v;
       __bf16 s0, s1, s2;
       split3(v, s0, s1, s2);
-      const __bf16 zero = (__bf16)0.f;
-#pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        const int e = ((2 * ty + (qq >> 1)) * F::XW + 2 * tx + (qq & 1)) * F::PSD + l31;
-        const bool on = q == qq;
-        X[e] = on ? s0 : zero;
-        X[F::XPL + e] = on ? s1 : zero;
-        X[2 * F::XPL + e] = on ? s2 : zero;
+      if (q < 4) {
+        const int e = ((2 * ty + (q >> 1)) * F::XW + 2 * tx + (q & 1)) * F::PSD + l31;
+        X[e] = s0;
+        X[F::XPL + e] = s1;
+        X[2 * F::XPL + e] = s2;
       }
-    }
-  }
-  // the rows' padding pixels (2 TX .. XW) stay zero
-  if constexpr (F::XW > 2 * TX) {
-    constexpr int PADV = (F::XW - 2 * TX) * (F::PSD / 8);   // 16-byte vectors per row and plane
-    for (int f = tid; f < 3 * F::R * PADV; f += NT) {
-      const int pr = f / PADV, c = f - pr * PADV;            // (plane, row), vector
-      const int p = pr / F::R, row = pr - p * F::R;
-      *reinterpret_cast<u32x4*>(X + p * F::XPL + (row * F::XW + 2 * TX) * F::PSD + 8 * c) =
-          u32x4{0u, 0u, 0u, 0u};
     }
   }
   // ---- the frames' halo: fp32 -> bf16 (exact), pixel stride 4 ----
