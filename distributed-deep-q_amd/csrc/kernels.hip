@@ -1626,9 +1626,14 @@ int wgrad_splits_for(int layer, int B, int S, int* np) {
   const int nts[3] = {0, 2 * 5, 2 * 3};
   // about 256 workgroups each (24 / 40 slabs at 64x64 B=32: fewer, larger
   // slabs than at 512 -- pair 30.0 -> 27.7 us, reduce 21.9 -> 19.2)
-  const int target[3] = {0, 256, 256};
+  int target = 256;
+  // 16 x 16 maps: at least 16 rows per group -- a slab is the whole weight
+  // matrix whatever the rows behind it (deepq16: conv3 on 8 slabs instead of
+  // 40, conv2 on 16 instead of 24; 0.0915 -> 0.0896 ms per step, same-box
+  // A/B; at 32 x 32 the same rule measured 0.1238 -> 0.1247)
+  if (S <= 16) target = std::min(target, std::max(nts[layer], nts[layer] * (B * H) / 16));
   int G, RPG;
-  wgrads_groups(B * H, nts[layer], &G, &RPG, target[layer]);
+  wgrads_groups(B * H, nts[layer], &G, &RPG, target);
   return G;
 }
 
