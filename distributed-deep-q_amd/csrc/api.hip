@@ -1022,7 +1022,9 @@ static int enqueue_fwd_bwd_x(ddq_ctx* c, const NetBuffers& nb, void (*mark)(void
                              const Prefetch* pf = nullptr) {
   HIP_TRY(c, launch_forward(nb, 2, c->stream, mark, marg, false));
   if (mark) mark(marg, "head");
-  HIP_TRY(c, launch_head(nb, c->stream, bump));   // fused apply: the draw counter advances here
+  // fused apply: the draw counter advances here (pipelined: with the next
+  // step's draw, kernels.hip head_draw)
+  HIP_TRY(c, launch_head(nb, c->stream, bump, nb.fa.on ? pf : nullptr));
   hipError_t e = launch_backward(nb, c->stream, mark, marg, book >= 0, book, bump,
                                  overlap ? fc4_bucket_start : nullptr, c, pf);
   if (e != hipSuccess && !c->comm_err.empty()) {

@@ -110,7 +110,8 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s, void (*ma
                           bool out = true);
 // bump (fused apply only): the step's draw-counter advance, done here so the
 // slab-reduce launch can carry the next step's draw + gather
-hipError_t launch_head(const NetBuffers& nb, hipStream_t s, ReplayMeta* bump = nullptr);
+hipError_t launch_head(const NetBuffers& nb, hipStream_t s, ReplayMeta* bump = nullptr,
+                       const Prefetch* pf = nullptr);
 bool fused_apply_ok(const ParamLayout& L);
 // book: the slab reduce also does the apply bookkeeping (target period
 // book_period); fc4_done: called right after the fc4 weight gradient is
@@ -130,6 +131,7 @@ struct Prefetch {
   ReplayMeta* meta;
   uint64_t seed;
   int B, S, gx, ng;                 // ng = 0: no prefetch blocks
+  int predrawn;                     // 1: the head launch drew the set into idx already
   int32_t* idx;
   int32_t* idx_log;                 // NetBuffers::idx_log / log_cap of the step
   int64_t log_cap;

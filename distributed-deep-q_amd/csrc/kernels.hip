@@ -638,7 +638,29 @@ struct HeadArgs {
   ReplayMeta* bump;
   const __bf16* wks;
   int64_t wks_plane, wks2_off, wkst_off, wks3_off, wkst3_off;
+  // pipelined fused steps: one extra block draws the NEXT step's sorted index
+  // set into didx and advances the draw counter (instead of every prefetch
+  // block of the slab-reduce launch drawing it again, and block 0 bumping)
+  ReplayMeta* dmeta;
+  int32_t* didx;
+  uint64_t dseed;
+  int32_t* dlog;
+  int64_t dlog_cap;
 };
+
+__device__ __forceinline__ void head_draw(const HeadArgs& H) {
+  __shared__ int64_t cand[256];
+  __shared__ int bad_any;
+  const uint64_t ctr = H.dmeta->counter + 1;     // the advance this launch makes, below
+  draw_sorted(H.dmeta, H.B, H.dseed, ctr, cand, &bad_any);
+  const int t = threadIdx.x;
+  if (t < H.B) {
+    H.didx[t] = (int32_t)cand[t];
+    log_draw(H.dlog, H.dlog_cap, ctr, H.B, t, (int32_t)cand[t]);
+  }
+  __syncthreads();                                // every thread has read the counter
+  if (t == 0) H.dmeta->counter = ctr;
+}
 
 // One head block b
 __device__ __forceinline__ void head_body(const HeadArgs& H, int b, char* smem) {
@@ -666,6 +688,10 @@ __device__ __forceinline__ void head_body(const HeadArgs& H, int b, char* smem) 
   __shared__ float red[8][8];
   __shared__ float qp[8];
   const int n = threadIdx.x, w = n >> 6;
+  if (b == B + 34) {                              // (launched only with dmeta)
+    head_draw(H);
+    return;
+  }
   if (b >= B + 25) {
     wkst_tap<64, 9>(H.wks, H.wks_plane, H.wks3_off, H.wkst3_off, b - B - 25, smem);
     return;
@@ -989,8 +1015,16 @@ static Fc4DgradArgs fc4_dgrad_args(const NetBuffers& nb, bool& narrow, int& ndx,
   return f;
 }
 
-hipError_t launch_head(const NetBuffers& nb, hipStream_t s, ReplayMeta* bump) {
-  ddq_launch(fc4_head_kernel, dim3(nb.B + 25 + 9), dim3(kFc4), 0, s, head_args(nb, bump));
+hipError_t launch_head(const NetBuffers& nb, hipStream_t s, ReplayMeta* bump, const Prefetch* pf) {
+  HeadArgs H = head_args(nb, bump);
+  int extra = 0;
+  if (pf && pf->ng > 0 && H.bump && nb.B <= 256) {   // the next step's draw moves here
+    H.dmeta = H.bump;
+    H.bump = nullptr;
+    H.didx = pf->idx; H.dseed = pf->seed; H.dlog = pf->idx_log; H.dlog_cap = pf->log_cap;
+    extra = 1;
+  }
+  ddq_launch(fc4_head_kernel, dim3(nb.B + 25 + 9 + extra), dim3(kFc4), 0, s, H);
   return hipGetLastError();
 }
 
@@ -1180,6 +1214,11 @@ __device__ __forceinline__ void prefetch_body(const Prefetch& pf, int g) {
   __shared__ int64_t cand[256];
   __shared__ int bad_any;
   const int bx = g % pf.gx, b = (g / pf.gx) % pf.B, z = g / (pf.gx * pf.B);
+  if (pf.predrawn) {   // the head launch drew the set (head_draw): gather only
+    gather_body(pf.st, pf.act, pf.rew, pf.nt, pf.meta, (int64_t)pf.idx[b], pf.S, pf.sQ, pf.sP,
+                pf.action, pf.reward, pf.nonterm, bx, b, z);
+    return;
+  }
   const uint64_t ctr = pf.meta->counter;
   draw_sorted(pf.meta, pf.B, pf.seed, ctr, cand, &bad_any);
   if (g == 0 && threadIdx.x < pf.B) {
@@ -1494,6 +1533,7 @@ Prefetch make_prefetch(const NetBuffers& next, const uint8_t* st, const uint8_t*
   Prefetch pf;
   pf.st = st; pf.act = act; pf.rew = rew; pf.nt = nt; pf.meta = meta; pf.seed = seed;
   pf.B = next.B; pf.S = next.S;
+  pf.predrawn = 0;
   pf.gx = (next.S * next.S / 4 + 255) / 256;
   pf.ng = pf.gx * next.B * 2;
   pf.idx = next.idx; pf.sQ = next.state; pf.sP = next.next_state;
@@ -1864,7 +1904,10 @@ hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(voi
       fat.rest = !nb.fa.ext;
     }
     Prefetch pf{};
-    if (pre && nb.fa.on) pf = *pre;
+    if (pre && nb.fa.on) {
+      pf = *pre;
+      pf.predrawn = bump != nullptr && nb.B <= 256;   // launch_head drew it (head_draw)
+    }
     ddq_launch(wgrad_reduce_kernel, dim3(pf.ng + nub + kFc4 / 64 + nfa), dim3(256), 0, s,
                        nb.wpart, nb.grad, d[0], d[1], d[2], nub, nb.iter,
                        book ? nb.opt_init : nullptr, book_period,
