@@ -1161,7 +1161,7 @@ __device__ __forceinline__ void fc4_wgrad_sum(int B, int K, const float* __restr
 // the gradient sum; the gradient is written to grad as well (the step's
 // gradient stays observable), then the update rule runs (and the P copy on a
 // sync step).
-constexpr int kFc4ApplyR = 4;
+constexpr int kFc4ApplyR = 4;   // 2 / 8 rows per wave measured 18.9 / 25.0 us against 13.4
 __device__ __forceinline__ void fc4_apply_tile(const ApplyTail& t, const ApplyArgs& a, int B,
                                                int K, const float* dh4, const float* x, int blk) {
   constexpr int R = kFc4ApplyR;
