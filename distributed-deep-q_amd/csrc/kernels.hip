@@ -1077,9 +1077,12 @@ __device__ __forceinline__ void apply_elems(const ApplyTail& t, const ApplyArgs&
 #pragma unroll
   for (int e = 0; e < 4; ++e) th[e] = apply_one(a, first, i + e, th[e], g[e], st[e]);
   const float4 o4 = make_float4(th[0], th[1], th[2], th[3]);
-  *reinterpret_cast<float4*>(t.theta + i) = o4;
-  if (a.rule != 0) *reinterpret_cast<float4*>(t.opt + i) = make_float4(st[0], st[1], st[2], st[3]);
-  if (sync) *reinterpret_cast<float4*>(t.thetaP + i) = o4;
+  // write-through (split.h wt_store4): no dirty theta / state lines for the
+  // launch's end to write back
+  const uint32_t nb = (uint32_t)(((a.n + 3) & ~3ll) * 4), ib = (uint32_t)(i * 4);
+  wt_store4(wt_rsrc(t.theta, nb), ib, o4);
+  if (a.rule != 0) wt_store4(wt_rsrc(t.opt, nb), ib, make_float4(st[0], st[1], st[2], st[3]));
+  if (sync) wt_store4(wt_rsrc(t.thetaP, nb), ib, o4);
 #pragma unroll
   for (int l = 0; l < 3; ++l) {
     const ConvDims& d = a.conv[l];
@@ -1419,8 +1422,9 @@ __global__ __launch_bounds__(256) void apply_shard_kernel(
     for (int e = 0; e < 4; ++e)
       th[e] = (i + e < a.n) ? apply_one(a, first && w == 0, i + e, th[e], g[e], st[e]) : 0.f;
   }
-  *reinterpret_cast<float4*>(theta + i) = make_float4(th[0], th[1], th[2], th[3]);
-  if (a.rule != 0) *reinterpret_cast<float4*>(opt + i) = make_float4(st[0], st[1], st[2], st[3]);
+  const uint32_t nb = (uint32_t)((off + len) * 4), ib = (uint32_t)(i * 4);   // the shard's end
+  wt_store4(wt_rsrc(theta, nb), ib, make_float4(th[0], th[1], th[2], th[3]));
+  if (a.rule != 0) wt_store4(wt_rsrc(opt, nb), ib, make_float4(st[0], st[1], st[2], st[3]));
 }
 
 // After the theta all-gather: conv kernel layouts of Q, and P <- Q (weights
@@ -1436,7 +1440,7 @@ __global__ __launch_bounds__(256) void refresh_kernel(const float* __restrict__ 
   if (i >= a.n || (!sync && i >= a.conv[2].w_off + (int64_t)a.conv[2].cout * a.conv[2].cin * 9))
     return;
   const float4 o4 = *reinterpret_cast<const float4*>(theta + i);
-  if (sync) *reinterpret_cast<float4*>(thetaP + i) = o4;
+  if (sync) wt_store4(wt_rsrc(thetaP, (uint32_t)(((a.n + 3) & ~3ll) * 4)), (uint32_t)(i * 4), o4);
   const float th[4] = {o4.x, o4.y, o4.z, o4.w};
 #pragma unroll
   for (int l = 0; l < 3; ++l) {
