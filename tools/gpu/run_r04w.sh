@@ -1,6 +1,6 @@
-# Round 4: write-through theta / state stores in the apply, owner-apply and
-# refresh kernels -- the exchange and async suites on the product, then the
-# world-1 exchange paths of the product and the plain-store build, alternating.
+# Round 4 exchange-path A/B: the exchange, async and chain suites on the
+# product, then the world-1 exchange paths of the product and the variant
+# build ab/$V (default nowt), alternating.  Usage: [V=name] bash tools/gpu/run_r04w.sh
 set -e
 mkdir -p gpurun_out/w
 R=$GRAFT_REPO_ROOT
@@ -8,7 +8,7 @@ timeout -k 10 700 python -u -m pytest tests/test_gpu_exchange.py tests/test_gpu_
 tail -1 gpurun_out/w/tests.log
 Q="--steps 100 --warmup 20 --chunks 0 --no-cpu-baseline --no-gather-stress --no-sweep --no-messaging --no-isolated"
 for i in 1 2; do
-  for lib in product nowt; do
+  for lib in product ${V:-nowt}; do
     if [ $lib = product ]; then LIBP=""; else LIBP=$R/distributed-deep-q_amd/ab/$lib/libddq_hip.so; fi
     DDQ_LIB_PATH=$LIBP timeout -k 10 300 python bench.py $Q > gpurun_out/w/${lib}_$i.json 2> gpurun_out/w/${lib}_$i.err || { echo BENCH_FAILED $lib; tail -5 gpurun_out/w/${lib}_$i.err; exit 1; }
     python3 - gpurun_out/w/${lib}_$i.json $lib <<'PY'
