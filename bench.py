@@ -50,8 +50,14 @@ def kernel_flops(B, S):
     fc = 2.0 * B * 512 * k4
     # conv2_dgrad: conv2's data gradient with conv1's weight gradient fused
     # into its tiles (split.h w1_tile_wgrad): c2 split + c1 split3 FLOPs
+    # deepq16's four launches (csrc/small.h, small_bwd.h): K1 tower_fwd (conv1..3
+    # of both towers), K2 fc4_chain (fc4 forward of both towers, data and weight
+    # gradients), K3 tower_bwd (conv3 / conv2 data gradients, conv1's weight
+    # gradient), K4 wgrad_apply (conv2 / conv3 weight gradients)
     return {"conv1_fwd": 2 * c1, "conv2_fwd": 2 * c2, "conv3_fwd": 2 * c3, "fc4_fwd": 2 * fc,
-            "fc4_bwd": fc, "conv3_dgrad": c3, "conv23_wgrad": c2 + c3, "conv2_dgrad": c2 + c1}
+            "fc4_bwd": fc, "conv3_dgrad": c3, "conv23_wgrad": c2 + c3, "conv2_dgrad": c2 + c1,
+            "tower_fwd": 2 * (c1 + c2 + c3), "fc4_chain": 4 * fc, "tower_bwd": c3 + c2 + c1,
+            "wgrad_apply": c2 + c3}
 
 
 def kernel_parts(B, S):
@@ -65,6 +71,16 @@ def kernel_parts(B, S):
             "conv3_fwd": [(2 * c3, "split")], "conv3_dgrad": [(c3, "split")],
             "conv23_wgrad": [(c2 + c3, "split")],
             "conv2_dgrad": [(c2, "split"), (c1, "split3")]}
+
+
+def small_parts(B, S):
+    """deepq16's fused launches: (FLOPs, arithmetic) parts (fc4 on the f32 MFMA)."""
+    p = kernel_parts(B, S)
+    fc = 2.0 * B * 512 * 64 * (S // 8) ** 2
+    return {"tower_fwd": p["conv1_fwd"] + p["conv2_fwd"] + p["conv3_fwd"],
+            "fc4_chain": [(4 * fc, "f32")],
+            "tower_bwd": p["conv3_dgrad"] + p["conv2_dgrad"],
+            "wgrad_apply": p["conv23_wgrad"]}
 
 
 # rocprof kernel symbol (prefix) of each profiled step kernel
@@ -81,6 +97,10 @@ KERNEL_SYMBOL = {
     "conv2_dgrad": "void ddq::split_conv_kernel<64, 64, 32, 5,",
     "wgrad_reduce": "ddq::wgrad_reduce_kernel",
     "apply": "ddq::apply_kernel",
+    "tower_fwd": "void ddq::sm16::tower_fwd16_kernel",
+    "fc4_chain": "ddq::sm16::fc4_chain16_kernel",
+    "tower_bwd": "void ddq::sm16::tower_bwd16_kernel",
+    "wgrad_apply": "ddq::sm16::wgrad16_kernel",
 }
 
 # How each MFMA kernel computes its f32-exact result (csrc/split.h, wgrads.h):
@@ -91,6 +111,8 @@ KERNEL_SYMBOL = {
 KERNEL_ARITH = {
     "conv1_fwd": "split3", "conv2_fwd": "split", "conv3_fwd": "split", "conv23_wgrad": "split",
     "conv2_dgrad": "split+split3", "conv3_dgrad": "split", "fc4_fwd": "split", "fc4_bwd": "split",
+    "tower_fwd": "split+split3", "tower_bwd": "split+split3", "wgrad_apply": "split",
+    "fc4_chain": "f32",
 }
 BF16_MFMA_PEAK = 2.5e15       # MI355X_MICROARCH.md: dense bf16
 
@@ -102,7 +124,9 @@ def arith_peak(kernel, kind=None):
 
 def ideal_s(kernel, B, S):
     """Seconds of a kernel's FLOPs at the peaks of the arithmetic each part runs."""
-    return sum(f / arith_peak(kernel, kind) for f, kind in kernel_parts(B, S)[kernel])
+    parts = kernel_parts(B, S)
+    parts.update(small_parts(B, S))
+    return sum(f / arith_peak(kernel, kind) for f, kind in parts[kernel])
 
 
 def pmc_traffic(label, B, S):

@@ -278,6 +278,19 @@ int ddq_create(ddq_ctx** out, int device, const ddq_net_desc* desc) {
     TRY(dalloc(c, &nb.dconv3, (size_t)B * S3 * S3 * 64));
     TRY(dalloc(c, &nb.dconv2s, (size_t)3 * B * S3 * S3 * 64));
     TRY(dalloc(c, &nb.dconv3s, (size_t)3 * B * S3 * S3 * 64));
+    // DDQ_NO_SMALL=1: the general kernels at S = 16 too (A/B, diagnosis)
+    const char* ns = getenv("DDQ_NO_SMALL");
+    nb.small = S == 16 && B <= 256 && !(ns && ns[0] == '1');
+    if (nb.small) {
+      TRY(dalloc(c, &nb.qpart, (size_t)32 * 2 * B * 4));
+      TRY(dalloc(c, &nb.dpart, (size_t)32 * B * 256));
+      TRY(dalloc(c, &nb.csync, 64));
+      TRY(dalloc(c, &nb.dconv2x, (size_t)3 * B * 4096));
+      int G2, G3;
+      small_groups(B, &G2, &G3);
+      TRY(dalloc(c, &nb.slab2, (size_t)10 * G2 * (32 * 5 * 32 + 32)));
+      TRY(dalloc(c, &nb.slab3, (size_t)6 * G3 * (32 * 3 * 64 + 32)));
+    }
     int64_t off = 0;
     const int cout[3] = {32, 64, 64};
     for (int l = 0; l < 3; ++l) {
@@ -792,13 +805,21 @@ int ddq_write_minibatch(ddq_ctx* c, const float* state, const float* action, con
 // the apply bookkeeping with target period `book` (saves a launch).
 static int enqueue_fwd_bwd(ddq_ctx* c, const NetBuffers& nb, void (*mark)(void*, const char*),
                            void* marg, int book = -1, ReplayMeta* bump = nullptr) {
-  HIP_TRY(c, launch_forward(nb, 2, c->stream, mark, marg, false));
-  if (mark) mark(marg, "head");
-  HIP_TRY(c, launch_head(nb, c->stream));
+  if (nb.small) {
+    HIP_TRY(c, launch_small_fwd_head(nb, c->stream, mark, marg));
+  } else {
+    HIP_TRY(c, launch_forward(nb, 2, c->stream, mark, marg, false));
+    if (mark) mark(marg, "head");
+    HIP_TRY(c, launch_head(nb, c->stream));
+  }
   // one stream: forking the weight-gradient kernels onto a side stream cost
   // more in cross-stream graph edges (6-14 us idle each, measured) than the
   // overlap returned, as every kernel here fills the GPU on its own
-  HIP_TRY(c, launch_backward(nb, c->stream, mark, marg, book >= 0, book, bump));
+  if (nb.small)
+    HIP_TRY(c, launch_small_bwd(nb, c->stream, mark, marg, book >= 0, book, bump, nullptr, nullptr,
+                                nullptr));
+  else
+    HIP_TRY(c, launch_backward(nb, c->stream, mark, marg, book >= 0, book, bump));
   return DDQ_OK;
 }
 static int enqueue_fwd_bwd(ddq_ctx* c, void (*mark)(void*, const char*), void* marg) {
@@ -1020,13 +1041,19 @@ static hipError_t fc4_bucket_start(void* arg) {
 static int enqueue_fwd_bwd_x(ddq_ctx* c, const NetBuffers& nb, void (*mark)(void*, const char*),
                              void* marg, int book, ReplayMeta* bump, bool overlap,
                              const Prefetch* pf = nullptr) {
-  HIP_TRY(c, launch_forward(nb, 2, c->stream, mark, marg, false));
-  if (mark) mark(marg, "head");
-  // fused apply: the draw counter advances here (pipelined: with the next
-  // step's draw, kernels.hip head_draw)
-  HIP_TRY(c, launch_head(nb, c->stream, bump, nb.fa.on ? pf : nullptr));
-  hipError_t e = launch_backward(nb, c->stream, mark, marg, book >= 0, book, bump,
-                                 overlap ? fc4_bucket_start : nullptr, c, pf);
+  if (nb.small) {
+    HIP_TRY(c, launch_small_fwd_head(nb, c->stream, mark, marg, bump, nb.fa.on ? pf : nullptr));
+  } else {
+    HIP_TRY(c, launch_forward(nb, 2, c->stream, mark, marg, false));
+    if (mark) mark(marg, "head");
+    // fused apply: the draw counter advances here (pipelined: with the next
+    // step's draw, kernels.hip head_draw)
+    HIP_TRY(c, launch_head(nb, c->stream, bump, nb.fa.on ? pf : nullptr));
+  }
+  hipError_t e = nb.small ? launch_small_bwd(nb, c->stream, mark, marg, book >= 0, book, bump,
+                                             overlap ? fc4_bucket_start : nullptr, c, pf)
+                          : launch_backward(nb, c->stream, mark, marg, book >= 0, book, bump,
+                                            overlap ? fc4_bucket_start : nullptr, c, pf);
   if (e != hipSuccess && !c->comm_err.empty()) {
     std::string m = c->comm_err;
     c->comm_err.clear();
@@ -1130,7 +1157,10 @@ static int enqueue_train(ddq_ctx* c, const ddq_step_cfg* cfg, const NetBuffers& 
   // exchange-free steps: fc4's weight update rides on the slab-reduce launch
   const int ex = has_exchange(c, cfg) ? cfg->exchange : DDQ_EXCHANGE_NONE;
   const bool ar_overlap = ex == DDQ_EXCHANGE_ALLREDUCE && cfg->overlap && c->comm;
-  if ((ex == DDQ_EXCHANGE_NONE || ar_overlap) && fused_apply_ok(nb.L)) {
+  // (deepq16: fc4's parameters are final and applied inside the fc4 chain,
+  // K2, before any bucket could be summed: the overlapped all-reduce takes the
+  // plain apply launch there)
+  if ((ex == DDQ_EXCHANGE_NONE || (ar_overlap && !nb.small)) && fused_apply_ok(nb.L)) {
     const ddq_update_cfg& u = cfg->update;
     nb.fa.on = 1;
     nb.fa.ext = ar_overlap ? 1 : 0;

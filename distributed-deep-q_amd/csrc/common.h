@@ -33,6 +33,21 @@ inline void ddq_launch(F kern, const dim3& grid, const dim3& block, uint32_t sme
   }
 }
 
+// Phase stamps of variant builds (make variant DEFS=-DDDQ_STAMPS, read by
+// ddq_debug_stamps / tools/gpu/stamps.py): lane 0 of a workgroup records the
+// 100 MHz real-time clock at a kernel's phase boundaries.  Empty otherwise.
+#ifdef DDQ_STAMPS
+constexpr int kStampSlots = 48, kStampBlocks = 512;
+extern __device__ uint64_t g_stamps[kStampBlocks * kStampSlots];
+#define DDQ_STAMP(slot)                                                        \
+  do {                                                                         \
+    if (threadIdx.x == 0 && blockIdx.x < kStampBlocks)                         \
+      g_stamps[blockIdx.x * kStampSlots + (slot)] = wall_clock64();            \
+  } while (0)
+#else
+#define DDQ_STAMP(slot) do { } while (0)
+#endif
+
 constexpr int kWave = 64;          // CDNA wavefront
 constexpr int kActions = 4;        // barista/constants.py:8
 constexpr int kFrames = 4;         // expgain.py:9

@@ -95,6 +95,13 @@ struct NetBuffers {
   int book_inc;                     // param-server iterations per apply (1, or W: server mode)
   int head_bump;                    // the head kernel advances the draw counter without a
                                     // fused apply (async gradients: sample_gather draws)
+  // deepq16 step (small.h, small_bwd.h): fc4 chain partials and its fan-in words
+  int small;                        // S == 16, B <= 256: the four-launch step
+  float *qpart, *dpart;             // [32][2][B][4] Q_out / P_out partials, [32][B][256] dpool3
+  int32_t* csync;                   // fan-in words: K2 [0..2] (arrivals, generation,
+                                    // timeout), K4 [8..40) (a pair per tile, timeout at 40)
+  __bf16* dconv2x;                  // split expanded dconv2 NHWC (B, 8, 8, 64) (K3 -> K4)
+  float *slab2, *slab3;             // K4's per-group slabs of conv2 / conv3 tiles
 };
 
 // fused device draw + gather for the step (B <= 256); counter advanced by the
@@ -108,6 +115,12 @@ hipError_t launch_gather(const NetBuffers& nb, const uint8_t* st, const uint8_t*
 hipError_t launch_sample(const NetBuffers& nb, ReplayMeta* meta, uint64_t seed, hipStream_t s);
 hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s, void (*mark)(void*, const char*), void* mark_arg,
                           bool out = true);
+// deepq16 (nb.small): K1 (towers + the head's bookkeeping: latch, bump /
+// next draw, as launch_head's) and K2 (fc4 chain) in place of launch_forward
+// + launch_head
+hipError_t launch_small_fwd_head(const NetBuffers& nb, hipStream_t s,
+                                 void (*mark)(void*, const char*), void* mark_arg,
+                                 ReplayMeta* bump = nullptr, const struct Prefetch* pf = nullptr);
 // bump (fused apply only): the step's draw-counter advance, done here so the
 // slab-reduce launch can carry the next step's draw + gather
 hipError_t launch_head(const NetBuffers& nb, hipStream_t s, ReplayMeta* bump = nullptr,
@@ -117,6 +130,14 @@ bool fused_apply_ok(const ParamLayout& L);
 // book_period); fc4_done: called right after the fc4 weight gradient is
 // enqueued (the overlapped all-reduce starts there); pf (fused apply only):
 // the next step's draw + gather as blocks of the slab-reduce launch.
+// deepq16 (nb.small): K3 (data gradients, conv1's weight gradient slabs)
+// and K4 (conv weight gradients + fused apply + bookkeeping + next gather) in
+// place of launch_backward (same arguments)
+hipError_t launch_small_bwd(const NetBuffers& nb, hipStream_t s, void (*mark)(void*, const char*),
+                            void* mark_arg, bool book, int book_period, ReplayMeta* bump,
+                            hipError_t (*fc4_done)(void*), void* fc4_done_arg,
+                            const struct Prefetch* pf);
+void small_groups(int B, int* G2, int* G3);
 hipError_t launch_backward(const NetBuffers& nb, hipStream_t s, void (*mark)(void*, const char*),
                            void* mark_arg, bool book = false, int book_period = 0,
                            ReplayMeta* bump = nullptr, hipError_t (*fc4_done)(void*) = nullptr,

@@ -4,6 +4,7 @@
 #include "wgrads.h"
 #include "fc.h"
 #include "split.h"
+#include "small.h"
 
 namespace ddq {
 
@@ -11,6 +12,23 @@ namespace ddq {
 // appends it to the error message)
 thread_local const char* g_launch_where = "";
 thread_local ExtTiming g_ext_timing;
+#ifdef DDQ_STAMPS
+__device__ uint64_t g_stamps[kStampBlocks * kStampSlots];
+}  // namespace ddq
+// variant builds only (common.h DDQ_STAMP): copy the stamp table out, then
+// clear it.  0 = ok, -1 = size mismatch, -3 = HIP error (ddq_hip.h codes)
+extern "C" int ddq_debug_stamps(uint64_t* out, int64_t n) {
+  using namespace ddq;
+  const size_t bytes = sizeof(uint64_t) * kStampBlocks * kStampSlots;
+  if (n * (int64_t)sizeof(uint64_t) != (int64_t)bytes) return -1;
+  if (hipDeviceSynchronize() != hipSuccess) return -3;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), bytes) != hipSuccess) return -3;
+  static uint64_t zeros[kStampBlocks * kStampSlots];
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), zeros, bytes) != hipSuccess) return -3;
+  return 0;
+}
+namespace ddq {
+#endif
 #define DDQ_STR2(x) #x
 #define DDQ_STR(x) DDQ_STR2(x)
 #define CHECK_LAUNCH(x)                                             \
@@ -661,6 +679,42 @@ __device__ __forceinline__ void head_draw(const HeadArgs& H) {
   __syncthreads();                                // every thread has read the counter
   if (t == 0) H.dmeta->counter = ctr;
 }
+
+// K1's extra workgroup (small.h): the fused apply's latch, then the draw
+// counter's advance or the next step's draw (launch_head's, for S = 16)
+namespace sm16 {
+__device__ void book_block(const BookArgs& k) {
+  if (k.latch && threadIdx.x == 0) {
+    k.latch[2] = (k.latch[0] == 0);
+    k.latch[3] = k.period > 0 && ((*k.iter + k.inc) % k.period) == 0;
+  }
+  if (k.dmeta) {
+    __shared__ int64_t cand[256];
+    __shared__ int bad_any;
+    const uint64_t ctr = k.dmeta->counter + 1;
+    draw_sorted(k.dmeta, k.B, k.dseed, ctr, cand, &bad_any);
+    const int t = threadIdx.x;
+    if (t < k.B) {
+      k.didx[t] = (int32_t)cand[t];
+      log_draw(k.dlog, k.dlog_cap, ctr, k.B, t, (int32_t)cand[t]);
+    }
+    __syncthreads();
+    if (t == 0) k.dmeta->counter = ctr;
+  } else if (k.bump && threadIdx.x == 0) {
+    k.bump->counter += 1;
+  }
+}
+
+hipError_t launch_tower_fwd16(const TowerArgs& t, hipStream_t s) {
+  constexpr int K2 = 6, K3 = 5;
+  auto kern = tower_fwd16_kernel<K2, K3>;
+  static std::atomic<uint64_t> attr{0};
+  if (hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(kern), attr, kFwdSmem)) return e;
+  const bool book = t.bk.latch || t.bk.bump || t.bk.dmeta;
+  ddq_launch(kern, dim3(t.B * t.nz + (book ? 1 : 0)), dim3(kThreads), kFwdSmem, s, t);
+  return hipGetLastError();
+}
+}  // namespace sm16
 
 // One head block b
 __device__ __forceinline__ void head_body(const HeadArgs& H, int b, char* smem) {
@@ -1563,6 +1617,10 @@ hipError_t launch_apply(const NetBuffers& nb, int rule, float lr, float decay, f
   return hipGetLastError();
 }
 
+}  // namespace ddq
+#include "small_bwd.h"
+namespace ddq {
+
 // ---------------------------------------------------------------------------
 // layer geometry
 // ---------------------------------------------------------------------------
@@ -1713,13 +1771,39 @@ __global__ __launch_bounds__(512) void fc4_bwd_kernel(const Fc4DgradArgs d, cons
         make_float4(g[r][0], g[r][1], g[r][2], g[r][3]);
 }
 
+// K1 of the S = 16 step (small.h); bk: its extra workgroup's bookkeeping
+static sm16::TowerArgs tower_args(const NetBuffers& nb, int nz, const sm16::BookArgs* bk) {
+  const ParamLayout& L = nb.L;
+  sm16::TowerArgs t{};
+  t.B = nb.B; t.nz = nz;
+  t.in[0] = nb.state; t.in[1] = nb.next_state;
+  for (int z = 0; z < 2; ++z) {
+    t.wks[z] = nb.wks[z];
+    t.bias1[z] = nb.theta[z] + L.b[0];
+    t.bias2[z] = nb.theta[z] + L.b[1];
+    t.bias3[z] = nb.theta[z] + L.b[2];
+    t.pool3[z] = nb.pool3[z];
+  }
+  t.wks_plane = L.wks_total; t.wks_off2 = L.wks_off[1]; t.wks_off3 = L.wks_off[2];
+  t.pool1s = nb.pool1s[0]; t.pool2s = nb.pool2s[0];
+  t.mask1 = nb.mask1; t.mask2 = nb.mask2; t.mask3 = nb.mask3;
+  if (bk) t.bk = *bk;
+  return t;
+}
+
 hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
                           void (*mark)(void*, const char*), void* marg, bool out) {
   const ParamLayout& L = nb.L;
   const int B = nb.B, S = nb.S;
   auto M = [&](const char* n) { if (mark) mark(marg, n); };
   const float* in[2] = {nb.state, nb.next_state};
-  if (!nb.fwd_only || nb.fwd_only == 1) {
+  // deepq16: conv1 -> pool3 of each (image, tower) in one workgroup (small.h)
+  const bool tower = !nb.fwd_only && S == sm16::kS;
+  if (tower) {
+    M("tower_fwd");
+    CHECK_LAUNCH(sm16::launch_tower_fwd16(tower_args(nb, nz, nullptr), s));
+  }
+  if (!tower && (!nb.fwd_only || nb.fwd_only == 1)) {
     // conv1 (train_val.prototxt:39-78): bf16 matrix cores, fp32-exact
     // (split.h): frames are exact in bf16, so 3 MFMAs per 32x32x16 block; the
     // pooled output goes out split (conv2's input) and, for the Q tower, fp32
@@ -1738,7 +1822,7 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     M("conv1_fwd");
     CHECK_LAUNCH(pick_tile(kConv1Fwd, S, S).launch(c1, nz, s, L.wks_total));
   }
-  if (!nb.fwd_only || nb.fwd_only == 2) {
+  if (!tower && (!nb.fwd_only || nb.fwd_only == 2)) {
     // conv2 (train_val.prototxt:79-118): split bf16, 16x16 tiles, 16 waves of
     // one 32x32 block each (kConv2Fwd: edge-fitting tiles on other maps)
     const int H = S / 2;
@@ -1758,7 +1842,7 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     M("conv2_fwd");
     CHECK_LAUNCH(pick_tile(kConv2Fwd, H, H).launch(a2, nz, s));
   }
-  if (!nb.fwd_only || nb.fwd_only == 3) {
+  if (!tower && (!nb.fwd_only || nb.fwd_only == 3)) {
     // conv3 (train_val.prototxt:119-158): split bf16, 8x8 tiles (kConv3Fwd), two k groups
     // of 4 waves; pool3 (= fc4's input) fp32 in Caffe order, routing bytes
     // NHWC (the backward expands dpool3 through them)
@@ -1794,6 +1878,118 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
                      nb.theta[0] + L.w[4], nb.theta[0] + L.b[4], nb.theta[1] + L.w[4],
                      nb.theta[1] + L.b[4], nb.h4[0], nb.h4[1], nb.q_out, nb.p_out);
   CHECK_LAUNCH(hipGetLastError());
+  return hipSuccess;
+}
+
+hipError_t launch_small_fwd_head(const NetBuffers& nb, hipStream_t s,
+                                 void (*mark)(void*, const char*), void* marg, ReplayMeta* bump,
+                                 const Prefetch* pf) {
+  const ParamLayout& L = nb.L;
+  auto M = [&](const char* n) { if (mark) mark(marg, n); };
+  // the head's bookkeeping (launch_head / head_args), by K1's extra workgroup
+  sm16::BookArgs bk{};
+  bk.latch = nb.fa.on ? nb.opt_init : nullptr;
+  bk.iter = nb.iter; bk.period = nb.fa.period; bk.inc = nb.book_inc; bk.B = nb.B;
+  ReplayMeta* hb = (nb.fa.on || nb.head_bump) ? bump : nullptr;
+  if (pf && pf->ng > 0 && hb && nb.B <= 256) {
+    bk.dmeta = hb;
+    bk.didx = pf->idx; bk.dseed = pf->seed; bk.dlog = pf->idx_log; bk.dlog_cap = pf->log_cap;
+  } else {
+    bk.bump = hb;
+  }
+  M("tower_fwd");
+  CHECK_LAUNCH(sm16::launch_tower_fwd16(tower_args(nb, 2, &bk), s));
+  sm16::ChainArgs c{};
+  c.B = nb.B;
+  c.x[0] = nb.pool3[0]; c.x[1] = nb.pool3[1];
+  c.th[0] = nb.theta[0]; c.th[1] = nb.theta[1];
+  c.w4_off = L.w[3]; c.b4_off = L.b[3]; c.w5_off = L.w[4]; c.b5_off = L.b[4];
+  c.action = nb.action; c.reward = nb.reward; c.nonterm = nb.nonterm; c.gamma = nb.gamma;
+  c.qpart = nb.qpart; c.dpart = nb.dpart; c.sync = nb.csync;
+  c.q_out = nb.q_out; c.p_out = nb.p_out; c.q_sa = nb.q_sa; c.p_sa = nb.p_sa;
+  c.target = nb.target; c.loss = nb.loss; c.grad = nb.grad;
+  c.apply = nb.fa.on && !nb.fa.ext;
+  c.store_grad = nb.fa.store_grad;
+  c.aa = apply_args(nb, nb.fa.rule, nb.fa.lr, nb.fa.decay, nb.fa.eps, nb.fa.momentum, nb.fa.wd,
+                    nb.fa.period);
+  c.at = apply_tail(nb);
+  c.wks = nb.wks[0]; c.wks_plane = L.wks_total; c.wks2_off = L.wks_off[1];
+  c.wkst_off = L.wkst_off; c.wks3_off = L.wks_off[2]; c.wkst3_off = L.wkst3_off;
+  static std::atomic<uint64_t> attr{0};
+  CHECK_LAUNCH(ensure_dyn_lds(reinterpret_cast<const void*>(sm16::fc4_chain16_kernel), attr,
+                              sm16::kChainSmem));
+  M("fc4_chain");
+  ddq_launch(sm16::fc4_chain16_kernel, dim3(sm16::kFcBlk + sm16::kWkstBlocks), dim3(512),
+             sm16::kChainSmem, s, c);
+  CHECK_LAUNCH(hipGetLastError());
+  return hipSuccess;
+}
+
+void small_groups(int B, int* G2, int* G3) {
+  // conv2 tiles: groups of >= 2 images (16 at most: 160 workgroups); conv3
+  // tiles: 8 groups of >= 4 images (48 workgroups) -- co-resident with room
+  *G2 = std::max(1, std::min(16, B / 2));
+  *G3 = std::max(1, std::min(8, B / 4));
+}
+
+hipError_t launch_small_bwd(const NetBuffers& nb, hipStream_t s,
+                            void (*mark)(void*, const char*), void* marg, bool book,
+                            int book_period, ReplayMeta* bump, hipError_t (*fc4_done)(void*),
+                            void* fc4_done_arg, const Prefetch* pre) {
+  const ParamLayout& L = nb.L;
+  const int B = nb.B;
+  auto M = [&](const char* n) { if (mark) mark(marg, n); };
+  // fc4's weight gradient is final since K2: the overlapped all-reduce starts
+  if (fc4_done) CHECK_LAUNCH(fc4_done(fc4_done_arg));
+  {
+    sm16::BwdArgs a{};
+    a.B = B; a.dpart = nb.dpart;
+    a.mask1 = nb.mask1; a.mask2 = nb.mask2; a.mask3 = nb.mask3;
+    a.wks = nb.wks[0]; a.wks_plane = L.wks_total; a.wkst_off = L.wkst_off; a.wkst3_off = L.wkst3_off;
+    a.frames = nb.state;
+    a.dconv3x = nb.dconv3s; a.dconv2x = nb.dconv2x;
+    a.w1part = nb.wpart + nb.wpart_off[0]; a.w1_np = nb.wnp[0];
+    constexpr int K3 = 5, KD = 6;
+    auto kern = sm16::tower_bwd16_kernel<K3, KD>;
+    static std::atomic<uint64_t> attr{0};
+    CHECK_LAUNCH(ensure_dyn_lds(reinterpret_cast<const void*>(kern), attr, sm16::kBwdSmem));
+    M("tower_bwd");
+    ddq_launch(kern, dim3(B), dim3(sm16::kThreads), sm16::kBwdSmem, s, a);
+    CHECK_LAUNCH(hipGetLastError());
+  }
+  {
+    sm16::WgArgs w{};
+    w.B = B;
+    small_groups(B, &w.G2, &w.G3);
+    w.ipg2 = (B + w.G2 - 1) / w.G2; w.ipg3 = (B + w.G3 - 1) / w.G3;
+    w.pool1s = nb.pool1s[0]; w.pool2s = nb.pool2s[0];
+    w.dconv2x = nb.dconv2x; w.dconv3x = nb.dconv3s;
+    w.w1part = nb.wpart + nb.wpart_off[0]; w.w1_np = nb.wnp[0];
+    w.slab2 = nb.slab2; w.slab3 = nb.slab3;
+    w.sync = nb.csync + 8;
+    w.grad = nb.grad;
+    for (int l = 0; l < 3; ++l) { w.w_off[l] = L.w[l]; w.b_off[l] = L.b[l]; }
+    conv_dims(L, w.cd);
+    w.apply = nb.fa.on && !nb.fa.ext;
+    w.aa = apply_args(nb, nb.fa.rule, nb.fa.lr, nb.fa.decay, nb.fa.eps, nb.fa.momentum, nb.fa.wd,
+                      nb.fa.period);
+    w.at = apply_tail(nb);
+    w.book = book; w.book_period = book_period; w.book_inc = nb.book_inc;
+    w.iter = nb.iter;
+    w.bump = book && !nb.fa.on ? bump : nullptr;
+    if (pre && nb.fa.on) {
+      w.pf = *pre;
+      w.pf.predrawn = bump != nullptr && B <= 256;   // K1 drew it (its book block)
+    }
+    static std::atomic<uint64_t> attr{0};
+    CHECK_LAUNCH(ensure_dyn_lds(reinterpret_cast<const void*>(sm16::wgrad16_kernel), attr,
+                                sm16::kWgSmem));
+    M("wgrad_apply");
+    ddq_launch(sm16::wgrad16_kernel,
+               dim3(w.pf.ng + sm16::kT2 * w.G2 + sm16::kT3 * w.G3 + sm16::kW1Blocks), dim3(256),
+               sm16::kWgSmem, s, w);
+    CHECK_LAUNCH(hipGetLastError());
+  }
   return hipSuccess;
 }
 
