@@ -278,13 +278,17 @@ int ddq_create(ddq_ctx** out, int device, const ddq_net_desc* desc) {
     TRY(dalloc(c, &nb.dconv3, (size_t)B * S3 * S3 * 64));
     TRY(dalloc(c, &nb.dconv2s, (size_t)3 * B * S3 * S3 * 64));
     TRY(dalloc(c, &nb.dconv3s, (size_t)3 * B * S3 * S3 * 64));
+    if (S == 16) {   // K1 (tower_fwd16s): the pool2 halves' exchange; meeting words
+      TRY(dalloc(c, &nb.xchg, (size_t)B * 2 * 2 * 1536));
+      TRY(dalloc(c, &nb.pairc, (size_t)B * 2));
+      TRY(dalloc(c, &nb.csync, 64));
+    }
     // DDQ_NO_SMALL=1: the general kernels at S = 16 too (A/B, diagnosis)
     const char* ns = getenv("DDQ_NO_SMALL");
     nb.small = S == 16 && B <= 256 && !(ns && ns[0] == '1');
     if (nb.small) {
       TRY(dalloc(c, &nb.qpart, (size_t)32 * 2 * B * 4));
       TRY(dalloc(c, &nb.dpart, (size_t)32 * B * 256));
-      TRY(dalloc(c, &nb.csync, 64));
       TRY(dalloc(c, &nb.dconv2x, (size_t)3 * B * 4096));
       int G2, G3;
       small_groups(B, &G2, &G3);
@@ -378,6 +382,18 @@ int ddq_synchronize(ddq_ctx* c) {
   TRY(set_dev(c));
   if (c->cs) HIP_TRY(c, hipStreamSynchronize(c->cs));   // owner duties of async ticks
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (c->nb.csync) {                  // the small-map kernels' sticky spin-timeout words
+    int32_t w[64];
+    HIP_TRY(c, hipMemcpy(w, c->nb.csync, sizeof(w), hipMemcpyDeviceToHost));
+    const int at[3] = {2, 40, 48};
+    const char* who[3] = {"fc4 chain fan-in", "wgrad slab reduce", "tower pool2 exchange"};
+    for (int k = 0; k < 3; ++k)
+      if (w[at[k]]) {
+        HIP_TRY(c, hipMemset(c->nb.csync + at[k], 0, 4));
+        return fail(c, DDQ_ESTATE, "small-map step: %s meeting timed out (results invalid)",
+                    who[k]);
+      }
+  }
   return DDQ_OK;
 }
 

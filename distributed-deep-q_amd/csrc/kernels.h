@@ -98,10 +98,13 @@ struct NetBuffers {
   // deepq16 step (small.h, small_bwd.h): fc4 chain partials and its fan-in words
   int small;                        // S == 16, B <= 256: the four-launch step
   float *qpart, *dpart;             // [32][2][B][4] Q_out / P_out partials, [32][B][256] dpool3
-  int32_t* csync;                   // fan-in words: K2 [0..2] (arrivals, generation,
-                                    // timeout), K4 [8..40) (a pair per tile, timeout at 40)
+  int32_t* csync;                   // meeting words: K2 [0..2] (64-bit counter, timeout),
+                                    // K4 [8..40) (a 64-bit counter per tile, timeout at
+                                    // 40), K1's split form: timeout at 48
   __bf16* dconv2x;                  // split expanded dconv2 NHWC (B, 8, 8, 64) (K3 -> K4)
   float *slab2, *slab3;             // K4's per-group slabs of conv2 / conv3 tiles
+  __bf16* xchg;                     // K1 split form: pool2 halves [B][2][2][1536]
+  uint64_t* pairc;                  // K1 split form: meeting counters [B][2]
 };
 
 // fused device draw + gather for the step (B <= 256); counter advanced by the

@@ -515,7 +515,10 @@ hipError_t launch_u8_to_nhwc(const uint8_t* src, int n, int S, float* dst, hipSt
 // ---------------------------------------------------------------------------
 // Caffe (co,ci,ky,kx) -> kernel layout (co,ky,kx,ci) for the three convs
 // ---------------------------------------------------------------------------
-struct ConvDims { int64_t w_off, wks_off; int cout, cin, ks; };
+// wkst_off > 0 (deepq16 contexts): the layer's transposed + flipped split copy
+// for its data gradient, Wt[ci][T-1 - tap][co], is rewritten with the forward
+// layout by every update (no per-step transpose launch; small_bwd.h K3 reads it)
+struct ConvDims { int64_t w_off, wks_off; int cout, cin, ks; int64_t wkst_off = 0; };
 
 // e: Caffe-order element (co, ci, ky, kx) of the layer's weight (< 2^31);
 // returns its offset in the split forward layout (split.h):
@@ -536,6 +539,12 @@ __device__ __forceinline__ int wks_local(const ConvDims& d, int e) {
 __device__ __forceinline__ void put_conv_weight(const ConvDims& d, int e, float v, __bf16* wks,
                                                 int64_t wks_plane) {
   store_split(wks, wks_plane, d.wks_off + wks_local(d, e), v);
+  if (d.wkst_off) {
+    const int kk = d.ks * d.ks, per = d.cin * kk;
+    const int co = e / per, rem = e - co * per;
+    const int ci = rem / kk, tap = rem - ci * kk;
+    store_split(wks, wks_plane, d.wkst_off + ((int64_t)ci * kk + kk - 1 - tap) * d.cout + co, v);
+  }
 }
 
 __global__ void relayout_kernel(const float* __restrict__ theta, __bf16* __restrict__ wks,
@@ -550,6 +559,10 @@ __global__ void relayout_kernel(const float* __restrict__ theta, __bf16* __restr
 static void conv_dims(const ParamLayout& L, ConvDims* d) {
   const int cout[3] = {32, 64, 64}, cin[3] = {4, 32, 64}, ks[3] = {7, 5, 3};
   for (int i = 0; i < 3; ++i) d[i] = {L.w[i], L.wks_off[i], cout[i], cin[i], ks[i]};
+  if (L.S == sm16::kS) {   // deepq16: the data gradients' copies with every update
+    d[1].wkst_off = L.wkst_off;
+    d[2].wkst_off = L.wkst3_off;
+  }
 }
 
 hipError_t launch_relayout(const NetBuffers& nb, int z, hipStream_t s) {
@@ -706,11 +719,22 @@ __device__ void book_block(const BookArgs& k) {
 }
 
 hipError_t launch_tower_fwd16(const TowerArgs& t, hipStream_t s) {
+  const bool book = t.bk.latch || t.bk.bump || t.bk.dmeta;
+  if (t.xchg && 2 * t.B * t.nz <= 256) {
+    // split form: two workgroups per (image, tower), every pair resident at
+    // once (<= 256 workgroups of one per CU: their meet cannot wait on an
+    // undispatched partner)
+    constexpr int K2 = 5, K3 = 4;   // (tap pairs in flight)
+    auto kern = tower_fwd16s_kernel<K2, K3>;
+    static std::atomic<uint64_t> attr{0};
+    if (hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(kern), attr, kFwdSmemS)) return e;
+    ddq_launch(kern, dim3(2 * t.B * t.nz + (book ? 1 : 0)), dim3(kThreads), kFwdSmemS, s, t);
+    return hipGetLastError();
+  }
   constexpr int K2 = 6, K3 = 5;
   auto kern = tower_fwd16_kernel<K2, K3>;
   static std::atomic<uint64_t> attr{0};
   if (hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(kern), attr, kFwdSmem)) return e;
-  const bool book = t.bk.latch || t.bk.bump || t.bk.dmeta;
   ddq_launch(kern, dim3(t.B * t.nz + (book ? 1 : 0)), dim3(kThreads), kFwdSmem, s, t);
   return hipGetLastError();
 }
@@ -1788,6 +1812,8 @@ static sm16::TowerArgs tower_args(const NetBuffers& nb, int nz, const sm16::Book
   t.pool1s = nb.pool1s[0]; t.pool2s = nb.pool2s[0];
   t.mask1 = nb.mask1; t.mask2 = nb.mask2; t.mask3 = nb.mask3;
   if (bk) t.bk = *bk;
+  t.xchg = nb.xchg; t.pairc = nb.pairc;
+  t.timeout = nb.csync ? nb.csync + 48 : nullptr;   // (csync: allocated at S = 16)
   return t;
 }
 
@@ -1913,14 +1939,11 @@ hipError_t launch_small_fwd_head(const NetBuffers& nb, hipStream_t s,
   c.aa = apply_args(nb, nb.fa.rule, nb.fa.lr, nb.fa.decay, nb.fa.eps, nb.fa.momentum, nb.fa.wd,
                     nb.fa.period);
   c.at = apply_tail(nb);
-  c.wks = nb.wks[0]; c.wks_plane = L.wks_total; c.wks2_off = L.wks_off[1];
-  c.wkst_off = L.wkst_off; c.wks3_off = L.wks_off[2]; c.wkst3_off = L.wkst3_off;
   static std::atomic<uint64_t> attr{0};
   CHECK_LAUNCH(ensure_dyn_lds(reinterpret_cast<const void*>(sm16::fc4_chain16_kernel), attr,
                               sm16::kChainSmem));
   M("fc4_chain");
-  ddq_launch(sm16::fc4_chain16_kernel, dim3(sm16::kFcBlk + sm16::kWkstBlocks), dim3(512),
-             sm16::kChainSmem, s, c);
+  ddq_launch(sm16::fc4_chain16_kernel, dim3(sm16::kFcBlk), dim3(512), sm16::kChainSmem, s, c);
   CHECK_LAUNCH(hipGetLastError());
   return hipSuccess;
 }
@@ -1949,12 +1972,20 @@ hipError_t launch_small_bwd(const NetBuffers& nb, hipStream_t s,
     a.frames = nb.state;
     a.dconv3x = nb.dconv3s; a.dconv2x = nb.dconv2x;
     a.w1part = nb.wpart + nb.wpart_off[0]; a.w1_np = nb.wnp[0];
-    constexpr int K3 = 5, KD = 6;
-    auto kern = sm16::tower_bwd16_kernel<K3, KD>;
-    static std::atomic<uint64_t> attr{0};
-    CHECK_LAUNCH(ensure_dyn_lds(reinterpret_cast<const void*>(kern), attr, sm16::kBwdSmem));
     M("tower_bwd");
-    ddq_launch(kern, dim3(B), dim3(sm16::kThreads), sm16::kBwdSmem, s, a);
+    if (2 * B <= 256) {   // split form: two workgroups per image
+      constexpr int K3 = 5, KD = 5;   // (KD: tap pairs in flight)
+      auto kern = sm16::tower_bwd16s_kernel<K3, KD>;
+      static std::atomic<uint64_t> attr{0};
+      CHECK_LAUNCH(ensure_dyn_lds(reinterpret_cast<const void*>(kern), attr, sm16::kBwdSmem));
+      ddq_launch(kern, dim3(2 * B), dim3(sm16::kThreads), sm16::kBwdSmem, s, a);
+    } else {
+      constexpr int K3 = 5, KD = 6;
+      auto kern = sm16::tower_bwd16_kernel<K3, KD>;
+      static std::atomic<uint64_t> attr{0};
+      CHECK_LAUNCH(ensure_dyn_lds(reinterpret_cast<const void*>(kern), attr, sm16::kBwdSmem));
+      ddq_launch(kern, dim3(B), dim3(sm16::kThreads), sm16::kBwdSmem, s, a);
+    }
     CHECK_LAUNCH(hipGetLastError());
   }
   {
@@ -1981,13 +2012,20 @@ hipError_t launch_small_bwd(const NetBuffers& nb, hipStream_t s,
       w.pf = *pre;
       w.pf.predrawn = bump != nullptr && B <= 256;   // K1 drew it (its book block)
     }
+    // LDS: a round buffer per tile layer, two only where a group has more
+    // than one round (deepq16 B = 32: conv3's one round of 4 images, conv2's
+    // two of one -- 67.5 KB, two workgroups a CU)
+    const int r2 = (w.ipg2 + sm16::Wg2::NI - 1) / sm16::Wg2::NI;
+    const int r3 = (w.ipg3 + sm16::Wg3::NI - 1) / sm16::Wg3::NI;
+    const int lds = std::max({(r2 > 1 ? 2 : 1) * sm16::Wg2::BUF * 2,
+                              (r3 > 1 ? 2 : 1) * sm16::Wg3::BUF * 2, 4 * 16 * 64 * 4});
     static std::atomic<uint64_t> attr{0};
     CHECK_LAUNCH(ensure_dyn_lds(reinterpret_cast<const void*>(sm16::wgrad16_kernel), attr,
                                 sm16::kWgSmem));
     M("wgrad_apply");
     ddq_launch(sm16::wgrad16_kernel,
-               dim3(w.pf.ng + sm16::kT2 * w.G2 + sm16::kT3 * w.G3 + sm16::kW1Blocks), dim3(256),
-               sm16::kWgSmem, s, w);
+               dim3(sm16::kT3 * w.G3 + sm16::kT2 * w.G2 + sm16::kW1Blocks + w.pf.ng), dim3(256),
+               lds, s, w);
     CHECK_LAUNCH(hipGetLastError());
   }
   return hipSuccess;

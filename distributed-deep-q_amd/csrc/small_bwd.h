@@ -24,8 +24,9 @@ namespace sm16 {
 //            them, dpart[j][b][k] = sum_n dh4[b][n] W4[n][k] (K3 sums the 32
 //            partials in order); dW4 rows, db4, dW5 columns (and workgroup
 //            0: db5) -- all final here, so the fused apply updates them here.
-// The launch is 32 fc4 workgroups (all resident: one per CU at most) plus
-// 34 blocks of conv2's / conv3's transposed split weights (wkst_tap) for K3.
+// The launch is 32 fc4 workgroups (all resident: one per CU at most).  (The
+// transposed split weights K3 reads are rewritten by every update at S = 16:
+// kernels.hip put_conv_weight.)
 // ---------------------------------------------------------------------------
 constexpr int kFcN = 16;                 // fc4 outputs per workgroup
 constexpr int kFcBlk = 512 / kFcN;       // 32 workgroups
@@ -44,10 +45,11 @@ constexpr int CH_QP = CH_DH + kMaxB * kFcN;
 constexpr int CH_DQ = CH_QP + 2 * kMaxB * 4;
 constexpr int CH_TMP = CH_DQ + kMaxB * 4;          // squared errors [kMaxB]
 constexpr int CH_W5 = CH_TMP + kMaxB;             // Q's Q_out columns of the units [4][16]
-constexpr int kChainSmemF = CH_W5 + 64;
+constexpr int CH_PS = CH_W5 + 64;                 // theta / state of the 84 unit-sum params
+constexpr int CH_MB = CH_PS + 2 * 96;             // the minibatch's action (4), reward, nonterm
+constexpr int kChainSmemF = CH_MB + 6 * kMaxB;
 constexpr int kChainSmem = kChainSmemF * 4;
 static_assert(kChainSmem <= 160 * 1024, "K2 LDS");
-constexpr int kWkstBlocks = 25 + 9;
 
 struct ChainArgs {
   int B;
@@ -65,9 +67,6 @@ struct ChainArgs {
   int store_grad;                  // fused apply: W4's gradient to grad as well
   ApplyArgs aa;
   ApplyTail at;
-  // the transposed split weights of conv2 / conv3's data gradients (K3)
-  const __bf16* wks;
-  int64_t wks_plane, wks2_off, wkst_off, wks3_off, wkst3_off;
 };
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
@@ -76,33 +75,6 @@ typedef float f32x4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 ld_sc1_f4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 16);
   return __builtin_bit_cast(float4, v);
-}
-
-// n workgroups meet: returns in each once all n have arrived (their stores
-// write-through and drained: visible to sc1 loads, MI355X_MICROARCH.md
-// inter-workgroup visibility, table row 1).  One monotonic 64-bit counter per
-// meeting point, never reset: arrival `old` belongs to the group ending at
-// (old / n + 1) n, which its last arriver reaches with its own add (no
-// reset / generation round trips on the release path).  Bounded: a spin past
-// ~0.1 s records a timeout and goes on (wrong results, no hang).
-__device__ __forceinline__ void meet(uint64_t* ctr, uint32_t n, int32_t* timeout) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint64_t old = __hip_atomic_fetch_add(ctr, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t target = (old / n + 1) * n;
-    if (old + 1 != target) {
-      int spins = 0;
-      while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > (1 << 21)) {
-          __hip_atomic_store(timeout, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-    }
-  }
-  __syncthreads();
 }
 
 // Sum of 64 lanes' values in a fixed butterfly order (deterministic)
@@ -116,12 +88,6 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
   extern __shared__ __attribute__((aligned(16))) float csm[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int bid = blockIdx.x;
-  if (bid >= kFcBlk) {            // conv2's / conv3's transposed split weights
-    const int t = bid - kFcBlk;
-    if (t < 25) wkst_tap<32, 25>(c.wks, c.wks_plane, c.wks2_off, c.wkst_off, t, reinterpret_cast<char*>(csm));
-    else wkst_tap<64, 9>(c.wks, c.wks_plane, c.wks3_off, c.wkst3_off, t - 25, reinterpret_cast<char*>(csm));
-    return;
-  }
   DDQ_STAMP(16);
   const int B = c.B, n0 = bid * kFcN;
   const int nch = (B + kBC - 1) / kBC;
@@ -163,6 +129,20 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
   }
   DDQ_XLOAD(0)
   float w5q = tid < 64 ? c.th[0][c.w5_off + (tid >> 4) * 512 + n0 + (tid & 15)] : 0.f;
+  // theta / optimizer state of the parameters the unit sums update (db4 and
+  // dW5 columns of the units: q = 0..79; b5: q = 80..83, workgroup 0), read
+  // now so phase B's updates wait on no load
+  auto uparam = [&](int q) -> int64_t {
+    return q < 80 ? ((q >> 4) == 0 ? c.b4_off + n0 + (q & 15) : c.w5_off + ((q >> 4) - 1) * 512 + n0 + (q & 15))
+                  : c.b5_off + (q - 80);
+  };
+  float pth = 0.f, pst = 0.f;
+  const bool ap0 = c.apply != 0;
+  if (ap0 && tid < 84) {
+    const int64_t i = uparam(tid);
+    pth = c.at.theta[i];
+    if (c.aa.rule != 0) pst = c.at.opt[i];
+  }
   float b4v[4], w5v[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -178,6 +158,9 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
     *reinterpret_cast<float4*>(WS + (z * kFcN + n) * kXP + 4 * k4) = wv[u];
   }
   if (tid < 64) csm[CH_W5 + tid] = w5q;
+  if (tid < 84) { csm[CH_PS + tid] = pth; csm[CH_PS + 96 + tid] = pst; }
+  for (int e = tid; e < 6 * B; e += 512)             // action one-hot, reward, non_terminal
+    csm[CH_MB + e] = e < 4 * B ? c.action[e] : (e < 5 * B ? c.reward[e - 4 * B] : c.nonterm[e - 5 * B]);
 
   // ---- phase A, chunk by chunk of 32 images ----
   for (int ch = 0; ch < nch; ++ch) {
@@ -257,14 +240,14 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
   for (int b = tid; b < B; b += 512) {
     const float* qp = QP + b * 4;
     const float* pp = QP + (kMaxB + b) * 4;
-    const float* ac = c.action + b * 4;
+    const float* ac = csm + CH_MB + b * 4;
     float qs = qp[0] * ac[0];
     qs += qp[1] * ac[1];
     qs += qp[2] * ac[2];
     qs += qp[3] * ac[3];
     float ps = fmaxf(fmaxf(pp[0], pp[1]), fmaxf(pp[2], pp[3]));
-    ps = ps * c.nonterm[b];
-    const float tg = c.gamma * ps + 1.0f * c.reward[b];
+    ps = ps * csm[CH_MB + 5 * B + b];
+    const float tg = c.gamma * ps + 1.0f * csm[CH_MB + 4 * B + b];
     const float diff = qs - tg;
     const float gsc = diff / (float)B;
 #pragma unroll
@@ -290,36 +273,53 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
   __syncthreads();
   // loss, db5 (workgroup 0) and db4, dW5 of the units: sums over the batch,
   // lane l taking samples l, l + 64, ... in order, then a fixed butterfly
-  // across the wave (deterministic)
+  // across the wave -- a wave's 11 quantities side by side (independent
+  // shuffles), deterministic
   {
-    const int nq = (bid == 0 ? 5 : 0) + 5 * kFcN;   // [5 (wg 0): db5 0..3, loss] + 80 unit sums
-    for (int qq = wid; qq < nq; qq += 8) {
-      const bool head = bid == 0 && qq < 5;
-      const int q = head ? qq : qq - (bid == 0 ? 5 : 0);
-      float p = 0.f;
+    constexpr int QW = 11;                           // quantities a wave: 8 x 11 >= 85
+    const int hq = bid == 0 ? 5 : 0, nq = hq + 5 * kFcN;
+    float p[QW];
+#pragma unroll
+    for (int j = 0; j < QW; ++j) {
+      const int qq = wid + 8 * j;
+      p[j] = 0.f;
+      if (qq >= nq) continue;                        // (wave-uniform)
+      const bool head = qq < hq;
+      const int q = head ? qq : qq - hq;
       for (int b = lane; b < B; b += 64) {
-        if (head) p += q < 4 ? DQ[b * 4 + q] : TMP[b];
+        if (head) p[j] += q < 4 ? DQ[b * 4 + q] : TMP[b];
         else {
-          const int r = q >> 4, n = q & 15;       // r 0: db4, 1..4: dW5[r - 1]
-          p += r == 0 ? DH[b * kFcN + n] : DQ[b * 4 + r - 1] * H[b * kFcN + n];
+          const int r = q >> 4, n = q & 15;          // r 0: db4, 1..4: dW5[r - 1]
+          p[j] += r == 0 ? DH[b * kFcN + n] : DQ[b * 4 + r - 1] * H[b * kFcN + n];
         }
       }
-      const float v = wave_sum(p);
-      if (lane == 0) {
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+      for (int j = 0; j < QW; ++j) p[j] += __shfl_xor(p[j], o);
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < QW; ++j) {
+        const int qq = wid + 8 * j;
+        if (qq >= nq) continue;
+        const bool head = qq < hq;
+        const int q = head ? qq : qq - hq;
+        const float v = p[j];
         if (head && q == 4) {
           *c.loss = v / (float)B / 2.f;
-        } else {
-          const int r = q >> 4, n = q & 15;
-          const int64_t i = head ? c.b5_off + q : (r == 0 ? c.b4_off + n0 + n : c.w5_off + (r - 1) * 512 + n0 + n);
-          const bool is_bias = head || r == 0;
-          c.grad[i] = v;
-          if (ap) {
-            float st = (c.aa.rule != 0 && !first) ? c.at.opt[i] : 0.f;
-            const float th = apply_rule(c.aa, first, is_bias, c.at.theta[i], v, st);
-            c.at.theta[i] = th;
-            if (c.aa.rule != 0) c.at.opt[i] = st;
-            if (sync) c.at.thetaP[i] = th;
-          }
+          continue;
+        }
+        const int pq = head ? 80 + q : q;            // the preloaded parameter's slot
+        const int64_t i = uparam(pq);
+        const bool is_bias = head || (q >> 4) == 0;
+        c.grad[i] = v;
+        if (ap) {
+          float st = (c.aa.rule != 0 && !first) ? csm[CH_PS + 96 + pq] : 0.f;
+          const float th = apply_rule(c.aa, first, is_bias, csm[CH_PS + pq], v, st);
+          c.at.theta[i] = th;
+          if (c.aa.rule != 0) c.at.opt[i] = st;
+          if (sync) c.at.thetaP[i] = th;
         }
       }
     }
@@ -816,6 +816,374 @@ __global__ __launch_bounds__(kThreads) void tower_bwd16_kernel(const BwdArgs a) 
 }
 
 
+// K3, split form (2 B <= 256 workgroups): two workgroups per image, h = the
+// half of conv2's data-gradient channels (conv1's output channels) each
+// computes -- and so of conv1's weight-gradient rows.  Both compute conv3's
+// data gradient in full (no exchange: conv2's data gradient needs all of
+// dconv2).  conv2's data gradient on 16x16x32: waves (m block of 16 pixels,
+// 32-channel k step) = 4 x 2; the dconv2 image at pixel stride 80 (MF 1).
+constexpr int DS_CS = 80;                                              // dconv2 image (MF 1)
+constexpr int WDH_CW = 80, WDH_PL = 16 * WDH_CW, WDH_SLOT = 3 * WDH_PL;  // conv2 dgrad half taps
+constexpr int WDHP_SLOT = 2 * WDH_SLOT;                                // a pair of taps
+constexpr int BS_RED2 = B_RING2;                                      // (over the dead ring)
+static_assert(12 * DS_CS <= D2_RS && B_RING2 + 3 * WDHP_SLOT * 2 <= B_HALO, "K3 split LDS");
+
+// conv2 data-gradient half tap pairs (taps 2s, 2s + 1; 25 repeats 24)
+struct WDHPair {
+  u32x4 r[2];
+  __device__ __forceinline__ void load(const __bf16* __restrict__ wk, int64_t plane, int s,
+                                       int half, int tid) {
+    const int f = tid < 384 ? tid : 383;
+    const int p = f >> 7, q = f & 127, n = q >> 3, c8 = q & 7;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int tap = min(2 * s + u, 24);
+      r[u] = *reinterpret_cast<const u32x4*>(wk + p * plane + ((16 * half + n) * 25 + tap) * 64 + 8 * c8);
+    }
+  }
+  __device__ __forceinline__ void store(__bf16* slot, int tid) const {
+    if (tid >= 384) return;
+    const int p = tid >> 7, q = tid & 127, n = q >> 3, c8 = q & 7;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      *reinterpret_cast<u32x4*>(slot + u * WDH_SLOT + p * WDH_PL + n * WDH_CW + 8 * c8) = r[u];
+  }
+};
+// conv2 data-gradient half taps: 3 planes x 16 ci x 64 co = 384 vectors
+struct WDHTap {
+  u32x4 r;
+  __device__ __forceinline__ void load(const __bf16* __restrict__ wk, int64_t plane, int tap,
+                                       int half, int tid) {
+    const int f = tid < 384 ? tid : 383;
+    const int p = f >> 7, q = f & 127, n = q >> 3, c8 = q & 7;
+    r = *reinterpret_cast<const u32x4*>(wk + p * plane + ((16 * half + n) * 25 + tap) * 64 + 8 * c8);
+  }
+  __device__ __forceinline__ void store(__bf16* slot, int tid) const {
+    if (tid >= 384) return;
+    const int p = tid >> 7, q = tid & 127, n = q >> 3, c8 = q & 7;
+    *reinterpret_cast<u32x4*>(slot + p * WDH_PL + n * WDH_CW + 8 * c8) = r;
+  }
+};
+
+template <int K3, int KD>
+__global__ __launch_bounds__(kThreads) void tower_bwd16s_kernel(const BwdArgs a) {
+  static_assert(K3 >= 3 && KD >= 3, "ring: tap t + 2 is stored from registers at tap t");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int l31 = lane & 31, h = lane >> 5;
+  const int b = blockIdx.x >> 1, half = blockIdx.x & 1, B = a.B;
+  DDQ_STAMP(8);
+  const __bf16* __restrict__ wt3 = a.wks + a.wkst3_off;
+  const __bf16* __restrict__ wt2 = a.wks + a.wkst_off;
+  const int64_t wpl = a.wks_plane;
+  __bf16* D3 = reinterpret_cast<__bf16*>(smem + B_D3);
+  __bf16* D2 = reinterpret_cast<__bf16*>(smem + B_D2);
+  uint8_t* m3 = reinterpret_cast<uint8_t*>(smem + B_M3);
+  uint8_t* m2 = reinterpret_cast<uint8_t*>(smem + B_M2);
+  uint8_t* m1 = reinterpret_cast<uint8_t*>(smem + B_M1);
+  float* dp3 = reinterpret_cast<float*>(smem + B_DP3);
+  float* scr = reinterpret_cast<float*>(smem + B_SCR);
+  __bf16* ring3 = reinterpret_cast<__bf16*>(smem + B_RING3);
+  __bf16* ring2 = reinterpret_cast<__bf16*>(smem + B_RING2);
+  float* red2 = reinterpret_cast<float*>(smem + BS_RED2);
+  __bf16* X = reinterpret_cast<__bf16*>(smem + B_X1);
+  __bf16* halo = reinterpret_cast<__bf16*>(smem + B_HALO);
+  float* bsm = reinterpret_cast<float*>(smem + B_BIAS);
+
+  // ---- prologue: dpool3's partials (4 float4 a thread: group jg = tid / 64
+  // sums j = 4 jg .. 4 jg + 3 of float4 k4 = tid % 64), the routing bytes,
+  // then the first taps of both weight streams and the frames' halo ----
+  float4 pv[4];
+  {
+    const int k4 = tid & 63, jg = tid >> 6;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      pv[u] = *reinterpret_cast<const float4*>(a.dpart + ((int64_t)(4 * jg + u) * B + b) * 256 + 4 * k4);
+  }
+  u32x4 mv = u32x4{0u, 0u, 0u, 0u};
+  if (tid < 16) mv = reinterpret_cast<const u32x4*>(a.mask3 + (size_t)b * 256)[tid];
+  else if (tid < 80) mv = reinterpret_cast<const u32x4*>(a.mask2 + (size_t)b * 1024)[tid - 16];
+  else if (tid < 208) mv = reinterpret_cast<const u32x4*>(a.mask1 + (size_t)b * 2048)[tid - 80];
+  W3Tap w3[K3];
+#pragma unroll
+  for (int k = 0; k < K3; ++k) w3[k].load(wt3, wpl, k, tid);
+  // frames halo (conv1's weight gradient): 22 x 22 pixels, zero outside
+  float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
+  {
+    const int hy = tid / 22, hx = tid - 22 * (tid / 22);
+    const int gy = hy - 3, gx = hx - 3;
+    if (tid < 484 && (unsigned)gy < 16u && (unsigned)gx < 16u)
+      hv = *reinterpret_cast<const float4*>(a.frames + (((size_t)b * 16 + gy) * 16 + gx) * 4);
+  }
+  // zero the dconv3 image (halo + unrouted), then the sums
+  for (int f = tid; f < (3 * P2_PL) / 8; f += kThreads) reinterpret_cast<u32x4*>(D3)[f] = u32x4{0u, 0u, 0u, 0u};
+  {
+    float4 s4 = pv[0];
+#pragma unroll
+    for (int u = 1; u < 4; ++u) { s4.x += pv[u].x; s4.y += pv[u].y; s4.z += pv[u].z; s4.w += pv[u].w; }
+    reinterpret_cast<float4*>(scr)[tid] = s4;                 // [jg][k4]
+  }
+  if (tid < 16) reinterpret_cast<u32x4*>(m3)[tid] = mv;
+  else if (tid < 80) reinterpret_cast<u32x4*>(m2)[tid - 16] = mv;
+  else if (tid < 208) reinterpret_cast<u32x4*>(m1)[tid - 80] = mv;
+  __syncthreads();
+  if (tid < 256) {                                            // groups summed in order
+    float v = scr[tid];
+#pragma unroll
+    for (int g = 1; g < 8; ++g) v += scr[g * 256 + tid];
+    dp3[tid] = v;                                             // Caffe k = c * 4 + y * 2 + x
+  }
+  __syncthreads();
+  // dconv3 (4 x 4 x 64): dpool3 at the routed quadrant of each 2 x 2 window
+  for (int e = tid; e < 1024; e += kThreads) {
+    const int px = e >> 6, c = e & 63, y = px >> 2, x = px & 3;
+    const int pw = (y >> 1) * 2 + (x >> 1);
+    const int q = ((y & 1) << 1) | (x & 1);
+    const float v = m3[pw * 64 + c] == q ? dp3[c * 4 + pw] : 0.f;
+    lds_split3(D3 + (y + 1) * P2_RS + (x + 1) * P2_CS + c, P2_PL, v);
+  }
+  w3[0].store(ring3, tid);
+  w3[1].store(ring3 + W3_SLOT, tid);
+  __syncthreads();
+  DDQ_STAMP(9);
+
+  // ---- conv3 data gradient: 9 taps on 16x16x32 (K1's conv3 loop) ----
+  WDHPair wd[KD];
+  const int wn3 = wid & 3, wk3g = wid >> 2;
+  const int r16 = lane & 15, kq = lane >> 4;
+  {
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f}, cor = {0.f, 0.f, 0.f, 0.f};
+    const int win = r16 >> 2, y = 2 * (win >> 1) + ((r16 >> 1) & 1), x = 2 * (win & 1) + (r16 & 1);
+    const int abase = y * P2_RS + x * P2_CS + 32 * wk3g + 8 * kq;
+    const int bbase = (16 * wn3 + r16) * W3_CW + 32 * wk3g + 8 * kq;
+    bf16x8 av[2][3], bv[2][3];
+    auto ops = [&](int t, int set) {
+      const __bf16* wb = ring3 + (t % 3) * W3_SLOT;
+      const __bf16* pa = D3 + (t / 3) * P2_RS + (t % 3) * P2_CS;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        av[set][p] = *reinterpret_cast<const bf16x8*>(pa + p * P2_PL + abase);
+        bv[set][p] = *reinterpret_cast<const bf16x8*>(wb + p * W3_PL + bbase);
+      }
+    };
+    ops(0, 0);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      if (t + K3 < 9) {
+        w3[(t + K3) % K3].load(wt3, wpl, t + K3, tid);
+      } else if (t + K3 - 9 < KD) {   // conv2's data-gradient taps under conv3's last ones
+        wd[t + K3 - 9].load(wt2, wpl, t + K3 - 9, half, tid);
+      }
+      if (t + 1 < 9) ops(t + 1, (t + 1) & 1);
+      const int c = t & 1;
+      cor = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[c][2], bv[c][0], cor, 0, 0, 0);
+      cor = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[c][1], bv[c][1], cor, 0, 0, 0);
+      cor = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[c][0], bv[c][2], cor, 0, 0, 0);
+      cor = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[c][1], bv[c][0], cor, 0, 0, 0);
+      cor = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[c][0], bv[c][1], cor, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[c][0], bv[c][0], acc, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + 2 < 9) w3[(t + 2) % K3].store(ring3 + ((t + 2) % 3) * W3_SLOT, tid);
+      __syncthreads();
+    }
+    acc += cor;
+    DDQ_STAMP(10);
+    if (wk3g == 1) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) scr[(wn3 * 4 + e) * 64 + lane] = acc[e];
+    }
+    // zero the dconv2 image (over the dead ring) while the sums land
+    for (int f = tid; f < (3 * D2_PL) / 8; f += kThreads) reinterpret_cast<u32x4*>(D2)[f] = u32x4{0u, 0u, 0u, 0u};
+    // the conv2 data-gradient taps conv3's tail did not issue (it has K3 steps)
+#pragma unroll
+    for (int k = (K3 < 9 ? K3 : 9); k < KD; ++k) wd[k].load(wt2, wpl, k, half, tid);   // (pairs)
+    __syncthreads();
+    if (wk3g == 0) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] += scr[(wn3 * 4 + e) * 64 + lane];
+      // lane: dpool2 at pool2 pixels of window kq (rows 4 kq + i), channel
+      // 16 wn3 + r16 -> the routed quadrant of its 2 x 2 conv2-output window
+      const int c = 16 * wn3 + r16;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int y = 2 * (kq >> 1) + (i >> 1), x = 2 * (kq & 1) + (i & 1);
+        const int q = m2[(y * 4 + x) * 64 + c];
+        if (q < 4)
+          lds_split3(D2 + (2 * y + (q >> 1) + 2) * D2_RS + (2 * x + (q & 1) + 2) * DS_CS + c, D2_PL,
+                     acc[i]);
+      }
+    }
+  }
+  __syncthreads();
+  wd[0].store(ring2, tid);
+  wd[1].store(ring2 + WDHP_SLOT, tid);
+  __syncthreads();
+  DDQ_STAMP(11);
+
+  // ---- conv2 data gradient, channels [16 half, +16): 25 taps on 16x16x32;
+  // waves (m block of 16 pixels, k step of 32 co) = 4 x 2 ----
+  {
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    const int mb = wid & 3, kk = wid >> 2;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f}, cor = {0.f, 0.f, 0.f, 0.f};
+    const int m = 16 * mb + r16;
+    const int win = m >> 2, y = 2 * (win >> 2) + ((m >> 1) & 1), x = 2 * (win & 3) + (m & 1);
+    const int abase = y * D2_RS + x * DS_CS + 32 * kk + 8 * kq;
+    const int bbase = r16 * WDH_CW + 32 * kk + 8 * kq;
+    // 13 steps of a tap pair (2s, 2s + 1): one barrier a pair
+    bf16x8 av[2][2][3], bv[2][2][3];
+    auto ops = [&](int st, int set) {
+      const __bf16* wb = ring2 + (st % 3) * WDHP_SLOT;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int t = min(2 * st + u, 24);
+        const __bf16* pa = D2 + (t / 5) * D2_RS + (t % 5) * DS_CS;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          av[set][u][p] = *reinterpret_cast<const bf16x8*>(pa + p * D2_PL + abase);
+          bv[set][u][p] = *reinterpret_cast<const bf16x8*>(wb + u * WDH_SLOT + p * WDH_PL + bbase);
+        }
+      }
+    };
+    constexpr int NS = 13;
+    ops(0, 0);
+#pragma unroll
+    for (int st = 0; st < NS; ++st) {
+      if (st + KD < NS) wd[(st + KD) % KD].load(wt2, wpl, st + KD, half, tid);
+      if (st + 1 < NS) ops(st + 1, (st + 1) & 1);
+      const int c = st & 1;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (2 * st + u >= 25) continue;
+        cor = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[c][u][2], bv[c][u][0], cor, 0, 0, 0);
+        cor = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[c][u][1], bv[c][u][1], cor, 0, 0, 0);
+        cor = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[c][u][0], bv[c][u][2], cor, 0, 0, 0);
+        cor = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[c][u][1], bv[c][u][0], cor, 0, 0, 0);
+        cor = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[c][u][0], bv[c][u][1], cor, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[c][u][0], bv[c][u][0], acc, 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (st + 2 < NS) wd[(st + 2) % KD].store(ring2 + ((st + 2) % 3) * WDHP_SLOT, tid);
+      __syncthreads();
+    }
+    acc += cor;
+    DDQ_STAMP(12);
+    // the two k steps meet in LDS, summed in order by k step 0
+    if (kk == 1) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red2[(mb * 4 + e) * 64 + lane] = acc[e];
+    }
+    __syncthreads();
+    float bsum = 0.f;
+    if (kk == 0) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] += red2[(mb * 4 + e) * 64 + lane];
+    }
+    __syncthreads();
+    for (int f = tid; f < (3 * X1_PL) / 8; f += kThreads) reinterpret_cast<u32x4*>(X)[f] = u32x4{0u, 0u, 0u, 0u};
+    if (tid < 484) {   // the frames' halo (fp32 -> bf16 exact), pixel stride 4 bf16
+      const int hy = tid / 22, hx = tid - 22 * (tid / 22);
+      __bf16 q4[4] = {(__bf16)hv.x, (__bf16)hv.y, (__bf16)hv.z, (__bf16)hv.w};
+      *reinterpret_cast<uint2*>(halo + hy * X1_IROW + 4 * hx) = *reinterpret_cast<uint2*>(q4);
+    }
+    __syncthreads();
+    if (kk == 0) {
+      // lane: dpool1 at pixels 16 mb + 4 kq + i (window 4 mb + kq of the 8 x 8
+      // pool1 grid), channel 16 half + r16 -> pool1's routed quadrant of
+      // dconv1, stored at image channel r16 (channels 16..31 stay zero)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int wn = 4 * mb + kq;
+        const int y = 2 * (wn >> 2) + (i >> 1), x = 2 * (wn & 3) + (i & 1);
+        const int q = m1[(y * 8 + x) * 32 + 16 * half + r16];
+        if (q < 4) {
+          bsum += acc[i];
+          lds_split3(X + ((2 * y + (q >> 1)) * 16 + 2 * x + (q & 1)) * 32 + r16, X1_PL, acc[i]);
+        }
+      }
+    }
+    bsm[tid] = bsum;
+  }
+  __syncthreads();
+  DDQ_STAMP(13);
+
+  // ---- conv1's weight gradient (split.h w1_tile_wgrad, one 16-pixel segment
+  // per row): wave u < 7 = tap row ky, 16 conv1 rows x 3 MFMAs ----
+  {
+    const int gq = lane >> 4, iq = (lane & 15) >> 2, ip = lane & 3;
+    const int pix0 = 8 * (gq >> 1) + iq;
+    const int chn = 16 * (gq & 1) + 4 * ip;
+    f32x16 wacc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) wacc[e] = 0.f;
+    if (wid < 7) {
+      const int ky = wid;
+      const __bf16* pa0 = X + pix0 * 32 + chn;
+      const __bf16* pb0 = halo + ky * X1_IROW + 4 * pix0 + chn;
+#pragma unroll 4
+      for (int row = 0; row < 16; ++row) {
+        bf16x8 av[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          const __bf16* pa = pa0 + p * X1_PL + row * 16 * 32;
+          av[p] = tr_pair(pa, pa + 4 * 32);
+        }
+        const __bf16* pb = pb0 + row * X1_IROW;
+        const bf16x8 bv = tr_pair(pb, pb + 16);
+        wacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2], bv, wacc, 0, 0, 0);
+        wacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], bv, wacc, 0, 0, 0);
+        wacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv, wacc, 0, 0, 0);
+      }
+    }
+    __syncthreads();                                  // X / halo reads done
+    float* ured = reinterpret_cast<float*>(X);        // [7][16][64]
+    if (wid < 7) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) ured[(wid * 16 + e) * 64 + lane] = wacc[e];
+    }
+    __syncthreads();
+    // the image's slab, 16-byte write-through stores: item = (ky, row r,
+    // half h2, columns 4q..4q+3 < 28); rows co = (r & 3) + 8 (r >> 2) + 4 h2
+    const uint32_t slab = (uint32_t)b * 32u * (uint32_t)a.w1_np;
+    const __amdgpu_buffer_rsrc_t rs =
+        wt_rsrc(a.w1part, (uint32_t)((size_t)B * 32u * (uint32_t)a.w1_np * 4));
+    for (int f = tid; f < 7 * 16 * 14; f += kThreads) {
+      const int ky = f / 224, rem = f - ky * 224;
+      const int r = rem / 14, g = rem - r * 14, h2 = g / 7, q = g - h2 * 7;
+      const int co = (r & 3) + 8 * (r >> 2) + 4 * h2;
+      if (co >= 16) continue;                         // (the image's zero channels)
+      const float4 v = *reinterpret_cast<const float4*>(ured + (ky * 16 + r) * 64 + 32 * h2 + 4 * q);
+      wt_store4(rs, (slab + (uint32_t)((16 * half + co) * a.w1_np + ky * 28 + 4 * q)) * 4, v);
+    }
+    if (tid < 16) {   // bias: channel tid's lanes (r16 = tid) of the k-step-0 waves, in order
+      float v = 0.f;
+      for (int w = 0; w < 4; ++w)
+        for (int g = 0; g < 4; ++g) v += bsm[w * 64 + 16 * g + tid];
+      wt_store(rs, (slab + (uint32_t)((16 * half + tid) * a.w1_np + 196)) * 4, v);
+    }
+  }
+  // ---- dconv3 / dconv2 expanded + split, NHWC, out of the images ----
+  {
+    const int64_t E3 = (int64_t)B * 1024, E2 = (int64_t)B * 4096;
+    // (each half writes half of the vectors: channels [32 half, +32))
+    for (int f = tid; f < 3 * 16 * 4; f += kThreads) {
+      const int p = f / 64, r = f % 64, px = r >> 2, c = 4 * half + (r & 3);
+      const u32x4 v = *reinterpret_cast<const u32x4*>(D3 + p * P2_PL + ((px >> 2) + 1) * P2_RS +
+                                                       ((px & 3) + 1) * P2_CS + 8 * c);
+      *reinterpret_cast<u32x4*>(a.dconv3x + p * E3 + ((size_t)b * 16 + px) * 64 + 8 * c) = v;
+    }
+    for (int f = tid; f < 3 * 64 * 4; f += kThreads) {
+      const int p = f / 256, r = f % 256, px = r >> 2, c = 4 * half + (r & 3);
+      const u32x4 v = *reinterpret_cast<const u32x4*>(D2 + p * D2_PL + ((px >> 3) + 2) * D2_RS +
+                                                       ((px & 7) + 2) * DS_CS + 8 * c);
+      *reinterpret_cast<u32x4*>(a.dconv2x + p * E2 + ((size_t)b * 64 + px) * 64 + 8 * c) = v;
+    }
+  }
+  DDQ_STAMP(14);
+}
+
+
 // ---------------------------------------------------------------------------
 // K4: conv2's and conv3's weight gradients, conv1's (the B slabs of K3
 // summed), every conv parameter's update, the step's bookkeeping and the next
@@ -894,12 +1262,14 @@ struct WgArgs {
 // Apply one final conv gradient element (layer l, Caffe index i, local e of
 // the layer's weight or bias): grad, and with the fused apply theta / state,
 // the split forward layout, P on a sync step.
+// th0 / st0: the element's theta and optimizer state, loaded by the caller
+// ahead of the sums
 __device__ __forceinline__ void conv_final(const WgArgs& a, int l, bool is_w, int64_t i, int e,
-                                           float v, bool first, bool sync) {
+                                           float v, float th0, float st0, bool first, bool sync) {
   a.grad[i] = v;
   if (!a.apply) return;
-  float st = (a.aa.rule != 0 && !first) ? a.at.opt[i] : 0.f;
-  const float th = apply_rule(a.aa, first, !is_w, a.at.theta[i], v, st);
+  float st = (a.aa.rule != 0 && !first) ? st0 : 0.f;
+  const float th = apply_rule(a.aa, first, !is_w, th0, v, st);
   a.at.theta[i] = th;
   if (a.aa.rule != 0) a.at.opt[i] = st;
   if (sync) a.at.thetaP[i] = th;
@@ -1000,7 +1370,8 @@ __device__ __forceinline__ void wg_tile(const WgArgs& a, char* smem, int tile, i
   // zero both buffers under round 0's loads: the input halo columns stay
   // zero (staging writes in-range columns only; out-of-range rows are
   // staged as zero vectors)
-  for (int f = tid; f < (2 * W::BUF) / 8; f += 256) reinterpret_cast<u32x4*>(buf)[f] = u32x4{0u, 0u, 0u, 0u};
+  for (int f = tid; f < ((nround > 1 ? 2 : 1) * W::BUF) / 8; f += 256)
+    reinterpret_cast<u32x4*>(buf)[f] = u32x4{0u, 0u, 0u, 0u};
   __syncthreads();
   for (int rr = 0; rr < nround; ++rr) {
     store(rr);
@@ -1093,63 +1464,105 @@ __device__ __forceinline__ void wg_tile(const WgArgs& a, char* smem, int tile, i
   }
   if (tid < 32) wt_store(srs, (uint32_t)((W::ELEMS + tid) * 4), ky == 0 ? bsum : 0.f);
   // ---- meet the tile's other groups, then sum and update a slice ----
-  uint64_t* ctr = reinterpret_cast<uint64_t*>(a.sync) + (L == 1 ? 0 : kT2) + tile;
-  DDQ_STAMP(SB + 3);
-  meet(ctr, G, a.sync + 32);
-  DDQ_STAMP(SB + 4);
+  // the slice this workgroup finishes: its elements' Caffe index, theta and
+  // optimizer state loaded before the meeting (they do not depend on it)
   const int sl = (W::SLAB + G - 1) / G, e0 = g * sl, e1 = min(W::SLAB, e0 + sl);
+  constexpr int EPT = 8;                              // elements a thread per chunk (one chunk
+  uint64_t* ctr = reinterpret_cast<uint64_t*>(a.sync) + (L == 1 ? 0 : kT2) + tile;   // at G >= 4)
   const __amdgpu_buffer_rsrc_t rall = __builtin_amdgcn_make_buffer_rsrc(
       slabs + (int64_t)tile * G * W::SLAB, (short)0, (int)(G * W::SLAB * 4), 0x00020000);
-  for (int e = e0 + tid; e < e1; e += 256) {
-    // every group's value loaded first (G <= 16), then summed in group order
-    float t[16];
+  if (e0 >= e1) meet(ctr, G, a.sync + 32);            // an empty slice still arrives
+  for (int c0 = e0; c0 < e1; c0 += 256 * EPT) {
+    int64_t ci_[EPT];
+    int le_[EPT];
+    float th_[EPT], st_[EPT];
 #pragma unroll
-    for (int gg = 0; gg < 16; ++gg)
-      t[gg] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                            rall, (int)(gg < G ? (gg * W::SLAB + e) * 4 : 0x80000000u), 0, 16));
-    float v = t[0];
+    for (int k = 0; k < EPT; ++k) {
+      const int e = c0 + tid + 256 * k;
+      ci_[k] = -1; le_[k] = 0; th_[k] = 0.f; st_[k] = 0.f;
+      if (e >= e1) continue;
+      if (e < W::ELEMS) {
+        const int col = e % (KS * W::CIN), co = 32 * cb + e / (KS * W::CIN);
+        const int kx = col / W::CIN, ci = col % W::CIN;
+        le_[k] = ((co * W::CIN + ci) * KS + ky) * KS + kx;         // Caffe (co, ci, ky, kx)
+        ci_[k] = a.w_off[L] + le_[k];
+      } else if (ky == 0) {
+        le_[k] = 32 * cb + e - W::ELEMS;
+        ci_[k] = a.b_off[L] + le_[k];
+      }
+      if (ci_[k] >= 0 && a.apply) {
+        th_[k] = a.at.theta[ci_[k]];
+        if (a.aa.rule != 0) st_[k] = a.at.opt[ci_[k]];
+      }
+    }
+    if (c0 == e0) {
+      DDQ_STAMP(SB + 3);
+      meet(ctr, G, a.sync + 32);
+      DDQ_STAMP(SB + 4);
+    }
 #pragma unroll
-    for (int gg = 1; gg < 16; ++gg)
-      if (gg < G) v += t[gg];
-    if (e < W::ELEMS) {
-      const int col = e % (KS * W::CIN), co = 32 * cb + e / (KS * W::CIN);
-      const int kx = col / W::CIN, ci = col % W::CIN;
-      const int le = ((co * W::CIN + ci) * KS + ky) * KS + kx;     // Caffe (co, ci, ky, kx)
-      conv_final(a, L, true, a.w_off[L] + le, le, v, first, sync);
-    } else if (ky == 0) {
-      const int co = 32 * cb + e - W::ELEMS;
-      conv_final(a, L, false, a.b_off[L] + co, co, v, first, sync);
+    for (int k = 0; k < EPT; ++k) {
+      const int e = c0 + tid + 256 * k;
+      if (e >= e1) continue;
+      // every group's value loaded first (G <= 16), then summed in group order
+      float t[16];
+#pragma unroll
+      for (int gg = 0; gg < 16; ++gg)
+        t[gg] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                              rall, (int)(gg < G ? (gg * W::SLAB + e) * 4 : 0x80000000u), 0, 16));
+      float v = t[0];
+#pragma unroll
+      for (int gg = 1; gg < 16; ++gg)
+        if (gg < G) v += t[gg];
+      if (ci_[k] >= 0) conv_final(a, L, e < W::ELEMS, ci_[k], le_[k], v, th_[k], st_[k], first, sync);
     }
   }
   DDQ_STAMP(SB + 5);
 }
 
+// Block order: conv3's tiles (the longest chains) first, conv2's, then
+// conv1's slab sums and the next step's gather (short, no meeting) -- every
+// meeting workgroup is dispatched before any block that could hold a CU.
 __global__ __launch_bounds__(256) void wgrad16_kernel(const WgArgs a) {
   extern __shared__ __attribute__((aligned(16))) char wsm[];
   int bid = blockIdx.x;
-  if (bid < a.pf.ng) {                                 // the next step's gather
-    prefetch_body(a.pf, bid);
-    return;
-  }
-  bid -= a.pf.ng;
   const bool first = a.apply && a.at.opt_init[2] != 0, sync = a.apply && a.at.opt_init[3] != 0;
   const int n2 = kT2 * a.G2, n3 = kT3 * a.G3;
-  if (bid < n2) {
-    wg_tile<Wg2, 1>(a, wsm, bid % kT2, bid / kT2, a.G2, a.ipg2, a.slab2, first, sync);
-    return;
-  }
-  bid -= n2;
   if (bid < n3) {
     wg_tile<Wg3, 2>(a, wsm, bid % kT3, bid / kT3, a.G3, a.ipg3, a.slab3, first, sync);
     return;
   }
   bid -= n3;
+  if (bid < n2) {
+    wg_tile<Wg2, 1>(a, wsm, bid % kT2, bid / kT2, a.G2, a.ipg2, a.slab2, first, sync);
+    return;
+  }
+  bid -= n2;
+  if (bid >= kW1Blocks) {                              // the next step's gather
+    prefetch_body(a.pf, bid - kW1Blocks);
+    return;
+  }
   // conv1: the B per-image slabs summed in image order, element by element
   if (bid == 0 && threadIdx.x == 0 && a.book)
     apply_book(a.iter, const_cast<int32_t*>(a.at.opt_init), a.book_period, a.bump, a.book_inc);
   const int np = a.w1_np;
   for (int e = bid * 256 + threadIdx.x; e < 32 * 197; e += kW1Blocks * 256) {
     const int co = e / 197, n = e - co * 197;
+    int le;
+    int64_t i;
+    if (n < 196) {
+      const int ky = n / 28, kx = (n % 28) >> 2, ci = n & 3;
+      le = ((co * 4 + ci) * 7 + ky) * 7 + kx;                    // Caffe (co, ci, ky, kx)
+      i = a.w_off[0] + le;
+    } else {
+      le = co;
+      i = a.b_off[0] + co;
+    }
+    float th0 = 0.f, st0 = 0.f;                                   // ahead of the slab loads
+    if (a.apply) {
+      th0 = a.at.theta[i];
+      if (a.aa.rule != 0) st0 = a.at.opt[i];
+    }
     const float* src = a.w1part + co * np + n;
     float v = 0.f;
     int b0 = 0;
@@ -1161,13 +1574,7 @@ __global__ __launch_bounds__(256) void wgrad16_kernel(const WgArgs a) {
       for (int u = 0; u < 8; ++u) v += t[u];
     }
     for (; b0 < a.B; ++b0) v += src[(int64_t)b0 * 32 * np];
-    if (n < 196) {
-      const int ky = n / 28, kx = (n % 28) >> 2, ci = n & 3;
-      const int le = ((co * 4 + ci) * 7 + ky) * 7 + kx;           // Caffe (co, ci, ky, kx)
-      conv_final(a, 0, true, a.w_off[0] + le, le, v, first, sync);
-    } else {
-      conv_final(a, 0, false, a.b_off[0] + co, co, v, first, sync);
-    }
+    conv_final(a, 0, n < 196, i, le, v, th0, st0, first, sync);
   }
 }
 

@@ -178,6 +178,10 @@ FULL_PASS_CASES = [
     (32, 4, "uniform", "x3"), (48, 4, "snake", "x3"), (56, 4, "uniform", "x3"),
     (80, 4, "snake", "x3"), (88, 4, "uniform", "x3"), (104, 4, "snake", "x3"),
     (112, 4, "uniform", "x3"), (120, 4, "snake", "x3"),
+    # the small-map step's group splits: one group per tile (B = 1, 2), a
+    # slice longer than one chunk (B = 8: two conv3 groups), ragged groups
+    (16, 1, "snake", "x3"), (16, 2, "uniform", "x3"), (16, 8, "snake", "x3"),
+    (16, 12, "uniform", "x3"), (16, 100, "snake", "x3"),
 ]
 
 
