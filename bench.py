@@ -132,7 +132,7 @@ def ideal_s(kernel, B, S):
 def pmc_traffic(label, B, S):
     """(HBM bytes per launch of `label`, source file) from the newest committed
     step-only PMC summary (profiles/rNN_pmc_step.json: the bench's step chain
-    alone, no exchange-path dispatches; tools/gpu/run_measure.sh: FETCH_SIZE x2
+    alone, no exchange-path dispatches; tools/gpu/run.sh PMC=...: FETCH_SIZE x2
     + WRITE_SIZE, MI355X_MICROARCH.md gfx950 correction) -- a separate
     rocprofv3 --pmc run of the same bench command, NOT measured in this run;
     valid for the bench default shape only."""
@@ -192,15 +192,16 @@ def make_net(B, S, replay, device, rank):
 
 def preheat(B, S, local, ms):
     """Bring the chip to its running clocks before the measured context's W
-    warmup steps: a THROWAWAY context (own weights, own 1024-slot replay ring,
-    exchange-free) runs pipelined step chains for `ms` wall milliseconds.
+    warmup steps: a THROWAWAY context (own weights, own max(1024, 4 B)-slot
+    replay ring, exchange-free) runs pipelined step chains for `ms` wall milliseconds.
     The measured context's state is untouched.  Measured
     (tools/gpu/first_launch.py, profiles/r04_clock_ramp.txt): a chip idle
     for 10 ms runs the next 20 steps at 0.155-0.164 ms against 0.146 when
     busy, and 5 warmup steps (0.7 ms) do not bring it back."""
     if ms <= 0:
         return None
-    hot = make_net(B, S, 1024, local, 0)
+    ring = max(1024, 4 * B)                 # a ring the batch can draw from (B < valid)
+    hot = make_net(B, S, ring, local, 0)
     cfg = hot.step_cfg("rmsprop", lr=1e-4, target_period=10, exchange="none", seed=99)
     hot.step_prepare(cfg, "pipelined")
     t0 = time.perf_counter()
@@ -211,8 +212,8 @@ def preheat(B, S, local, ms):
         n += 24
     return hot, {"ms": round((time.perf_counter() - t0) * 1e3, 1), "steps": n,
                  "work": "pipelined step chains of a throwaway context (own weights and "
-                         "1024-slot replay, no exchange) before the W warmup steps; the "
-                         "measured context is untouched"}
+                         "%d-slot replay, no exchange) before the W warmup steps; the "
+                         "measured context is untouched" % ring}
 
 
 def cpu_model():

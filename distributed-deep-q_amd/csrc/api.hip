@@ -2094,12 +2094,18 @@ int ddq_profile_step(ddq_ctx* c, const ddq_step_cfg* cfg, char* names, float* us
   c->marks.clear();
   c->ev_used = 0;
   if (c->steps == 0) TRY(initial_target_sync(c, cfg));
+  g_profiling = true;
+  g_unmarked = 0;
   const int rc = enqueue_step(c, cfg, mark_cb, c);
+  g_profiling = false;
   mark_settle(c);
   TRY(rc);
   c->steps++;
   c->applied += step_inc(c, cfg);
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (g_unmarked)   // (the step itself ran and counts)
+    return fail(c, DDQ_ESTATE, "profile: %d kernel launch(es) of the step ran without a mark "
+                "(their time is in no entry)", g_unmarked);
   const int k = (int)c->marks.size();
   *n = k;
   for (int i = 0; i < k && i < cap; ++i) {

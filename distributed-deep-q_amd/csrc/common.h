@@ -20,6 +20,10 @@ struct ExtTiming {
   hipEvent_t start = nullptr, stop = nullptr;
 };
 extern thread_local ExtTiming g_ext_timing;
+// ddq_profile_step: while it enqueues a step, every launch no mark armed is
+// counted (the step's table would silently miss its time)
+extern thread_local bool g_profiling;
+extern thread_local int g_unmarked;
 
 template <class F, class... Args>
 inline void ddq_launch(F kern, const dim3& grid, const dim3& block, uint32_t smem, hipStream_t s,
@@ -29,6 +33,7 @@ inline void ddq_launch(F kern, const dim3& grid, const dim3& block, uint32_t sme
     g_ext_timing = ExtTiming{};
     hipExtLaunchKernelGGL(kern, grid, block, smem, s, t.start, t.stop, 0, args...);
   } else {
+    if (g_profiling) ++g_unmarked;
     hipLaunchKernelGGL(kern, grid, block, smem, s, args...);
   }
 }

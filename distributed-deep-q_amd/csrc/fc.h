@@ -49,93 +49,9 @@ struct Fc4FwdArgs {
   float* part;                     // [split][nz][B][512]
 };
 
-// The x tile (BT*32 rows x kFc4KLen) is common to the workgroup's four waves:
-// it is loaded once, coalesced, and shared through LDS (loading it per wave
-// quadrupled the x traffic through L1/L2: 7.2 -> 5.3 us in isolation).
-template <int BT>
-__global__ __launch_bounds__(256) void fc4_fwd_direct_kernel(const Fc4FwdArgs a) {
-  constexpr int XS = kFc4KLen + 4;     // padded LDS row (floats)
-  __shared__ __attribute__((aligned(16))) float xs[BT * 32 * XS];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int l31 = lane & 31, h = lane >> 5;
-  // blockIdx.z = batch tile * nz + tower (B > 64: BT*32-row batch tiles)
-  const int z = blockIdx.z % a.nz, split = blockIdx.y;
-  const int bt0 = (blockIdx.z / a.nz) * (BT * 32);
-  const int n0 = blockIdx.x * 128 + w * 32;
-  const int K = a.K;
-  const int k0 = split * kFc4KLen;
-  const __amdgpu_buffer_rsrc_t rw = fc_rsrc(z ? a.w[1] : a.w[0], (uint32_t)(512 * K * 4));
-  const __amdgpu_buffer_rsrc_t rx = fc_rsrc(z ? a.x[1] : a.x[0], (uint32_t)(a.B * K * 4));
-  const uint32_t wrow = (uint32_t)((n0 + l31) * K + h * 16) * 4;
-
-  f32x16 acc[BT];
-#pragma unroll
-  for (int t = 0; t < BT; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-
-  // the x tile's loads first: the LDS barrier below then waits for them only,
-  // and the MFMAs of k block kb for their own W loads (W loads issued first:
-  // 6.3 -> 5.2 us in isolation, tools/ubench/fc4_ubench)
-  constexpr int kC4 = kFc4KLen / 4;                  // float4 per x row
-  constexpr int NX = BT * 32 * kC4 / 256;
-  static_assert(NX * 256 == BT * 32 * kC4, "x tile / workgroup");
-  float4 xv[NX];
-#pragma unroll
-  for (int it = 0; it < NX; ++it) {
-    const int f = threadIdx.x + 256 * it;
-    const int r = f / kC4, c4 = f % kC4;
-    const int k = k0 + 4 * c4;                       // rows b >= B / k >= K read 0
-    xv[it] = fc_ld4(rx, k < K ? (uint32_t)((bt0 + r) * K + k) * 4 : kFcOOB);
-  }
-  float4 wv[kFc4KLen / 32][4];
-#pragma unroll
-  for (int kb = 0; kb < kFc4KLen / 32; ++kb) {
-    const int k = k0 + kb * 32;
-    const bool kin = k < K;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) wv[kb][i] = fc_ld4(rw, kin ? wrow + (k + 4 * i) * 4 : kFcOOB);
-  }
-#pragma unroll
-  for (int it = 0; it < NX; ++it) {
-    const int f = threadIdx.x + 256 * it;
-    *reinterpret_cast<float4*>(xs + (f / kC4) * XS + 4 * (f % kC4)) = xv[it];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int kb = 0; kb < kFc4KLen / 32; ++kb) {
-    float4 xa[BT][4];
-#pragma unroll
-    for (int t = 0; t < BT; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        xa[t][i] = *reinterpret_cast<const float4*>(xs + (t * 32 + l31) * XS + kb * 32 + h * 16 +
-                                                    4 * i);
-#pragma unroll
-    for (int j = 0; j < 16; ++j)
-#pragma unroll
-      for (int t = 0; t < BT; ++t)
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(xa[t][j >> 2], j & 3),
-                                                      f4get(wv[kb][j >> 2], j & 3), acc[t], 0,
-                                                      0, 0);
-  }
-  // rows = b, columns = n: lanes store consecutive n
-  // partials written through (split.h wt_store): the head reads them next
-  const __amdgpu_buffer_rsrc_t rp =
-      wt_rsrc(a.part, (uint32_t)((size_t)gridDim.y * a.nz * a.B * 512 * 4));
-  const uint32_t dbase = (uint32_t)((((size_t)(split * a.nz + z) * a.B) * 512 + n0 + l31) * 4);
-#pragma unroll
-  for (int t = 0; t < BT; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int b = bt0 + t * 32 + fc_acc_row(r, lane);
-      if (b < a.B) wt_store(rp, dbase + (uint32_t)b * 2048, acc[t][r]);
-    }
-}
-
-// The same tile on the bf16 matrix cores with fp32-exact split operands
-// (split.h): the f32 MFMA's 64 cycles per 2 k left the wave's 64 MFMAs
-// (4096 cycles) behind its W4 loads.  Per 32-k block a lane's 16 consecutive
+// The forward tile on the bf16 matrix cores with fp32-exact split operands
+// (split.h; an f32-MFMA form's 64 cycles per 2 k left the wave's 64 MFMAs,
+// 4096 cycles, behind its W4 loads).  Per 32-k block a lane's 16 consecutive
 // k (16h .. 16h+15) are two 8-k halves, one per 32x32x16 step: step s pairs
 // k = 16h + 8s + e of both operands (a permutation of the block's k, the
 // same for A and B), 6 MFMAs a step (192 cycles against 1024 per block).  The
@@ -261,7 +177,7 @@ __global__ __launch_bounds__(256) void fc4_fwd_split_kernel(const Fc4FwdArgs a) 
 
 inline int fc4_fwd_splits(int K) { return (K + kFc4KLen - 1) / kFc4KLen; }
 
-inline hipError_t launch_fc4_fwd_direct(const Fc4FwdArgs& a, hipStream_t st) {
+inline hipError_t launch_fc4_fwd(const Fc4FwdArgs& a, hipStream_t st) {
   if (a.B <= 32) {
     ddq_launch(fc4_fwd_split_kernel<1>, dim3(512 / 128, fc4_fwd_splits(a.K), a.nz),
                        dim3(256), 0, st, a);
@@ -393,12 +309,6 @@ __device__ __forceinline__ void fc4_dgrad_body(const Fc4DgradArgs& a, float (*re
     base[(size_t)H3 * 64] = (mk == 2) ? v : 0.f;
     base[(size_t)H3 * 64 + 64] = (mk == 3) ? v : 0.f;
   }
-}
-
-template <bool SPLIT>
-__global__ __launch_bounds__(512) void fc4_dgrad_direct_kernel(const Fc4DgradArgs a) {
-  __shared__ float red[8][1024];
-  fc4_dgrad_body<SPLIT>(a, red, blockIdx.x, blockIdx.y);
 }
 
 

@@ -12,6 +12,8 @@ namespace ddq {
 // appends it to the error message)
 thread_local const char* g_launch_where = "";
 thread_local ExtTiming g_ext_timing;
+thread_local bool g_profiling = false;
+thread_local int g_unmarked = 0;
 #ifdef DDQ_STAMPS
 __device__ uint64_t g_stamps[kStampBlocks * kStampSlots];
 }  // namespace ddq
@@ -1896,7 +1898,7 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
   f.B = B; f.K = 64 * s4 * s4; f.nz = nz; f.part = nb.fc4_part;
   for (int z = 0; z < 2; ++z) { f.x[z] = nb.pool3[z]; f.w[z] = nb.theta[z] + L.w[3]; }
   M("fc4_fwd");
-  CHECK_LAUNCH(launch_fc4_fwd_direct(f, s));
+  CHECK_LAUNCH(launch_fc4_fwd(f, s));
   if (!out) return hipSuccess;   // training: reduce + Q_out fused into the head kernel
   M("fc4_reduce_out");
   ddq_launch(fc4_reduce_out_kernel, dim3(B, nz), dim3(kFc4), 0, s, nb.fc4_part,
@@ -2012,13 +2014,13 @@ hipError_t launch_small_bwd(const NetBuffers& nb, hipStream_t s,
       w.pf = *pre;
       w.pf.predrawn = bump != nullptr && B <= 256;   // K1 drew it (its book block)
     }
-    // LDS: a round buffer per tile layer, two only where a group has more
-    // than one round (deepq16 B = 32: conv3's one round of 4 images, conv2's
-    // two of one -- 67.5 KB, two workgroups a CU)
+    // LDS: a round buffer per tile layer, two where a group has more than one
+    // round; at least the wave sums + a one-group tile's sums
     const int r2 = (w.ipg2 + sm16::Wg2::NI - 1) / sm16::Wg2::NI;
     const int r3 = (w.ipg3 + sm16::Wg3::NI - 1) / sm16::Wg3::NI;
-    const int lds = std::max({(r2 > 1 ? 2 : 1) * sm16::Wg2::BUF * 2,
-                              (r3 > 1 ? 2 : 1) * sm16::Wg3::BUF * 2, 4 * 16 * 64 * 4});
+    (void)r2; (void)r3;   // (two buffers always: the staging's dummy slot follows them)
+    const int lds = std::max({2 * sm16::Wg2::BUF * 2, 2 * sm16::Wg3::BUF * 2,
+                              4 * 16 * 64 * 4 + sm16::Wg3::SLAB * 4}) + 16;
     static std::atomic<uint64_t> attr{0};
     CHECK_LAUNCH(ensure_dyn_lds(reinterpret_cast<const void*>(sm16::wgrad16_kernel), attr,
                                 sm16::kWgSmem));

@@ -89,6 +89,9 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int bid = blockIdx.x;
   DDQ_STAMP(16);
+#ifdef DDQ_EXP_K2_EMPTY
+  return;
+#endif
   const int B = c.B, n0 = bid * kFcN;
   const int nch = (B + kBC - 1) / kBC;
   float* WS = csm + CH_WS;
@@ -138,6 +141,8 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
   };
   float pth = 0.f, pst = 0.f;
   const bool ap0 = c.apply != 0;
+  // the update's flags (latched by K1's book block), loaded now
+  const bool first = ap0 && c.at.opt_init[2] != 0, sync = ap0 && c.at.opt_init[3] != 0;
   if (ap0 && tid < 84) {
     const int64_t i = uparam(tid);
     pth = c.at.theta[i];
@@ -218,6 +223,16 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
     }
   }
   DDQ_STAMP(18);
+  // the W4 rows' theta / state (the tail's update), loaded under the fan-in
+  float w4th[2][4], w4st[2][4];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t e = c.w4_off + (int64_t)(n0 + 4 * kq + i) * kFcK + 16 * (2 * wid + u) + lr;
+      w4th[u][i] = ap0 ? c.at.theta[e] : 0.f;
+      w4st[u][i] = ap0 && c.aa.rule != 0 ? c.at.opt[e] : 0.f;
+    }
   meet(reinterpret_cast<uint64_t*>(c.sync), kFcBlk, c.sync + 2);
   DDQ_STAMP(19);
 
@@ -260,8 +275,8 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
     }
   }
   __syncthreads();
-  const bool ap = c.apply != 0;
-  const bool first = ap && c.at.opt_init[2] != 0, sync = ap && c.at.opt_init[3] != 0;
+  DDQ_STAMP(44);
+  const bool ap = ap0;
   // dh4 of the workgroup's units: (dQ W5) masked by h4 > 0 (ReLU backward)
   for (int e = tid; e < B * kFcN; e += 512) {
     const int b = e >> 4, n = e & 15;
@@ -271,45 +286,35 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
     DH[e] = H[e] > 0.f ? v : 0.f;
   }
   __syncthreads();
+  DDQ_STAMP(45);
   // loss, db5 (workgroup 0) and db4, dW5 of the units: sums over the batch,
-  // lane l taking samples l, l + 64, ... in order, then a fixed butterfly
-  // across the wave -- a wave's 11 quantities side by side (independent
-  // shuffles), deterministic
+  // four threads a quantity (thread r of the four: samples r, r + 4, ... in
+  // order), combined by two quad shuffles (fixed order, deterministic)
   {
-    constexpr int QW = 11;                           // quantities a wave: 8 x 11 >= 85
     const int hq = bid == 0 ? 5 : 0, nq = hq + 5 * kFcN;
-    float p[QW];
-#pragma unroll
-    for (int j = 0; j < QW; ++j) {
-      const int qq = wid + 8 * j;
-      p[j] = 0.f;
-      if (qq >= nq) continue;                        // (wave-uniform)
-      const bool head = qq < hq;
-      const int q = head ? qq : qq - hq;
-      for (int b = lane; b < B; b += 64) {
-        if (head) p[j] += q < 4 ? DQ[b * 4 + q] : TMP[b];
-        else {
-          const int r = q >> 4, n = q & 15;          // r 0: db4, 1..4: dW5[r - 1]
-          p[j] += r == 0 ? DH[b * kFcN + n] : DQ[b * 4 + r - 1] * H[b * kFcN + n];
+    const int qq = tid >> 2, r4 = tid & 3;
+    const bool head = qq < hq;
+    const int q = head ? qq : qq - hq;
+    float v = 0.f;
+    if (qq < nq) {
+      if (head) {
+        for (int b = r4; b < B; b += 4) v += q < 4 ? DQ[b * 4 + q] : TMP[b];
+      } else {
+        const int r = q >> 4, n = q & 15;            // r 0: db4, 1..4: dW5[r - 1]
+        if (r == 0) {
+          for (int b = r4; b < B; b += 4) v += DH[b * kFcN + n];
+        } else {
+          for (int b = r4; b < B; b += 4) v += DQ[b * 4 + r - 1] * H[b * kFcN + n];
         }
       }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1)
-#pragma unroll
-      for (int j = 0; j < QW; ++j) p[j] += __shfl_xor(p[j], o);
-    if (lane == 0) {
-#pragma unroll
-      for (int j = 0; j < QW; ++j) {
-        const int qq = wid + 8 * j;
-        if (qq >= nq) continue;
-        const bool head = qq < hq;
-        const int q = head ? qq : qq - hq;
-        const float v = p[j];
-        if (head && q == 4) {
-          *c.loss = v / (float)B / 2.f;
-          continue;
-        }
+    v += __shfl_xor(v, 1);
+    v += __shfl_xor(v, 2);
+    DDQ_STAMP(46);
+    if (r4 == 0 && qq < nq) {
+      if (head && q == 4) {
+        *c.loss = v / (float)B / 2.f;
+      } else {
         const int pq = head ? 80 + q : q;            // the preloaded parameter's slot
         const int64_t i = uparam(pq);
         const bool is_bias = head || (q >> 4) == 0;
@@ -401,8 +406,8 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
       const float g = gw[u][i];
       if (!ap || c.store_grad) c.grad[e] = g;
       if (ap) {
-        float st = (c.aa.rule != 0 && !first) ? c.at.opt[e] : 0.f;
-        const float th = apply_rule(c.aa, first, false, c.at.theta[e], g, st);
+        float st = (c.aa.rule != 0 && !first) ? w4st[u][i] : 0.f;
+        const float th = apply_rule(c.aa, first, false, w4th[u][i], g, st);
         c.at.theta[e] = th;
         if (c.aa.rule != 0) c.at.opt[e] = st;
         if (sync) c.at.thetaP[e] = th;
@@ -1224,7 +1229,7 @@ struct Wg16 {
   static constexpr int VIN = NI * 3 * HW * HW * (CIN / 8);
   static constexpr int VD = NI * 3 * NPX * 4;
   static constexpr int PIN = (VIN + 255) / 256, PD = (VD + 255) / 256;
-  static constexpr int kSmem = 2 * BUF * 2 > 4 * 16 * 64 * 4 ? 2 * BUF * 2 : 4 * 16 * 64 * 4;
+  static constexpr int kSmem = (2 * BUF * 2 > 4 * 16 * 64 * 4 ? 2 * BUF * 2 : 4 * 16 * 64 * 4) + 16;
 };
 using Wg2 = Wg16<32, 5, 8>;
 using Wg3 = Wg16<64, 3, 4>;
@@ -1279,12 +1284,44 @@ __device__ __forceinline__ void conv_final(const WgArgs& a, int l, bool is_w, in
   }
 }
 
-template <class W, int L>
+// Element e of a tile's slab (layout [co 32][kx KX][ci CIN], then the 32
+// biases of tiles holding tap (ky, kx) = (0, 0)): its Caffe index within the
+// layer (le) and flat index (returned); -1 for no element
+template <class W, int L, int KX>
+__device__ __forceinline__ int64_t tile_elem(const WgArgs& a, int e, int ky, int kx0, int cb,
+                                             int& le) {
+  constexpr int KS = W::KS, ELEMS = 32 * KX * W::CIN;
+  if (e < ELEMS) {
+    const int col = e % (KX * W::CIN), co = 32 * cb + e / (KX * W::CIN);
+    const int kx = kx0 + col / W::CIN, ci = col % W::CIN;
+    le = ((co * W::CIN + ci) * KS + ky) * KS + kx;               // Caffe (co, ci, ky, kx)
+    return a.w_off[L] + le;
+  }
+  le = 0;
+  if (ky != 0 || kx0 != 0) return -1;
+  le = 32 * cb + e - ELEMS;
+  return a.b_off[L] + le;
+}
+
+// One weight-gradient tile: output channels [32 cb, +32) x tap row ky x KX
+// taps (KX == KS: the whole row; KX == 1: tap kx0 alone), over the images of
+// group g.  The rounds' operands are loaded D rounds ahead (a register ring),
+// staged through two LDS buffers; the 4 waves' accumulators are summed in
+// fixed order in LDS.  G == 1: the tile's sums are final and applied here;
+// G > 1: the group's slab, a meeting of the tile's G groups, and this group's
+// slice of the tile summed over the slabs in group order and applied.
+template <class W, int L, int KX, int D>
 __device__ __forceinline__ void wg_tile(const WgArgs& a, char* smem, int tile, int g, int G, int ipg,
                                         float* slabs, bool first, bool sync) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   constexpr int KS = W::KS;
-  const int ky = tile >> 1, cb = tile & 1, B = a.B;
+  constexpr int NT = KX * W::NCB;                      // accumulators per wave
+  constexpr int ELEMS = 32 * KX * W::CIN, SLAB = ELEMS + 32;
+  const int cb = tile & 1;
+  const int ky = KX == KS ? tile >> 1 : tile / (2 * KS);
+  const int kx0 = KX == KS ? 0 : (tile >> 1) % KS;
+  const bool has_bias = ky == 0 && kx0 == 0;
+  const int B = a.B;
   const int i0 = g * ipg, i1 = min(B, i0 + ipg);
   const int nimg = max(0, i1 - i0);
   const int nround = (nimg + W::NI - 1) / W::NI;
@@ -1293,20 +1330,19 @@ __device__ __forceinline__ void wg_tile(const WgArgs& a, char* smem, int tile, i
   const __bf16* dsrc = L == 1 ? a.dconv2x : a.dconv3x;
   const int64_t Ein = (int64_t)B * W::NPX * W::CIN, Ed = (int64_t)B * W::NPX * 64;
   constexpr uint32_t kOOB = 0x80000000u;
-  const __amdgpu_buffer_rsrc_t rin[3] = {
-      __builtin_amdgcn_make_buffer_rsrc((void*)in, (short)0, (int)(Ein * 2), 0x00020000),
-      __builtin_amdgcn_make_buffer_rsrc((void*)(in + Ein), (short)0, (int)(Ein * 2), 0x00020000),
-      __builtin_amdgcn_make_buffer_rsrc((void*)(in + 2 * Ein), (short)0, (int)(Ein * 2), 0x00020000)};
-  const __amdgpu_buffer_rsrc_t rd[3] = {
-      __builtin_amdgcn_make_buffer_rsrc((void*)dsrc, (short)0, (int)(Ed * 2), 0x00020000),
-      __builtin_amdgcn_make_buffer_rsrc((void*)(dsrc + Ed), (short)0, (int)(Ed * 2), 0x00020000),
-      __builtin_amdgcn_make_buffer_rsrc((void*)(dsrc + 2 * Ed), (short)0, (int)(Ed * 2), 0x00020000)};
+  // one descriptor per tensor over its three contiguous planes, the plane in
+  // the offset (a descriptor chosen per lane would be a waterfall loop)
+  const __amdgpu_buffer_rsrc_t rin =
+      __builtin_amdgcn_make_buffer_rsrc((void*)in, (short)0, (int)(3 * Ein * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rd =
+      __builtin_amdgcn_make_buffer_rsrc((void*)dsrc, (short)0, (int)(3 * Ed * 2), 0x00020000);
   constexpr int SB = L == 1 ? 24 : 32;               // stamp slots (DDQ_STAMPS builds)
   DDQ_STAMP(SB);
-  // staging of round rr: registers first (every load issued), then LDS
-  u32x4 vin[W::PIN], vd[W::PD];
-  float bsum = 0.f;                                   // ky == 0: bias partials (below)
-  auto load = [&](int rr) {
+  // the operand ring: round rr in slot rr % D (every index compile-time after
+  // unrolling: registers, no scratch)
+  u32x4 vin[D][W::PIN], vd[D][W::PD];
+  float bsum = 0.f;                                   // has_bias: bias partials (below)
+  auto load = [&](int rr, int d) {
 #pragma unroll
     for (int u = 0; u < W::PIN; ++u) {
       const int f = tid + 256 * u;
@@ -1317,8 +1353,8 @@ __device__ __forceinline__ void wg_tile(const WgArgs& a, char* smem, int tile, i
       const int img = i0 + rr * W::NI + ii;
       const int yi = y + ky - W::PAD;
       const bool ok = f < W::VIN && img < i1 && (unsigned)yi < (unsigned)W::HW;
-      const uint32_t o = (uint32_t)((((img * W::HW + yi) * W::HW + x) * W::CIN + 8 * c8) * 2);
-      vin[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rin[p], (int)(ok ? o : kOOB), 0, 0));
+      const uint32_t o = (uint32_t)((p * Ein + ((img * W::HW + yi) * W::HW + x) * W::CIN + 8 * c8) * 2);
+      vin[d][u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rin, (int)(ok ? o : kOOB), 0, 0));
     }
 #pragma unroll
     for (int u = 0; u < W::PD; ++u) {
@@ -1327,35 +1363,36 @@ __device__ __forceinline__ void wg_tile(const WgArgs& a, char* smem, int tile, i
       const int px = q1 % W::NPX, q2 = q1 / W::NPX, p = q2 % 3, ii = q2 / 3;
       const int img = i0 + rr * W::NI + ii;
       const bool ok = f < W::VD && img < i1;
-      const uint32_t o = (uint32_t)((((img * W::NPX + px) * 64) + 32 * cb + 8 * c8) * 2);
-      vd[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rd[p], (int)(ok ? o : kOOB), 0, 0));
+      const uint32_t o = (uint32_t)((p * Ed + ((img * W::NPX + px) * 64) + 32 * cb + 8 * c8) * 2);
+      vd[d][u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rd, (int)(ok ? o : kOOB), 0, 0));
     }
   };
-  auto store = [&](int rr) {
+  // (branch-free: a vector past the round lands in a dummy 16-byte slot after
+  // the two buffers -- a store under a branch would make its wait vmcnt(0))
+  auto store = [&](int rr, int d) {
     __bf16* bb = buf + (rr & 1) * W::BUF;
+    __bf16* dummy = buf + 2 * W::BUF;
 #pragma unroll
     for (int u = 0; u < W::PIN; ++u) {
       const int f = tid + 256 * u;
-      if (f >= W::VIN) continue;
       const int c8 = f % (W::CIN / 8), q1 = f / (W::CIN / 8);
       const int x = q1 % W::HW, q2 = q1 / W::HW, y = q2 % W::HW, q3 = q2 / W::HW;
       const int p = q3 % 3, ii = q3 / 3;
-      *reinterpret_cast<u32x4*>(bb + ii * W::IMG + p * W::IN_PL + (y * W::SW + x + W::PAD) * W::PSI + 8 * c8) = vin[u];
+      __bf16* dst = bb + ii * W::IMG + p * W::IN_PL + (y * W::SW + x + W::PAD) * W::PSI + 8 * c8;
+      *reinterpret_cast<u32x4*>(f < W::VIN ? dst : dummy) = vin[d][u];
     }
 #pragma unroll
     for (int u = 0; u < W::PD; ++u) {
       const int f = tid + 256 * u;
-      if (f >= W::VD) continue;
       const int c8 = f & 3, q1 = f >> 2;
       const int px = q1 % W::NPX, q2 = q1 / W::NPX, p = q2 % 3, ii = q2 / 3;
-      *reinterpret_cast<u32x4*>(bb + ii * W::IMG + 3 * W::IN_PL + p * W::D_PL + px * W::PSD + 8 * c8) = vd[u];
+      __bf16* dst = bb + ii * W::IMG + 3 * W::IN_PL + p * W::D_PL + px * W::PSD + 8 * c8;
+      *reinterpret_cast<u32x4*>(f < W::VD ? dst : dummy) = vd[d][u];
     }
   };
-  // bias (ky == 0 tiles): the waves sum the staged dconv planes of their
-  // units' pixels (fp32 value = sum of the three planes), channel-wise
-  f32x16 acc[W::NT];
+  f32x16 acc[NT];
 #pragma unroll
-  for (int t = 0; t < W::NT; ++t)
+  for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
   const int gq = lane >> 4, iq = (lane & 15) >> 2, ip = lane & 3;
@@ -1366,67 +1403,95 @@ __device__ __forceinline__ void wg_tile(const WgArgs& a, char* smem, int tile, i
   // pixels of the lane's two transposed reads (p, p + 4): (y, x) in the map
   const int jA = 16 * s + pix0, jB = jA + 4;
   const int yA = jA / W::HW, xA = jA % W::HW, yB = jB / W::HW, xB = jB % W::HW;
-  if (nround > 0) load(0);
-  // zero both buffers under round 0's loads: the input halo columns stay
+  // (every ring load is issued unconditionally -- rounds past the group read
+  // zeros out of range -- so the waits before a round's staging count only
+  // the loads issued before its own: a conditional load would force vmcnt(0))
+#pragma unroll
+  for (int d = 0; d < D; ++d) load(d, d);
+  // zero both buffers under the first loads: the input halo columns stay
   // zero (staging writes in-range columns only; out-of-range rows are
   // staged as zero vectors)
   for (int f = tid; f < ((nround > 1 ? 2 : 1) * W::BUF) / 8; f += 256)
     reinterpret_cast<u32x4*>(buf)[f] = u32x4{0u, 0u, 0u, 0u};
-  __syncthreads();
-  for (int rr = 0; rr < nround; ++rr) {
-    store(rr);
-    __syncthreads();                                  // round rr staged; round rr - 1 computed
-    if (rr == 0) DDQ_STAMP(SB + 1);
-    if (rr + 1 < nround) load(rr + 1);
-    __builtin_amdgcn_sched_barrier(0);
-    const int img = i0 + rr * W::NI + ii;
-    if (img < i1) {
-      const __bf16* bb = buf + (rr & 1) * W::BUF + ii * W::IMG;
-      bf16x8 av[3];
+  // the direct apply's first elements: theta / state loaded under the rounds
+  constexpr int EPD = (SLAB + 255) / 256 < 12 ? (SLAB + 255) / 256 : 12;
+  float dth[EPD], dst[EPD];
+  {
+    const __amdgpu_buffer_rsrc_t rth = __builtin_amdgcn_make_buffer_rsrc(a.at.theta, (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rst = __builtin_amdgcn_make_buffer_rsrc(a.at.opt, (short)0, 0x7fffffff, 0x00020000);
+    const bool want = G == 1 && a.apply, wst = want && a.aa.rule != 0;
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        const __bf16* pa = bb + 3 * W::IN_PL + p * W::D_PL + chn;
-        av[p] = tr_pair(pa + jA * W::PSD, pa + jB * W::PSD);
-      }
-#pragma unroll
-      for (int kx = 0; kx < KS; ++kx) {
-#pragma unroll
-        for (int c = 0; c < W::NCB; ++c) {
-          bf16x8 bv[3];
-#pragma unroll
-          for (int p = 0; p < 3; ++p) {
-            const __bf16* pb = bb + p * W::IN_PL + 32 * c + chn;
-            bv[p] = tr_pair(pb + (yA * W::SW + xA + kx) * W::PSI, pb + (yB * W::SW + xB + kx) * W::PSI);
-          }
-          const int t = kx * W::NCB + c;
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2], bv[0], acc[t], 0, 0, 0);
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], bv[1], acc[t], 0, 0, 0);
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[2], acc[t], 0, 0, 0);
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], bv[0], acc[t], 0, 0, 0);
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[1], acc[t], 0, 0, 0);
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[0], acc[t], 0, 0, 0);
-        }
-      }
+    for (int k = 0; k < EPD; ++k) {   // (unconditional loads, as the ring's)
+      int le;
+      const int e = tid + 256 * k;
+      const int64_t ci = e < SLAB ? tile_elem<W, L, KX>(a, e, ky, kx0, cb, le) : -1;
+      dth[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                             rth, (int)(want && ci >= 0 ? (uint32_t)ci * 4 : kOOB), 0, 0));
+      dst[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                             rst, (int)(wst && ci >= 0 ? (uint32_t)ci * 4 : kOOB), 0, 0));
     }
-    if (ky == 0) {
-      // bias partial (tap row 0 tiles): thread = (channel c = tid & 31, pixel
-      // slice tid >> 5) over the round's 64 staged dconv pixels, the fp32
-      // value of a split element being the sum of its planes
-      const __bf16* bb = buf + (rr & 1) * W::BUF;
-      const int c = tid & 31;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int q = 8 * (tid >> 5) + k;               // pixel q of the round (NI images)
-        const int iq2 = q / W::NPX, px = q % W::NPX;
-        if (i0 + rr * W::NI + iq2 < i1) {
-          const __bf16* pd = bb + iq2 * W::IMG + 3 * W::IN_PL + px * W::PSD + c;
-          bsum += ((float)pd[0] + (float)pd[W::D_PL]) + (float)pd[2 * W::D_PL];
-        }
-      }
-    }
-    __syncthreads();                                  // round rr's reads done (its buffer is reused)
   }
-  if (ky == 0) {   // the 8 pixel slices of each channel, in order
+  __syncthreads();
+  for (int r0 = 0; r0 < nround; r0 += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int rr = r0 + d;
+      if (rr >= nround) break;
+      store(rr, d);
+      __syncthreads();                                // round rr staged; round rr - 1 computed
+      if (rr == 0) DDQ_STAMP(SB + 1);
+      load(rr + D, d);
+      __builtin_amdgcn_sched_barrier(0);
+      const int img = i0 + rr * W::NI + ii;
+      if (img < i1) {
+        const __bf16* bb = buf + (rr & 1) * W::BUF + ii * W::IMG;
+        bf16x8 av[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          const __bf16* pa = bb + 3 * W::IN_PL + p * W::D_PL + chn;
+          av[p] = tr_pair(pa + jA * W::PSD, pa + jB * W::PSD);
+        }
+#pragma unroll
+        for (int kk = 0; kk < KX; ++kk) {
+          const int kx = kx0 + kk;
+#pragma unroll
+          for (int c = 0; c < W::NCB; ++c) {
+            bf16x8 bv[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+              const __bf16* pb = bb + p * W::IN_PL + 32 * c + chn;
+              bv[p] = tr_pair(pb + (yA * W::SW + xA + kx) * W::PSI, pb + (yB * W::SW + xB + kx) * W::PSI);
+            }
+            const int t = kk * W::NCB + c;
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[2], bv[0], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], bv[1], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[2], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[1], bv[0], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[1], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], bv[0], acc[t], 0, 0, 0);
+          }
+        }
+      }
+      if (has_bias) {
+        // bias partial: thread = (channel c = tid & 31, pixel slice tid >> 5)
+        // over the round's 64 staged dconv pixels, the fp32 value of a split
+        // element being the sum of its planes
+        const __bf16* bb = buf + (rr & 1) * W::BUF;
+        const int c = tid & 31;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int q = 8 * (tid >> 5) + k;               // pixel q of the round (NI images)
+          const int iq2 = q / W::NPX, px = q % W::NPX;
+          if (i0 + rr * W::NI + iq2 < i1) {
+            const __bf16* pd = bb + iq2 * W::IMG + 3 * W::IN_PL + px * W::PSD + c;
+            bsum += ((float)pd[0] + (float)pd[W::D_PL]) + (float)pd[2 * W::D_PL];
+          }
+        }
+      }
+      __syncthreads();                                // round rr's reads done (its buffer is reused)
+    }
+  }
+  if (has_bias) {   // the 8 pixel slices of each channel, in order
     float* bred = reinterpret_cast<float*>(smem);
     bred[tid] = bsum;
     __syncthreads();
@@ -1438,17 +1503,18 @@ __device__ __forceinline__ void wg_tile(const WgArgs& a, char* smem, int tile, i
     }
   }
   DDQ_STAMP(SB + 2);
-  // ---- the waves' tiles summed in fixed order -> the group's slab ----
+  // ---- the waves' tiles summed in fixed order -> LDS (G == 1) or the slab ----
   float* red = reinterpret_cast<float*>(smem);        // [4 waves][16][64]
-  float* slab = slabs + ((int64_t)tile * G + g) * W::SLAB;
-  const __amdgpu_buffer_rsrc_t srs = wt_rsrc(slab, (uint32_t)(W::SLAB * 4));
+  float* fin = red + 4 * 16 * 64;                     // G == 1: the tile's sums [SLAB]
+  float* slab = slabs + ((int64_t)tile * G + g) * SLAB;
+  const __amdgpu_buffer_rsrc_t srs = wt_rsrc(slab, (uint32_t)(SLAB * 4));
 #pragma unroll
-  for (int t = 0; t < W::NT; ++t) {
+  for (int t = 0; t < NT; ++t) {
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < 16; ++r) red[(wid * 16 + r) * 64 + lane] = acc[t][r];
     __syncthreads();
-    {   // thread = (tile row r, lanes 4q..4q+3): 16-byte write-through store
+    {   // thread = (tile row r, lanes 4q..4q+3)
       const int r = tid >> 4, l0 = 4 * (tid & 15);
       const int e = r * 64 + l0;
       const float4 a0 = *reinterpret_cast<const float4*>(red + e);
@@ -1458,19 +1524,45 @@ __device__ __forceinline__ void wg_tile(const WgArgs& a, char* smem, int tile, i
       const float4 v = make_float4((a0.x + a1.x) + (a2.x + a3.x), (a0.y + a1.y) + (a2.y + a3.y),
                                    (a0.z + a1.z) + (a2.z + a3.z), (a0.w + a1.w) + (a2.w + a3.w));
       const int co = (r & 3) + 8 * (r >> 2) + 4 * (l0 >> 5);
-      const int kx = t / W::NCB, c = t % W::NCB;
-      wt_store4(srs, (uint32_t)(((co * KS + kx) * W::CIN + 32 * c + (l0 & 31)) * 4), v);
+      const int kk = t / W::NCB, c = t % W::NCB;
+      const int o = (co * KX + kk) * W::CIN + 32 * c + (l0 & 31);
+      if (G == 1) *reinterpret_cast<float4*>(fin + o) = v;
+      else wt_store4(srs, (uint32_t)(o * 4), v);
     }
   }
-  if (tid < 32) wt_store(srs, (uint32_t)((W::ELEMS + tid) * 4), ky == 0 ? bsum : 0.f);
+  if (G == 1) {
+    if (tid < 32) fin[ELEMS + tid] = has_bias ? bsum : 0.f;
+    __syncthreads();
+    DDQ_STAMP(SB + 3);
+    DDQ_STAMP(SB + 4);
+    for (int c0 = 0; c0 < SLAB; c0 += 256 * EPD) {
+#pragma unroll
+      for (int k = 0; k < EPD; ++k) {
+        const int e = c0 + tid + 256 * k;
+        if (e >= SLAB) continue;
+        int le;
+        const int64_t ci = tile_elem<W, L, KX>(a, e, ky, kx0, cb, le);
+        if (ci < 0) continue;
+        float th = dth[k], st = dst[k];
+        if (c0 > 0 && a.apply) {                      // past the preloaded chunk
+          th = a.at.theta[ci];
+          st = a.aa.rule != 0 ? a.at.opt[ci] : 0.f;
+        }
+        conv_final(a, L, e < ELEMS, ci, le, fin[e], th, st, first, sync);
+      }
+    }
+    DDQ_STAMP(SB + 5);
+    return;
+  }
+  if (tid < 32) wt_store(srs, (uint32_t)((ELEMS + tid) * 4), has_bias ? bsum : 0.f);
   // ---- meet the tile's other groups, then sum and update a slice ----
   // the slice this workgroup finishes: its elements' Caffe index, theta and
   // optimizer state loaded before the meeting (they do not depend on it)
-  const int sl = (W::SLAB + G - 1) / G, e0 = g * sl, e1 = min(W::SLAB, e0 + sl);
+  const int sl = (SLAB + G - 1) / G, e0 = g * sl, e1 = min(SLAB, e0 + sl);
   constexpr int EPT = 8;                              // elements a thread per chunk (one chunk
   uint64_t* ctr = reinterpret_cast<uint64_t*>(a.sync) + (L == 1 ? 0 : kT2) + tile;   // at G >= 4)
   const __amdgpu_buffer_rsrc_t rall = __builtin_amdgcn_make_buffer_rsrc(
-      slabs + (int64_t)tile * G * W::SLAB, (short)0, (int)(G * W::SLAB * 4), 0x00020000);
+      slabs + (int64_t)tile * G * SLAB, (short)0, (int)(G * SLAB * 4), 0x00020000);
   if (e0 >= e1) meet(ctr, G, a.sync + 32);            // an empty slice still arrives
   for (int c0 = e0; c0 < e1; c0 += 256 * EPT) {
     int64_t ci_[EPT];
@@ -1481,15 +1573,7 @@ __device__ __forceinline__ void wg_tile(const WgArgs& a, char* smem, int tile, i
       const int e = c0 + tid + 256 * k;
       ci_[k] = -1; le_[k] = 0; th_[k] = 0.f; st_[k] = 0.f;
       if (e >= e1) continue;
-      if (e < W::ELEMS) {
-        const int col = e % (KS * W::CIN), co = 32 * cb + e / (KS * W::CIN);
-        const int kx = col / W::CIN, ci = col % W::CIN;
-        le_[k] = ((co * W::CIN + ci) * KS + ky) * KS + kx;         // Caffe (co, ci, ky, kx)
-        ci_[k] = a.w_off[L] + le_[k];
-      } else if (ky == 0) {
-        le_[k] = 32 * cb + e - W::ELEMS;
-        ci_[k] = a.b_off[L] + le_[k];
-      }
+      ci_[k] = tile_elem<W, L, KX>(a, e, ky, kx0, cb, le_[k]);
       if (ci_[k] >= 0 && a.apply) {
         th_[k] = a.at.theta[ci_[k]];
         if (a.aa.rule != 0) st_[k] = a.at.opt[ci_[k]];
@@ -1500,21 +1584,30 @@ __device__ __forceinline__ void wg_tile(const WgArgs& a, char* smem, int tile, i
       meet(ctr, G, a.sync + 32);
       DDQ_STAMP(SB + 4);
     }
+    // every group's value of every element loaded first (G <= GM), summed in
+    // group order, then the stores
+    constexpr int GM = L == 1 ? 16 : 8;
+    float vs[EPT];
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
       const int e = c0 + tid + 256 * k;
-      if (e >= e1) continue;
-      // every group's value loaded first (G <= 16), then summed in group order
-      float t[16];
+      vs[k] = 0.f;
+      if (c0 + 256 * k >= e1) continue;                // (wave-uniform: no element left)
+      float t[GM];
 #pragma unroll
-      for (int gg = 0; gg < 16; ++gg)
+      for (int gg = 0; gg < GM; ++gg)
         t[gg] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                              rall, (int)(gg < G ? (gg * W::SLAB + e) * 4 : 0x80000000u), 0, 16));
+                                              rall, (int)(gg < G && e < e1 ? (gg * SLAB + e) * 4 : 0x80000000u), 0, 16));
       float v = t[0];
 #pragma unroll
-      for (int gg = 1; gg < 16; ++gg)
+      for (int gg = 1; gg < GM; ++gg)
         if (gg < G) v += t[gg];
-      if (ci_[k] >= 0) conv_final(a, L, e < W::ELEMS, ci_[k], le_[k], v, th_[k], st_[k], first, sync);
+      vs[k] = v;
+    }
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+      const int e = c0 + tid + 256 * k;
+      if (e < e1 && ci_[k] >= 0) conv_final(a, L, e < ELEMS, ci_[k], le_[k], vs[k], th_[k], st_[k], first, sync);
     }
   }
   DDQ_STAMP(SB + 5);
@@ -1526,22 +1619,28 @@ __device__ __forceinline__ void wg_tile(const WgArgs& a, char* smem, int tile, i
 __global__ __launch_bounds__(256) void wgrad16_kernel(const WgArgs a) {
   extern __shared__ __attribute__((aligned(16))) char wsm[];
   int bid = blockIdx.x;
+#ifdef DDQ_EXP_K4_EMPTY
+  return;
+#endif
   const bool first = a.apply && a.at.opt_init[2] != 0, sync = a.apply && a.at.opt_init[3] != 0;
   const int n2 = kT2 * a.G2, n3 = kT3 * a.G3;
   if (bid < n3) {
-    wg_tile<Wg3, 2>(a, wsm, bid % kT3, bid / kT3, a.G3, a.ipg3, a.slab3, first, sync);
+    wg_tile<Wg3, 2, 3, 2>(a, wsm, bid % kT3, bid / kT3, a.G3, a.ipg3, a.slab3, first, sync);
     return;
   }
   bid -= n3;
   if (bid < n2) {
-    wg_tile<Wg2, 1>(a, wsm, bid % kT2, bid / kT2, a.G2, a.ipg2, a.slab2, first, sync);
+    wg_tile<Wg2, 1, 5, 2>(a, wsm, bid % kT2, bid / kT2, a.G2, a.ipg2, a.slab2, first, sync);
     return;
   }
   bid -= n2;
   if (bid >= kW1Blocks) {                              // the next step's gather
+    DDQ_STAMP(42);
     prefetch_body(a.pf, bid - kW1Blocks);
+    DDQ_STAMP(43);
     return;
   }
+  DDQ_STAMP(40);
   // conv1: the B per-image slabs summed in image order, element by element
   if (bid == 0 && threadIdx.x == 0 && a.book)
     apply_book(a.iter, const_cast<int32_t*>(a.at.opt_init), a.book_period, a.bump, a.book_inc);
@@ -1576,6 +1675,7 @@ __global__ __launch_bounds__(256) void wgrad16_kernel(const WgArgs a) {
     for (; b0 < a.B; ++b0) v += src[(int64_t)b0 * 32 * np];
     conv_final(a, 0, n < 196, i, le, v, th0, st0, first, sync);
   }
+  DDQ_STAMP(41);
 }
 
 }  // namespace sm16

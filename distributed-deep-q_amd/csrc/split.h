@@ -739,11 +739,13 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
   // plane extent of the split source: (B, H, W, CPT), pooled (B, H/2, W/2, CPT) for DGRAD
   const uint32_t src_elems = DGRAD ? (uint32_t)(a.B * (a.H >> 1) * (a.W >> 1) * CPT)
                                    : (uint32_t)(a.B * a.H * a.W * CPT);
-  __amdgpu_buffer_rsrc_t rin[3];
-#pragma unroll
-  for (int p = 0; p < 3; ++p)
-    rin[p] = __builtin_amdgcn_make_buffer_rsrc((void*)(in + p * a.in_elems), (short)0,
-                                               (int)(src_elems * 2), 0x00020000);
+  // one descriptor over the three planes (plane p at p * in_elems), the plane
+  // in the offset: a descriptor chosen per lane compiles to a waterfall loop
+  // (one serialised load per distinct descriptor).  An out-of-image vector's
+  // offset is kOOB (past every plane); an in-image offset never leaves its
+  // own plane's src_elems.
+  const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)in, (short)0, (int)((2 * (uint32_t)a.in_elems + src_elems) * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t rroute =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.in_route, (short)0, (int)src_elems, 0x00020000);
   constexpr int NV = C::PH * C::PW * (CP / 8);             // 16-byte vectors per plane
@@ -774,7 +776,7 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
         const uint32_t o = (uint32_t)(((b * (a.H >> 1) + (gy >> 1)) * (a.W >> 1) + (gx >> 1)) * CPT +
                                       ch * CP + 8 * c8);
         const u32x4 uw = __builtin_bit_cast(
-            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rin[p], (int)(in_img ? o * 2 : kOOB), 0, 0));
+            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rin, (int)(in_img ? (p * (uint32_t)a.in_elems + o) * 2 : kOOB), 0, 0));
         const u32x2 m = __builtin_bit_cast(
             u32x2, __builtin_amdgcn_raw_buffer_load_b64(rroute, (int)(in_img ? o : kOOB), 0, 0));
         const uint32_t q4 = ((((gy & 1) << 1) | (gx & 1))) * 0x01010101u;
@@ -786,7 +788,7 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
       } else {
         const uint32_t o = (uint32_t)(((b * a.H + gy) * a.W + gx) * CPT + ch * CP + 8 * c8);
         v[u] = __builtin_bit_cast(
-            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rin[p], (int)(in_img ? o * 2 : kOOB), 0, 0));
+            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rin, (int)(in_img ? (p * (uint32_t)a.in_elems + o) * 2 : kOOB), 0, 0));
       }
     }
   };

@@ -35,7 +35,8 @@
 extern "C" {
 #endif
 
-#define DDQ_ABI_VERSION 4
+#define DDQ_ABI_VERSION 5   /* 5: ddq_step_cfg.reserved -> flags; ddq_synchronize reports a
+                              small-map step's spin timeout as DDQ_ESTATE */
 
 enum ddq_status {
   DDQ_OK = 0,
@@ -154,6 +155,9 @@ int ddq_abi_version(void);
 int ddq_set_stream(ddq_ctx* ctx, void* hip_stream);
 /* The ctx's HIP stream (e.g. for torch.cuda.ExternalStream events). */
 int ddq_get_stream(const ddq_ctx* ctx, void** hip_stream);
+/* Wait for the ctx's streams.  DDQ_ESTATE (and the flag cleared) when a
+ * small-map (S = 16) step's inter-workgroup meeting timed out since the last
+ * call: the launches went on, so that step's results are invalid. */
 int ddq_synchronize(ddq_ctx* ctx);
 
 /* ---------------- parameters ------------------------------------------- */

@@ -9,6 +9,9 @@ usage: RANK=r WORLD_SIZE=W MASTER_ADDR=127.0.0.1 MASTER_PORT=p \
 EXCHANGE "async-graph": the async exchange stepped as graph replays mixed with
 eager rounds (ddq_step_graph_async: one eager round, one K-round graph, then
 eager rounds after the replay -- the comm-stream ordering of ADVICE r03).
+"sharded-pipelined" / "server-pipelined": that exchange's R steps as one
+ddq_step_pipelined_async chain (the next step's draw + gather inside the
+shard-apply launch).
 """
 import os
 import sys
@@ -46,13 +49,18 @@ def main():
     n.replay_import(*member_data(rank), 0, N)
     ddist.setup_comm(n, rank, world)
     graph = exchange == "async-graph"
-    cfg = n.step_cfg("rmsprop", lr=LR, target_period=PERIOD,
-                     exchange="async" if graph else exchange, seed=SEED)
+    piped = exchange.endswith("-pipelined")
+    ex = "async" if graph else exchange.replace("-pipelined", "")
+    cfg = n.step_cfg("rmsprop", lr=LR, target_period=PERIOD, exchange=ex, seed=SEED)
     done = 0
     if graph:   # K = PERIOD / gcd(W, PERIOD) rounds per graph, after one eager round
         k = 1 + PERIOD // np.gcd(world, PERIOD)
         n.step_graph(cfg, min(k, rounds))
         done = min(k, rounds)
+    if piped:
+        n.step_prepare(cfg, "pipelined")
+        n.step_pipelined(cfg, rounds)
+        done = rounds
     for _ in range(rounds - done):
         n.step(cfg)
     n.synchronize()

@@ -56,7 +56,7 @@ def test_struct_layouts_match_header():
 
 
 def test_abi_version(lib):
-    assert lib.ddq_abi_version() == 4
+    assert lib.ddq_abi_version() == 5
 
 
 @pytest.mark.parametrize("batch,frame,ok", [(1024, 256, True), (1024, 512, False),

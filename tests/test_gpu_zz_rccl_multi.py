@@ -78,8 +78,8 @@ def _group(ddq, exchange, world, rounds):
         n.replay_import(*W_.member_data(r), 0, W_.N)
         nets.append(n)
     arr = ddq.DeepQNet.group_init(nets)
-    cfg = nets[0].step_cfg("rmsprop", lr=W_.LR, target_period=W_.PERIOD,
-                           exchange="async" if exchange == "async-graph" else exchange,
+    ex = "async" if exchange == "async-graph" else exchange.replace("-pipelined", "")
+    cfg = nets[0].step_cfg("rmsprop", lr=W_.LR, target_period=W_.PERIOD, exchange=ex,
                            seed=W_.SEED)
     for _ in range(rounds):
         ddq.DeepQNet.group_step(nets, cfg, arr)
@@ -91,7 +91,8 @@ def _group(ddq, exchange, world, rounds):
 
 
 @pytest.mark.skipif("_ngpu() < 2")
-@pytest.mark.parametrize("exchange", ["async", "async-graph", "server", "sharded", "allreduce"])
+@pytest.mark.parametrize("exchange", ["async", "async-graph", "server", "sharded", "allreduce",
+                                      "sharded-pipelined", "server-pipelined"])
 def test_rccl_two_ranks_equal_in_process_group(exchange, tmp_path):
     import ddq
     world, rounds = 2, 5            # 10 async ticks: special updates at iterations 4 and 8
@@ -106,3 +107,16 @@ def test_rccl_two_ranks_equal_in_process_group(exchange, tmp_path):
         sl = slice(0, P) if exchange == "allreduce" else slice(r * L, min((r + 1) * L, P))
         np.testing.assert_array_equal(ranks[r]["opt"][sl], group[r]["opt"][sl],
                                       err_msg="%s rank %d owner optimizer state" % (exchange, r))
+
+
+@pytest.mark.parametrize("exchange", ["sharded-pipelined", "server-pipelined"])
+def test_rccl_worker_world1_pipelined(exchange, tmp_path):
+    """The worker's pipelined modes at world size 1 (runs on a one-GPU box):
+    the RCCL communicator of one rank, the R steps as one pipelined chain,
+    equal to the in-process group of one stepped round by round."""
+    import ddq
+    world, rounds = 1, 6
+    ranks = _run_ranks(exchange, world, rounds, tmp_path)
+    group = _group(ddq, exchange, world, rounds)
+    for key in ("q", "p", "grad", "opt"):
+        np.testing.assert_array_equal(ranks[0][key], group[0][key], err_msg="%s %s" % (exchange, key))

@@ -1,5 +1,5 @@
 """Per-kernel SQ counter breakdown from several rocprofv3 --pmc passes
-(tools/gpu/run_pmc2.sh): mean per dispatch, then derived per-wave shares.
+(tools/gpu/run.sh PMC=...): mean per dispatch, then derived per-wave shares.
 
 Usage: python tools/pmc_detail.py <pass dir> [<pass dir> ...]"""
 import collections
