@@ -857,6 +857,20 @@ def main():
     args.eager = mode == "eager"
     args.pipeline = mode == "pipelined"
     args.no_overlap = not ov
+    # the same command without the preheat: W warmup steps, then 20 timed steps
+    # on a chip fresh from idle (the measured context goes on from there)
+    cold = None
+    if args.preheat_ms > 0 and world == 1:
+        run(args.warmup)
+        net.synchronize()
+        t0 = time.perf_counter()
+        run(20)
+        net.synchronize()
+        cdt = time.perf_counter() - t0
+        cold = {"value": round(20 / cdt, 2), "ms_per_step": round(cdt / 20 * 1e3, 4), "steps": 20,
+                "warmup": args.warmup,
+                "note": "W warmup + 20 timed steps before the preheat, chip fresh from idle "
+                        "(clock ramp: profiles/r04_clock_ramp.txt)"}
     heated = preheat(B, S, local, args.preheat_ms)
     run(args.warmup)
     net.synchronize()
@@ -918,6 +932,35 @@ def main():
     step_flops = net.step_flops()
     step_rl = step_roofline(B, S, net.num_params)
     traffic, traffic_src = pmc_traffic(dom, B, S)
+    # the dominant kernel unprofiled in graph replay: (graph step with conv2's
+    # forward launched twice) - (graph step), same step mode, median of 3
+    # alternations (the difference is one launch + one dependent boundary, an
+    # upper bound on the kernel; the eager dispatch events a lower one)
+    graph_us = None
+    if dom == "conv2_fwd" and not args.eager and ticket is None and world == 1 and S != 16:
+        cfg2 = net.step_cfg(args.rule, lr=1e-4, target_period=10, seed=ddist.index_seed(1234, rank),
+                            store_grads=not args.no_grad_store, repeat_conv2=True)
+        cfg1 = net.step_cfg(args.rule, lr=1e-4, target_period=10, seed=ddist.index_seed(1234, rank),
+                            store_grads=not args.no_grad_store)
+
+        def tgraph(c, n=240):
+            if args.pipeline:
+                net.step_prepare(c, "pipelined")
+                go = lambda k: net.step_pipelined(c, k)   # noqa: E731
+            else:
+                go = lambda k: net.step_graph(c, k)       # noqa: E731
+            go(24)
+            net.synchronize()
+            t0 = time.perf_counter()
+            go(n)
+            net.synchronize()
+            return (time.perf_counter() - t0) / n * 1e6
+
+        diffs = []
+        for _ in range(3):
+            a = tgraph(cfg1)
+            diffs.append(tgraph(cfg2) - a)
+        graph_us = float(np.median(diffs))
 
     if rank == 0:
         out = {
@@ -928,6 +971,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "preheat": heated[1] if heated is not None else None,
+            "no_preheat_20": cold,
             "ms_per_step": round(dt / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
@@ -937,6 +981,7 @@ def main():
             "config": {"workload": "deepq Snake DQN step, batch 32/GPU, 4-frame %dx%d, "
                                    "%d-slot HBM replay, %s apply, target sync every 10"
                                    % (S, S, args.replay, args.rule),
+                       "preheat_ms": args.preheat_ms,
                        "global_batch": B * world, "frame": S,
                        "parallelism": "dp%d" % world, "graph": not args.eager,
                        "exchange": (args.exchange + ("" if args.no_overlap or
@@ -961,6 +1006,14 @@ def main():
                                              "kernel's own dispatch start / stop "
                                              "(hipExtLaunchKernel events on the ctx stream)"
                                              % max(1, args.profile_steps),
+                         "kernel_us_graph": None if graph_us is None else round(graph_us, 3),
+                         "frac_graph": None if not graph_us else
+                         round(flops[dom] / (graph_us * 1e-6) / dom_peak, 4),
+                         "kernel_us_graph_timing": "unprofiled graph replay: (step with the "
+                                                   "kernel launched twice) - (step), median of 3; "
+                                                   "one launch + one dependent boundary (upper "
+                                                   "bound: frac_graph is a lower bound, frac from "
+                                                   "the eager dispatch events an upper one)",
                          "isolated_us": None if iso_us is None else round(iso_us, 3),
                          "isolated_timing": "the same layer, 100 back-to-back launches on one "
                                             "cache-warm input (not the roofline figure)",

@@ -1170,6 +1170,7 @@ static int enqueue_train(ddq_ctx* c, const ddq_step_cfg* cfg, const NetBuffers& 
                          ReplayMeta* bump = nullptr) {
   NetBuffers nb = nb_in;
   nb.book_inc = step_inc(c, cfg);
+  nb.dup_conv2 = (cfg->flags & DDQ_STEP_REPEAT_CONV2_FWD) != 0;
   // exchange-free steps: fc4's weight update rides on the slab-reduce launch
   const int ex = has_exchange(c, cfg) ? cfg->exchange : DDQ_EXCHANGE_NONE;
   const bool ar_overlap = ex == DDQ_EXCHANGE_ALLREDUCE && cfg->overlap && c->comm;
@@ -1260,8 +1261,10 @@ static int check_step(ddq_ctx* c, const ddq_step_cfg* cfg) {
                 c->nb.B, (long long)c->valid);
   if (cfg->exchange < DDQ_EXCHANGE_NONE || cfg->exchange > DDQ_EXCHANGE_ASYNC)
     return fail(c, DDQ_EINVAL, "unknown exchange %d", cfg->exchange);
-  if (cfg->flags & ~DDQ_STEP_NO_GRAD_STORE)
+  if (cfg->flags & ~(DDQ_STEP_NO_GRAD_STORE | DDQ_STEP_REPEAT_CONV2_FWD))
     return fail(c, DDQ_EINVAL, "unknown step flags 0x%x", (unsigned)cfg->flags);
+  if ((cfg->flags & DDQ_STEP_REPEAT_CONV2_FWD) && c->nb.S == 16)
+    return fail(c, DDQ_EINVAL, "DDQ_STEP_REPEAT_CONV2_FWD: no separate conv2 launch at S = 16");
   if (cfg->exchange != DDQ_EXCHANGE_NONE && c->nranks > 1 && !c->comm && !c->local)
     return fail(c, DDQ_ESTATE, "no communicator");
   return DDQ_OK;

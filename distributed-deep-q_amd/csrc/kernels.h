@@ -90,6 +90,7 @@ struct NetBuffers {
   ParamLayout L;
   float gamma;
   int fwd_only;                     // launch_forward: 0 = every layer, l + 1 = conv layer l only
+  int dup_conv2 = 0;                // DDQ_STEP_REPEAT_CONV2_FWD (measurement): conv2 fwd twice
   FusedApplyCfg fa;                 // on: head latches the apply flags, the slab reduce
                                     // applies (FusedApplyCfg)
   int book_inc;                     // param-server iterations per apply (1, or W: server mode)

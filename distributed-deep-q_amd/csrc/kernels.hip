@@ -1869,6 +1869,7 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     a2.mask[0] = nb.mask2; a2.mask[1] = nullptr;
     M("conv2_fwd");
     CHECK_LAUNCH(pick_tile(kConv2Fwd, H, H).launch(a2, nz, s));
+    if (nb.dup_conv2) CHECK_LAUNCH(pick_tile(kConv2Fwd, H, H).launch(a2, nz, s));
   }
   if (!tower && (!nb.fwd_only || nb.fwd_only == 3)) {
     // conv3 (train_val.prototxt:119-158): split bf16, 8x8 tiles (kConv3Fwd), two k groups

@@ -52,6 +52,7 @@ class StepCfg(ctypes.Structure):
 
 
 STEP_NO_GRAD_STORE = 1     # include/ddq_hip.h DDQ_STEP_NO_GRAD_STORE
+STEP_REPEAT_CONV2_FWD = 2  # include/ddq_hip.h DDQ_STEP_REPEAT_CONV2_FWD (measurement only)
 
 ABI_VERSION = 5
 EXCHANGES = {"none": 0, "allreduce": 1, "sharded": 2, "server": 3, "async": 4}

@@ -331,15 +331,18 @@ class DeepQNet:
 
     # -------------------------------------------------------------------- step
     def step_cfg(self, rule="rmsprop", lr=1e-4, target_period=10, allreduce=False, seed=0,
-                 exchange=None, overlap=False, store_grads=True, **kw):
+                 exchange=None, overlap=False, store_grads=True, repeat_conv2=False, **kw):
         """exchange: "none" | "allreduce" | "sharded" | "server" | "async" (include/ddq_hip.h
         enum ddq_exchange); allreduce=True is shorthand for "allreduce".
         store_grads=False: exchange-free steps do not store fc4's weight gradient
-        (DDQ_STEP_NO_GRAD_STORE; the update is the same, bit for bit)."""
+        (DDQ_STEP_NO_GRAD_STORE; the update is the same, bit for bit).
+        repeat_conv2=True: measurement only, conv2's forward launched twice
+        (DDQ_STEP_REPEAT_CONV2_FWD; bench.py's graph-replay kernel figure)."""
         if exchange is None:
             exchange = "allreduce" if allreduce else "none"
         ex = _lib.EXCHANGES[exchange] if isinstance(exchange, str) else int(exchange)
-        flags = 0 if store_grads else _lib.STEP_NO_GRAD_STORE
+        flags = (0 if store_grads else _lib.STEP_NO_GRAD_STORE) | \
+            (_lib.STEP_REPEAT_CONV2_FWD if repeat_conv2 else 0)
         return _lib.StepCfg(_lib.update_cfg(rule, lr, **kw), int(target_period), ex, int(seed),
                             int(bool(overlap)), flags)
 

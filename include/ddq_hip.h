@@ -143,6 +143,12 @@ typedef struct ddq_step_cfg {
  * The update is unchanged, bit for bit.  No effect on exchanged steps (their
  * gradient is what is exchanged). */
 #define DDQ_STEP_NO_GRAD_STORE 1
+/* Measurement only (bench.py's graph-replay kernel figure): every step
+ * launches conv2's forward twice (the launch is idempotent: same inputs, same
+ * outputs), so (graph step time with it - without it) is that kernel's
+ * unprofiled in-graph time.  Not at S = 16 (conv2 runs inside the fused tower
+ * launch there). */
+#define DDQ_STEP_REPEAT_CONV2_FWD 2
 
 /* ---------------- context ---------------------------------------------- */
 /* caffe.Net(prototxt, model) + set_mode_gpu + set_phase_test

@@ -388,8 +388,10 @@ def test_fused_apply_matches_separate_apply(ddq, ref, rule):
     assert not np.array_equal(a.get_flat(0), theta)
 
 
-@pytest.mark.parametrize("S,rule,lr", [(16, "rmsprop", 1e-4), (64, "sgd", 1e-5)])
-def test_no_grad_store_keeps_the_update(ddq, ref, S, rule, lr):
+@pytest.mark.parametrize("S,rule,lr,frames", [(16, "rmsprop", 1e-4, "random"),
+                                               (64, "sgd", 1e-5, "random"),
+                                               (64, "rmsprop", 1e-4, "snake")])
+def test_no_grad_store_keeps_the_update(ddq, ref, S, rule, lr, frames):
     """DDQ_STEP_NO_GRAD_STORE (exchange-free steps do not store fc4's weight
     gradient; bench --no-grad-store) against the default: identical indices,
     parameters of both towers and optimizer state, bit for bit, over eager,
@@ -399,10 +401,15 @@ def test_no_grad_store_keeps_the_update(ddq, ref, S, rule, lr):
     B, N = 32, 300
     rng = np.random.default_rng(41)
     theta = init_params_flat(S, seed=42)          # the bench's initialisation: live ReLUs
-    st = rng.integers(0, 256, (N, 4, S, S)).astype(np.uint8)
-    acts = rng.integers(0, 4, N).astype(np.uint8)
-    rws = rng.integers(-1, 2, N).astype(np.int16)
-    nts = (rng.random(N) > 0.1).astype(np.uint8)
+    if frames == "snake":   # the bench's replay contents (bench.py fill_replay)
+        from ddq.expgain import synthetic_transitions
+        st, acts, rws, nts = synthetic_transitions(N, S, seed=1000)
+        nts = np.asarray(nts).astype(np.uint8)
+    else:
+        st = rng.integers(0, 256, (N, 4, S, S)).astype(np.uint8)
+        acts = rng.integers(0, 4, N).astype(np.uint8)
+        rws = rng.integers(-1, 2, N).astype(np.int16)
+        nts = (rng.random(N) > 0.1).astype(np.uint8)
     nets = []
     for _ in range(2):
         n = ddq.DeepQNet(batch=B, frame=S)
@@ -411,9 +418,10 @@ def test_no_grad_store_keeps_the_update(ddq, ref, S, rule, lr):
         n.replay_create(N)
         n.replay_import(st, acts, rws, nts, 0, N)
         nets.append(n)
-    # (64x64 on this small random ring: sgd at a small rate -- lagged rmsprop
+    # (64x64 on a small random ring: sgd at a small rate -- lagged rmsprop
     # from c = g^2 diverges there within a few steps, as the reference's rule
-    # does, and dead ReLUs would leave nothing to compare)
+    # does, and dead ReLUs would leave nothing to compare; on the bench's Snake
+    # frames rmsprop stays live)
     for n, store in zip(nets, (True, False)):
         cfg = n.step_cfg(rule, lr=lr, target_period=3, seed=4, store_grads=store)
         n.step(cfg)
