@@ -85,6 +85,10 @@ struct ddq_ctx {
   int agraph_rounds = 0;
   int64_t agraph_phase = -1;       // iteration % period the graph was captured at
   ddq_step_cfg acfg{};
+  // ticket-order ticks of this rank's own gradient as graphs, one per (P pull
+  // due, special update due): ddq_async_tick replays instead of re-enqueueing
+  hipGraphExec_t tgexec[4] = {nullptr, nullptr, nullptr, nullptr};
+  ddq_step_cfg tcfg{};
   std::string comm_err;
   // graph
   hipGraph_t graph = nullptr;
@@ -339,6 +343,7 @@ int ddq_destroy(ddq_ctx* c) {
   if (c->stream) hipStreamSynchronize(c->stream);
   invalidate_graph(c);
   if (c->agexec) hipGraphExecDestroy(c->agexec);
+  for (auto& g : c->tgexec) if (g) hipGraphExecDestroy(g);
   for (auto& e : c->ev_pool) hipEventDestroy(e);
   if (c->comm) ncclCommDestroy(c->comm);
   for (void* p : c->allocs) hipFree(p);
@@ -1341,11 +1346,17 @@ static int async_begin(ddq_ctx* c, const ddq_step_cfg* cfg) {
 // applied to the owned shard on arrival (iteration += 1, the launch's own
 // bookkeeping), and the central P shard updated when this tick's pull (at
 // iteration it) is a special update.
-static int async_owner_apply(ddq_ctx* c, const ddq_step_cfg* cfg, int64_t it) {
+// own: the push is this rank's own gradient -- applied from the gradient
+// buffer in place (no copy to gsl), and the worker's copy of the shard written
+// beside the central one (no pull copy)
+static int async_owner_apply(ddq_ctx* c, const ddq_step_cfg* cfg, int64_t it, bool own) {
   const ddq_update_cfg& u = cfg->update;
   const int64_t L = c->shard_len, off = (int64_t)c->rank * L;
+  // (the apply kernel indexes the gradient slice from the shard's start)
+  const float* g = own ? c->nb.grad + off : c->gsl;
   HIP_TRY(c, launch_apply_shard(c->nb, u.rule, u.lr, u.decay, u.eps, u.momentum, u.weight_decay,
-                                c->gsl, off, L, L, 1, c->cs, c->own, c->applied == 0 ? 1 : 0));
+                                g, off, L, L, 1, c->cs, c->own, c->applied == 0 ? 1 : 0, nullptr,
+                                own ? c->nb.theta[0] : nullptr));
   if (cfg->target_period > 0 && it % cfg->target_period == 0)
     HIP_TRY(c, hipMemcpyAsync(c->pown + off, c->own + off, L * 4, hipMemcpyDeviceToDevice, c->cs));
   return DDQ_OK;
@@ -1393,10 +1404,7 @@ static int rccl_async_tick(ddq_ctx* c, const ddq_step_cfg* cfg, int w) {
     }
     NCCL_TRY(c, ncclGroupEnd());
   }
-  if (r == w)
-    HIP_TRY(c, hipMemcpyAsync(c->gsl, nb.grad + (size_t)r * L, L * 4, hipMemcpyDeviceToDevice,
-                              c->cs));
-  TRY(async_owner_apply(c, cfg, it));
+  TRY(async_owner_apply(c, cfg, it, r == w));
   // pull: the owners' shards to worker w
   if (W > 1) {
     NCCL_TRY(c, ncclGroupStart());
@@ -1413,9 +1421,7 @@ static int rccl_async_tick(ddq_ctx* c, const ddq_step_cfg* cfg, int w) {
     }
     NCCL_TRY(c, ncclGroupEnd());
   }
-  if (r == w) {
-    HIP_TRY(c, hipMemcpyAsync(nb.theta[0] + (size_t)r * L, c->own + (size_t)r * L, L * 4,
-                              hipMemcpyDeviceToDevice, c->cs));
+  if (r == w) {   // (the own shard of theta[0]: written by the owner apply)
     if (pull_p)
       HIP_TRY(c, hipMemcpyAsync(nb.theta[1] + (size_t)r * L, c->pown + (size_t)r * L, L * 4,
                                 hipMemcpyDeviceToDevice, c->cs));
@@ -1481,6 +1487,44 @@ int ddq_async_ready(ddq_ctx* c, int32_t* ready) {
   return DDQ_OK;
 }
 
+static int after_async_graph(ddq_ctx* c);
+
+// This rank's own tick (worker == rank) as a graph.  Its launches depend on
+// the host state only through whether this tick pulls P and whether its
+// iteration is a special update (and the first apply of all: eager), so two
+// bits pick the graph; the capture leaves the host bookkeeping as it was.
+static int ensure_tick_graph(ddq_ctx* c, const ddq_step_cfg* cfg, int key) {
+  if (memcmp(&c->tcfg, cfg, sizeof(*cfg)) != 0) {
+    for (auto& g : c->tgexec)
+      if (g) { hipGraphExecDestroy(g); g = nullptr; }
+    c->tcfg = *cfg;
+  }
+  if (c->tgexec[key]) return DDQ_OK;
+  const int64_t applied = c->applied, ticks = c->async_ticks;
+  const std::vector<int64_t> last = c->last_pull;
+  HIP_TRY(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+  c->acapture = true;
+  c->grad_ev_captured = false;
+  int rc = DDQ_OK;
+  hipError_t e = hipEventRecord(c->cev[0], c->stream);   // the comm stream joins
+  if (e == hipSuccess) e = hipStreamWaitEvent(c->cs, c->cev[0], 0);
+  if (e != hipSuccess) rc = fail(c, DDQ_EHIP, "tick graph fork: %s", hipGetErrorString(e));
+  if (rc == DDQ_OK) rc = rccl_async_tick(c, cfg, c->rank);
+  hipGraph_t g = nullptr;
+  e = hipStreamEndCapture(c->stream, &g);
+  c->acapture = false;
+  c->applied = applied;
+  c->async_ticks = ticks;
+  c->last_pull = last;
+  if (rc != DDQ_OK) { if (g) hipGraphDestroy(g); return rc; }
+  if (e != hipSuccess) return fail(c, DDQ_EHIP, "hipStreamEndCapture: %s", hipGetErrorString(e));
+  e = hipGraphInstantiate(&c->tgexec[key], g, nullptr, nullptr, 0);
+  hipGraphDestroy(g);
+  if (e != hipSuccess) return fail(c, DDQ_EHIP, "hipGraphInstantiate: %s", hipGetErrorString(e));
+  HIP_TRY(c, hipGraphUpload(c->tgexec[key], c->stream));
+  return DDQ_OK;
+}
+
 int ddq_async_tick(ddq_ctx* c, const ddq_step_cfg* cfg, int32_t worker) {
   TRY(check_step(c, cfg));
   if (cfg->exchange != DDQ_EXCHANGE_ASYNC) return fail(c, DDQ_EINVAL, "cfg exchange is not async");
@@ -1489,6 +1533,19 @@ int ddq_async_tick(ddq_ctx* c, const ddq_step_cfg* cfg, int32_t worker) {
   TRY(set_dev(c));
   TRY(async_prepare(c, cfg));
   c->rr_rounds = 0;   // the round-robin graph's steady state no longer holds
+  // this rank's own ticks (the heavy ones: its next gradient) replay a graph;
+  // the other workers' ticks (a receive, the owner apply, a send) stay eager
+  if (worker == c->rank && c->applied > 0 && !getenv("DDQ_NO_TICK_GRAPHS")) {
+    const int64_t it = c->applied + 1;
+    const bool pull_p = async_pull_p(cfg, c->last_pull[worker], it);
+    const bool special = cfg->target_period > 0 && it % cfg->target_period == 0;
+    const int key = (pull_p ? 2 : 0) | (special ? 1 : 0);
+    TRY(ensure_tick_graph(c, cfg, key));
+    HIP_TRY(c, hipGraphLaunch(c->tgexec[key], c->stream));
+    TRY(after_async_graph(c));
+    async_advance(c, worker, it);
+    return DDQ_OK;
+  }
   return rccl_async_tick(c, cfg, worker);
 }
 
@@ -1842,7 +1899,7 @@ static int group_async_tick(ddq_ctx** ctxs, int W, const ddq_step_cfg* cfg, int 
     HIP_TRY(c, hipStreamWaitEvent(c->cs, cw->grad_ev, 0));
     HIP_TRY(c, hipMemcpyAsync(c->gsl, cw->nb.grad + (size_t)r * L, L * 4,
                               hipMemcpyDeviceToDevice, c->cs));
-    TRY(async_owner_apply(c, cfg, it));
+    TRY(async_owner_apply(c, cfg, it, false));
     HIP_TRY(c, hipMemcpyAsync(cw->nb.theta[0] + (size_t)r * L, c->own + (size_t)r * L, L * 4,
                               hipMemcpyDeviceToDevice, c->cs));
     if (pull_p)

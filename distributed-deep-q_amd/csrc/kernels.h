@@ -180,7 +180,7 @@ hipError_t launch_apply_shard(const NetBuffers& nb, int rule, float lr, float de
                               float momentum, float wd, const float* gsl, int64_t off,
                               int64_t len, int64_t slice, int W, hipStream_t s,
                               float* theta = nullptr, int first = -1,
-                              const Prefetch* pre = nullptr);
+                              const Prefetch* pre = nullptr, float* mirror = nullptr);
 // force_sync >= 0: P <- Q decided by the host instead of the latched flag
 hipError_t launch_refresh(const NetBuffers& nb, hipStream_t s, int force_sync = -1);
 // one apply's bookkeeping (first-call / sync latches, iteration += 1)

@@ -1476,7 +1476,7 @@ __global__ void apply_book_kernel(int64_t* iter, int32_t* opt_init, int period) 
 __global__ __launch_bounds__(256) void apply_shard_kernel(
     float* __restrict__ theta, const float* __restrict__ gsl, float* __restrict__ opt,
     int32_t* __restrict__ opt_init, int64_t off, int64_t len, int64_t slice, int W,
-    ApplyArgs a, int first_host, int64_t* iter, Prefetch pf) {
+    ApplyArgs a, int first_host, int64_t* iter, Prefetch pf, float* __restrict__ mirror) {
   if ((int)blockIdx.x < pf.ng) {
     prefetch_body(pf, blockIdx.x);
     return;
@@ -1505,6 +1505,9 @@ __global__ __launch_bounds__(256) void apply_shard_kernel(
   const uint32_t nb = (uint32_t)((off + len) * 4), ib = (uint32_t)(i * 4);   // the shard's end
   wt_store4(wt_rsrc(theta, nb), ib, make_float4(th[0], th[1], th[2], th[3]));
   if (a.rule != 0) wt_store4(wt_rsrc(opt, nb), ib, make_float4(st[0], st[1], st[2], st[3]));
+  // (async owner applying its own worker's push: the worker's copy of the
+  // shard too, instead of a pull copy after the apply)
+  if (mirror) wt_store4(wt_rsrc(mirror, nb), ib, make_float4(th[0], th[1], th[2], th[3]));
 }
 
 // After the theta all-gather: conv kernel layouts of Q, and P <- Q (weights
@@ -1579,7 +1582,7 @@ bool fused_apply_ok(const ParamLayout& L) {
 hipError_t launch_apply_shard(const NetBuffers& nb, int rule, float lr, float decay, float eps,
                               float momentum, float wd, const float* gsl, int64_t off,
                               int64_t len, int64_t slice, int W, hipStream_t s, float* theta,
-                              int first, const Prefetch* pre) {
+                              int first, const Prefetch* pre, float* mirror) {
   const ApplyArgs a = apply_args(nb, rule, lr, decay, eps, momentum, wd, 0);
   Prefetch pf{};
   if (pre) pf = *pre;
@@ -1587,7 +1590,7 @@ hipError_t launch_apply_shard(const NetBuffers& nb, int rule, float lr, float de
   if (blocks + pf.ng > 0)
     ddq_launch(apply_shard_kernel, dim3((uint32_t)(blocks + pf.ng)), dim3(256), 0, s,
                        theta ? theta : nb.theta[0], gsl, nb.opt, nb.opt_init, off, len, slice, W,
-                       a, first, nb.iter, pf);
+                       a, first, nb.iter, pf, mirror);
   return hipGetLastError();
 }
 

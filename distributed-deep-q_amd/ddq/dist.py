@@ -144,9 +144,17 @@ class AsyncTicketLoop:
         self.store = dist.PrefixStore("i%d" % self.instance, store)
         self.next = 0            # next ticket to execute
         self.holding = False     # this rank holds a ticket not yet executed
+        self.mine = -1           # ... that ticket's number
 
-    def run(self, npush, poll_s=20e-6, timeout_s=600.0):
-        """Execute the next npush ticks (whoever pushes); returns their workers."""
+    def run(self, npush, poll_s=50e-6, spin_s=2e-3, timeout_s=600.0):
+        """Execute the next npush ticks (whoever pushes); returns their workers.
+
+        The loop spins (no sleep) for spin_s after its last progress -- a
+        sleep of tens of microseconds lasts several times that and the device
+        idles meanwhile -- then polls every poll_s.  A ticket this rank takes
+        is its own to execute: when it is the next one, no store read is
+        needed (one add + one set per own push; other ranks' tickets: one
+        check + one get)."""
         net, store = self.net, self.store
         net.async_begin(self.cfg)
         order = []
@@ -155,23 +163,30 @@ class AsyncTicketLoop:
         while self.next < end:
             progressed = False
             if not self.holding and net.async_ready():
-                t = store.add("ticket", 1) - 1
-                store.set("tk/%d" % t, str(self.rank))
+                self.mine = store.add("ticket", 1) - 1
+                store.set("tk/%d" % self.mine, str(self.rank))
                 self.holding = True
                 progressed = True
-            key = "tk/%d" % self.next
-            if store.check([key]):
-                w = int(store.get(key))
+            w = None
+            if self.holding and self.mine == self.next:
+                w = self.rank
+            else:
+                key = "tk/%d" % self.next
+                if store.check([key]):
+                    w = int(store.get(key))
+            if w is not None:
                 net.async_tick(self.cfg, w)
                 order.append(w)
                 if w == self.rank:
                     self.holding = False
                 self.next += 1
                 progressed = True
+            now = time.perf_counter()
             if progressed:
-                idle_since = time.perf_counter()
+                idle_since = now
             else:
-                if time.perf_counter() - idle_since > timeout_s:
+                if now - idle_since > timeout_s:
                     raise RuntimeError("async ticket loop: no progress for %.0f s" % timeout_s)
-                time.sleep(poll_s)
+                if now - idle_since > spin_s:
+                    time.sleep(poll_s)
         return order
