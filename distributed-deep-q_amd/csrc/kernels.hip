@@ -517,10 +517,10 @@ hipError_t launch_u8_to_nhwc(const uint8_t* src, int n, int S, float* dst, hipSt
 // ---------------------------------------------------------------------------
 // Caffe (co,ci,ky,kx) -> kernel layout (co,ky,kx,ci) for the three convs
 // ---------------------------------------------------------------------------
-// wkst_off > 0 (deepq16 contexts): the layer's transposed + flipped split copy
-// for its data gradient, Wt[ci][T-1 - tap][co], is rewritten with the forward
-// layout by every update (no per-step transpose launch; small_bwd.h K3 reads it)
-struct ConvDims { int64_t w_off, wks_off; int cout, cin, ks; int64_t wkst_off = 0; };
+// (the data gradients' transposed + flipped copies, Wt[ci][T-1 - tap][co], are
+// made from the forward layout per step: wkst_tap, by the head launch's or the
+// deepq16 tower launch's extra workgroups)
+struct ConvDims { int64_t w_off, wks_off; int cout, cin, ks; };
 
 // e: Caffe-order element (co, ci, ky, kx) of the layer's weight (< 2^31);
 // returns its offset in the split forward layout (split.h):
@@ -541,12 +541,6 @@ __device__ __forceinline__ int wks_local(const ConvDims& d, int e) {
 __device__ __forceinline__ void put_conv_weight(const ConvDims& d, int e, float v, __bf16* wks,
                                                 int64_t wks_plane) {
   store_split(wks, wks_plane, d.wks_off + wks_local(d, e), v);
-  if (d.wkst_off) {
-    const int kk = d.ks * d.ks, per = d.cin * kk;
-    const int co = e / per, rem = e - co * per;
-    const int ci = rem / kk, tap = rem - ci * kk;
-    store_split(wks, wks_plane, d.wkst_off + ((int64_t)ci * kk + kk - 1 - tap) * d.cout + co, v);
-  }
 }
 
 __global__ void relayout_kernel(const float* __restrict__ theta, __bf16* __restrict__ wks,
@@ -561,10 +555,6 @@ __global__ void relayout_kernel(const float* __restrict__ theta, __bf16* __restr
 static void conv_dims(const ParamLayout& L, ConvDims* d) {
   const int cout[3] = {32, 64, 64}, cin[3] = {4, 32, 64}, ks[3] = {7, 5, 3};
   for (int i = 0; i < 3; ++i) d[i] = {L.w[i], L.wks_off[i], cout[i], cin[i], ks[i]};
-  if (L.S == sm16::kS) {   // deepq16: the data gradients' copies with every update
-    d[1].wkst_off = L.wkst_off;
-    d[2].wkst_off = L.wkst3_off;
-  }
 }
 
 hipError_t launch_relayout(const NetBuffers& nb, int z, hipStream_t s) {
@@ -720,8 +710,14 @@ __device__ void book_block(const BookArgs& k) {
   }
 }
 
+__device__ void tower_transpose(const TowerArgs& a, int x, char* smem) {
+  if (x < 25) wkst_tap<32, 25>(a.wks[0], a.wks_plane, a.wks2_off, a.wkst_off, x, smem);
+  else wkst_tap<64, 9>(a.wks[0], a.wks_plane, a.wks3_off, a.wkst3_off, x - 25, smem);
+}
+
 hipError_t launch_tower_fwd16(const TowerArgs& t, hipStream_t s) {
   const bool book = t.bk.latch || t.bk.bump || t.bk.dmeta;
+  const int extra = (book ? 1 : 0) + t.ntr;
   if (t.xchg && 2 * t.B * t.nz <= 256) {
     // split form: two workgroups per (image, tower), every pair resident at
     // once (<= 256 workgroups of one per CU: their meet cannot wait on an
@@ -730,14 +726,14 @@ hipError_t launch_tower_fwd16(const TowerArgs& t, hipStream_t s) {
     auto kern = tower_fwd16s_kernel<K2, K3>;
     static std::atomic<uint64_t> attr{0};
     if (hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(kern), attr, kFwdSmemS)) return e;
-    ddq_launch(kern, dim3(2 * t.B * t.nz + (book ? 1 : 0)), dim3(kThreads), kFwdSmemS, s, t);
+    ddq_launch(kern, dim3(2 * t.B * t.nz + extra), dim3(kThreads), kFwdSmemS, s, t);
     return hipGetLastError();
   }
   constexpr int K2 = 6, K3 = 5;
   auto kern = tower_fwd16_kernel<K2, K3>;
   static std::atomic<uint64_t> attr{0};
   if (hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(kern), attr, kFwdSmem)) return e;
-  ddq_launch(kern, dim3(t.B * t.nz + (book ? 1 : 0)), dim3(kThreads), kFwdSmem, s, t);
+  ddq_launch(kern, dim3(t.B * t.nz + extra), dim3(kThreads), kFwdSmem, s, t);
   return hipGetLastError();
 }
 }  // namespace sm16
@@ -1819,6 +1815,10 @@ static sm16::TowerArgs tower_args(const NetBuffers& nb, int nz, const sm16::Book
   if (bk) t.bk = *bk;
   t.xchg = nb.xchg; t.pairc = nb.pairc;
   t.timeout = nb.csync ? nb.csync + 48 : nullptr;   // (csync: allocated at S = 16)
+  // K3's transposed weights, from this launch's Q weights (its extra blocks)
+  t.ntr = 25 + 9;
+  t.wks2_off = L.wks_off[1]; t.wkst_off = L.wkst_off;
+  t.wks3_off = L.wks_off[2]; t.wkst3_off = L.wkst3_off;
   return t;
 }
 
@@ -1955,9 +1955,11 @@ hipError_t launch_small_fwd_head(const NetBuffers& nb, hipStream_t s,
 }
 
 void small_groups(int B, int* G2, int* G3) {
-  // conv2 tiles: groups of >= 2 images (16 at most: 160 workgroups); conv3
-  // tiles: 8 groups of >= 4 images (48 workgroups) -- co-resident with room
-  *G2 = std::max(1, std::min(16, B / 2));
+  // conv2 tiles: groups of >= 4 images (16 at most: 160 workgroups); conv3
+  // tiles: 8 groups of >= 4 images (48 workgroups) -- co-resident with room.
+  // (deepq16 B = 32, measured: G2 8 / 16 -> wgrad launch 17.1 / 20.2 us: half
+  // the write-through slab bytes, and the meeting's arrival skew with them)
+  *G2 = std::max(1, std::min(16, B / 4));
   *G3 = std::max(1, std::min(8, B / 4));
 }
 

@@ -86,6 +86,10 @@ struct TowerArgs {
   uint8_t *mask1, *mask2, *mask3;   // Q: NHWC routing bytes (0..3 first max, 4 ReLU'd)
   float* pool3[2];             // Caffe (B, 64, 2, 2)
   BookArgs bk;
+  // the data gradients' transposed split weights of Q (K3 reads them), made
+  // from wks[0] by ntr extra workgroups (25 conv2 taps, 9 conv3 taps)
+  int ntr;
+  int64_t wks2_off, wkst_off, wks3_off, wkst3_off;
   // split form (tower_fwd16s): the pool2 halves' exchange
   __bf16* xchg;                // [B][nz][2 halves][3 planes][16 px][32 ch]
   uint64_t* pairc;             // [B][nz] meeting counters
@@ -168,6 +172,7 @@ struct W3Tap {
 };
 
 __device__ void book_block(const BookArgs& k);
+__device__ void tower_transpose(const TowerArgs& a, int x, char* smem);
 
 // n workgroups meet: returns in each once all n have arrived (their stores
 // write-through and drained: visible to sc1 loads, MI355X_MICROARCH.md
@@ -215,7 +220,8 @@ __global__ __launch_bounds__(kThreads) void tower_fwd16_kernel(const TowerArgs a
   const int l31 = lane & 31, h = lane >> 5;
   const int bid = blockIdx.x;
   if (bid >= a.B * a.nz) {
-    book_block(a.bk);
+    if (bid - a.B * a.nz < a.ntr) tower_transpose(a, bid - a.B * a.nz, smem);
+    else book_block(a.bk);
     return;
   }
   DDQ_STAMP(0);
@@ -593,7 +599,8 @@ __global__ __launch_bounds__(kThreads) void tower_fwd16s_kernel(const TowerArgs 
   const int l31 = lane & 31, h = lane >> 5;
   const int bid = blockIdx.x;
   if (bid >= 2 * a.B * a.nz) {
-    book_block(a.bk);
+    if (bid - 2 * a.B * a.nz < a.ntr) tower_transpose(a, bid - 2 * a.B * a.nz, smem);
+    else book_block(a.bk);
     return;
   }
   DDQ_STAMP(0);

@@ -25,8 +25,8 @@ namespace sm16 {
 //            partials in order); dW4 rows, db4, dW5 columns (and workgroup
 //            0: db5) -- all final here, so the fused apply updates them here.
 // The launch is 32 fc4 workgroups (all resident: one per CU at most).  (The
-// transposed split weights K3 reads are rewritten by every update at S = 16:
-// kernels.hip put_conv_weight.)
+// transposed split weights K3 reads are made from the step's Q weights by K1's
+// extra workgroups: kernels.hip tower_transpose.)
 // ---------------------------------------------------------------------------
 constexpr int kFcN = 16;                 // fc4 outputs per workgroup
 constexpr int kFcBlk = 512 / kFcN;       // 32 workgroups
@@ -1604,6 +1604,12 @@ __device__ __forceinline__ void wg_tile(const WgArgs& a, char* smem, int tile, i
         if (gg < G) v += t[gg];
       vs[k] = v;
     }
+#ifdef DDQ_STAMPS
+    if (c0 == e0) {   // (phase stamps: the sums landed)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      DDQ_STAMP(SB + 6);
+    }
+#endif
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
       const int e = c0 + tid + 256 * k;

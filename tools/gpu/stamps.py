@@ -61,7 +61,9 @@ for r, t in enumerate(runs):
         if not len(tt):
             continue
         t0 = tt[:, lo].min()
-        seq = [16, 17, 18, 19, 20, 44, 45, 46, 21, 22, 23] if lo == 16 else range(lo, lo + (2 if lo >= 40 else 8))
+        seq = [16, 17, 18, 19, 20, 44, 45, 46, 21, 22, 23] if lo == 16 else \
+            ([lo, lo + 1, lo + 2, lo + 3, lo + 4, lo + 6, lo + 5] if lo in (24, 32) else
+             range(lo, lo + (2 if lo >= 40 else 8)))
         used = [k for k in seq if (tt[:, k] > 0).any()]
         rel = {k: (np.median(tt[:, k] - tt[:, lo]) * 10 / 1000, (tt[:, k].max() - t0) * 10 / 1000)
                for k in used}
