@@ -163,6 +163,19 @@ struct SplitCfg {
   static_assert(MF == 0 || CP % 32 == 0, "16x16x32: whole 32-channel k-steps");
 };
 
+// Row order of a 32-channel staging store (2 rows per 8-lane ds_write_b128
+// group, SplitWStage::row): rows n and n + d share a group, d the row distance
+// whose stride puts them 16 banks apart (d = 4 at 20 dwords, 2 at 24);
+// identity for other shapes
+template <int CP, int STRIDE>
+__device__ __forceinline__ int pair_rows(int n0) {
+  constexpr int DW = STRIDE / 2;                      // bf16 -> dwords
+  constexpr int D = (CP == 32 && (4 * DW) % 32 == 16) ? 4 : (CP == 32 && (2 * DW) % 32 == 16) ? 2 : 0;
+  if constexpr (D == 0) return n0;
+  const int r = n0 & (2 * D - 1);
+  return (n0 & ~(2 * D - 1)) | ((r >> 1) + (r & 1) * D);
+}
+
 // Weight staging of one (chunk, tap) (3 planes of N x CP bf16): a global ->
 // register load issued two steps ahead, a register -> LDS store after the
 // MFMAs of the step before it.  Native vector registers in an array indexed
@@ -176,15 +189,13 @@ struct SplitWStage {
   static_assert(kPer <= 12, "weight staging registers");
   u32x4 r[kPer];
   // ds_write_b128 serves 8 contiguous lanes per LDS cycle on banks (a/4) mod
-  // 32.  With 32-channel rows (4 vectors, row stride CW = 40 bf16 = 20 dwords)
-  // lanes 4-7 hit the banks of lanes 0-3 when they write row n + 1; writing
-  // rows n and n + 4 instead (80 dwords apart: the other 16 banks) is
-  // conflict-free -- a permutation of the rows within blocks of 8, the same
-  // for the load and the store of a lane
+  // 32.  With 32-channel rows (4 vectors) an 8-lane group writes two rows:
+  // rows n and n + 1 overlap in 8 banks at a row stride of 20 dwords (CW 40)
+  // or 24 (CW 48).  Rows n and n + d with d * stride = 16 (mod 32) take the
+  // other 16 banks: conflict-free (a permutation of the rows within blocks of
+  // 2d, the same for the load and the store of a lane)
   static __device__ __forceinline__ int row(int q) {
-    const int n0 = q / (CP / 8);
-    if (CP != 32 || C::CW != 40) return n0;
-    return (n0 & ~7) | ((n0 & 7) >> 1) | ((n0 & 1) << 2);
+    return pair_rows<CP, C::CW>(q / (CP / 8));
   }
 
   // tap t of chunk ch
@@ -759,12 +770,11 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
       const int f = live ? f0 : 0;
       const int p = f / NV, r = f - p * NV;
       const int pix0 = r / (CP / 8), c8 = r % (CP / 8);
-      // 32-channel pixels (20 dwords apart): pixels q and q + 4 share an
-      // 8-lane store group instead of q and q + 1 (SplitWStage::row)
+      // 32-channel pixels (20 or 24 dwords apart): pixels q and q + d share
+      // an 8-lane store group instead of q and q + 1 (pair_rows); the block
+      // of 2d pixels past the last whole one stays in order
       constexpr int NPX = C::PH * C::PW;
-      const int pix = (CP == 32 && C::CS == 40 && pix0 < (NPX & ~7))
-                          ? (pix0 & ~7) | ((pix0 & 7) >> 1) | ((pix0 & 1) << 2)
-                          : pix0;
+      const int pix = pix0 < (NPX & ~7) ? pair_rows<CP, C::CS>(pix0) : pix0;
       const int py = pix / C::PW, px = pix % C::PW;
       const int gy = y0 - a.pad + py, gx = x0 - a.pad + px;
       const bool in_img = live && (unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W;

@@ -30,6 +30,8 @@ if [ -n "$PROF" ]; then
     echo PROF_FAILED; tail -5 $R/gpurun_out/prof.err; exit 1; }
   cd $R
   python3 tools/trace_summary.py gpurun_out/prof prof | head -40
+  # (the per-dispatch trace stays on the box: gpurun_out is merged back <= 64 MiB)
+  find gpurun_out/prof -name "*kernel_trace.csv" -size +8M -delete
 fi
 if [ -n "$PMC" ]; then
   i=0
@@ -42,4 +44,7 @@ if [ -n "$PMC" ]; then
     cd $R
     i=$((i + 1))
   done
+  # per-kernel means of every pass -> one JSON (tools/pmc_json.py), raw rows dropped
+  python3 tools/pmc_json.py gpurun_out gpurun_out/pmc.json
+  find gpurun_out -path "*pmc_*" -name "*.csv" -delete
 fi
