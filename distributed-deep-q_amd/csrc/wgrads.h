@@ -278,7 +278,11 @@ __device__ __forceinline__ void wgrads_body(const WgradSArgs& a, char* smem, int
       const int px = dpx + 16 * u;
       if (px >= (W >> 1)) continue;
 #pragma unroll
-      for (int dx = 0; dx < 2; ++dx) {
+      for (int d2 = 0; d2 < 2; ++d2) {
+        // odd pooled pixels write their two expanded pixels in the other order:
+        // an 8-lane ds_write_b128 group (pooled pixels p, p + 1) then writes
+        // pixels 16 / 48 dwords apart, not 32 (banks (a/4) mod 32: conflict-free)
+        const int dx = d2 ^ (dpx & 1);
         const uint32_t qd = qy | dx;
         // per bf16 pair e (channels 2e, 2e+1): keep-masks from the routing bytes
         uint32_t keep[4];
