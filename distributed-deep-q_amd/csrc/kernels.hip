@@ -2016,6 +2016,9 @@ hipError_t launch_small_bwd(const NetBuffers& nb, hipStream_t s,
     w.book = book; w.book_period = book_period; w.book_inc = nb.book_inc;
     w.iter = nb.iter;
     w.bump = book && !nb.fa.on ? bump : nullptr;
+    w.w4_off = L.w[3];
+    w.nw4 = w.apply ? 32 : 0;
+    if (L.w[3] % 4) return hipErrorInvalidValue;   // (float4 rows; 94496 for this net)
     if (pre && nb.fa.on) {
       w.pf = *pre;
       w.pf.predrawn = bump != nullptr && B <= 256;   // K1 drew it (its book block)
@@ -2032,7 +2035,8 @@ hipError_t launch_small_bwd(const NetBuffers& nb, hipStream_t s,
                                 sm16::kWgSmem));
     M("wgrad_apply");
     ddq_launch(sm16::wgrad16_kernel,
-               dim3(sm16::kT3 * w.G3 + sm16::kT2 * w.G2 + sm16::kW1Blocks + w.pf.ng), dim3(256),
+               dim3(sm16::kT3 * w.G3 + sm16::kT2 * w.G2 + sm16::kW1Blocks + w.pf.ng + w.nw4),
+               dim3(256),
                lds, s, w);
     CHECK_LAUNCH(hipGetLastError());
   }

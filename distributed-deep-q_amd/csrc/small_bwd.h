@@ -64,7 +64,7 @@ struct ChainArgs {
   float *q_out, *p_out, *q_sa, *p_sa, *target, *loss;
   float* grad;                     // flat Q gradient
   int apply;                       // fused apply (flags latched by K1's book block)
-  int store_grad;                  // fused apply: W4's gradient to grad as well
+  int store_grad;                  // (unused: W4's gradient is always stored -- K4 applies it)
   ApplyArgs aa;
   ApplyTail at;
 };
@@ -223,16 +223,6 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
     }
   }
   DDQ_STAMP(18);
-  // the W4 rows' theta / state (the tail's update), loaded under the fan-in
-  float w4th[2][4], w4st[2][4];
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t e = c.w4_off + (int64_t)(n0 + 4 * kq + i) * kFcK + 16 * (2 * wid + u) + lr;
-      w4th[u][i] = ap0 ? c.at.theta[e] : 0.f;
-      w4st[u][i] = ap0 && c.aa.rule != 0 ? c.at.opt[e] : 0.f;
-    }
   meet(reinterpret_cast<uint64_t*>(c.sync), kFcBlk, c.sync + 2);
   DDQ_STAMP(19);
 
@@ -396,24 +386,16 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
     }
   }
   DDQ_STAMP(22);
-  // ---- W4 rows: gradient, and the update (the rows are this workgroup's) ----
+  // ---- W4 rows: the gradient (K4's W4 blocks apply it: the rmsprop update's
+  // correctly rounded divides and square roots, 8 a thread here, cost this
+  // launch 2.8 us at its end; K4 has CUs free for them) ----
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < 2; ++u)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int n = 4 * kq + i, k = 16 * (2 * wid + u) + lr;
-      const int64_t e = c.w4_off + (int64_t)(n0 + n) * kFcK + k;
-      const float g = gw[u][i];
-      if (!ap || c.store_grad) c.grad[e] = g;
-      if (ap) {
-        float st = (c.aa.rule != 0 && !first) ? w4st[u][i] : 0.f;
-        const float th = apply_rule(c.aa, first, false, w4th[u][i], g, st);
-        c.at.theta[e] = th;
-        if (c.aa.rule != 0) c.at.opt[e] = st;
-        if (sync) c.at.thetaP[e] = th;
-      }
+      c.grad[c.w4_off + (int64_t)(n0 + n) * kFcK + k] = gw[u][i];
     }
-  }
   DDQ_STAMP(23);
 }
 
@@ -1262,6 +1244,9 @@ struct WgArgs {
   int64_t* iter;
   ReplayMeta* bump;
   Prefetch pf;
+  // the fused apply's fc4 weight update (K2 stored the gradient): nw4 blocks
+  int64_t w4_off;
+  int nw4;
 };
 
 // Apply one final conv gradient element (layer l, Caffe index i, local e of
@@ -1619,6 +1604,28 @@ __device__ __forceinline__ void wg_tile(const WgArgs& a, char* smem, int tile, i
   DDQ_STAMP(SB + 5);
 }
 
+// fc4's weights (512 x 256 at S = 16) updated from the gradient K2 stored, 4
+// consecutive elements a thread (coalesced), the rules of the other apply
+// sites (apply_rule, no FMA contraction: bit-identical updates)
+__device__ __forceinline__ void w4_apply(const WgArgs& a, int blk, bool first, bool sync) {
+  constexpr int64_t n = 512LL * kFcK;
+  for (int64_t j = ((int64_t)blk * 256 + threadIdx.x) * 4; j < n; j += (int64_t)a.nw4 * 256 * 4) {
+    const int64_t i = a.w4_off + j;
+    const float4 g = *reinterpret_cast<const float4*>(a.grad + i);
+    const float4 t = *reinterpret_cast<const float4*>(a.at.theta + i);
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.aa.rule != 0 && !first) o = *reinterpret_cast<const float4*>(a.at.opt + i);
+    const float gg[4] = {g.x, g.y, g.z, g.w};
+    float th[4] = {t.x, t.y, t.z, t.w}, st[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) th[e] = apply_rule(a.aa, first, false, th[e], gg[e], st[e]);
+    const float4 t4 = make_float4(th[0], th[1], th[2], th[3]);
+    *reinterpret_cast<float4*>(a.at.theta + i) = t4;
+    if (a.aa.rule != 0) *reinterpret_cast<float4*>(a.at.opt + i) = make_float4(st[0], st[1], st[2], st[3]);
+    if (sync) *reinterpret_cast<float4*>(a.at.thetaP + i) = t4;
+  }
+}
+
 // Block order: conv3's tiles (the longest chains) first, conv2's, then
 // conv1's slab sums and the next step's gather (short, no meeting) -- every
 // meeting workgroup is dispatched before any block that could hold a CU.
@@ -1640,10 +1647,10 @@ __global__ __launch_bounds__(256) void wgrad16_kernel(const WgArgs a) {
     return;
   }
   bid -= n2;
-  if (bid >= kW1Blocks) {                              // the next step's gather
-    DDQ_STAMP(42);
-    prefetch_body(a.pf, bid - kW1Blocks);
-    DDQ_STAMP(43);
+  if (bid >= kW1Blocks) {   // the next step's gather, then the fc4 weights' update
+    const int x = bid - kW1Blocks;
+    if (x < a.pf.ng) prefetch_body(a.pf, x);
+    else w4_apply(a, x - a.pf.ng, first, sync);
     return;
   }
   DDQ_STAMP(40);

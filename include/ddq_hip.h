@@ -139,7 +139,9 @@ typedef struct ddq_step_cfg {
 /* Exchange-free steps: fc4's weight gradient (96 % of the parameters) is
  * computed and applied tile by tile inside the slab-reduce launch and NOT
  * stored to the gradient buffer (8.4 MB of writes per step at 64x64), so
- * ddq_get_grads after such a step returns that block of an earlier step.
+ * ddq_get_grads after such a step returns that block of an earlier step
+ * (at S = 16 the block is stored regardless: the fused step's last launch
+ * applies it from there).
  * The update is unchanged, bit for bit.  No effect on exchanged steps (their
  * gradient is what is exchanged). */
 #define DDQ_STEP_NO_GRAD_STORE 1

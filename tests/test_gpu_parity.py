@@ -440,4 +440,7 @@ def test_no_grad_store_keeps_the_update(ddq, ref, S, rule, lr, frames):
     keep[off:off + cnt] = False
     np.testing.assert_array_equal(ga[keep], gb[keep])
     assert np.count_nonzero(ga[~keep]) > cnt // 100     # a's last fc4 gradient, stored
-    assert not np.array_equal(ga[~keep], gb[~keep])
+    if S == 16:   # the small-map step stores it regardless (K4's apply reads it)
+        np.testing.assert_array_equal(ga[~keep], gb[~keep])
+    else:
+        assert not np.array_equal(ga[~keep], gb[~keep])
