@@ -103,3 +103,14 @@ def test_missing_library_raises(tmp_path):
             _lib.load(str(tmp_path / "nope.so"))
     finally:
         _lib._lib = saved
+
+
+def test_header_constants_match_binding():
+    """ddq/_lib.py's copies of the header's #defines (step flags, ABI version)."""
+    from ddq import _lib
+    txt = open(HEADER).read()
+    defs = {k: int(v) for k, v in re.findall(r"#define\s+(DDQ_\w+)\s+(\d+)", txt)}
+    assert defs["DDQ_ABI_VERSION"] == _lib.ABI_VERSION
+    assert defs["DDQ_STEP_NO_GRAD_STORE"] == _lib.STEP_NO_GRAD_STORE
+    assert defs["DDQ_STEP_REPEAT_CONV2_FWD"] == _lib.STEP_REPEAT_CONV2_FWD
+    assert _lib.STEP_NO_GRAD_STORE & _lib.STEP_REPEAT_CONV2_FWD == 0
