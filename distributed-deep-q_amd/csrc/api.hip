@@ -298,6 +298,11 @@ int ddq_create(ddq_ctx** out, int device, const ddq_net_desc* desc) {
       small_groups(B, &G2, &G3);
       TRY(dalloc(c, &nb.slab2, (size_t)10 * G2 * (32 * 5 * 32 + 32)));
       TRY(dalloc(c, &nb.slab3, (size_t)6 * G3 * (32 * 3 * 64 + 32)));
+      nb.small_G = B > 32 ? (B + 31) / 32 : 1;   // <= 8: 32 G fc4 workgroups, all resident
+      if (nb.small_G > 1) {
+        TRY(dalloc(c, &nb.upart, (size_t)nb.small_G * 32 * 96));
+        TRY(dalloc(c, &nb.w4part, (size_t)nb.small_G * 512 * 256));
+      }
     }
     int64_t off = 0;
     const int cout[3] = {32, 64, 64};

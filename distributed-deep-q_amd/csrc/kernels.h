@@ -98,6 +98,9 @@ struct NetBuffers {
                                     // fused apply (async gradients: sample_gather draws)
   // deepq16 step (small.h, small_bwd.h): fc4 chain partials and its fan-in words
   int small;                        // S == 16, B <= 256: the four-launch step
+  int small_G = 1;                  // its fc4 chain's image chunks (B > 32: ceil(B / 32))
+  float* upart = nullptr;           // [G][32][96] unit-sum partials (G > 1)
+  float* w4part = nullptr;          // [G][512][256] fc4 weight-gradient partials (G > 1)
   float *qpart, *dpart;             // [32][2][B][4] Q_out / P_out partials, [32][B][256] dpool3
   int32_t* csync;                   // meeting words: K2 [0..2] (64-bit counter, timeout),
                                     // K4 [8..40) (a 64-bit counter per tile, timeout at

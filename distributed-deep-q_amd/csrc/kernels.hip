@@ -1945,11 +1945,13 @@ hipError_t launch_small_fwd_head(const NetBuffers& nb, hipStream_t s,
   c.aa = apply_args(nb, nb.fa.rule, nb.fa.lr, nb.fa.decay, nb.fa.eps, nb.fa.momentum, nb.fa.wd,
                     nb.fa.period);
   c.at = apply_tail(nb);
+  c.G = nb.small_G; c.upart = nb.upart; c.w4part = nb.w4part;
+  if (c.G > 8 || (c.G > 1 && (!c.upart || !c.w4part))) return hipErrorInvalidValue;
   static std::atomic<uint64_t> attr{0};
   CHECK_LAUNCH(ensure_dyn_lds(reinterpret_cast<const void*>(sm16::fc4_chain16_kernel), attr,
                               sm16::kChainSmem));
   M("fc4_chain");
-  ddq_launch(sm16::fc4_chain16_kernel, dim3(sm16::kFcBlk), dim3(512), sm16::kChainSmem, s, c);
+  ddq_launch(sm16::fc4_chain16_kernel, dim3(sm16::kFcBlk * c.G), dim3(512), sm16::kChainSmem, s, c);
   CHECK_LAUNCH(hipGetLastError());
   return hipSuccess;
 }
@@ -1970,8 +1972,9 @@ hipError_t launch_small_bwd(const NetBuffers& nb, hipStream_t s,
   const ParamLayout& L = nb.L;
   const int B = nb.B;
   auto M = [&](const char* n) { if (mark) mark(marg, n); };
-  // fc4's weight gradient is final since K2: the overlapped all-reduce starts
-  if (fc4_done) CHECK_LAUNCH(fc4_done(fc4_done_arg));
+  // fc4's weight gradient is final since K2 (B <= 32; else after K4's chunk
+  // sums): the overlapped all-reduce starts
+  if (fc4_done && nb.small_G == 1) CHECK_LAUNCH(fc4_done(fc4_done_arg));
   {
     sm16::BwdArgs a{};
     a.B = B; a.dpart = nb.dpart;
@@ -2017,7 +2020,10 @@ hipError_t launch_small_bwd(const NetBuffers& nb, hipStream_t s,
     w.iter = nb.iter;
     w.bump = book && !nb.fa.on ? bump : nullptr;
     w.w4_off = L.w[3];
-    w.nw4 = w.apply ? 32 : 0;
+    w.G = nb.small_G; w.upart = nb.upart; w.w4part = nb.w4part;
+    w.b4_off = L.b[3]; w.w5_off = L.w[4]; w.b5_off = L.b[4]; w.loss = nb.loss;
+    w.nw4 = (w.apply || w.G > 1) ? 32 : 0;
+    w.nus = w.G > 1 ? 1 : 0;
     if (L.w[3] % 4) return hipErrorInvalidValue;   // (float4 rows; 94496 for this net)
     if (pre && nb.fa.on) {
       w.pf = *pre;
@@ -2035,11 +2041,13 @@ hipError_t launch_small_bwd(const NetBuffers& nb, hipStream_t s,
                                 sm16::kWgSmem));
     M("wgrad_apply");
     ddq_launch(sm16::wgrad16_kernel,
-               dim3(sm16::kT3 * w.G3 + sm16::kT2 * w.G2 + sm16::kW1Blocks + w.pf.ng + w.nw4),
+               dim3(sm16::kT3 * w.G3 + sm16::kT2 * w.G2 + sm16::kW1Blocks + w.pf.ng + w.nw4 +
+                    w.nus),
                dim3(256),
                lds, s, w);
     CHECK_LAUNCH(hipGetLastError());
   }
+  if (fc4_done && nb.small_G > 1) CHECK_LAUNCH(fc4_done(fc4_done_arg));   // (chunk sums done)
   return hipSuccess;
 }
 

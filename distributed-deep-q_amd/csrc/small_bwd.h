@@ -64,6 +64,12 @@ struct ChainArgs {
   float *q_out, *p_out, *q_sa, *p_sa, *target, *loss;
   float* grad;                     // flat Q gradient
   int apply;                       // fused apply (flags latched by K1's book block)
+  // B > 32: G = ceil(B / 32) image chunks, one per workgroup of a unit block
+  // (32 G workgroups); the batch sums become per-chunk partials K4 sums in
+  // chunk order: upart [G][32][96] (unit sums, db5, loss), w4part [G][512][256]
+  int G;
+  float* upart;
+  float* w4part;
   int store_grad;                  // (unused: W4's gradient is always stored -- K4 applies it)
   ApplyArgs aa;
   ApplyTail at;
@@ -89,11 +95,11 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int bid = blockIdx.x;
   DDQ_STAMP(16);
-#ifdef DDQ_EXP_K2_EMPTY
-  return;
-#endif
-  const int B = c.B, n0 = bid * kFcN;
-  const int nch = (B + kBC - 1) / kBC;
+  // unit block jb, image chunk cc: images [lo, hi) (G == 1: all of them)
+  const int G = c.G, jb = bid % kFcBlk, cc = bid / kFcBlk;
+  const int B = c.B, n0 = jb * kFcN;
+  const int lo = G > 1 ? cc * kBC : 0, hi = G > 1 ? min(B, lo + kBC) : B;
+  const int nch = (hi - lo + kBC - 1) / kBC;
   float* WS = csm + CH_WS;
   float* XS = csm + CH_XS;
   float* RED = csm + CH_RED;
@@ -122,7 +128,7 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
     const int f = tid + u * 512;                                                               \
     const int z = f >> 11, b = (f >> 6) & 31, k4 = f & 63;                                     \
     xv[u] = make_float4(0.f, 0.f, 0.f, 0.f);                                                   \
-    if ((bb0) + b < B) xv[u] = *reinterpret_cast<const float4*>(c.x[z] + (int64_t)((bb0) + b) * kFcK + 4 * k4); \
+    if ((bb0) + b < hi) xv[u] = *reinterpret_cast<const float4*>(c.x[z] + (int64_t)((bb0) + b) * kFcK + 4 * k4); \
   }
 #define DDQ_XSTORE()                                                                           \
   _Pragma("unroll") for (int u = 0; u < 8; ++u) {                                              \
@@ -130,7 +136,7 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
     const int z = f >> 11, b = (f >> 6) & 31, k4 = f & 63;                                     \
     *reinterpret_cast<float4*>(XS + (z * kBC + b) * kXP + 4 * k4) = xv[u];                     \
   }
-  DDQ_XLOAD(0)
+  DDQ_XLOAD(lo)
   float w5q = tid < 64 ? c.th[0][c.w5_off + (tid >> 4) * 512 + n0 + (tid & 15)] : 0.f;
   // theta / optimizer state of the parameters the unit sums update (db4 and
   // dW5 columns of the units: q = 0..79; b5: q = 80..83, workgroup 0), read
@@ -140,7 +146,7 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
                   : c.b5_off + (q - 80);
   };
   float pth = 0.f, pst = 0.f;
-  const bool ap0 = c.apply != 0;
+  const bool ap0 = c.apply != 0 && G == 1;   // (G > 1: K4 applies the batch sums)
   // the update's flags (latched by K1's book block), loaded now
   const bool first = ap0 && c.at.opt_init[2] != 0, sync = ap0 && c.at.opt_init[3] != 0;
   if (ap0 && tid < 84) {
@@ -169,7 +175,7 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
 
   // ---- phase A, chunk by chunk of 32 images ----
   for (int ch = 0; ch < nch; ++ch) {
-    const int bb0 = ch * kBC;
+    const int bb0 = lo + ch * kBC;
     if (ch) {
       __syncthreads();                             // previous chunk's XS reads done
       DDQ_XLOAD(bb0)
@@ -213,9 +219,9 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
         q[a] += __shfl_xor(q[a], 16);
         q[a] += __shfl_xor(q[a], 32);
       }
-      if (b < B) {
+      if (b < hi) {
         if (kq == 0)                               // write-through: the fan-in's hand-off
-          wt_store4(rq, (uint32_t)((((bid * 2 + wz) * B + b) * 4) * 4), make_float4(q[0], q[1], q[2], q[3]));
+          wt_store4(rq, (uint32_t)((((jb * 2 + wz) * B + b) * 4) * 4), make_float4(q[0], q[1], q[2], q[3]));
         if (wz == 0)
 #pragma unroll
           for (int i = 0; i < 4; ++i) H[b * kFcN + 4 * kq + i] = hv[i];
@@ -223,12 +229,13 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
     }
   }
   DDQ_STAMP(18);
-  meet(reinterpret_cast<uint64_t*>(c.sync), kFcBlk, c.sync + 2);
+  meet(reinterpret_cast<uint64_t*>(c.sync), kFcBlk * G, c.sync + 2);
   DDQ_STAMP(19);
 
   // ---- phase B: every sample's Q_out / P_out (partials summed in j order) ----
-  for (int p = tid; p < 2 * B; p += 512) {
-    const int z = p / B, b = p - z * B;
+  const int nbi = hi - lo;
+  for (int p = tid; p < 2 * nbi; p += 512) {
+    const int z = p / nbi, b = lo + p - z * nbi;
     float4 v[kFcBlk];
 #pragma unroll
     for (int j = 0; j < kFcBlk; ++j) v[j] = ld_sc1_f4(rq, (uint32_t)((((j * 2 + z) * B + b) * 4) * 4));
@@ -242,7 +249,7 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
   __syncthreads();
   DDQ_STAMP(20);
   // head (ELTWISE PROD, SLICE, SUM, MAX, target, EUCLIDEAN_LOSS): as head_body
-  for (int b = tid; b < B; b += 512) {
+  for (int b = lo + tid; b < hi; b += 512) {
     const float* qp = QP + b * 4;
     const float* pp = QP + (kMaxB + b) * 4;
     const float* ac = csm + CH_MB + b * 4;
@@ -258,7 +265,7 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
 #pragma unroll
     for (int a = 0; a < 4; ++a) DQ[b * 4 + a] = ac[a] * gsc;
     TMP[b] = diff * diff;
-    if (bid == 0) {
+    if (jb == 0) {
       c.q_sa[b] = qs; c.p_sa[b] = ps; c.target[b] = tg;
       *reinterpret_cast<float4*>(c.q_out + b * 4) = *reinterpret_cast<const float4*>(qp);
       *reinterpret_cast<float4*>(c.p_out + b * 4) = *reinterpret_cast<const float4*>(pp);
@@ -268,7 +275,7 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
   DDQ_STAMP(44);
   const bool ap = ap0;
   // dh4 of the workgroup's units: (dQ W5) masked by h4 > 0 (ReLU backward)
-  for (int e = tid; e < B * kFcN; e += 512) {
+  for (int e = lo * kFcN + tid; e < hi * kFcN; e += 512) {
     const int b = e >> 4, n = e & 15;
     const float* w5 = csm + CH_W5 + n;
     const float* dq = DQ + b * 4;
@@ -281,27 +288,29 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
   // four threads a quantity (thread r of the four: samples r, r + 4, ... in
   // order), combined by two quad shuffles (fixed order, deterministic)
   {
-    const int hq = bid == 0 ? 5 : 0, nq = hq + 5 * kFcN;
+    const int hq = jb == 0 ? 5 : 0, nq = hq + 5 * kFcN;
     const int qq = tid >> 2, r4 = tid & 3;
     const bool head = qq < hq;
     const int q = head ? qq : qq - hq;
     float v = 0.f;
     if (qq < nq) {
       if (head) {
-        for (int b = r4; b < B; b += 4) v += q < 4 ? DQ[b * 4 + q] : TMP[b];
+        for (int b = lo + r4; b < hi; b += 4) v += q < 4 ? DQ[b * 4 + q] : TMP[b];
       } else {
         const int r = q >> 4, n = q & 15;            // r 0: db4, 1..4: dW5[r - 1]
         if (r == 0) {
-          for (int b = r4; b < B; b += 4) v += DH[b * kFcN + n];
+          for (int b = lo + r4; b < hi; b += 4) v += DH[b * kFcN + n];
         } else {
-          for (int b = r4; b < B; b += 4) v += DQ[b * 4 + r - 1] * H[b * kFcN + n];
+          for (int b = lo + r4; b < hi; b += 4) v += DQ[b * 4 + r - 1] * H[b * kFcN + n];
         }
       }
     }
     v += __shfl_xor(v, 1);
     v += __shfl_xor(v, 2);
     DDQ_STAMP(46);
-    if (r4 == 0 && qq < nq) {
+    if (r4 == 0 && qq < nq && G > 1) {   // the chunk's partial: K4 sums the chunks
+      c.upart[(cc * kFcBlk + jb) * 96 + (head ? (q == 4 ? 84 : 80 + q) : q)] = v;
+    } else if (r4 == 0 && qq < nq) {
       if (head && q == 4) {
         *c.loss = v / (float)B / 2.f;
       } else {
@@ -326,7 +335,7 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
   // wave wid: dW4 k blocks 2 wid, 2 wid + 1; dpart tiles (b block, k block)
   f32x4v gw[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   for (int ch = 0; ch < nch; ++ch) {
-    const int bb0 = ch * kBC;
+    const int bb0 = lo + ch * kBC;
     if (nch > 1) {                                 // reload the chunk's x_Q (one chunk: resident)
       __syncthreads();
 #pragma unroll
@@ -334,12 +343,12 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
         const int f = tid + u * 512;
         const int b = f >> 6, k4 = f & 63;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (bb0 + b < B) v = *reinterpret_cast<const float4*>(c.x[0] + (int64_t)(bb0 + b) * kFcK + 4 * k4);
+        if (bb0 + b < hi) v = *reinterpret_cast<const float4*>(c.x[0] + (int64_t)(bb0 + b) * kFcK + 4 * k4);
         *reinterpret_cast<float4*>(XS + b * kXP + 4 * k4) = v;
       }
     }
     __syncthreads();
-    const int nb = min(kBC, B - bb0);
+    const int nb = min(kBC, hi - bb0);
     // dW4: A[n][k = b] = DH[b][n], B[k = b][col] = x_Q[b][col]; the chunk's
     // 8 b quads' operands read first (rows past B are zero in XS, DH read 0)
     {
@@ -366,7 +375,7 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const int n = 4 * s + kq;
-        dav[u][s] = b < B ? DH[b * kFcN + n] : 0.f;
+        dav[u][s] = b < hi ? DH[b * kFcN + n] : 0.f;
         dbv[u][s] = WS[n * kXP + 16 * kb + lr];
       }
     }
@@ -381,7 +390,7 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int bi = bb0 + 16 * bbk + 4 * kq + i;
-        if (bi < B) c.dpart[((int64_t)bid * B + bi) * kFcK + 16 * kb + lr] = d[i];
+        if (bi < hi) c.dpart[((int64_t)jb * B + bi) * kFcK + 16 * kb + lr] = d[i];
       }
     }
   }
@@ -394,7 +403,8 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int n = 4 * kq + i, k = 16 * (2 * wid + u) + lr;
-      c.grad[c.w4_off + (int64_t)(n0 + n) * kFcK + k] = gw[u][i];
+      if (G > 1) c.w4part[((int64_t)cc * 512 + n0 + n) * kFcK + k] = gw[u][i];
+      else c.grad[c.w4_off + (int64_t)(n0 + n) * kFcK + k] = gw[u][i];
     }
   DDQ_STAMP(23);
 }
@@ -857,7 +867,6 @@ __global__ __launch_bounds__(kThreads) void tower_bwd16s_kernel(const BwdArgs a)
   static_assert(K3 >= 3 && KD >= 3, "ring: tap t + 2 is stored from registers at tap t");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int l31 = lane & 31, h = lane >> 5;
   const int b = blockIdx.x >> 1, half = blockIdx.x & 1, B = a.B;
   DDQ_STAMP(8);
   const __bf16* __restrict__ wt3 = a.wks + a.wkst3_off;
@@ -1247,6 +1256,14 @@ struct WgArgs {
   // the fused apply's fc4 weight update (K2 stored the gradient): nw4 blocks
   int64_t w4_off;
   int nw4;
+  // B > 32 (K2's G image chunks): the fc4 weight gradient and the unit sums
+  // (db4, dW5, db5, loss) summed over the chunks' partials in chunk order
+  // here (nw4 blocks, then nus blocks), stored, and applied when apply
+  int G, nus;
+  const float* upart;
+  const float* w4part;
+  int64_t b4_off, w5_off, b5_off;
+  float* loss;
 };
 
 // Apply one final conv gradient element (layer l, Caffe index i, local e of
@@ -1321,7 +1338,7 @@ __device__ __forceinline__ void wg_tile(const WgArgs& a, char* smem, int tile, i
       __builtin_amdgcn_make_buffer_rsrc((void*)in, (short)0, (int)(3 * Ein * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t rd =
       __builtin_amdgcn_make_buffer_rsrc((void*)dsrc, (short)0, (int)(3 * Ed * 2), 0x00020000);
-  constexpr int SB = L == 1 ? 24 : 32;               // stamp slots (DDQ_STAMPS builds)
+  [[maybe_unused]] constexpr int SB = L == 1 ? 24 : 32;   // stamp slots (DDQ_STAMPS builds)
   DDQ_STAMP(SB);
   // the operand ring: round rr in slot rr % D (every index compile-time after
   // unrolling: registers, no scratch)
@@ -1611,7 +1628,18 @@ __device__ __forceinline__ void w4_apply(const WgArgs& a, int blk, bool first, b
   constexpr int64_t n = 512LL * kFcK;
   for (int64_t j = ((int64_t)blk * 256 + threadIdx.x) * 4; j < n; j += (int64_t)a.nw4 * 256 * 4) {
     const int64_t i = a.w4_off + j;
-    const float4 g = *reinterpret_cast<const float4*>(a.grad + i);
+    float4 g;
+    if (a.G > 1) {   // the chunks' partials in chunk order -> the gradient
+      g = *reinterpret_cast<const float4*>(a.w4part + j);
+      for (int cc = 1; cc < a.G; ++cc) {
+        const float4 p = *reinterpret_cast<const float4*>(a.w4part + (int64_t)cc * n + j);
+        g.x += p.x; g.y += p.y; g.z += p.z; g.w += p.w;
+      }
+      *reinterpret_cast<float4*>(a.grad + i) = g;
+      if (!a.apply) continue;
+    } else {
+      g = *reinterpret_cast<const float4*>(a.grad + i);
+    }
     const float4 t = *reinterpret_cast<const float4*>(a.at.theta + i);
     float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
     if (a.aa.rule != 0 && !first) o = *reinterpret_cast<const float4*>(a.at.opt + i);
@@ -1623,6 +1651,30 @@ __device__ __forceinline__ void w4_apply(const WgArgs& a, int blk, bool first, b
     *reinterpret_cast<float4*>(a.at.theta + i) = t4;
     if (a.aa.rule != 0) *reinterpret_cast<float4*>(a.at.opt + i) = make_float4(st[0], st[1], st[2], st[3]);
     if (sync) *reinterpret_cast<float4*>(a.at.thetaP + i) = t4;
+  }
+}
+
+// B > 32: the unit sums' partials (K2 upart) summed in chunk order -> db4,
+// dW5 (32 blocks x 80), db5 (4), loss; stored, and applied when apply
+__device__ __forceinline__ void units_apply(const WgArgs& a, bool first, bool sync) {
+  for (int q = threadIdx.x; q < kFcBlk * 85; q += 256) {
+    const int jb = q / 85, qq = q - jb * 85;
+    if (qq >= 80 && jb != 0) continue;                // (db5, loss: block 0's)
+    float v = a.upart[jb * 96 + qq];
+    for (int cc = 1; cc < a.G; ++cc) v += a.upart[(cc * kFcBlk + jb) * 96 + qq];
+    if (qq == 84) { *a.loss = v / (float)a.B / 2.f; continue; }
+    const int n0 = jb * kFcN;
+    const int64_t i = qq >= 80 ? a.b5_off + (qq - 80)
+                               : ((qq >> 4) == 0 ? a.b4_off + n0 + (qq & 15)
+                                                 : a.w5_off + ((qq >> 4) - 1) * 512 + n0 + (qq & 15));
+    const bool is_bias = qq >= 80 || (qq >> 4) == 0;
+    a.grad[i] = v;
+    if (!a.apply) continue;
+    float st = (a.aa.rule != 0 && !first) ? a.at.opt[i] : 0.f;
+    const float th = apply_rule(a.aa, first, is_bias, a.at.theta[i], v, st);
+    a.at.theta[i] = th;
+    if (a.aa.rule != 0) a.at.opt[i] = st;
+    if (sync) a.at.thetaP[i] = th;
   }
 }
 
@@ -1647,10 +1699,11 @@ __global__ __launch_bounds__(256) void wgrad16_kernel(const WgArgs a) {
     return;
   }
   bid -= n2;
-  if (bid >= kW1Blocks) {   // the next step's gather, then the fc4 weights' update
-    const int x = bid - kW1Blocks;
-    if (x < a.pf.ng) prefetch_body(a.pf, x);
-    else w4_apply(a, x - a.pf.ng, first, sync);
+  if (bid >= kW1Blocks) {   // the fc4 weights' (and unit sums') update, then the next
+    const int x = bid - kW1Blocks;   // step's gather (B = 256: 512 short blocks, last)
+    if (x < a.nw4) w4_apply(a, x, first, sync);
+    else if (x < a.nw4 + a.nus) units_apply(a, first, sync);
+    else prefetch_body(a.pf, x - a.nw4 - a.nus);
     return;
   }
   DDQ_STAMP(40);
@@ -1678,6 +1731,13 @@ __global__ __launch_bounds__(256) void wgrad16_kernel(const WgArgs a) {
     const float* src = a.w1part + co * np + n;
     float v = 0.f;
     int b0 = 0;
+    for (; b0 + 32 <= a.B; b0 += 32) {   // 32 loads in flight a round (B = 256: 8 rounds)
+      float t[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) t[u] = src[(int64_t)(b0 + u) * 32 * np];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) v += t[u];
+    }
     for (; b0 + 8 <= a.B; b0 += 8) {
       float t[8];
 #pragma unroll

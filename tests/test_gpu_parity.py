@@ -346,15 +346,17 @@ def test_rccl_world1_allreduce_and_step(ddq, ref):
     np.testing.assert_array_equal(nets[0].get_flat(0), nets[1].get_flat(0))
 
 
-@pytest.mark.parametrize("rule", ["rmsprop", "adagrad", "momentum"])
-def test_fused_apply_matches_separate_apply(ddq, ref, rule):
+@pytest.mark.parametrize("rule,B", [("rmsprop", 16), ("adagrad", 16), ("momentum", 16),
+                                    ("rmsprop", 100)])
+def test_fused_apply_matches_separate_apply(ddq, ref, rule, B):
     """The fused fc4-weight apply (slab-reduce launch, draw counter advanced by
     the head kernel; exchange-free steps) against the separate apply launch
     the exchanges use (a one-member in-process group with the all-reduce
     exchange: sum of one slice, then the plain apply): identical parameters,
     optimizer state and P<-Q syncs over eager, pipelined and graph chains that
-    cross sync steps."""
-    S, B, N = 16, 16, 300
+    cross sync steps.  B = 100: the fc4 chain's four image chunks, their
+    partial sums reduced in the weight-gradient launch."""
+    S, N = 16, 300
     rng = np.random.default_rng(31)
     theta = ref.flatten(ref.init_params(S, seed=8))
     st = rng.integers(0, 256, (N, 4, S, S)).astype(np.uint8)
