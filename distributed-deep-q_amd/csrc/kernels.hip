@@ -400,58 +400,60 @@ __global__ __launch_bounds__(256) void bm_emit_kernel(const uint32_t* __restrict
   }
 }
 
-// u8 (C,H,W) slots -> f32 Caffe (n,4,S,S).  A workgroup converts 1024
-// consecutive 4-byte words of the output's u8 image: 4 independent dword
-// loads per thread at stride 256 (each wave instruction reads 256 contiguous
-// bytes) and 4 float4 non-temporal stores (each wave instruction writes 1 KiB
-// contiguous).  blockIdx.y = 0: state from idx, 1: next_state from idx+1
-// (N-1 wraps to 0; only the last sorted index can, replay.py:160-166) plus
-// one-hot action, reward, non_terminal of idx+1.
+// u8 (C,H,W) slots -> f32 Caffe (n,4,S,S).  blockIdx.x = (row b, slice):
+// a row's wps 4-byte words are cut into cpr slices of 512, so the slot index
+// is one uniform load a workgroup (no per-lane divide, no per-lane index
+// load ahead of the data load).  Each thread: 2 dword loads at stride 256
+// (a wave instruction reads 256 contiguous bytes), then 2 float4
+// non-temporal stores (a wave instruction writes 1 KiB contiguous).  Against
+// the round-4 flat kernel (1024 words a workgroup, per-lane divmod + index
+// load; 4.38 TB/s at n = 32768) this is 5.9 TB/s; 1 or 4 words a thread,
+// more words per thread and plain stores were all slower.
+// blockIdx.y = 0: state from idx, 1: next_state from idx+1 (N-1 wraps to 0;
+// only the last sorted index can, replay.py:160-166) plus one-hot action,
+// reward, non_terminal of idx+1.
+constexpr int kGatherWpt = 2;
 __global__ __launch_bounds__(256) void gather_nchw_kernel(
     const uint8_t* __restrict__ st, const uint8_t* __restrict__ act,
     const int16_t* __restrict__ rew, const uint8_t* __restrict__ nt, ReplayMeta* meta,
-    const int32_t* __restrict__ idx, int n, FastDiv wps, float* __restrict__ s0,
+    const int32_t* __restrict__ idx, int n, uint32_t wps, FastDiv cpr, float* __restrict__ s0,
     float* __restrict__ s1, float* __restrict__ action, float* __restrict__ reward,
     float* __restrict__ nonterm) {
   typedef float fv4 __attribute__((ext_vector_type(4)));
   const int z = blockIdx.y;
   const int64_t N = meta->capacity;
-  const uint64_t total = (uint64_t)n * wps.d;
-  const uint32_t* src = reinterpret_cast<const uint32_t*>(st);
-  fv4* dst = reinterpret_cast<fv4*>(z ? s1 : s0);
-  uint32_t v[4];
-  uint64_t g[4];
+  uint32_t b, part;
+  cpr.divmod(blockIdx.x, b, part);
+  const int64_t i = idx[b];
+  const int64_t slot = z ? ((i + 1 == N) ? 0 : i + 1) : i;
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(st) + (uint64_t)slot * wps;
+  fv4* dst = reinterpret_cast<fv4*>(z ? s1 : s0) + (uint64_t)b * wps;
+  uint32_t v[kGatherWpt];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    g[k] = (uint64_t)blockIdx.x * 1024 + k * 256 + threadIdx.x;
-    v[k] = 0;
-    if (g[k] < total) {
-      uint32_t b, q;
-      wps.divmod((uint32_t)g[k], b, q);
-      const int64_t i = idx[b];
-      const int64_t slot = z ? ((i + 1 == N) ? 0 : i + 1) : i;
-      v[k] = src[(uint64_t)slot * wps.d + q];
-    }
+  for (int k = 0; k < kGatherWpt; ++k) {
+    const uint32_t q = part * (256 * kGatherWpt) + k * 256 + threadIdx.x;
+    v[k] = q < wps ? src[q] : 0u;
   }
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    if (g[k] < total) {
+  for (int k = 0; k < kGatherWpt; ++k) {
+    const uint32_t q = part * (256 * kGatherWpt) + k * 256 + threadIdx.x;
+    if (q < wps) {
       const fv4 f = {(float)(v[k] & 255), (float)((v[k] >> 8) & 255),
                      (float)((v[k] >> 16) & 255), (float)(v[k] >> 24)};
-      __builtin_nontemporal_store(f, dst + g[k]);
+      __builtin_nontemporal_store(f, dst + q);
     }
   }
   if (z == 1) {
-    const uint32_t b = blockIdx.x * 256 + threadIdx.x;   // first blocks: per-row scalars
-    if ((int)b < n) {
-      const int64_t i = idx[b];
-      const int64_t nxt = (i + 1 == N) ? 0 : i + 1;
+    const uint32_t r = blockIdx.x * 256 + threadIdx.x;   // first blocks: per-row scalars
+    if ((int)r < n) {
+      const int64_t j = idx[r];
+      const int64_t nxt = (j + 1 == N) ? 0 : j + 1;
       const int a = act[nxt];
       if (a >= kActions) meta->err = 1;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) action[(size_t)b * 4 + k] = (k == a) ? 1.f : 0.f;
-      reward[b] = (float)rew[nxt];
-      nonterm[b] = nt[nxt] ? 1.f : 0.f;
+      for (int k = 0; k < 4; ++k) action[(size_t)r * 4 + k] = (k == a) ? 1.f : 0.f;
+      reward[r] = (float)rew[nxt];
+      nonterm[r] = nt[nxt] ? 1.f : 0.f;
     }
   }
 }
@@ -474,10 +476,10 @@ hipError_t launch_gather_nchw(const uint8_t* st, const uint8_t* act, const int16
                               int S, float* s0, float* s1, float* action, float* reward,
                               float* nonterm, hipStream_t s) {
   const uint32_t wps = (uint32_t)(S * S);          // 4-byte words per slot
-  const uint64_t tot = (uint64_t)n * wps;           // < 2^31 (n <= 2^31 / S^2 checked)
-  const uint64_t blocks = std::max<uint64_t>((tot + 1023) / 1024, (uint64_t)(n + 255) / 256);
-  ddq_launch(gather_nchw_kernel, dim3((uint32_t)blocks, 2), dim3(256), 0, s, st, act,
-                     rew, nt, meta, idx, n, FastDiv(wps), s0, s1, action, reward, nonterm);
+  const uint32_t per = 256u * kGatherWpt;
+  const uint32_t cpr = (wps + per - 1) / per;       // n * cpr < 2^31 (n <= 2^31 / S^2 checked)
+  ddq_launch(gather_nchw_kernel, dim3((uint32_t)n * cpr, 2), dim3(256), 0, s, st, act, rew, nt,
+             meta, idx, n, wps, FastDiv(cpr), s0, s1, action, reward, nonterm);
   return hipGetLastError();
 }
 
