@@ -1147,17 +1147,32 @@ static int enqueue_exchange_apply(ddq_ctx* c, const ddq_step_cfg* cfg, const Net
   if (mark) mark(marg, ex == DDQ_EXCHANGE_SHARDED ? "reduce_scatter" : "all_to_all");
   if (ex == DDQ_EXCHANGE_SHARDED)
     NCCL_TRY(c, ncclReduceScatter(nb.grad, c->gsl, len, ncclFloat, ncclSum, c->comm, c->stream));
-  else
-    NCCL_TRY(c, ncclAllToAll(nb.grad, c->gsl, len, ncclFloat, c->comm, c->stream));
+  else if (W > 1) {
+    // all-to-all without the rank's own slice: the owner apply reads that one
+    // in place from nb.grad (no self copy of len floats through RCCL)
+    NCCL_TRY(c, ncclGroupStart());
+    for (int p = 0; p < W; ++p) {
+      if (p == c->rank) continue;
+      NCCL_TRY(c, ncclSend(nb.grad + (size_t)p * len, len, ncclFloat, p, c->comm, c->stream));
+      NCCL_TRY(c, ncclRecv(c->gsl + (size_t)p * len, len, ncclFloat, p, c->comm, c->stream));
+    }
+    NCCL_TRY(c, ncclGroupEnd());
+  }
   if (mark) mark(marg, "apply_shard");
   HIP_TRY(c, launch_apply_shard(nb, u.rule, u.lr, u.decay, u.eps, u.momentum, u.weight_decay,
                                 c->gsl, (int64_t)c->rank * len, (int64_t)len, (int64_t)len,
-                                ex == DDQ_EXCHANGE_SHARDED ? 1 : W, c->stream, nullptr, -1, pf));
+                                ex == DDQ_EXCHANGE_SHARDED ? 1 : W, c->stream, nullptr, -1, pf,
+                                nullptr, -1, c->rank,
+                                ex == DDQ_EXCHANGE_SHARDED ? nullptr
+                                                           : nb.grad + (size_t)c->rank * len));
   if (mark) mark(marg, "all_gather");
   NCCL_TRY(c, ncclAllGather(nb.theta[0] + (size_t)c->rank * len, nb.theta[0], len, ncclFloat,
                             c->comm, c->stream));
+  // the owner's shard was refreshed by its apply: the other ranks' shards
+  // only (no launch when one rank owns every parameter)
   if (mark) mark(marg, "refresh");
-  HIP_TRY(c, launch_refresh(nb, c->stream));
+  HIP_TRY(c, launch_refresh(nb, c->stream, -1, (int64_t)c->rank * len,
+                            (int64_t)(c->rank + 1) * len));
   return DDQ_OK;
 }
 
@@ -1354,6 +1369,13 @@ static int async_begin(ddq_ctx* c, const ddq_step_cfg* cfg) {
 // own: the push is this rank's own gradient -- applied from the gradient
 // buffer in place (no copy to gsl), and the worker's copy of the shard written
 // beside the central one (no pull copy)
+// -- and, from the same values, that shard's kernel layouts and (on a tick that
+// updates the central P) the worker's P shard and its layouts: the worker's
+// refreshes after the pull skip the shard (async_after_pull)
+static bool async_p_now(const ddq_step_cfg* cfg, int64_t it) {
+  return cfg->target_period > 0 && it % cfg->target_period == 0;
+}
+
 static int async_owner_apply(ddq_ctx* c, const ddq_step_cfg* cfg, int64_t it, bool own) {
   const ddq_update_cfg& u = cfg->update;
   const int64_t L = c->shard_len, off = (int64_t)c->rank * L;
@@ -1361,21 +1383,27 @@ static int async_owner_apply(ddq_ctx* c, const ddq_step_cfg* cfg, int64_t it, bo
   const float* g = own ? c->nb.grad + off : c->gsl;
   HIP_TRY(c, launch_apply_shard(c->nb, u.rule, u.lr, u.decay, u.eps, u.momentum, u.weight_decay,
                                 g, off, L, L, 1, c->cs, c->own, c->applied == 0 ? 1 : 0, nullptr,
-                                own ? c->nb.theta[0] : nullptr));
-  if (cfg->target_period > 0 && it % cfg->target_period == 0)
+                                own ? c->nb.theta[0] : nullptr,
+                                own ? (async_p_now(cfg, it) ? 2 : 1) : 0));
+  if (async_p_now(cfg, it))
     HIP_TRY(c, hipMemcpyAsync(c->pown + off, c->own + off, L * 4, hipMemcpyDeviceToDevice, c->cs));
   return DDQ_OK;
 }
 
 // Worker side after its pull (theta[0], and theta[1] when pull_p, hold the
 // central model; the ctx stream waited for them): kernel layouts of Q (and
-// P), then the next gradient.
-static int async_after_pull(ddq_ctx* c, const ddq_step_cfg* cfg, bool pull_p) {
-  HIP_TRY(c, launch_refresh(c->nb, c->stream, 0));
+// P), then the next gradient.  own: the worker's own shard was refreshed by
+// its owner apply (Q; P too when this tick updated the central P: p_own).
+static int async_after_pull(ddq_ctx* c, const ddq_step_cfg* cfg, bool pull_p, bool own = false,
+                            bool p_own = false) {
+  const int64_t lo = own ? (int64_t)c->rank * c->shard_len : 0;
+  const int64_t hi = own ? lo + c->shard_len : 0;
+  p_own = p_own && own;
+  HIP_TRY(c, launch_refresh(c->nb, c->stream, 0, lo, hi));
   if (pull_p) {   // P's layouts from the pulled P weights
     NetBuffers pb = c->nb;
     pb.theta[0] = c->nb.theta[1]; pb.wks[0] = c->nb.wks[1];
-    HIP_TRY(c, launch_refresh(pb, c->stream, 0));
+    HIP_TRY(c, launch_refresh(pb, c->stream, 0, p_own ? lo : 0, p_own ? hi : 0));
   }
   return async_compute(c, cfg);
 }
@@ -1426,13 +1454,15 @@ static int rccl_async_tick(ddq_ctx* c, const ddq_step_cfg* cfg, int w) {
     }
     NCCL_TRY(c, ncclGroupEnd());
   }
-  if (r == w) {   // (the own shard of theta[0]: written by the owner apply)
-    if (pull_p)
+  if (r == w) {   // (the own shard of theta[0]: written by the owner apply;
+                  // of theta[1] too when this tick updated the central P)
+    const bool p_own = async_p_now(cfg, it);
+    if (pull_p && !p_own)
       HIP_TRY(c, hipMemcpyAsync(nb.theta[1] + (size_t)r * L, c->pown + (size_t)r * L, L * 4,
                                 hipMemcpyDeviceToDevice, c->cs));
     HIP_TRY(c, hipEventRecord(c->tick_ev, c->cs));
     HIP_TRY(c, hipStreamWaitEvent(c->stream, c->tick_ev, 0));
-    TRY(async_after_pull(c, cfg, pull_p));
+    TRY(async_after_pull(c, cfg, pull_p, true, p_own));
   }
   async_advance(c, w, it);
   return DDQ_OK;

@@ -179,13 +179,24 @@ hipError_t launch_relayout(const NetBuffers& nb, int z, hipStream_t s);
 // and the apply's bookkeeping (iteration += 1) done by the launch itself
 // (async owner applies); -1: the flags latched by a prior launch_book.
 // pre: the next step's draw + gather as extra blocks (pipelined steps)
+// refresh_own != 0: the launch also does launch_refresh's work for its own
+// shard (conv kernel layouts of nb.wks[0]; the P <- Q copy into nb.theta[1] /
+// nb.wks[1] when a sync is due: -1 the latched flag decides, 1 no sync, 2
+// sync), from the values it applied; the refresh after the all-gather / pull
+// then skips that shard.  own_g: slice own_w
+// is read from there (the rank's own gradient in place) instead of gsl
 hipError_t launch_apply_shard(const NetBuffers& nb, int rule, float lr, float decay, float eps,
                               float momentum, float wd, const float* gsl, int64_t off,
                               int64_t len, int64_t slice, int W, hipStream_t s,
                               float* theta = nullptr, int first = -1,
-                              const Prefetch* pre = nullptr, float* mirror = nullptr);
-// force_sync >= 0: P <- Q decided by the host instead of the latched flag
-hipError_t launch_refresh(const NetBuffers& nb, hipStream_t s, int force_sync = -1);
+                              const Prefetch* pre = nullptr, float* mirror = nullptr,
+                              int refresh_own = 0, int own_w = -1,
+                              const float* own_g = nullptr);
+// force_sync >= 0: P <- Q decided by the host instead of the latched flag.
+// [skip_lo, skip_hi): a range already refreshed (an owner's refresh_own
+// apply); nothing is launched when it covers every parameter
+hipError_t launch_refresh(const NetBuffers& nb, hipStream_t s, int force_sync = -1,
+                          int64_t skip_lo = 0, int64_t skip_hi = 0);
 // one apply's bookkeeping (first-call / sync latches, iteration += 1)
 hipError_t launch_book(const NetBuffers& nb, int period, hipStream_t s);
 hipError_t launch_sum_slices(float* out, const float* in, int W, int64_t len, int64_t slice,

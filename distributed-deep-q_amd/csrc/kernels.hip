@@ -1471,10 +1471,41 @@ __global__ void apply_book_kernel(int64_t* iter, int32_t* opt_init, int period) 
 // Blocks [0, pf.ng): the next step's draw + gather (pipelined sharded /
 // server steps: the step's bookkeeping in the slab reduce advanced the draw
 // counter already).
+// launch_refresh's per-float4 work: the P copy on a sync step and, for conv
+// weights, the kernel layouts of Q (and P on a sync step)
+__device__ __forceinline__ void refresh_elems(const ApplyArgs& a, bool sync, int64_t i,
+                                              const float (&th)[4], float* __restrict__ thetaP,
+                                              __bf16* wks, __bf16* wksP, int64_t wks_plane) {
+  if (sync)
+    wt_store4(wt_rsrc(thetaP, (uint32_t)(((a.n + 3) & ~3ll) * 4)), (uint32_t)(i * 4),
+              make_float4(th[0], th[1], th[2], th[3]));
+#pragma unroll
+  for (int l = 0; l < 3; ++l) {
+    const ConvDims& d = a.conv[l];
+    const int64_t e0 = i - d.w_off;
+    if (e0 >= 0 && e0 < (int64_t)d.cout * d.cin * d.ks * d.ks) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        put_conv_weight(d, (int)e0 + e, th[e], wks, wks_plane);
+        if (sync) put_conv_weight(d, (int)e0 + e, th[e], wksP, wks_plane);
+      }
+    }
+  }
+}
+
+struct RefreshOut {
+  float* thetaP;
+  __bf16* wks;
+  __bf16* wksP;
+  int64_t wks_plane;
+  int mode;   // 0 off; 1 sync = the latched flag; 2 / 3 sync decided by the host: no / yes
+};
+
 __global__ __launch_bounds__(256) void apply_shard_kernel(
     float* __restrict__ theta, const float* __restrict__ gsl, float* __restrict__ opt,
     int32_t* __restrict__ opt_init, int64_t off, int64_t len, int64_t slice, int W,
-    ApplyArgs a, int first_host, int64_t* iter, Prefetch pf, float* __restrict__ mirror) {
+    ApplyArgs a, int first_host, int64_t* iter, Prefetch pf, float* __restrict__ mirror,
+    RefreshOut ro, int own_w, const float* __restrict__ own_g) {
   if ((int)blockIdx.x < pf.ng) {
     prefetch_body(pf, blockIdx.x);
     return;
@@ -1494,7 +1525,9 @@ __global__ __launch_bounds__(256) void apply_shard_kernel(
   float th[4] = {t4.x, t4.y, t4.z, t4.w};
   float st[4] = {s4.x, s4.y, s4.z, s4.w};
   for (int w = 0; w < W; ++w) {
-    const float4 g4 = *reinterpret_cast<const float4*>(gsl + (int64_t)w * slice + j);
+    // (slice own_w: read in place from the rank's own gradient, not received)
+    const float* gw = w == own_w ? own_g : gsl + (int64_t)w * slice;
+    const float4 g4 = *reinterpret_cast<const float4*>(gw + j);
     const float g[4] = {g4.x, g4.y, g4.z, g4.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e)
@@ -1506,6 +1539,9 @@ __global__ __launch_bounds__(256) void apply_shard_kernel(
   // (async owner applying its own worker's push: the worker's copy of the
   // shard too, instead of a pull copy after the apply)
   if (mirror) wt_store4(wt_rsrc(mirror, nb), ib, make_float4(th[0], th[1], th[2], th[3]));
+  if (ro.mode)
+    refresh_elems(a, ro.mode == 1 ? opt_init[3] != 0 : ro.mode == 3, i, th, ro.thetaP, ro.wks,
+                  ro.wksP, ro.wks_plane);
 }
 
 // After the theta all-gather: conv kernel layouts of Q, and P <- Q (weights
@@ -1515,26 +1551,16 @@ __global__ __launch_bounds__(256) void refresh_kernel(const float* __restrict__ 
                                                       const int32_t* __restrict__ opt_init,
                                                       float* __restrict__ thetaP, __bf16* wks,
                                                       __bf16* wksP, int64_t wks_plane,
-                                                      ApplyArgs a, int force) {
+                                                      ApplyArgs a, int force, int64_t skip_lo,
+                                                      int64_t skip_hi) {
   const bool sync = force >= 0 ? force != 0 : opt_init[3] != 0;
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  if (i >= a.n || (!sync && i >= a.conv[2].w_off + (int64_t)a.conv[2].cout * a.conv[2].cin * 9))
+  if (i >= a.n || (i >= skip_lo && i < skip_hi) ||
+      (!sync && i >= a.conv[2].w_off + (int64_t)a.conv[2].cout * a.conv[2].cin * 9))
     return;
   const float4 o4 = *reinterpret_cast<const float4*>(theta + i);
-  if (sync) wt_store4(wt_rsrc(thetaP, (uint32_t)(((a.n + 3) & ~3ll) * 4)), (uint32_t)(i * 4), o4);
   const float th[4] = {o4.x, o4.y, o4.z, o4.w};
-#pragma unroll
-  for (int l = 0; l < 3; ++l) {
-    const ConvDims& d = a.conv[l];
-    const int64_t e0 = i - d.w_off;
-    if (e0 >= 0 && e0 < (int64_t)d.cout * d.cin * d.ks * d.ks) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        put_conv_weight(d, (int)e0 + e, th[e], wks, wks_plane);
-        if (sync) put_conv_weight(d, (int)e0 + e, th[e], wksP, wks_plane);
-      }
-    }
-  }
+  refresh_elems(a, sync, i, th, thetaP, wks, wksP, wks_plane);
 }
 
 // out[0..len) = sum_w in[w][0..len) in rank order (in-process group exchange)
@@ -1580,24 +1606,30 @@ bool fused_apply_ok(const ParamLayout& L) {
 hipError_t launch_apply_shard(const NetBuffers& nb, int rule, float lr, float decay, float eps,
                               float momentum, float wd, const float* gsl, int64_t off,
                               int64_t len, int64_t slice, int W, hipStream_t s, float* theta,
-                              int first, const Prefetch* pre, float* mirror) {
+                              int first, const Prefetch* pre, float* mirror, int refresh_own,
+                              int own_w, const float* own_g) {
   const ApplyArgs a = apply_args(nb, rule, lr, decay, eps, momentum, wd, 0);
   Prefetch pf{};
   if (pre) pf = *pre;
+  // (shard starts are multiples of 64: a float4 never straddles two shards)
+  const RefreshOut ro{nb.theta[1], nb.wks[0], nb.wks[1], nb.L.wks_total,
+                      refresh_own < 0 ? 1 : refresh_own == 0 ? 0 : refresh_own == 1 ? 2 : 3};
   const int64_t blocks = (len / 4 + 255) / 256;
   if (blocks + pf.ng > 0)
     ddq_launch(apply_shard_kernel, dim3((uint32_t)(blocks + pf.ng)), dim3(256), 0, s,
                        theta ? theta : nb.theta[0], gsl, nb.opt, nb.opt_init, off, len, slice, W,
-                       a, first, nb.iter, pf, mirror);
+                       a, first, nb.iter, pf, mirror, ro, own_g ? own_w : -1, own_g);
   return hipGetLastError();
 }
 
 
-hipError_t launch_refresh(const NetBuffers& nb, hipStream_t s, int force_sync) {
+hipError_t launch_refresh(const NetBuffers& nb, hipStream_t s, int force_sync, int64_t skip_lo,
+                          int64_t skip_hi) {
   const ApplyArgs a = apply_args(nb, 0, 0.f, 0.f, 0.f, 0.f, 0.f, 0);
+  if (skip_lo <= 0 && skip_hi >= a.n) return hipSuccess;
   ddq_launch(refresh_kernel, dim3((uint32_t)((a.n / 4 + 255) / 256)), dim3(256), 0, s,
                      nb.theta[0], nb.opt_init, nb.theta[1], nb.wks[0], nb.wks[1],
-                     nb.L.wks_total, a, force_sync);
+                     nb.L.wks_total, a, force_sync, skip_lo, skip_hi);
   return hipGetLastError();
 }
 
