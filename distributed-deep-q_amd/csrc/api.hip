@@ -1312,12 +1312,15 @@ static int check_step(ddq_ctx* c, const ddq_step_cfg* cfg) {
 // Worker side: the minibatch draw + gather and the forward/backward on the
 // model this worker last pulled (no apply bookkeeping: the owners keep the
 // iteration), into nb.grad, on the ctx stream; grad_ev marks it ready.
-static int async_compute(ddq_ctx* c, const ddq_step_cfg* cfg) {
+// drawn: the minibatch was drawn + gathered already (by the owner apply of
+// this worker's own push, async_owner_apply)
+static int async_compute(ddq_ctx* c, const ddq_step_cfg* cfg, bool drawn = false) {
   NetBuffers nb = c->nb;
   if (nb.B <= 256) {   // one draw + gather launch; the head advances the counter
     nb.head_bump = 1;
-    HIP_TRY(c, launch_sample_gather(nb, c->r_state, c->r_action, c->r_reward, c->r_nonterm,
-                                    c->r_meta, cfg->seed, c->stream));
+    if (!drawn)
+      HIP_TRY(c, launch_sample_gather(nb, c->r_state, c->r_action, c->r_reward, c->r_nonterm,
+                                      c->r_meta, cfg->seed, c->stream));
     TRY(enqueue_fwd_bwd_x(c, nb, nullptr, nullptr, -1, c->r_meta, false));
   } else {
     HIP_TRY(c, launch_sample(nb, c->r_meta, cfg->seed, c->stream));
@@ -1376,14 +1379,22 @@ static bool async_p_now(const ddq_step_cfg* cfg, int64_t it) {
   return cfg->target_period > 0 && it % cfg->target_period == 0;
 }
 
-static int async_owner_apply(ddq_ctx* c, const ddq_step_cfg* cfg, int64_t it, bool own) {
+// draw: the launch also draws + gathers the worker's next minibatch (B <=
+// 256; the caller ordered every ctx-stream op before it, and the worker's
+// compute after it), as async_compute's draw launch would
+static int async_owner_apply(ddq_ctx* c, const ddq_step_cfg* cfg, int64_t it, bool own,
+                             bool draw = false) {
   const ddq_update_cfg& u = cfg->update;
   const int64_t L = c->shard_len, off = (int64_t)c->rank * L;
   // (the apply kernel indexes the gradient slice from the shard's start)
   const float* g = own ? c->nb.grad + off : c->gsl;
+  Prefetch pf{};
+  if (draw)
+    pf = make_prefetch(c->nb, c->r_state, c->r_action, c->r_reward, c->r_nonterm, c->r_meta,
+                       cfg->seed);
   HIP_TRY(c, launch_apply_shard(c->nb, u.rule, u.lr, u.decay, u.eps, u.momentum, u.weight_decay,
-                                g, off, L, L, 1, c->cs, c->own, c->applied == 0 ? 1 : 0, nullptr,
-                                own ? c->nb.theta[0] : nullptr,
+                                g, off, L, L, 1, c->cs, c->own, c->applied == 0 ? 1 : 0,
+                                draw ? &pf : nullptr, own ? c->nb.theta[0] : nullptr,
                                 own ? (async_p_now(cfg, it) ? 2 : 1) : 0));
   if (async_p_now(cfg, it))
     HIP_TRY(c, hipMemcpyAsync(c->pown + off, c->own + off, L * 4, hipMemcpyDeviceToDevice, c->cs));
@@ -1395,7 +1406,7 @@ static int async_owner_apply(ddq_ctx* c, const ddq_step_cfg* cfg, int64_t it, bo
 // P), then the next gradient.  own: the worker's own shard was refreshed by
 // its owner apply (Q; P too when this tick updated the central P: p_own).
 static int async_after_pull(ddq_ctx* c, const ddq_step_cfg* cfg, bool pull_p, bool own = false,
-                            bool p_own = false) {
+                            bool p_own = false, bool drawn = false) {
   const int64_t lo = own ? (int64_t)c->rank * c->shard_len : 0;
   const int64_t hi = own ? lo + c->shard_len : 0;
   p_own = p_own && own;
@@ -1405,7 +1416,7 @@ static int async_after_pull(ddq_ctx* c, const ddq_step_cfg* cfg, bool pull_p, bo
     pb.theta[0] = c->nb.theta[1]; pb.wks[0] = c->nb.wks[1];
     HIP_TRY(c, launch_refresh(pb, c->stream, 0, p_own ? lo : 0, p_own ? hi : 0));
   }
-  return async_compute(c, cfg);
+  return async_compute(c, cfg, drawn);
 }
 
 // Host bookkeeping of a tick (every rank / member: the same tick sequence).
@@ -1424,8 +1435,16 @@ static int rccl_async_tick(ddq_ctx* c, const ddq_step_cfg* cfg, int w) {
   NetBuffers& nb = c->nb;
   const int64_t it = c->applied + 1;    // iteration after this tick's apply
   const bool pull_p = async_pull_p(cfg, c->last_pull[w], it);
-  if (r == w && (!c->acapture || c->grad_ev_captured))
+  // the own push's owner apply draws + gathers this worker's next minibatch:
+  // it follows everything on the ctx stream so far (the gradient, and any
+  // replay insert enqueued since), not only grad_ev
+  const bool draw = r == w && nb.B <= 256;
+  if (draw) {
+    HIP_TRY(c, hipEventRecord(c->cev[0], c->stream));
+    HIP_TRY(c, hipStreamWaitEvent(c->cs, c->cev[0], 0));
+  } else if (r == w && (!c->acapture || c->grad_ev_captured)) {
     HIP_TRY(c, hipStreamWaitEvent(c->cs, c->grad_ev, 0));
+  }
   // push: worker w's gradient slices to their owners
   if (W > 1) {
     NCCL_TRY(c, ncclGroupStart());
@@ -1437,7 +1456,7 @@ static int rccl_async_tick(ddq_ctx* c, const ddq_step_cfg* cfg, int w) {
     }
     NCCL_TRY(c, ncclGroupEnd());
   }
-  TRY(async_owner_apply(c, cfg, it, r == w));
+  TRY(async_owner_apply(c, cfg, it, r == w, draw));
   // pull: the owners' shards to worker w
   if (W > 1) {
     NCCL_TRY(c, ncclGroupStart());
@@ -1462,7 +1481,7 @@ static int rccl_async_tick(ddq_ctx* c, const ddq_step_cfg* cfg, int w) {
                                 hipMemcpyDeviceToDevice, c->cs));
     HIP_TRY(c, hipEventRecord(c->tick_ev, c->cs));
     HIP_TRY(c, hipStreamWaitEvent(c->stream, c->tick_ev, 0));
-    TRY(async_after_pull(c, cfg, pull_p, true, p_own));
+    TRY(async_after_pull(c, cfg, pull_p, true, p_own, draw));
   }
   async_advance(c, w, it);
   return DDQ_OK;
