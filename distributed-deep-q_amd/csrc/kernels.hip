@@ -1970,6 +1970,7 @@ hipError_t launch_small_fwd_head(const NetBuffers& nb, hipStream_t s,
   c.x[0] = nb.pool3[0]; c.x[1] = nb.pool3[1];
   c.th[0] = nb.theta[0]; c.th[1] = nb.theta[1];
   c.w4_off = L.w[3]; c.b4_off = L.b[3]; c.w5_off = L.w[4]; c.b5_off = L.b[4];
+  if (L.w[3] % 4) return hipErrorInvalidValue;   // (dW4 rows stored as float4)
   c.action = nb.action; c.reward = nb.reward; c.nonterm = nb.nonterm; c.gamma = nb.gamma;
   c.qpart = nb.qpart; c.dpart = nb.dpart; c.sync = nb.csync;
   c.q_out = nb.q_out; c.p_out = nb.p_out; c.q_sa = nb.q_sa; c.p_sa = nb.p_sa;

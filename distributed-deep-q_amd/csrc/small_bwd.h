@@ -360,11 +360,13 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
 #pragma unroll
         for (int u = 0; u < 2; ++u) bv8[q][u] = XS[b * kXP + 16 * (2 * wid + u) + lr];
       }
+      // (transposed tile, A = x_Q, B = dh4: D rows = k, columns = n -- a lane's
+      // 4 values are consecutive k of one row n, stored as one 16-byte vector)
 #pragma unroll
       for (int q = 0; q < 8; ++q)
 #pragma unroll
         for (int u = 0; u < 2; ++u)
-          gw[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(av8[q], bv8[q][u], gw[u], 0, 0, 0);
+          gw[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(bv8[q][u], av8[q], gw[u], 0, 0, 0);
     }
     // dpart: tiles (b block bb, k block kb), 2 x 16 per chunk, 4 per wave
     float dav[4][4], dbv[4][4];
@@ -384,14 +386,16 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
       const int tI = wid * 4 + u, bbk = tI >> 4, kb = tI & 15;
       if (16 * bbk >= nb) continue;                 // (wave-uniform)
       f32x4v d = {0.f, 0.f, 0.f, 0.f};
+      // the transposed tile (A = the W4 columns, B = dh4; the same products in
+      // the same n order): D rows = k 16 kb + 4 kq + i, column = image
+      // 16 bbk + lr, so a lane holds 4 consecutive k of one image -- one
+      // 16-byte store instead of four 4-byte ones
 #pragma unroll
-      for (int s = 0; s < 4; ++s) d = __builtin_amdgcn_mfma_f32_16x16x4f32(dav[u][s], dbv[u][s], d, 0, 0, 0);
-      // D rows = images 16 bbk + 4 kq + i, column = k 16 kb + lr
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int bi = bb0 + 16 * bbk + 4 * kq + i;
-        if (bi < hi) c.dpart[((int64_t)jb * B + bi) * kFcK + 16 * kb + lr] = d[i];
-      }
+      for (int s = 0; s < 4; ++s) d = __builtin_amdgcn_mfma_f32_16x16x4f32(dbv[u][s], dav[u][s], d, 0, 0, 0);
+      const int bi = bb0 + 16 * bbk + lr;
+      if (bi < hi)
+        *reinterpret_cast<float4*>(c.dpart + ((int64_t)jb * B + bi) * kFcK + 16 * kb + 4 * kq) =
+            make_float4(d[0], d[1], d[2], d[3]);
     }
   }
   DDQ_STAMP(22);
@@ -399,13 +403,12 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
   // correctly rounded divides and square roots, 8 a thread here, cost this
   // launch 2.8 us at its end; K4 has CUs free for them) ----
 #pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int n = 4 * kq + i, k = 16 * (2 * wid + u) + lr;
-      if (G > 1) c.w4part[((int64_t)cc * 512 + n0 + n) * kFcK + k] = gw[u][i];
-      else c.grad[c.w4_off + (int64_t)(n0 + n) * kFcK + k] = gw[u][i];
-    }
+  for (int u = 0; u < 2; ++u) {
+    const int n = lr, k = 16 * (2 * wid + u) + 4 * kq;   // (w4_off % 4 == 0: launch check)
+    const float4 v = make_float4(gw[u][0], gw[u][1], gw[u][2], gw[u][3]);
+    if (G > 1) *reinterpret_cast<float4*>(c.w4part + ((int64_t)cc * 512 + n0 + n) * kFcK + k) = v;
+    else *reinterpret_cast<float4*>(c.grad + c.w4_off + (int64_t)(n0 + n) * kFcK + k) = v;
+  }
   DDQ_STAMP(23);
 }
 
