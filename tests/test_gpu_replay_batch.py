@@ -94,6 +94,36 @@ def test_batch_sampler_semantics_and_gather(ddq, ref, head):
     net.close()
 
 
+@pytest.mark.parametrize("S", [24, 40])
+def test_batch_gather_partial_row_slices(ddq, ref, S):
+    """The gather cuts a slot's S*S 4-byte words into 512-word slices a
+    workgroup: at S = 24 / 40 (576 / 1600 words) the last slice is partial.
+    Bit-exact against the oracle's gather of the same draw."""
+    N, n = 700, 150
+    rng = np.random.default_rng(S)
+    st = rng.integers(0, 256, (N, 4, S, S)).astype(np.uint8)
+    ac = rng.integers(0, 4, N).astype(np.uint8)
+    rw = rng.integers(-1, 2, N).astype(np.int16)
+    nt = rng.random(N) > 0.1
+    net = ddq.DeepQNet(batch=4, frame=S)
+    net.replay_create(N)
+    net.replay_import(st, ac, rw, nt.astype(np.uint8), 0, N)
+    r = ref.ReplayRef((4, S, S), N)
+    r.state, r.action, r.reward, r.non_terminal = st, ac, rw, nt
+    r.head, r.valid = 0, N
+    bufs = net.batch_buffers(n)
+    for _ in range(3):
+        net.replay_sample_batch(bufs, seed=9)
+        out = host(bufs)
+        s_ref, a_ref, r_ref, ns_ref, nt_ref = r.gather(out["idx"].astype(np.int64))
+        np.testing.assert_array_equal(out["state"], s_ref)
+        np.testing.assert_array_equal(out["next_state"], ns_ref)
+        np.testing.assert_array_equal(out["action"], a_ref)
+        np.testing.assert_array_equal(out["reward"], r_ref)
+        np.testing.assert_array_equal(out["non_terminal"], nt_ref)
+    net.close()
+
+
 def test_batch_sampler_uniform(ddq):
     """Chi-square of per-slot hit counts over many draws (valid=512, n=128)."""
     S, N, n, draws = 16, 512, 128, 400
