@@ -1986,7 +1986,8 @@ hipError_t launch_small_fwd_head(const NetBuffers& nb, hipStream_t s,
   CHECK_LAUNCH(ensure_dyn_lds(reinterpret_cast<const void*>(sm16::fc4_chain16_kernel), attr,
                               sm16::kChainSmem));
   M("fc4_chain");
-  ddq_launch(sm16::fc4_chain16_kernel, dim3(sm16::kFcBlk * c.G), dim3(512), sm16::kChainSmem, s, c);
+  // one tower a workgroup: kFcBlk G of the P tower, then kFcBlk G of Q
+  ddq_launch(sm16::fc4_chain16_kernel, dim3(2 * sm16::kFcBlk * c.G), dim3(512), sm16::kChainSmem, s, c);
   CHECK_LAUNCH(hipGetLastError());
   return hipSuccess;
 }

@@ -39,7 +39,7 @@ constexpr int kMaxB = 256;
 constexpr int CH_WS = 0;
 constexpr int CH_XS = CH_WS + 2 * kFcN * kXP;
 constexpr int CH_RED = CH_XS + 2 * kBC * kXP;
-constexpr int CH_H = CH_RED + 2 * 2 * 4 * 64;
+constexpr int CH_H = CH_RED + 3 * 2 * 4 * 64;
 constexpr int CH_DH = CH_H + kMaxB * kFcN;
 constexpr int CH_QP = CH_DH + kMaxB * kFcN;
 constexpr int CH_DQ = CH_QP + 2 * kMaxB * 4;
@@ -95,8 +95,14 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int bid = blockIdx.x;
   DDQ_STAMP(16);
-  // unit block jb, image chunk cc: images [lo, hi) (G == 1: all of them)
-  const int G = c.G, jb = bid % kFcBlk, cc = bid / kFcBlk;
+  // one tower a workgroup: the P tower's kFcBlk G workgroups first (they run
+  // phase A, publish their Q_out partials and leave without waiting, so the
+  // Q tower's, which do wait, always find them dispatched), then the Q
+  // tower's.  Unit block jb, image chunk cc: images [lo, hi) (G == 1: all)
+  const int G = c.G, nH = kFcBlk * G;
+  const bool ptower = bid < nH;
+  const int zt = ptower ? 1 : 0, qb = ptower ? bid : bid - nH;
+  const int jb = qb % kFcBlk, cc = qb / kFcBlk;
   const int B = c.B, n0 = jb * kFcN;
   const int lo = G > 1 ? cc * kBC : 0, hi = G > 1 ? min(B, lo + kBC) : B;
   const int nch = (hi - lo + kBC - 1) / kBC;
@@ -112,32 +118,33 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
   const __amdgpu_buffer_rsrc_t rq = wt_rsrc(c.qpart, (uint32_t)(kFcBlk * 2 * B * 16));
 
   // ---- every global load of phase A's first chunk issued before the first
-  // LDS store: W4 rows [n0, n0 + 16) of both towers (2 x 16 x 64 float4),
-  // the chunk's pool3 rows (2 x 32 x 64 float4), the units' own fc4 bias and
-  // Q_out columns ----
-  float4 wv[4], xv[8];
+  // LDS store: the tower's W4 rows [n0, n0 + 16) (16 x 64 float4), the
+  // chunk's pool3 rows (32 x 64 float4), the units' own fc4 bias and Q_out
+  // columns ----
+  float4 wv[2], xv[4];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
+  for (int u = 0; u < 2; ++u) {
     const int f = tid + u * 512;
-    const int z = f >> 10, n = (f >> 6) & 15, k4 = f & 63;
-    wv[u] = *reinterpret_cast<const float4*>(c.th[z] + c.w4_off + (int64_t)(n0 + n) * kFcK + 4 * k4);
+    const int n = f >> 6, k4 = f & 63;
+    wv[u] = *reinterpret_cast<const float4*>(c.th[zt] + c.w4_off + (int64_t)(n0 + n) * kFcK + 4 * k4);
   }
-  const int wz = wid >> 2, wb = (wid >> 1) & 1, wkh = wid & 1;
+  // phase A waves: (image half wb, k quarter wkq)
+  const int wb = (wid >> 1) & 1, wkq = 2 * (wid >> 2) + (wid & 1);
 #define DDQ_XLOAD(bb0)                                                                         \
-  _Pragma("unroll") for (int u = 0; u < 8; ++u) {                                              \
+  _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                              \
     const int f = tid + u * 512;                                                               \
-    const int z = f >> 11, b = (f >> 6) & 31, k4 = f & 63;                                     \
+    const int b = f >> 6, k4 = f & 63;                                                         \
     xv[u] = make_float4(0.f, 0.f, 0.f, 0.f);                                                   \
-    if ((bb0) + b < hi) xv[u] = *reinterpret_cast<const float4*>(c.x[z] + (int64_t)((bb0) + b) * kFcK + 4 * k4); \
+    if ((bb0) + b < hi) xv[u] = *reinterpret_cast<const float4*>(c.x[zt] + (int64_t)((bb0) + b) * kFcK + 4 * k4); \
   }
 #define DDQ_XSTORE()                                                                           \
-  _Pragma("unroll") for (int u = 0; u < 8; ++u) {                                              \
+  _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                              \
     const int f = tid + u * 512;                                                               \
-    const int z = f >> 11, b = (f >> 6) & 31, k4 = f & 63;                                     \
-    *reinterpret_cast<float4*>(XS + (z * kBC + b) * kXP + 4 * k4) = xv[u];                     \
+    const int b = f >> 6, k4 = f & 63;                                                         \
+    *reinterpret_cast<float4*>(XS + b * kXP + 4 * k4) = xv[u];                                 \
   }
   DDQ_XLOAD(lo)
-  float w5q = tid < 64 ? c.th[0][c.w5_off + (tid >> 4) * 512 + n0 + (tid & 15)] : 0.f;
+  float w5q = tid < 64 && !ptower ? c.th[0][c.w5_off + (tid >> 4) * 512 + n0 + (tid & 15)] : 0.f;
   // theta / optimizer state of the parameters the unit sums update (db4 and
   // dW5 columns of the units: q = 0..79; b5: q = 80..83, workgroup 0), read
   // now so phase B's updates wait on no load
@@ -146,7 +153,7 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
                   : c.b5_off + (q - 80);
   };
   float pth = 0.f, pst = 0.f;
-  const bool ap0 = c.apply != 0 && G == 1;   // (G > 1: K4 applies the batch sums)
+  const bool ap0 = c.apply != 0 && G == 1 && !ptower;   // (G > 1: K4 applies the batch sums)
   // the update's flags (latched by K1's book block), loaded now
   const bool first = ap0 && c.at.opt_init[2] != 0, sync = ap0 && c.at.opt_init[3] != 0;
   if (ap0 && tid < 84) {
@@ -158,20 +165,22 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int n = n0 + 4 * kq + i;
-    b4v[i] = c.th[wz][c.b4_off + n];
+    b4v[i] = c.th[zt][c.b4_off + n];
 #pragma unroll
-    for (int a = 0; a < 4; ++a) w5v[a][i] = c.th[wz][c.w5_off + a * 512 + n];
+    for (int a = 0; a < 4; ++a) w5v[a][i] = c.th[zt][c.w5_off + a * 512 + n];
   }
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
+  for (int u = 0; u < 2; ++u) {
     const int f = tid + u * 512;
-    const int z = f >> 10, n = (f >> 6) & 15, k4 = f & 63;
-    *reinterpret_cast<float4*>(WS + (z * kFcN + n) * kXP + 4 * k4) = wv[u];
+    const int n = f >> 6, k4 = f & 63;
+    *reinterpret_cast<float4*>(WS + n * kXP + 4 * k4) = wv[u];
   }
-  if (tid < 64) csm[CH_W5 + tid] = w5q;
-  if (tid < 84) { csm[CH_PS + tid] = pth; csm[CH_PS + 96 + tid] = pst; }
-  for (int e = tid; e < 6 * B; e += 512)             // action one-hot, reward, non_terminal
-    csm[CH_MB + e] = e < 4 * B ? c.action[e] : (e < 5 * B ? c.reward[e - 4 * B] : c.nonterm[e - 5 * B]);
+  if (!ptower) {
+    if (tid < 64) csm[CH_W5 + tid] = w5q;
+    if (tid < 84) { csm[CH_PS + tid] = pth; csm[CH_PS + 96 + tid] = pst; }
+    for (int e = tid; e < 6 * B; e += 512)           // action one-hot, reward, non_terminal
+      csm[CH_MB + e] = e < 4 * B ? c.action[e] : (e < 5 * B ? c.reward[e - 4 * B] : c.nonterm[e - 5 * B]);
+  }
 
   // ---- phase A, chunk by chunk of 32 images ----
   for (int ch = 0; ch < nch; ++ch) {
@@ -183,14 +192,14 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
     DDQ_XSTORE()
     __syncthreads();
     DDQ_STAMP(17);
-    // wave (wz, wb, wkh): h[n][b] for its tower, 16 images, k half wkh;
-    // k-block k0: MFMA step s pairs k = k0 + 4 kq + s of both operands
+    // wave (wb, wkq): h[n][b] for 16 images, k quarter wkq; k-block k0:
+    // MFMA step s pairs k = k0 + 4 kq + s of both operands
     f32x4v acc = {0.f, 0.f, 0.f, 0.f};
-    const float* wrow = WS + (wz * kFcN + lr) * kXP + 4 * kq;
-    const float* xrow = XS + (wz * kBC + 16 * wb + lr) * kXP + 4 * kq;
+    const float* wrow = WS + lr * kXP + 4 * kq;
+    const float* xrow = XS + (16 * wb + lr) * kXP + 4 * kq;
 #pragma unroll
-    for (int kb = 0; kb < 8; ++kb) {
-      const int k0 = 128 * wkh + 16 * kb;
+    for (int kb = 0; kb < 4; ++kb) {
+      const int k0 = 64 * wkq + 16 * kb;
       const float4 av = *reinterpret_cast<const float4*>(wrow + k0);
       const float4 bv = *reinterpret_cast<const float4*>(xrow + k0);
       acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc, 0, 0, 0);
@@ -198,18 +207,20 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
       acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, acc, 0, 0, 0);
     }
-    if (wkh == 1) {
+    if (wkq != 0) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) RED[((wz * 2 + wb) * 4 + i) * 64 + lane] = acc[i];
+      for (int i = 0; i < 4; ++i) RED[(((wkq - 1) * 2 + wb) * 4 + i) * 64 + lane] = acc[i];
     }
     __syncthreads();
-    if (wkh == 0) {
+    if (wkq == 0) {
       // lane: units n = 4 kq + i, image b = 16 wb + lr (D rows / column)
       const int b = bb0 + 16 * wb + lr;
       float hv[4], q[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float v = acc[i] + RED[((wz * 2 + wb) * 4 + i) * 64 + lane] + b4v[i];
+      for (int i = 0; i < 4; ++i) {   // the k quarters summed in order
+        const float v = ((acc[i] + RED[((0 * 2 + wb) * 4 + i) * 64 + lane]) +
+                         RED[((1 * 2 + wb) * 4 + i) * 64 + lane]) +
+                        RED[((2 * 2 + wb) * 4 + i) * 64 + lane] + b4v[i];
         hv[i] = v > 0.f ? v : 0.f;                 // ReLU; dropout = identity (TEST phase)
 #pragma unroll
         for (int a = 0; a < 4; ++a) q[a] += hv[i] * w5v[a][i];
@@ -221,15 +232,23 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
       }
       if (b < hi) {
         if (kq == 0)                               // write-through: the fan-in's hand-off
-          wt_store4(rq, (uint32_t)((((jb * 2 + wz) * B + b) * 4) * 4), make_float4(q[0], q[1], q[2], q[3]));
-        if (wz == 0)
+          wt_store4(rq, (uint32_t)((((jb * 2 + zt) * B + b) * 4) * 4), make_float4(q[0], q[1], q[2], q[3]));
+        if (zt == 0)
 #pragma unroll
           for (int i = 0; i < 4; ++i) H[b * kFcN + 4 * kq + i] = hv[i];
       }
     }
   }
   DDQ_STAMP(18);
-  meet(reinterpret_cast<uint64_t*>(c.sync), kFcBlk * G, c.sync + 2);
+  if (ptower) {   // arrive (the partials drained, write-through) and leave
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0)
+      __hip_atomic_fetch_add(reinterpret_cast<uint64_t*>(c.sync), (uint64_t)1, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  meet(reinterpret_cast<uint64_t*>(c.sync), 2 * nH, c.sync + 2);
   DDQ_STAMP(19);
 
   // ---- phase B: every sample's Q_out / P_out (partials summed in j order) ----
