@@ -1982,12 +1982,15 @@ hipError_t launch_small_fwd_head(const NetBuffers& nb, hipStream_t s,
   c.at = apply_tail(nb);
   c.G = nb.small_G; c.upart = nb.upart; c.w4part = nb.w4part;
   if (c.G > 8 || (c.G > 1 && (!c.upart || !c.w4part))) return hipErrorInvalidValue;
-  static std::atomic<uint64_t> attr{0};
-  CHECK_LAUNCH(ensure_dyn_lds(reinterpret_cast<const void*>(sm16::fc4_chain16_kernel), attr,
+  // B <= 32: one tower a workgroup (kFcBlk of the P tower, then kFcBlk of
+  // Q); B > 32: both towers a workgroup, kFcBlk G (all resident)
+  const bool one = c.G == 1;
+  auto kern = one ? sm16::fc4_chain16_kernel<1> : sm16::fc4_chain16_kernel<2>;
+  static std::atomic<uint64_t> attr1{0}, attr2{0};
+  CHECK_LAUNCH(ensure_dyn_lds(reinterpret_cast<const void*>(kern), one ? attr1 : attr2,
                               sm16::kChainSmem));
   M("fc4_chain");
-  // one tower a workgroup: kFcBlk G of the P tower, then kFcBlk G of Q
-  ddq_launch(sm16::fc4_chain16_kernel, dim3(2 * sm16::kFcBlk * c.G), dim3(512), sm16::kChainSmem, s, c);
+  ddq_launch(kern, dim3((one ? 2 : 1) * sm16::kFcBlk * c.G), dim3(512), sm16::kChainSmem, s, c);
   CHECK_LAUNCH(hipGetLastError());
   return hipSuccess;
 }

@@ -39,7 +39,7 @@ constexpr int kMaxB = 256;
 constexpr int CH_WS = 0;
 constexpr int CH_XS = CH_WS + 2 * kFcN * kXP;
 constexpr int CH_RED = CH_XS + 2 * kBC * kXP;
-constexpr int CH_H = CH_RED + 3 * 2 * 4 * 64;
+constexpr int CH_H = CH_RED + 3 * 2 * 4 * 64;   // (k parts - 1 + tower slot) x half
 constexpr int CH_DH = CH_H + kMaxB * kFcN;
 constexpr int CH_QP = CH_DH + kMaxB * kFcN;
 constexpr int CH_DQ = CH_QP + 2 * kMaxB * 4;
@@ -90,6 +90,10 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// NZ towers a workgroup: 1 (B <= 32: 64 workgroups, below) or 2 (B > 32: G
+// chunks of 32 images, 32 G workgroups -- all resident with the launch's
+// 159 KB of LDS only if each carries both towers)
+template <int NZ>
 __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
   extern __shared__ __attribute__((aligned(16))) float csm[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -100,8 +104,8 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
   // Q tower's, which do wait, always find them dispatched), then the Q
   // tower's.  Unit block jb, image chunk cc: images [lo, hi) (G == 1: all)
   const int G = c.G, nH = kFcBlk * G;
-  const bool ptower = bid < nH;
-  const int zt = ptower ? 1 : 0, qb = ptower ? bid : bid - nH;
+  const bool ptower = NZ == 1 && bid < nH;
+  const int zt = ptower ? 1 : 0, qb = ptower ? bid : (NZ == 1 ? bid - nH : bid);
   const int jb = qb % kFcBlk, cc = qb / kFcBlk;
   const int B = c.B, n0 = jb * kFcN;
   const int lo = G > 1 ? cc * kBC : 0, hi = G > 1 ? min(B, lo + kBC) : B;
@@ -121,27 +125,32 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
   // LDS store: the tower's W4 rows [n0, n0 + 16) (16 x 64 float4), the
   // chunk's pool3 rows (32 x 64 float4), the units' own fc4 bias and Q_out
   // columns ----
-  float4 wv[2], xv[4];
+  float4 wv[2 * NZ], xv[4 * NZ];
+  // (slot z of WS / XS: the tower, or 0 for a one-tower workgroup)
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < 2 * NZ; ++u) {
     const int f = tid + u * 512;
-    const int n = f >> 6, k4 = f & 63;
-    wv[u] = *reinterpret_cast<const float4*>(c.th[zt] + c.w4_off + (int64_t)(n0 + n) * kFcK + 4 * k4);
+    const int z = NZ == 2 ? f >> 10 : zt, n = (f >> 6) & 15, k4 = f & 63;
+    wv[u] = *reinterpret_cast<const float4*>(c.th[z] + c.w4_off + (int64_t)(n0 + n) * kFcK + 4 * k4);
   }
-  // phase A waves: (image half wb, k quarter wkq)
-  const int wb = (wid >> 1) & 1, wkq = 2 * (wid >> 2) + (wid & 1);
+  // phase A waves: NZ 2 (tower wz, image half wb, k half); NZ 1 (image half
+  // wb, k quarter): wkq = the k part, of NKP
+  constexpr int NKP = NZ == 2 ? 2 : 4, NKB = 8 / (NKP / 2);
+  const int wz = NZ == 2 ? wid >> 2 : zt, wb = (wid >> 1) & 1;
+  const int wkq = NZ == 2 ? (wid & 1) : 2 * (wid >> 2) + (wid & 1);
+  const int wsl = NZ == 2 ? wz : 0;                  // the WS / XS slot of the wave's tower
 #define DDQ_XLOAD(bb0)                                                                         \
-  _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                              \
+  _Pragma("unroll") for (int u = 0; u < 4 * NZ; ++u) {                                         \
     const int f = tid + u * 512;                                                               \
-    const int b = f >> 6, k4 = f & 63;                                                         \
+    const int z = NZ == 2 ? f >> 11 : zt, b = (f >> 6) & 31, k4 = f & 63;                      \
     xv[u] = make_float4(0.f, 0.f, 0.f, 0.f);                                                   \
-    if ((bb0) + b < hi) xv[u] = *reinterpret_cast<const float4*>(c.x[zt] + (int64_t)((bb0) + b) * kFcK + 4 * k4); \
+    if ((bb0) + b < hi) xv[u] = *reinterpret_cast<const float4*>(c.x[z] + (int64_t)((bb0) + b) * kFcK + 4 * k4); \
   }
 #define DDQ_XSTORE()                                                                           \
-  _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                              \
+  _Pragma("unroll") for (int u = 0; u < 4 * NZ; ++u) {                                         \
     const int f = tid + u * 512;                                                               \
-    const int b = f >> 6, k4 = f & 63;                                                         \
-    *reinterpret_cast<float4*>(XS + b * kXP + 4 * k4) = xv[u];                                 \
+    const int zs = NZ == 2 ? f >> 11 : 0, b = (f >> 6) & 31, k4 = f & 63;                      \
+    *reinterpret_cast<float4*>(XS + (zs * kBC + b) * kXP + 4 * k4) = xv[u];                    \
   }
   DDQ_XLOAD(lo)
   float w5q = tid < 64 && !ptower ? c.th[0][c.w5_off + (tid >> 4) * 512 + n0 + (tid & 15)] : 0.f;
@@ -165,15 +174,15 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int n = n0 + 4 * kq + i;
-    b4v[i] = c.th[zt][c.b4_off + n];
+    b4v[i] = c.th[wz][c.b4_off + n];
 #pragma unroll
-    for (int a = 0; a < 4; ++a) w5v[a][i] = c.th[zt][c.w5_off + a * 512 + n];
+    for (int a = 0; a < 4; ++a) w5v[a][i] = c.th[wz][c.w5_off + a * 512 + n];
   }
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < 2 * NZ; ++u) {
     const int f = tid + u * 512;
-    const int n = f >> 6, k4 = f & 63;
-    *reinterpret_cast<float4*>(WS + n * kXP + 4 * k4) = wv[u];
+    const int zs = NZ == 2 ? f >> 10 : 0, n = (f >> 6) & 15, k4 = f & 63;
+    *reinterpret_cast<float4*>(WS + (zs * kFcN + n) * kXP + 4 * k4) = wv[u];
   }
   if (!ptower) {
     if (tid < 64) csm[CH_W5 + tid] = w5q;
@@ -192,14 +201,14 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
     DDQ_XSTORE()
     __syncthreads();
     DDQ_STAMP(17);
-    // wave (wb, wkq): h[n][b] for 16 images, k quarter wkq; k-block k0:
+    // wave: h[n][b] for its tower, 16 images, k part wkq of NKP; k-block k0:
     // MFMA step s pairs k = k0 + 4 kq + s of both operands
     f32x4v acc = {0.f, 0.f, 0.f, 0.f};
-    const float* wrow = WS + lr * kXP + 4 * kq;
-    const float* xrow = XS + (16 * wb + lr) * kXP + 4 * kq;
+    const float* wrow = WS + (wsl * kFcN + lr) * kXP + 4 * kq;
+    const float* xrow = XS + (wsl * kBC + 16 * wb + lr) * kXP + 4 * kq;
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-      const int k0 = 64 * wkq + 16 * kb;
+    for (int kb = 0; kb < NKB; ++kb) {
+      const int k0 = (kFcK / NKP) * wkq + 16 * kb;
       const float4 av = *reinterpret_cast<const float4*>(wrow + k0);
       const float4 bv = *reinterpret_cast<const float4*>(xrow + k0);
       acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc, 0, 0, 0);
@@ -207,9 +216,12 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
       acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, acc, 0, 0, 0);
     }
+    // RED slot of (k part p >= 1, this wave's tower slot and image half):
+    // NZ 2 has p = 1 only, NZ 1 slot 0 only -- (p - 1 + slot) is unique
+    auto rslot = [&](int p, int i) { return (((p - 1 + wsl) * 2 + wb) * 4 + i) * 64 + lane; };
     if (wkq != 0) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) RED[(((wkq - 1) * 2 + wb) * 4 + i) * 64 + lane] = acc[i];
+      for (int i = 0; i < 4; ++i) RED[rslot(wkq, i)] = acc[i];
     }
     __syncthreads();
     if (wkq == 0) {
@@ -217,10 +229,11 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
       const int b = bb0 + 16 * wb + lr;
       float hv[4], q[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {   // the k quarters summed in order
-        const float v = ((acc[i] + RED[((0 * 2 + wb) * 4 + i) * 64 + lane]) +
-                         RED[((1 * 2 + wb) * 4 + i) * 64 + lane]) +
-                        RED[((2 * 2 + wb) * 4 + i) * 64 + lane] + b4v[i];
+      for (int i = 0; i < 4; ++i) {   // the k parts summed in order
+        float v = acc[i];
+#pragma unroll
+        for (int p = 1; p < NKP; ++p) v += RED[rslot(p, i)];
+        v += b4v[i];
         hv[i] = v > 0.f ? v : 0.f;                 // ReLU; dropout = identity (TEST phase)
 #pragma unroll
         for (int a = 0; a < 4; ++a) q[a] += hv[i] * w5v[a][i];
@@ -232,8 +245,8 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
       }
       if (b < hi) {
         if (kq == 0)                               // write-through: the fan-in's hand-off
-          wt_store4(rq, (uint32_t)((((jb * 2 + zt) * B + b) * 4) * 4), make_float4(q[0], q[1], q[2], q[3]));
-        if (zt == 0)
+          wt_store4(rq, (uint32_t)((((jb * 2 + wz) * B + b) * 4) * 4), make_float4(q[0], q[1], q[2], q[3]));
+        if (wz == 0)
 #pragma unroll
           for (int i = 0; i < 4; ++i) H[b * kFcN + 4 * kq + i] = hv[i];
       }
@@ -248,7 +261,7 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
                              __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
-  meet(reinterpret_cast<uint64_t*>(c.sync), 2 * nH, c.sync + 2);
+  meet(reinterpret_cast<uint64_t*>(c.sync), 2 * nH / NZ, c.sync + 2);
   DDQ_STAMP(19);
 
   // ---- phase B: every sample's Q_out / P_out (partials summed in j order) ----
