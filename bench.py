@@ -932,36 +932,6 @@ def main():
     step_flops = net.step_flops()
     step_rl = step_roofline(B, S, net.num_params)
     traffic, traffic_src = pmc_traffic(dom, B, S)
-    # the dominant kernel unprofiled in graph replay: (graph step with conv2's
-    # forward launched twice) - (graph step), same step mode, median of 3
-    # alternations (the difference is one launch + one dependent boundary, an
-    # upper bound on the kernel; the eager dispatch events a lower one)
-    graph_us = None
-    if dom == "conv2_fwd" and not args.eager and ticket is None and world == 1 and S != 16:
-        cfg2 = net.step_cfg(args.rule, lr=1e-4, target_period=10, seed=ddist.index_seed(1234, rank),
-                            store_grads=not args.no_grad_store, repeat_conv2=True)
-        cfg1 = net.step_cfg(args.rule, lr=1e-4, target_period=10, seed=ddist.index_seed(1234, rank),
-                            store_grads=not args.no_grad_store)
-
-        def tgraph(c, n=240):
-            if args.pipeline:
-                net.step_prepare(c, "pipelined")
-                go = lambda k: net.step_pipelined(c, k)   # noqa: E731
-            else:
-                go = lambda k: net.step_graph(c, k)       # noqa: E731
-            go(24)
-            net.synchronize()
-            t0 = time.perf_counter()
-            go(n)
-            net.synchronize()
-            return (time.perf_counter() - t0) / n * 1e6
-
-        diffs = []
-        for _ in range(3):
-            a = tgraph(cfg1)
-            diffs.append(tgraph(cfg2) - a)
-        graph_us = float(np.median(diffs))
-
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -1006,14 +976,6 @@ def main():
                                              "kernel's own dispatch start / stop "
                                              "(hipExtLaunchKernel events on the ctx stream)"
                                              % max(1, args.profile_steps),
-                         "kernel_us_graph": None if graph_us is None else round(graph_us, 3),
-                         "frac_graph": None if not graph_us else
-                         round(flops[dom] / (graph_us * 1e-6) / dom_peak, 4),
-                         "kernel_us_graph_timing": "unprofiled graph replay: (step with the "
-                                                   "kernel launched twice) - (step), median of 3; "
-                                                   "one launch + one dependent boundary (upper "
-                                                   "bound: frac_graph is a lower bound, frac from "
-                                                   "the eager dispatch events an upper one)",
                          "isolated_us": None if iso_us is None else round(iso_us, 3),
                          "isolated_timing": "the same layer, 100 back-to-back launches on one "
                                             "cache-warm input (not the roofline figure)",

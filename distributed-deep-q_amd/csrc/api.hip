@@ -90,6 +90,9 @@ struct ddq_ctx {
   hipGraphExec_t tgexec[4] = {nullptr, nullptr, nullptr, nullptr};
   ddq_step_cfg tcfg{};
   std::string comm_err;
+  // ddq_inject_fault: armed failpoint, consumed by the next eager step
+  int fault = 0;
+  std::string small_off;           // why the small-map step is off at S = 16 (empty: on)
   // graph
   hipGraph_t graph = nullptr;
   hipGraphExec_t gexec = nullptr;     // one step
@@ -180,6 +183,15 @@ static int set_dev(ddq_ctx* c) {
 }
 
 static void invalidate_graph(ddq_ctx* c) {
+  // (the async tick / round graphs too: they bake in the index log and the
+  // other captured pointers that ddq_index_log_enable / set_stream replace)
+  for (auto& g : c->tgexec) {
+    if (g) hipGraphExecDestroy(g);
+    g = nullptr;
+  }
+  if (c->agexec) hipGraphExecDestroy(c->agexec);
+  c->agexec = nullptr;
+  c->agraph_rounds = 0;
   if (c->gexec) hipGraphExecDestroy(c->gexec);
   if (c->gexec_k) hipGraphExecDestroy(c->gexec_k);
   c->gexec_k = nullptr;
@@ -287,9 +299,18 @@ int ddq_create(ddq_ctx** out, int device, const ddq_net_desc* desc) {
       TRY(dalloc(c, &nb.pairc, (size_t)B * 2));
       TRY(dalloc(c, &nb.csync, 64));
     }
-    // DDQ_NO_SMALL=1: the general kernels at S = 16 too (A/B, diagnosis)
-    const char* ns = getenv("DDQ_NO_SMALL");
-    nb.small = S == 16 && B <= 256 && !(ns && ns[0] == '1');
+    // the four-launch small-map step needs every meeting launch's workgroups
+    // co-resident (small_coresident); otherwise the general kernels run
+    nb.small = 0;
+    if (S == 16 && B <= 256) {
+      int ok = 0;
+      char why[256] = "";
+      HIP_TRY(c, small_coresident(B, &ok, why, sizeof(why)));
+      nb.small = ok;
+      if (!ok) c->small_off = why;
+    } else {
+      c->small_off = S == 16 ? "batch > 256" : "frame != 16";
+    }
     if (nb.small) {
       TRY(dalloc(c, &nb.qpart, (size_t)32 * 2 * B * 4));
       TRY(dalloc(c, &nb.dpart, (size_t)32 * B * 256));
@@ -346,9 +367,7 @@ int ddq_destroy(ddq_ctx* c) {
   hipSetDevice(c->device);
   if (c->cs) hipStreamSynchronize(c->cs);
   if (c->stream) hipStreamSynchronize(c->stream);
-  invalidate_graph(c);
-  if (c->agexec) hipGraphExecDestroy(c->agexec);
-  for (auto& g : c->tgexec) if (g) hipGraphExecDestroy(g);
+  invalidate_graph(c);   // (every graph exec: the step, pipelined, async ones)
   for (auto& e : c->ev_pool) hipEventDestroy(e);
   if (c->comm) ncclCommDestroy(c->comm);
   for (void* p : c->allocs) hipFree(p);
@@ -399,12 +418,41 @@ int ddq_synchronize(ddq_ctx* c) {
     const char* who[3] = {"fc4 chain fan-in", "wgrad slab reduce", "tower pool2 exchange"};
     for (int k = 0; k < 3; ++k)
       if (w[at[k]]) {
-        HIP_TRY(c, hipMemset(c->nb.csync + at[k], 0, 4));
-        return fail(c, DDQ_ESTATE, "small-map step: %s meeting timed out (results invalid)",
-                    who[k]);
+        // the launches after the failure wrote no parameter, optimizer state
+        // or iteration (they read the sticky words); start the meeting
+        // counters afresh (a launch short of a party leaves them off by its
+        // count) and take the device iteration back as the host's
+        HIP_TRY(c, hipMemsetAsync(c->nb.csync, 0, 64 * sizeof(int32_t), c->stream));
+        if (c->nb.pairc)
+          HIP_TRY(c, hipMemsetAsync(c->nb.pairc, 0, (size_t)c->nb.B * 2 * sizeof(uint64_t), c->stream));
+        int64_t it = 0;
+        HIP_TRY(c, hipMemcpyAsync(&it, c->nb.iter, sizeof(it), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        c->applied = it;
+        return fail(c, DDQ_ESTATE,
+                    "small-map step: %s meeting timed out (that step and any after it up to "
+                    "this call applied nothing)", who[k]);
       }
   }
   return DDQ_OK;
+}
+
+int ddq_inject_fault(ddq_ctx* c, int32_t fault) {
+  if (!c) return fail(nullptr, DDQ_EINVAL, "null ctx");
+  if (fault == DDQ_FAULT_NONE) {
+    c->fault = 0;
+    return DDQ_OK;
+  }
+  if (fault != DDQ_FAULT_MEET_TIMEOUT) return fail(c, DDQ_EINVAL, "unknown fault %d", fault);
+  if (!c->nb.small) return fail(c, DDQ_ESTATE, "no small-map step on this ctx (S = 16, B <= 256)");
+  c->fault = fault;
+  return DDQ_OK;
+}
+
+int ddq_small_path(const ddq_ctx* c, char* why, int32_t cap) {
+  if (!c) return fail(nullptr, DDQ_EINVAL, "null ctx");
+  if (why && cap > 0) snprintf(why, (size_t)cap, "%s", c->small_off.c_str());
+  return c->nb.small ? 1 : 0;
 }
 
 // ---------------- parameters ----------------
@@ -1195,7 +1243,6 @@ static int enqueue_train(ddq_ctx* c, const ddq_step_cfg* cfg, const NetBuffers& 
                          ReplayMeta* bump = nullptr) {
   NetBuffers nb = nb_in;
   nb.book_inc = step_inc(c, cfg);
-  nb.dup_conv2 = (cfg->flags & DDQ_STEP_REPEAT_CONV2_FWD) != 0;
   // exchange-free steps: fc4's weight update rides on the slab-reduce launch
   const int ex = has_exchange(c, cfg) ? cfg->exchange : DDQ_EXCHANGE_NONE;
   const bool ar_overlap = ex == DDQ_EXCHANGE_ALLREDUCE && cfg->overlap && c->comm;
@@ -1286,10 +1333,8 @@ static int check_step(ddq_ctx* c, const ddq_step_cfg* cfg) {
                 c->nb.B, (long long)c->valid);
   if (cfg->exchange < DDQ_EXCHANGE_NONE || cfg->exchange > DDQ_EXCHANGE_ASYNC)
     return fail(c, DDQ_EINVAL, "unknown exchange %d", cfg->exchange);
-  if (cfg->flags & ~(DDQ_STEP_NO_GRAD_STORE | DDQ_STEP_REPEAT_CONV2_FWD))
+  if (cfg->flags & ~DDQ_STEP_NO_GRAD_STORE)
     return fail(c, DDQ_EINVAL, "unknown step flags 0x%x", (unsigned)cfg->flags);
-  if ((cfg->flags & DDQ_STEP_REPEAT_CONV2_FWD) && c->nb.S == 16)
-    return fail(c, DDQ_EINVAL, "DDQ_STEP_REPEAT_CONV2_FWD: no separate conv2 launch at S = 16");
   if (cfg->exchange != DDQ_EXCHANGE_NONE && c->nranks > 1 && !c->comm && !c->local)
     return fail(c, DDQ_ESTATE, "no communicator");
   return DDQ_OK;
@@ -1589,7 +1634,7 @@ int ddq_async_tick(ddq_ctx* c, const ddq_step_cfg* cfg, int32_t worker) {
   c->rr_rounds = 0;   // the round-robin graph's steady state no longer holds
   // this rank's own ticks (the heavy ones: its next gradient) replay a graph;
   // the other workers' ticks (a receive, the owner apply, a send) stay eager
-  if (worker == c->rank && c->applied > 0 && !getenv("DDQ_NO_TICK_GRAPHS")) {
+  if (worker == c->rank && c->applied > 0) {
     const int64_t it = c->applied + 1;
     const bool pull_p = async_pull_p(cfg, c->last_pull[worker], it);
     const bool special = cfg->target_period > 0 && it % cfg->target_period == 0;
@@ -1726,7 +1771,11 @@ int ddq_step_async(ddq_ctx* c, const ddq_step_cfg* cfg) {
   }
   TRY(check_not_async(c));
   if (c->steps == 0) TRY(initial_target_sync(c, cfg));
-  TRY(enqueue_step(c, cfg, nullptr, nullptr));
+  c->nb.fault_k2_short = c->fault == DDQ_FAULT_MEET_TIMEOUT;   // (this step's launches only)
+  c->fault = 0;
+  const int rc = enqueue_step(c, cfg, nullptr, nullptr);
+  c->nb.fault_k2_short = 0;
+  TRY(rc);
   c->steps++;
   c->applied += step_inc(c, cfg);
   return DDQ_OK;

@@ -90,7 +90,8 @@ struct NetBuffers {
   ParamLayout L;
   float gamma;
   int fwd_only;                     // launch_forward: 0 = every layer, l + 1 = conv layer l only
-  int dup_conv2 = 0;                // DDQ_STEP_REPEAT_CONV2_FWD (measurement): conv2 fwd twice
+  int fault_k2_short = 0;           // ddq_inject_fault (tests): this step's fc4 chain launch
+                                    // one workgroup short, so its fan-in meeting times out
   FusedApplyCfg fa;                 // on: head latches the apply flags, the slab reduce
                                     // applies (FusedApplyCfg)
   int book_inc;                     // param-server iterations per apply (1, or W: server mode)
@@ -125,6 +126,10 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s, void (*ma
 // deepq16 (nb.small): K1 (towers + the head's bookkeeping: latch, bump /
 // next draw, as launch_head's) and K2 (fc4 chain) in place of launch_forward
 // + launch_head
+// Every meeting launch of the small-map step has all of its meeting
+// workgroups resident at once on this device (meet() spins on the others):
+// *ok = 0 and why set otherwise (the ctx then runs the general kernels)
+hipError_t small_coresident(int B, int* ok, char* why, int nwhy);
 hipError_t launch_small_fwd_head(const NetBuffers& nb, hipStream_t s,
                                  void (*mark)(void*, const char*), void* mark_arg,
                                  ReplayMeta* bump = nullptr, const struct Prefetch* pf = nullptr);

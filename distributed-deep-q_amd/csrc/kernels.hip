@@ -1863,7 +1863,7 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
   auto M = [&](const char* n) { if (mark) mark(marg, n); };
   const float* in[2] = {nb.state, nb.next_state};
   // deepq16: conv1 -> pool3 of each (image, tower) in one workgroup (small.h)
-  const bool tower = !nb.fwd_only && S == sm16::kS;
+  const bool tower = !nb.fwd_only && nb.small;
   if (tower) {
     M("tower_fwd");
     CHECK_LAUNCH(sm16::launch_tower_fwd16(tower_args(nb, nz, nullptr), s));
@@ -1906,7 +1906,6 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     a2.mask[0] = nb.mask2; a2.mask[1] = nullptr;
     M("conv2_fwd");
     CHECK_LAUNCH(pick_tile(kConv2Fwd, H, H).launch(a2, nz, s));
-    if (nb.dup_conv2) CHECK_LAUNCH(pick_tile(kConv2Fwd, H, H).launch(a2, nz, s));
   }
   if (!tower && (!nb.fwd_only || nb.fwd_only == 3)) {
     // conv3 (train_val.prototxt:119-158): split bf16, 8x8 tiles (kConv3Fwd), two k groups
@@ -1990,7 +1989,8 @@ hipError_t launch_small_fwd_head(const NetBuffers& nb, hipStream_t s,
   CHECK_LAUNCH(ensure_dyn_lds(reinterpret_cast<const void*>(kern), one ? attr1 : attr2,
                               sm16::kChainSmem));
   M("fc4_chain");
-  ddq_launch(kern, dim3((one ? 2 : 1) * sm16::kFcBlk * c.G), dim3(512), sm16::kChainSmem, s, c);
+  ddq_launch(kern, dim3((one ? 2 : 1) * sm16::kFcBlk * c.G - (nb.fault_k2_short ? 1 : 0)), dim3(512),
+             sm16::kChainSmem, s, c);
   CHECK_LAUNCH(hipGetLastError());
   return hipSuccess;
 }
@@ -2002,6 +2002,54 @@ void small_groups(int B, int* G2, int* G3) {
   // the write-through slab bytes, and the meeting's arrival skew with them)
   *G2 = std::max(1, std::min(16, B / 4));
   *G3 = std::max(1, std::min(8, B / 4));
+}
+
+// K4's dynamic LDS (launch_small_bwd)
+static int wgrad16_lds() {
+  return std::max({2 * sm16::Wg2::BUF * 2, 2 * sm16::Wg3::BUF * 2,
+                   4 * 16 * 64 * 4 + sm16::Wg3::SLAB * 4}) + 16;
+}
+
+hipError_t small_coresident(int B, int* ok, char* why, int nwhy) {
+  *ok = 1;
+  int dev = 0, ncu = 0;
+  if (hipError_t e = hipGetDevice(&dev)) return e;
+  if (hipError_t e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev)) return e;
+  int G2, G3;
+  small_groups(B, &G2, &G3);
+  const int G = B > 32 ? (B + 31) / 32 : 1;
+  struct Launch {
+    const char* name;
+    const void* kern;
+    int threads, lds, meeting;   // meeting: workgroups that wait on each other
+  };
+  const Launch ls[] = {
+      // K1 split form (2 workgroups per (image, tower), B <= 64): pairs meet
+      {"tower_fwd16s", reinterpret_cast<const void*>(sm16::tower_fwd16s_kernel<5, 4>),
+       sm16::kThreads, sm16::kFwdSmemS, 4 * B <= 256 ? 4 * B : 0},
+      // K2: every fc4 workgroup meets (one tower a workgroup at B <= 32)
+      {"fc4_chain16", G == 1 ? reinterpret_cast<const void*>(sm16::fc4_chain16_kernel<1>)
+                             : reinterpret_cast<const void*>(sm16::fc4_chain16_kernel<2>),
+       512, sm16::kChainSmem, (G == 1 ? 2 : 1) * sm16::kFcBlk * G},
+      // K4: a tile's groups meet when it has more than one
+      {"wgrad16", reinterpret_cast<const void*>(sm16::wgrad16_kernel), 256, wgrad16_lds(),
+       (G3 > 1 ? sm16::kT3 * G3 : 0) + (G2 > 1 ? sm16::kT2 * G2 : 0)},
+  };
+  for (const Launch& l : ls) {
+    if (l.meeting == 0) continue;
+    if (hipError_t e = hipFuncSetAttribute(l.kern, hipFuncAttributeMaxDynamicSharedMemorySize, l.lds))
+      return e;
+    int per_cu = 0;
+    if (hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, l.kern, l.threads, l.lds))
+      return e;
+    if ((int64_t)per_cu * ncu < l.meeting) {
+      *ok = 0;
+      snprintf(why, nwhy, "%s: %d meeting workgroups, %d resident (%d per CU x %d CUs)", l.name,
+               l.meeting, per_cu * ncu, per_cu, ncu);
+      return hipSuccess;
+    }
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_small_bwd(const NetBuffers& nb, hipStream_t s,
@@ -2048,6 +2096,8 @@ hipError_t launch_small_bwd(const NetBuffers& nb, hipStream_t s,
     w.w1part = nb.wpart + nb.wpart_off[0]; w.w1_np = nb.wnp[0];
     w.slab2 = nb.slab2; w.slab3 = nb.slab3;
     w.sync = nb.csync + 8;
+    w.poison0 = nb.csync + 2;                  // K2's fan-in
+    w.poison1 = nb.csync + 48;                 // K1's pool2 exchange
     w.grad = nb.grad;
     for (int l = 0; l < 3; ++l) { w.w_off[l] = L.w[l]; w.b_off[l] = L.b[l]; }
     conv_dims(L, w.cd);
@@ -2073,8 +2123,7 @@ hipError_t launch_small_bwd(const NetBuffers& nb, hipStream_t s,
     const int r2 = (w.ipg2 + sm16::Wg2::NI - 1) / sm16::Wg2::NI;
     const int r3 = (w.ipg3 + sm16::Wg3::NI - 1) / sm16::Wg3::NI;
     (void)r2; (void)r3;   // (two buffers always: the staging's dummy slot follows them)
-    const int lds = std::max({2 * sm16::Wg2::BUF * 2, 2 * sm16::Wg3::BUF * 2,
-                              4 * 16 * 64 * 4 + sm16::Wg3::SLAB * 4}) + 16;
+    const int lds = wgrad16_lds();
     static std::atomic<uint64_t> attr{0};
     CHECK_LAUNCH(ensure_dyn_lds(reinterpret_cast<const void*>(sm16::wgrad16_kernel), attr,
                                 sm16::kWgSmem));

@@ -47,7 +47,8 @@ constexpr int CH_TMP = CH_DQ + kMaxB * 4;          // squared errors [kMaxB]
 constexpr int CH_W5 = CH_TMP + kMaxB;             // Q's Q_out columns of the units [4][16]
 constexpr int CH_PS = CH_W5 + 64;                 // theta / state of the 84 unit-sum params
 constexpr int CH_MB = CH_PS + 2 * 96;             // the minibatch's action (4), reward, nonterm
-constexpr int kChainSmemF = CH_MB + 6 * kMaxB;
+constexpr int CH_B5 = CH_MB + 6 * kMaxB;          // Q_out's biases of both towers [2][4]
+constexpr int kChainSmemF = CH_B5 + 8;
 constexpr int kChainSmem = kChainSmemF * 4;
 static_assert(kChainSmem <= 160 * 1024, "K2 LDS");
 
@@ -60,7 +61,8 @@ struct ChainArgs {
   float gamma;
   float* qpart;                    // [32][2][B][4]
   float* dpart;                    // [32][B][256]
-  int32_t* sync;                   // [0..1] the fan-in's 64-bit counter, [2] sticky spin timeout
+  int32_t* sync;                   // [0..1] the fan-in's 64-bit counter, [2] sticky spin timeout,
+                                   // [48] K1's (the pool2 halves' exchange)
   float *q_out, *p_out, *q_sa, *p_sa, *target, *loss;
   float* grad;                     // flat Q gradient
   int apply;                       // fused apply (flags latched by K1's book block)
@@ -163,6 +165,9 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
   };
   float pth = 0.f, pst = 0.f;
   const bool ap0 = c.apply != 0 && G == 1 && !ptower;   // (G > 1: K4 applies the batch sums)
+  // K1 failed its meeting: no update from this step (the word is read now,
+  // used after the fan-in)
+  const bool pois = ap0 && step_poisoned(c.sync + 48, nullptr);
   // the update's flags (latched by K1's book block), loaded now
   const bool first = ap0 && c.at.opt_init[2] != 0, sync = ap0 && c.at.opt_init[3] != 0;
   if (ap0 && tid < 84) {
@@ -187,6 +192,10 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
   if (!ptower) {
     if (tid < 64) csm[CH_W5 + tid] = w5q;
     if (tid < 84) { csm[CH_PS + tid] = pth; csm[CH_PS + 96 + tid] = pst; }
+    // Q_out's biases, read before the fan-in: workgroup 0 updates them in
+    // theta Q (and theta P on a sync step) after it, while other workgroups
+    // may still be summing their Q_out / P_out
+    if (tid < 8) csm[CH_B5 + tid] = (tid < 4 ? c.th[0] : c.th[1])[c.b5_off + (tid & 3)];
     for (int e = tid; e < 6 * B; e += 512)           // action one-hot, reward, non_terminal
       csm[CH_MB + e] = e < 4 * B ? c.action[e] : (e < 5 * B ? c.reward[e - 4 * B] : c.nonterm[e - 5 * B]);
   }
@@ -261,7 +270,7 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
                              __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
-  meet(reinterpret_cast<uint64_t*>(c.sync), 2 * nH / NZ, c.sync + 2);
+  const bool mbad = meet(reinterpret_cast<uint64_t*>(c.sync), 2 * nH / NZ, c.sync + 2);
   DDQ_STAMP(19);
 
   // ---- phase B: every sample's Q_out / P_out (partials summed in j order) ----
@@ -274,8 +283,8 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
     float4 s = v[0];
 #pragma unroll
     for (int j = 1; j < kFcBlk; ++j) { s.x += v[j].x; s.y += v[j].y; s.z += v[j].z; s.w += v[j].w; }
-    const float* th = c.th[z];
-    s.x += th[c.b5_off + 0]; s.y += th[c.b5_off + 1]; s.z += th[c.b5_off + 2]; s.w += th[c.b5_off + 3];
+    const float* b5 = csm + CH_B5 + 4 * z;
+    s.x += b5[0]; s.y += b5[1]; s.z += b5[2]; s.w += b5[3];
     *reinterpret_cast<float4*>(QP + (z * kMaxB + b) * 4) = s;
   }
   __syncthreads();
@@ -305,7 +314,7 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
   }
   __syncthreads();
   DDQ_STAMP(44);
-  const bool ap = ap0;
+  const bool ap = ap0 && !pois && !mbad;
   // dh4 of the workgroup's units: (dQ W5) masked by h4 > 0 (ReLU backward)
   for (int e = lo * kFcN + tid; e < hi * kFcN; e += 512) {
     const int b = e >> 4, n = e & 15;
@@ -1299,6 +1308,9 @@ struct WgArgs {
   const float* w4part;
   int64_t b4_off, w5_off, b5_off;
   float* loss;
+  // the sticky timeout words of this step's earlier meetings (K2's fan-in,
+  // K1's pool2 exchange): set, this launch writes no parameter / state
+  const int32_t *poison0, *poison1;
 };
 
 // Apply one final conv gradient element (layer l, Caffe index i, local e of
@@ -1307,9 +1319,10 @@ struct WgArgs {
 // th0 / st0: the element's theta and optimizer state, loaded by the caller
 // ahead of the sums
 __device__ __forceinline__ void conv_final(const WgArgs& a, int l, bool is_w, int64_t i, int e,
-                                           float v, float th0, float st0, bool first, bool sync) {
+                                           float v, float th0, float st0, bool first, bool sync,
+                                           bool ap) {
   a.grad[i] = v;
-  if (!a.apply) return;
+  if (!ap) return;
   float st = (a.aa.rule != 0 && !first) ? st0 : 0.f;
   const float th = apply_rule(a.aa, first, !is_w, th0, v, st);
   a.at.theta[i] = th;
@@ -1347,9 +1360,11 @@ __device__ __forceinline__ int64_t tile_elem(const WgArgs& a, int e, int ky, int
 // fixed order in LDS.  G == 1: the tile's sums are final and applied here;
 // G > 1: the group's slab, a meeting of the tile's G groups, and this group's
 // slice of the tile summed over the slabs in group order and applied.
+// ap: the fused apply writes (a.apply, no earlier meeting of the step failed);
+// a failed meeting of the tile's groups withholds the slice's writes too.
 template <class W, int L, int KX, int D>
 __device__ __forceinline__ void wg_tile(const WgArgs& a, char* smem, int tile, int g, int G, int ipg,
-                                        float* slabs, bool first, bool sync) {
+                                        float* slabs, bool first, bool sync, bool ap) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   constexpr int KS = W::KS;
   constexpr int NT = KX * W::NCB;                      // accumulators per wave
@@ -1585,7 +1600,7 @@ __device__ __forceinline__ void wg_tile(const WgArgs& a, char* smem, int tile, i
           th = a.at.theta[ci];
           st = a.aa.rule != 0 ? a.at.opt[ci] : 0.f;
         }
-        conv_final(a, L, e < ELEMS, ci, le, fin[e], th, st, first, sync);
+        conv_final(a, L, e < ELEMS, ci, le, fin[e], th, st, first, sync, ap);
       }
     }
     DDQ_STAMP(SB + 5);
@@ -1600,7 +1615,8 @@ __device__ __forceinline__ void wg_tile(const WgArgs& a, char* smem, int tile, i
   uint64_t* ctr = reinterpret_cast<uint64_t*>(a.sync) + (L == 1 ? 0 : kT2) + tile;   // at G >= 4)
   const __amdgpu_buffer_rsrc_t rall = __builtin_amdgcn_make_buffer_rsrc(
       slabs + (int64_t)tile * G * SLAB, (short)0, (int)(G * SLAB * 4), 0x00020000);
-  if (e0 >= e1) meet(ctr, G, a.sync + 32);            // an empty slice still arrives
+  if (e0 >= e1) (void)meet(ctr, G, a.sync + 32);      // an empty slice still arrives
+  bool apt = ap;
   for (int c0 = e0; c0 < e1; c0 += 256 * EPT) {
     int64_t ci_[EPT];
     int le_[EPT];
@@ -1618,7 +1634,7 @@ __device__ __forceinline__ void wg_tile(const WgArgs& a, char* smem, int tile, i
     }
     if (c0 == e0) {
       DDQ_STAMP(SB + 3);
-      meet(ctr, G, a.sync + 32);
+      apt = ap && !meet(ctr, G, a.sync + 32);
       DDQ_STAMP(SB + 4);
     }
     // every group's value of every element loaded first (G <= GM), summed in
@@ -1650,7 +1666,7 @@ __device__ __forceinline__ void wg_tile(const WgArgs& a, char* smem, int tile, i
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
       const int e = c0 + tid + 256 * k;
-      if (e < e1 && ci_[k] >= 0) conv_final(a, L, e < ELEMS, ci_[k], le_[k], vs[k], th_[k], st_[k], first, sync);
+      if (e < e1 && ci_[k] >= 0) conv_final(a, L, e < ELEMS, ci_[k], le_[k], vs[k], th_[k], st_[k], first, sync, apt);
     }
   }
   DDQ_STAMP(SB + 5);
@@ -1659,8 +1675,9 @@ __device__ __forceinline__ void wg_tile(const WgArgs& a, char* smem, int tile, i
 // fc4's weights (512 x 256 at S = 16) updated from the gradient K2 stored, 4
 // consecutive elements a thread (coalesced), the rules of the other apply
 // sites (apply_rule, no FMA contraction: bit-identical updates)
-__device__ __forceinline__ void w4_apply(const WgArgs& a, int blk, bool first, bool sync) {
+__device__ __forceinline__ void w4_apply(const WgArgs& a, int blk, bool first, bool sync, bool ap) {
   constexpr int64_t n = 512LL * kFcK;
+  if (a.G == 1 && !ap) return;
   for (int64_t j = ((int64_t)blk * 256 + threadIdx.x) * 4; j < n; j += (int64_t)a.nw4 * 256 * 4) {
     const int64_t i = a.w4_off + j;
     float4 g;
@@ -1671,7 +1688,7 @@ __device__ __forceinline__ void w4_apply(const WgArgs& a, int blk, bool first, b
         g.x += p.x; g.y += p.y; g.z += p.z; g.w += p.w;
       }
       *reinterpret_cast<float4*>(a.grad + i) = g;
-      if (!a.apply) continue;
+      if (!ap) continue;
     } else {
       g = *reinterpret_cast<const float4*>(a.grad + i);
     }
@@ -1691,7 +1708,7 @@ __device__ __forceinline__ void w4_apply(const WgArgs& a, int blk, bool first, b
 
 // B > 32: the unit sums' partials (K2 upart) summed in chunk order -> db4,
 // dW5 (32 blocks x 80), db5 (4), loss; stored, and applied when apply
-__device__ __forceinline__ void units_apply(const WgArgs& a, bool first, bool sync) {
+__device__ __forceinline__ void units_apply(const WgArgs& a, bool first, bool sync, bool ap) {
   for (int q = threadIdx.x; q < kFcBlk * 85; q += 256) {
     const int jb = q / 85, qq = q - jb * 85;
     if (qq >= 80 && jb != 0) continue;                // (db5, loss: block 0's)
@@ -1704,7 +1721,7 @@ __device__ __forceinline__ void units_apply(const WgArgs& a, bool first, bool sy
                                                  : a.w5_off + ((qq >> 4) - 1) * 512 + n0 + (qq & 15));
     const bool is_bias = qq >= 80 || (qq >> 4) == 0;
     a.grad[i] = v;
-    if (!a.apply) continue;
+    if (!ap) continue;
     float st = (a.aa.rule != 0 && !first) ? a.at.opt[i] : 0.f;
     const float th = apply_rule(a.aa, first, is_bias, a.at.theta[i], v, st);
     a.at.theta[i] = th;
@@ -1719,31 +1736,31 @@ __device__ __forceinline__ void units_apply(const WgArgs& a, bool first, bool sy
 __global__ __launch_bounds__(256) void wgrad16_kernel(const WgArgs a) {
   extern __shared__ __attribute__((aligned(16))) char wsm[];
   int bid = blockIdx.x;
-#ifdef DDQ_EXP_K4_EMPTY
-  return;
-#endif
   const bool first = a.apply && a.at.opt_init[2] != 0, sync = a.apply && a.at.opt_init[3] != 0;
+  // (read now, needed only at the writes: the operand loads do not wait on it)
+  const bool pois = a.apply && step_poisoned(a.poison0, a.poison1);
+  const bool ap = a.apply && !pois;
   const int n2 = kT2 * a.G2, n3 = kT3 * a.G3;
   if (bid < n3) {
-    wg_tile<Wg3, 2, 3, 2>(a, wsm, bid % kT3, bid / kT3, a.G3, a.ipg3, a.slab3, first, sync);
+    wg_tile<Wg3, 2, 3, 2>(a, wsm, bid % kT3, bid / kT3, a.G3, a.ipg3, a.slab3, first, sync, ap);
     return;
   }
   bid -= n3;
   if (bid < n2) {
-    wg_tile<Wg2, 1, 5, 2>(a, wsm, bid % kT2, bid / kT2, a.G2, a.ipg2, a.slab2, first, sync);
+    wg_tile<Wg2, 1, 5, 2>(a, wsm, bid % kT2, bid / kT2, a.G2, a.ipg2, a.slab2, first, sync, ap);
     return;
   }
   bid -= n2;
   if (bid >= kW1Blocks) {   // the fc4 weights' (and unit sums') update, then the next
     const int x = bid - kW1Blocks;   // step's gather (B = 256: 512 short blocks, last)
-    if (x < a.nw4) w4_apply(a, x, first, sync);
-    else if (x < a.nw4 + a.nus) units_apply(a, first, sync);
+    if (x < a.nw4) w4_apply(a, x, first, sync, ap);
+    else if (x < a.nw4 + a.nus) units_apply(a, first, sync, ap);
     else prefetch_body(a.pf, x - a.nw4 - a.nus);
     return;
   }
   DDQ_STAMP(40);
   // conv1: the B per-image slabs summed in image order, element by element
-  if (bid == 0 && threadIdx.x == 0 && a.book)
+  if (bid == 0 && threadIdx.x == 0 && a.book && !pois)   // (no update: no iteration)
     apply_book(a.iter, const_cast<int32_t*>(a.at.opt_init), a.book_period, a.bump, a.book_inc);
   const int np = a.w1_np;
   for (int e = bid * 256 + threadIdx.x; e < 32 * 197; e += kW1Blocks * 256) {
@@ -1781,7 +1798,7 @@ __global__ __launch_bounds__(256) void wgrad16_kernel(const WgArgs a) {
       for (int u = 0; u < 8; ++u) v += t[u];
     }
     for (; b0 < a.B; ++b0) v += src[(int64_t)b0 * 32 * np];
-    conv_final(a, 0, n < 196, i, le, v, th0, st0, first, sync);
+    conv_final(a, 0, n < 196, i, le, v, th0, st0, first, sync, ap);
   }
   DDQ_STAMP(41);
 }

@@ -52,9 +52,9 @@ class StepCfg(ctypes.Structure):
 
 
 STEP_NO_GRAD_STORE = 1     # include/ddq_hip.h DDQ_STEP_NO_GRAD_STORE
-STEP_REPEAT_CONV2_FWD = 2  # include/ddq_hip.h DDQ_STEP_REPEAT_CONV2_FWD (measurement only)
+FAULT_NONE, FAULT_MEET_TIMEOUT = 0, 1   # include/ddq_hip.h enum ddq_fault
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 EXCHANGES = {"none": 0, "allreduce": 1, "sharded": 2, "server": 3, "async": 4}
 
 
@@ -70,6 +70,8 @@ _SIGS = {
     "ddq_last_error": (ctypes.c_char_p, [_P]),
     "ddq_set_stream": (ctypes.c_int, [_P, _P]),
     "ddq_synchronize": (ctypes.c_int, [_P]),
+    "ddq_inject_fault": (ctypes.c_int, [_P, _i32]),
+    "ddq_small_path": (ctypes.c_int, [_P, ctypes.c_char_p, _i32]),
     "ddq_get_stream": (ctypes.c_int, [_P, ctypes.POINTER(_P)]),
     "ddq_num_params": (_i64, [_P]),
     "ddq_param_layout": (ctypes.c_int, [_P, ctypes.POINTER(BlobDesc), _i32, ctypes.POINTER(_i32)]),

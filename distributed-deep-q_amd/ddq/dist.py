@@ -151,15 +151,18 @@ class AsyncTicketLoop:
 
         The loop spins (no sleep) for spin_s after its last progress -- a
         sleep of tens of microseconds lasts several times that and the device
-        idles meanwhile -- then polls every poll_s.  A ticket this rank takes
-        is its own to execute: when it is the next one, no store read is
-        needed (one add + one set per own push; other ranks' tickets: one
-        check + one get)."""
+        idles meanwhile -- then polls every poll_s.  The spin polls only local
+        state (this worker's gradient readiness, its own ticket); the store
+        server is asked about other ranks' tickets at most once per poll_s, so
+        W spinning ranks do not flood it.  A ticket this rank takes is its own
+        to execute: when it is the next one, no store read is needed (one add
+        + one set per own push; other ranks' tickets: one check + one get)."""
         net, store = self.net, self.store
         net.async_begin(self.cfg)
         order = []
         end = self.next + int(npush)
         idle_since = time.perf_counter()
+        last_check = -1.0
         while self.next < end:
             progressed = False
             if not self.holding and net.async_ready():
@@ -171,9 +174,12 @@ class AsyncTicketLoop:
             if self.holding and self.mine == self.next:
                 w = self.rank
             else:
-                key = "tk/%d" % self.next
-                if store.check([key]):
-                    w = int(store.get(key))
+                now = time.perf_counter()
+                if now - last_check >= poll_s:
+                    last_check = now
+                    key = "tk/%d" % self.next
+                    if store.check([key]):
+                        w = int(store.get(key))
             if w is not None:
                 net.async_tick(self.cfg, w)
                 order.append(w)

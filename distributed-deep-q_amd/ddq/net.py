@@ -65,6 +65,20 @@ class DeepQNet:
     def synchronize(self):
         self._check(self.lib.ddq_synchronize(self.ctx))
 
+    def inject_fault(self, fault="meet_timeout"):
+        """Arm a failpoint (tests): "meet_timeout" -- the next eager step's fc4
+        chain launches one workgroup short (ddq_inject_fault); None disarms."""
+        f = _lib.FAULT_NONE if fault is None else {"meet_timeout": _lib.FAULT_MEET_TIMEOUT}[fault]
+        self._check(self.lib.ddq_inject_fault(self.ctx, f))
+
+    def small_path(self):
+        """(on, reason off): the four-launch small-map step (S = 16) or not."""
+        buf = ctypes.create_string_buffer(256)
+        on = self.lib.ddq_small_path(self.ctx, buf, 256)
+        if on < 0:
+            self._check(on)
+        return bool(on), buf.value.decode()
+
     # ------------------------------------------------------------- parameters
     def stream(self):
         """The ctx's HIP stream handle (int), e.g. for torch.cuda.ExternalStream."""
@@ -331,18 +345,15 @@ class DeepQNet:
 
     # -------------------------------------------------------------------- step
     def step_cfg(self, rule="rmsprop", lr=1e-4, target_period=10, allreduce=False, seed=0,
-                 exchange=None, overlap=False, store_grads=True, repeat_conv2=False, **kw):
+                 exchange=None, overlap=False, store_grads=True, **kw):
         """exchange: "none" | "allreduce" | "sharded" | "server" | "async" (include/ddq_hip.h
         enum ddq_exchange); allreduce=True is shorthand for "allreduce".
         store_grads=False: exchange-free steps do not store fc4's weight gradient
-        (DDQ_STEP_NO_GRAD_STORE; the update is the same, bit for bit).
-        repeat_conv2=True: measurement only, conv2's forward launched twice
-        (DDQ_STEP_REPEAT_CONV2_FWD; bench.py's graph-replay kernel figure)."""
+        (DDQ_STEP_NO_GRAD_STORE; the update is the same, bit for bit)."""
         if exchange is None:
             exchange = "allreduce" if allreduce else "none"
         ex = _lib.EXCHANGES[exchange] if isinstance(exchange, str) else int(exchange)
-        flags = (0 if store_grads else _lib.STEP_NO_GRAD_STORE) | \
-            (_lib.STEP_REPEAT_CONV2_FWD if repeat_conv2 else 0)
+        flags = 0 if store_grads else _lib.STEP_NO_GRAD_STORE
         return _lib.StepCfg(_lib.update_cfg(rule, lr, **kw), int(target_period), ex, int(seed),
                             int(bool(overlap)), flags)
 

@@ -35,8 +35,11 @@
 extern "C" {
 #endif
 
-#define DDQ_ABI_VERSION 5   /* 5: ddq_step_cfg.reserved -> flags; ddq_synchronize reports a
-                              small-map step's spin timeout as DDQ_ESTATE */
+#define DDQ_ABI_VERSION 6   /* 5: ddq_step_cfg.reserved -> flags; ddq_synchronize reports a
+                              small-map step's spin timeout as DDQ_ESTATE.
+                              6: DDQ_STEP_REPEAT_CONV2_FWD removed (flag 2 is refused);
+                              a timed-out step applies nothing; ddq_inject_fault,
+                              ddq_small_path */
 
 enum ddq_status {
   DDQ_OK = 0,
@@ -145,12 +148,6 @@ typedef struct ddq_step_cfg {
  * The update is unchanged, bit for bit.  No effect on exchanged steps (their
  * gradient is what is exchanged). */
 #define DDQ_STEP_NO_GRAD_STORE 1
-/* Measurement only (bench.py's graph-replay kernel figure): every step
- * launches conv2's forward twice (the launch is idempotent: same inputs, same
- * outputs), so (graph step time with it - without it) is that kernel's
- * unprofiled in-graph time.  Not at S = 16 (conv2 runs inside the fused tower
- * launch there). */
-#define DDQ_STEP_REPEAT_CONV2_FWD 2
 
 /* ---------------- context ---------------------------------------------- */
 /* caffe.Net(prototxt, model) + set_mode_gpu + set_phase_test
@@ -163,10 +160,31 @@ int ddq_abi_version(void);
 int ddq_set_stream(ddq_ctx* ctx, void* hip_stream);
 /* The ctx's HIP stream (e.g. for torch.cuda.ExternalStream events). */
 int ddq_get_stream(const ddq_ctx* ctx, void** hip_stream);
-/* Wait for the ctx's streams.  DDQ_ESTATE (and the flag cleared) when a
- * small-map (S = 16) step's inter-workgroup meeting timed out since the last
- * call: the launches went on, so that step's results are invalid. */
+/* Wait for the ctx's streams.  DDQ_ESTATE when a small-map (S = 16) step's
+ * inter-workgroup meeting timed out since the last call.  The launches went
+ * on (no hang) but wrote no parameter, optimizer state, P copy or iteration
+ * from that step on (a fused-apply step; an exchanged step's gradient is
+ * invalid); this call clears the flag, restarts the meeting counters and
+ * takes the device iteration back, so the ctx steps on from the last good
+ * update. */
 int ddq_synchronize(ddq_ctx* ctx);
+
+/* Failpoints for the error paths' tests (no reference counterpart). */
+enum ddq_fault {
+  DDQ_FAULT_NONE = 0,          /* disarm                                        */
+  /* the next eager step (ddq_step_async) launches its fc4 chain one workgroup
+   * short, so the fan-in meeting times out: ddq_synchronize must then return
+   * DDQ_ESTATE with the model unchanged.  Small-map ctxs only (DDQ_ESTATE
+   * otherwise). */
+  DDQ_FAULT_MEET_TIMEOUT = 1
+};
+int ddq_inject_fault(ddq_ctx* ctx, int32_t fault);
+
+/* 1 when the ctx runs the four-launch small-map step (S = 16, B <= 256, and
+ * every meeting launch's workgroups fit the device at once: checked with the
+ * occupancy API at ddq_create), 0 when it runs the general kernels; why
+ * (nullable, cap bytes) receives the reason it is off. */
+int ddq_small_path(const ddq_ctx* ctx, char* why, int32_t cap);
 
 /* ---------------- parameters ------------------------------------------- */
 /* Number of fp32 parameters of ONE tower (228,132 at S=16,

@@ -56,7 +56,7 @@ def test_struct_layouts_match_header():
 
 
 def test_abi_version(lib):
-    assert lib.ddq_abi_version() == 5
+    assert lib.ddq_abi_version() == 6
 
 
 @pytest.mark.parametrize("batch,frame,ok", [(1024, 256, True), (1024, 512, False),
@@ -112,5 +112,7 @@ def test_header_constants_match_binding():
     defs = {k: int(v) for k, v in re.findall(r"#define\s+(DDQ_\w+)\s+(\d+)", txt)}
     assert defs["DDQ_ABI_VERSION"] == _lib.ABI_VERSION
     assert defs["DDQ_STEP_NO_GRAD_STORE"] == _lib.STEP_NO_GRAD_STORE
-    assert defs["DDQ_STEP_REPEAT_CONV2_FWD"] == _lib.STEP_REPEAT_CONV2_FWD
-    assert _lib.STEP_NO_GRAD_STORE & _lib.STEP_REPEAT_CONV2_FWD == 0
+    assert "DDQ_STEP_REPEAT_CONV2_FWD" not in defs          # ABI 6: removed (refused)
+    enums = dict((k, int(v)) for k, v in re.findall(r"(DDQ_FAULT_\w+)\s*=\s*(\d+)", txt))
+    assert enums == {"DDQ_FAULT_NONE": _lib.FAULT_NONE,
+                     "DDQ_FAULT_MEET_TIMEOUT": _lib.FAULT_MEET_TIMEOUT}

@@ -55,14 +55,26 @@ def ref_mod():
     return ref_numpy
 
 
+_RINGS = {}
+
+
+def ring_for(S):
+    """The bench's replay contents at 64x64 (bench.fill_replay, rank 0: a 4096-
+    transition pool tiled over 30 000 slots); at 16x16 (deepq16) 4096 slots."""
+    if S not in _RINGS:
+        from ddq.expgain import synthetic_transitions
+        pool = 4096
+        n = N if S == 64 else pool
+        st, ac, rw, nt = synthetic_transitions(pool, S, seed=1000 if S == 64 else 77)
+        reps = (n + pool - 1) // pool
+        _RINGS[S] = (np.tile(st, (reps, 1, 1, 1))[:n], np.tile(ac, reps)[:n],
+                     np.tile(rw, reps)[:n], np.tile(nt, reps)[:n])
+    return _RINGS[S]
+
+
 @pytest.fixture(scope="module")
 def ring():
-    from ddq.expgain import synthetic_transitions
-    pool = 4096
-    st, ac, rw, nt = synthetic_transitions(pool, S, seed=1000)   # bench.fill_replay, rank 0
-    reps = (N + pool - 1) // pool
-    return (np.tile(st, (reps, 1, 1, 1))[:N], np.tile(ac, reps)[:N], np.tile(rw, reps)[:N],
-            np.tile(nt, reps)[:N])
+    return ring_for(S)
 
 
 def oracle_chain(ref, theta, ring_arrays, log, rule, lr, period, S=S):
@@ -94,7 +106,7 @@ def oracle_chain(ref, theta, ring_arrays, log, rule, lr, period, S=S):
     return thq, thp, state, loss
 
 
-def make_net(ddq, theta, ring, log=64, S=S):
+def make_net(ddq, theta, ring, log=64, S=S, B=B):
     N = len(ring[0])
     net = ddq.DeepQNet(batch=B, frame=S)
     net.set_flat(0, theta)
@@ -114,16 +126,28 @@ def oracle_rule(ref, rule, th, g, state, lr):
     raise ValueError(rule)
 
 
-@pytest.mark.parametrize("rule,lr,calls", [("rmsprop", 1e-4, (25, 6)),
-                                           ("sgd", 1e-2, (17, 3, 1, 10))])
-def test_shipped_chain_teacher_forced(ref_mod, ring, rule, lr, calls):
+# (S, B, rule, lr, calls): the bench's C2 step (64x64) and deepq16 (16x16,
+# train_val.prototxt:8-11: the four-launch small-map step the bench's deepq16
+# line measures, with its fused apply in K2 / K4), plus deepq16 at C3's B = 256
+# (the fc4 chain in 8 image chunks, their partial sums applied by K4)
+TEACHER_FORCED = [(64, 32, "rmsprop", 1e-4, (25, 6)), (64, 32, "sgd", 1e-2, (17, 3, 1, 10)),
+                  (16, 32, "rmsprop", 1e-4, (25, 6)), (16, 32, "sgd", 1e-2, (17, 3, 1, 10)),
+                  (16, 256, "rmsprop", 1e-4, (9, 3))]
+
+
+@pytest.mark.parametrize("S,B,rule,lr,calls", TEACHER_FORCED)
+def test_shipped_chain_teacher_forced(ref_mod, S, B, rule, lr, calls):
     import ddq
     from ddq.params import init_params_flat
     from _parity import check_full_pass
     ref = ref_mod
+    ring = ring_for(S)
+    N = len(ring[0])
     theta = init_params_flat(S, seed=42)
     T = sum(calls)
-    chain = make_net(ddq, theta, ring)
+    chain = make_net(ddq, theta, ring, S=S, B=B)
+    if S == 16:
+        assert chain.small_path()[0], chain.small_path()
     cfg = chain.step_cfg(rule, lr=lr, target_period=10, seed=1234)
     for k in calls:
         chain.step_pipelined(cfg, k)
@@ -139,7 +163,7 @@ def test_shipped_chain_teacher_forced(ref_mod, ring, rule, lr, calls):
     r = ref.ReplayRef((4, S, S), N)
     r.state, r.action, r.reward, r.non_terminal = st, ac, rw, nt.astype(bool)
     r.head, r.valid = 0, N
-    eager = make_net(ddq, theta, ring)
+    eager = make_net(ddq, theta, ring, S=S, B=B)
     thq, thp = theta.copy(), theta.copy()
     state = None
     ties = 0
@@ -165,13 +189,16 @@ def test_shipped_chain_teacher_forced(ref_mod, ring, rule, lr, calls):
             close(gst, st_ref, what="step %d cache" % t, quiet=t not in (0, T - 1))
             state = gst
         thq, thp = gq, gp
-    print("%s: %d teacher-forced steps at rtol 1e-4, %d near-tie routings adopted" % (rule, T, ties))
+    print("%dx%d B=%d %s: %d teacher-forced steps at rtol 1e-4, %d near-tie routings adopted"
+          % (S, S, B, rule, T, ties))
     # the shipped chain IS that sequence of steps, bit for bit
     np.testing.assert_array_equal(chain.get_flat(0), eager.get_flat(0))
     np.testing.assert_array_equal(chain.get_flat(1), eager.get_flat(1))
     np.testing.assert_array_equal(chain.optimizer_state(), eager.optimizer_state())
     np.testing.assert_array_equal(chain.index_log(0, T), eager.index_log(0, T))
     assert float(chain.blob("loss")) == float(eager.blob("loss"))
+    chain.close()
+    eager.close()
 
 
 @pytest.mark.parametrize("rule,lr,calls", [("rmsprop", 1e-4, (1, 5)), ("sgd", 1e-2, (16, 8))])

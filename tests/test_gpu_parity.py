@@ -182,6 +182,8 @@ FULL_PASS_CASES = [
     # slice longer than one chunk (B = 8: two conv3 groups), ragged groups
     (16, 1, "snake", "x3"), (16, 2, "uniform", "x3"), (16, 8, "snake", "x3"),
     (16, 12, "uniform", "x3"), (16, 100, "snake", "x3"),
+    # S = 16 past the small-map step's B <= 256: the general kernels
+    (16, 300, "snake", "x3"),
 ]
 
 
@@ -347,7 +349,7 @@ def test_rccl_world1_allreduce_and_step(ddq, ref):
 
 
 @pytest.mark.parametrize("rule,B", [("rmsprop", 16), ("adagrad", 16), ("momentum", 16),
-                                    ("rmsprop", 100)])
+                                    ("rmsprop", 32), ("rmsprop", 100)])
 def test_fused_apply_matches_separate_apply(ddq, ref, rule, B):
     """The fused fc4-weight apply (slab-reduce launch, draw counter advanced by
     the head kernel; exchange-free steps) against the separate apply launch

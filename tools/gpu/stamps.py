@@ -65,8 +65,12 @@ for r, t in enumerate(runs):
             ([lo, lo + 1, lo + 2, lo + 3, lo + 4, lo + 6, lo + 5] if lo in (24, 32) else
              range(lo, lo + (2 if lo >= 40 else 8)))
         used = [k for k in seq if (tt[:, k] > 0).any()]
-        rel = {k: (np.median(tt[:, k] - tt[:, lo]) * 10 / 1000, (tt[:, k].max() - t0) * 10 / 1000)
-               for k in used}
+        # each slot over the workgroups that wrote it (K2's P-tower workgroups
+        # leave after slot 18; an unwritten slot is 0, not a time)
+        rel = {}
+        for k in used:
+            w = tt[tt[:, k] > 0]
+            rel[k] = (np.median(w[:, k] - w[:, lo]) * 10 / 1000, (w[:, k].max() - t0) * 10 / 1000)
         print("run %d slots %d+: %d blocks, span %.2f us; slot: median since own start / last "
               "since launch start (us): %s" % (r, lo, len(tt), (tt[:, used].max() - t0) * 10 / 1000,
                                             " ".join("%d:%.2f/%.2f" % (k, a, b) for k, (a, b) in rel.items())))
@@ -75,7 +79,7 @@ for r, t in enumerate(runs):
 for lo, name in ((24, "conv2"), (32, "conv3")):
     t = runs[-1]
     t0 = t[t[:, 16 if lo == 0 else 24] > 0][:, 24].min() if (t[:, 24] > 0).any() else 0
-    sel = np.nonzero(t[:, lo] > 0)[0]
+    sel = np.nonzero((t[:, lo] > 0) & (t[:, lo + 3] > 0))[0]
     arr = sorted(((t[b, lo + 3] - t0) * 10 / 1000, b, [(t[b, lo + k] - t[b, lo]) * 10 / 1000 for k in range(1, 6)])
                  for b in sel)[::-1]
     print("%s pre-meeting arrivals (us since launch), slowest 6: %s" % (
