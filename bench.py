@@ -345,10 +345,21 @@ def deepq16_line(steps=2000, warmup=100, rule="rmsprop"):
     net.synchronize()
     dt = (time.perf_counter() - t0) / steps
     rl = step_roofline(B, S, net.num_params)
+    # the four launches' own dispatch times (eager steps, hipExtLaunchKernel
+    # start / stop events on the ctx stream), median of 20, each against the
+    # peak of the arithmetic it runs (kernel_roofline)
+    prof = {}
+    for _ in range(20):
+        for name, us in net.profile_step(cfg):
+            prof.setdefault(name, []).append(us)
+    kus = {k: float(np.median(v)) for k, v in prof.items()}
+    small_path = net.small_path()[0]
     net.close()
     return {"batch": B, "frame": S, "updates_per_s": round(1 / dt, 2),
-            "ms_per_step": round(dt * 1e3, 4), "steps": steps,
+            "ms_per_step": round(dt * 1e3, 4), "steps": steps, "small_path": small_path,
             "step_ideal_us": rl["ideal_us"], "step_frac": round(rl["ideal_us"] * 1e-6 / dt, 4),
+            "kernels_us": {k: round(v, 2) for k, v in kus.items()},
+            "kernel_roofline": kernel_roofline(kus, B, S, net.num_params),
             "reference_published_fwd_bwd_ms": PUBLISHED_CPU_MS[16]}
 
 

@@ -333,12 +333,17 @@ def magnitudes(pQ, pP, state, action, reward, next_state, non_terminal, routes=N
         for i, ((_, _, k, pad), lname) in enumerate(zip(CONVS, names[:3])):
             W, b = pa[lname]
             ins.append(h)
-            m = conv_forward(h, W, b.reshape(-1), pad)
+            m_all = conv_forward(h, W, b.reshape(-1), pad)
             a_s = cache["act%d" % (i + 1)]
-            m = np.where(a_s > 0, m, 0.0)
+            m = np.where(a_s > 0, m_all, 0.0)
             if rts is not None and prefix == "Q":
                 code = np.asarray(rts[i + 1])
                 keep = code < 4
+                # a routed window's value is the conv sum at the routed pixel,
+                # whatever the float64 sign there: at an adopted near-tie (the
+                # GPU's max a tiny positive fp32 value, the oracle's <= 0) its
+                # magnitude is that sum's |terms|, not 0
+                m = m_all
                 win = m.reshape(B, m.shape[1], m.shape[2] // 2, 2, m.shape[3] // 2, 2).transpose(
                     0, 1, 2, 4, 3, 5).reshape(B, m.shape[1], m.shape[2] // 2, m.shape[3] // 2, 4)
                 h = np.take_along_axis(win, np.where(keep, code, 0)[..., None], -1)[..., 0] * keep
