@@ -180,38 +180,38 @@ __device__ void tower_transpose(const TowerArgs& a, int x, char* smem);
 // meeting point, never reset: arrival `old` belongs to the group ending at
 // (old / n + 1) n, which its last arriver reaches with its own add (no
 // reset / generation round trips on the release path).  Bounded: a spin past
-// ~0.1 s records a timeout in the sticky word and goes on (no hang).
-// Returns true (in every thread) when the meeting failed: this workgroup's
-// spin timed out, or the sticky word was already set when it arrived (a
-// party that arrives after the others gave up finds their mark; the word is
-// loaded beside the arrival add, so the release path waits on no extra
-// round trip).  Callers skip every parameter / optimizer-state write then:
-// a failed meeting leaves the model as it was (ddq_synchronize reports it).
-__device__ __forceinline__ bool meet(uint64_t* ctr, uint32_t n, int32_t* timeout) {
-  __shared__ int meet_bad;
+// ~0.1 s records a timeout in the sticky word and goes on (no hang); callers
+// read the word afterwards (meet_failed) and then write no parameter.
+__device__ __forceinline__ void meet(uint64_t* ctr, uint32_t n, int32_t* timeout) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    int bad;
-    const int32_t seen = __hip_atomic_load(timeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t old = __hip_atomic_fetch_add(ctr, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t target = (old / n + 1) * n;
-    bad = seen != 0;
     if (old + 1 != target) {
       int spins = 0;
       while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
         __builtin_amdgcn_s_sleep(1);
         if (++spins > (1 << 21)) {
           __hip_atomic_store(timeout, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          bad = 1;
           break;
         }
       }
     }
-    meet_bad = bad;
   }
   __syncthreads();
-  return meet_bad != 0;
+}
+
+// After a meet(): did this meeting (or an earlier one of the step) fail?  The
+// sticky word is set by a party whose spin gave up before it left the
+// meeting, and a party that arrives after the others gave up finds it set.
+// One sc1 load (L2-served: the word is written by other workgroups of this
+// launch), issued right after the meeting and consumed only where the
+// parameters are written, so no path waits on it.
+__device__ __forceinline__ int32_t meet_word(const int32_t* w) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(w), (short)0, 4, 0x00020000);
+  return __builtin_bit_cast(int32_t, __builtin_amdgcn_raw_buffer_load_b32(r, 0, 0, 16));
 }
 
 // An earlier launch of this step failed a meeting (its sticky timeout word,
@@ -822,7 +822,7 @@ __global__ __launch_bounds__(kThreads) void tower_fwd16s_kernel(const TowerArgs 
     }
     w3[0].store(ring3, tid);                         // (P1 / conv2's ring are dead)
     w3[1].store(ring3 + WH3_SLOT, tid);
-    (void)meet(a.pairc + pair, 2, a.timeout);   // (a failure: K2 / K4 see the sticky word)
+    meet(a.pairc + pair, 2, a.timeout);   // (a failure: K2 / K4 see the sticky word)
     const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<__bf16*>(theirs), (short)0, 3072, 0x00020000);
     if (tid < 192) {

@@ -47,8 +47,7 @@ constexpr int CH_TMP = CH_DQ + kMaxB * 4;          // squared errors [kMaxB]
 constexpr int CH_W5 = CH_TMP + kMaxB;             // Q's Q_out columns of the units [4][16]
 constexpr int CH_PS = CH_W5 + 64;                 // theta / state of the 84 unit-sum params
 constexpr int CH_MB = CH_PS + 2 * 96;             // the minibatch's action (4), reward, nonterm
-constexpr int CH_B5 = CH_MB + 6 * kMaxB;          // Q_out's biases of both towers [2][4]
-constexpr int kChainSmemF = CH_B5 + 8;
+constexpr int kChainSmemF = CH_MB + 6 * kMaxB;
 constexpr int kChainSmem = kChainSmemF * 4;
 static_assert(kChainSmem <= 160 * 1024, "K2 LDS");
 
@@ -192,10 +191,6 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
   if (!ptower) {
     if (tid < 64) csm[CH_W5 + tid] = w5q;
     if (tid < 84) { csm[CH_PS + tid] = pth; csm[CH_PS + 96 + tid] = pst; }
-    // Q_out's biases, read before the fan-in: workgroup 0 updates them in
-    // theta Q (and theta P on a sync step) after it, while other workgroups
-    // may still be summing their Q_out / P_out
-    if (tid < 8) csm[CH_B5 + tid] = (tid < 4 ? c.th[0] : c.th[1])[c.b5_off + (tid & 3)];
     for (int e = tid; e < 6 * B; e += 512)           // action one-hot, reward, non_terminal
       csm[CH_MB + e] = e < 4 * B ? c.action[e] : (e < 5 * B ? c.reward[e - 4 * B] : c.nonterm[e - 5 * B]);
   }
@@ -270,7 +265,8 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
                              __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
-  const bool mbad = meet(reinterpret_cast<uint64_t*>(c.sync), 2 * nH / NZ, c.sync + 2);
+  meet(reinterpret_cast<uint64_t*>(c.sync), 2 * nH / NZ, c.sync + 2);
+  const int32_t mword = ap0 ? meet_word(c.sync + 2) : 0;   // (consumed at the updates)
   DDQ_STAMP(19);
 
   // ---- phase B: every sample's Q_out / P_out (partials summed in j order) ----
@@ -283,8 +279,10 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
     float4 s = v[0];
 #pragma unroll
     for (int j = 1; j < kFcBlk; ++j) { s.x += v[j].x; s.y += v[j].y; s.z += v[j].z; s.w += v[j].w; }
-    const float* b5 = csm + CH_B5 + 4 * z;
-    s.x += b5[0]; s.y += b5[1]; s.z += b5[2]; s.w += b5[3];
+    // (Q_out's biases: nothing in this launch writes them -- at B <= 32 K4
+    // applies their update, as it applies every batch sum's at B > 32)
+    const float* th = c.th[z];
+    s.x += th[c.b5_off + 0]; s.y += th[c.b5_off + 1]; s.z += th[c.b5_off + 2]; s.w += th[c.b5_off + 3];
     *reinterpret_cast<float4*>(QP + (z * kMaxB + b) * 4) = s;
   }
   __syncthreads();
@@ -314,7 +312,7 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
   }
   __syncthreads();
   DDQ_STAMP(44);
-  const bool ap = ap0 && !pois && !mbad;
+  const bool ap = ap0 && !pois && mword == 0;
   // dh4 of the workgroup's units: (dQ W5) masked by h4 > 0 (ReLU backward)
   for (int e = lo * kFcN + tid; e < hi * kFcN; e += 512) {
     const int b = e >> 4, n = e & 15;
@@ -359,7 +357,8 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
         const int64_t i = uparam(pq);
         const bool is_bias = head || (q >> 4) == 0;
         c.grad[i] = v;
-        if (ap) {
+        // (b5 -- head -- is read by every workgroup above: K4 updates it)
+        if (ap && !head) {
           float st = (c.aa.rule != 0 && !first) ? csm[CH_PS + 96 + pq] : 0.f;
           const float th = apply_rule(c.aa, first, is_bias, csm[CH_PS + pq], v, st);
           c.at.theta[i] = th;
@@ -1615,8 +1614,8 @@ __device__ __forceinline__ void wg_tile(const WgArgs& a, char* smem, int tile, i
   uint64_t* ctr = reinterpret_cast<uint64_t*>(a.sync) + (L == 1 ? 0 : kT2) + tile;   // at G >= 4)
   const __amdgpu_buffer_rsrc_t rall = __builtin_amdgcn_make_buffer_rsrc(
       slabs + (int64_t)tile * G * SLAB, (short)0, (int)(G * SLAB * 4), 0x00020000);
-  if (e0 >= e1) (void)meet(ctr, G, a.sync + 32);      // an empty slice still arrives
-  bool apt = ap;
+  if (e0 >= e1) meet(ctr, G, a.sync + 32);            // an empty slice still arrives
+  int32_t mword = 0;
   for (int c0 = e0; c0 < e1; c0 += 256 * EPT) {
     int64_t ci_[EPT];
     int le_[EPT];
@@ -1634,7 +1633,8 @@ __device__ __forceinline__ void wg_tile(const WgArgs& a, char* smem, int tile, i
     }
     if (c0 == e0) {
       DDQ_STAMP(SB + 3);
-      apt = ap && !meet(ctr, G, a.sync + 32);
+      meet(ctr, G, a.sync + 32);
+      if (ap) mword = meet_word(a.sync + 32);           // (consumed at the updates)
       DDQ_STAMP(SB + 4);
     }
     // every group's value of every element loaded first (G <= GM), summed in
@@ -1666,7 +1666,8 @@ __device__ __forceinline__ void wg_tile(const WgArgs& a, char* smem, int tile, i
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
       const int e = c0 + tid + 256 * k;
-      if (e < e1 && ci_[k] >= 0) conv_final(a, L, e < ELEMS, ci_[k], le_[k], vs[k], th_[k], st_[k], first, sync, apt);
+      if (e < e1 && ci_[k] >= 0)
+        conv_final(a, L, e < ELEMS, ci_[k], le_[k], vs[k], th_[k], st_[k], first, sync, ap && mword == 0);
     }
   }
   DDQ_STAMP(SB + 5);
@@ -1704,6 +1705,20 @@ __device__ __forceinline__ void w4_apply(const WgArgs& a, int blk, bool first, b
     if (a.aa.rule != 0) *reinterpret_cast<float4*>(a.at.opt + i) = make_float4(st[0], st[1], st[2], st[3]);
     if (sync) *reinterpret_cast<float4*>(a.at.thetaP + i) = t4;
   }
+}
+
+// B <= 32: Q_out's biases from the gradient K2 stored (K2 leaves their update
+// here: every K2 workgroup reads them after its fan-in)
+__device__ __forceinline__ void b5_apply(const WgArgs& a, bool first, bool sync, bool ap) {
+  const int t = threadIdx.x;
+  if (!ap || t >= 4) return;
+  const int64_t i = a.b5_off + t;
+  const float v = a.grad[i];
+  float st = (a.aa.rule != 0 && !first) ? a.at.opt[i] : 0.f;
+  const float th = apply_rule(a.aa, first, true, a.at.theta[i], v, st);
+  a.at.theta[i] = th;
+  if (a.aa.rule != 0) a.at.opt[i] = st;
+  if (sync) a.at.thetaP[i] = th;
 }
 
 // B > 32: the unit sums' partials (K2 upart) summed in chunk order -> db4,
@@ -1753,7 +1768,10 @@ __global__ __launch_bounds__(256) void wgrad16_kernel(const WgArgs a) {
   bid -= n2;
   if (bid >= kW1Blocks) {   // the fc4 weights' (and unit sums') update, then the next
     const int x = bid - kW1Blocks;   // step's gather (B = 256: 512 short blocks, last)
-    if (x < a.nw4) w4_apply(a, x, first, sync, ap);
+    if (x < a.nw4) {
+      w4_apply(a, x, first, sync, ap);
+      if (x == 0 && a.G == 1) b5_apply(a, first, sync, ap);
+    }
     else if (x < a.nw4 + a.nus) units_apply(a, first, sync, ap);
     else prefetch_body(a.pf, x - a.nw4 - a.nus);
     return;
