@@ -3,6 +3,10 @@
 There is no fallback: if the HIP library is missing or fails to load, importing
 the product path raises.  Build it with ``make -C distributed-deep-q_amd`` (or
 ``python -c "import __graft_entry__ as g; g.build()"``).
+
+``load(mode="cpu")`` binds libddq_cpu.so instead: the same C-ABI computed on
+the host (cpu/twin.cpp), the reference's Caffe CPU mode (main.py --mode cpu).
+It is chosen explicitly -- never as a fallback for a missing GPU.
 """
 from __future__ import annotations
 
@@ -15,6 +19,8 @@ import numpy as np
 # path is the in-tree library
 LIB_PATH = os.environ.get("DDQ_LIB_PATH") or \
     os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libddq_hip.so")
+CPU_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libddq_cpu.so")
+MODES = ("gpu", "cpu")
 
 DDQ_OK, DDQ_EINVAL, DDQ_ENOMEM, DDQ_EHIP, DDQ_ERCCL, DDQ_ESTATE, DDQ_ERANGE = 0, -1, -2, -3, -4, -5, -6
 RULES = {"sgd": 0, "rmsprop": 1, "adagrad": 2, "momentum": 3}
@@ -134,14 +140,28 @@ _SIGS = {
 }
 
 EXPORTED = tuple(_SIGS)
-_lib = None
+_lib = None          # the HIP library (mode "gpu")
+_cpu_lib = None      # the CPU twin (mode "cpu")
 
 
-def load(path=LIB_PATH):
-    """Load libddq_hip.so (raises if it is absent -- no CPU fallback)."""
-    global _lib
+def load(path=None, mode="gpu"):
+    """Load libddq_hip.so (raises if it is absent -- no CPU fallback), or with
+    mode="cpu" the CPU twin libddq_cpu.so."""
+    global _lib, _cpu_lib
+    if mode not in MODES:
+        raise ValueError("mode must be one of %s" % (MODES,))
+    if mode == "cpu":
+        if _cpu_lib is not None:
+            return _cpu_lib
+        path = path or CPU_LIB_PATH
+        if not os.path.exists(path):
+            raise ImportError("libddq_cpu.so not found at %s; build it with "
+                              "`make -C distributed-deep-q_amd`" % path)
+        _cpu_lib = _bind(ctypes.CDLL(path))
+        return _cpu_lib
     if _lib is not None:
         return _lib
+    path = path or LIB_PATH
     if not os.path.exists(path):
         raise ImportError("libddq_hip.so not found at %s; build it with "
                           "`make -C distributed-deep-q_amd` (hipcc --offload-arch=gfx950)" % path)
@@ -149,21 +169,24 @@ def load(path=LIB_PATH):
         import torch  # noqa: F401
     except Exception:  # pragma: no cover - torch is plumbing only
         pass
-    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    _lib = _bind(ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL))
+    return _lib
+
+
+def _bind(lib):
     for name, (res, args) in _SIGS.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
     if lib.ddq_abi_version() != ABI_VERSION:
-        raise ImportError("libddq_hip.so ABI %d != binding ABI %d (rebuild)"
-                          % (lib.ddq_abi_version(), ABI_VERSION))
-    _lib = lib
+        raise ImportError("%s ABI %d != binding ABI %d (rebuild)"
+                          % (lib._name, lib.ddq_abi_version(), ABI_VERSION))
     return lib
 
 
-def check(rc, ctx=None):
+def check(rc, ctx=None, lib=None):
     if rc != DDQ_OK:
-        lib = load()
+        lib = lib or load()
         msg = lib.ddq_last_error(ctx)
         raise DDQError(rc, msg.decode() if msg else "")
     return rc

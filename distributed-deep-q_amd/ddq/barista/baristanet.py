@@ -62,9 +62,11 @@ class _Blob:
 
 class BaristaNet:
     def __init__(self, architecture, model, driver, dataset=None, logpath=None,
-                 reset_log=False, device=0):
+                 reset_log=False, device=0, mode="gpu"):
         batch, frame, gamma = parse_architecture(architecture)
-        self.dqn = DeepQNet(batch=batch, frame=frame, device=device, gamma=gamma)
+        # mode: main.py:149-151 caffe.set_mode_gpu / set_mode_cpu
+        self.mode = mode
+        self.dqn = DeepQNet(batch=batch, frame=frame, device=device, gamma=gamma, mode=mode)
         if model is not None and os.path.exists(str(model)):
             with np.load(model, allow_pickle=False) as f:
                 blobs = {k: f[k] for k in f.files}

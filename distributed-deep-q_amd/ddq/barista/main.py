@@ -8,7 +8,9 @@ the forward/backward pass on the GPU, push the Q gradients, reply.
         [--port 50001] [--driver 127.0.0.1:5500|None] [--dataset replay-dataset.hdf5]
         [--dset-size 1000] [--overwrite] [--debug] [--initial-replay 20000]
 
-``--mode`` accepts only ``gpu``: there is no CPU compute path.
+``--mode gpu`` (default) runs libddq_hip.so; ``--mode cpu`` runs the same
+step on the host through the CPU twin libddq_cpu.so (main.py:128,149-151, the
+reference's Caffe CPU mode: BASELINE configs[0]).
 """
 from __future__ import annotations
 
@@ -69,7 +71,7 @@ def get_args(argv=None):
     ap.add_argument("architecture")
     ap.add_argument("model")
     ap.add_argument("--solver", default=None)
-    ap.add_argument("--mode", default="gpu", choices=["gpu"])
+    ap.add_argument("--mode", default="gpu", choices=["gpu", "cpu"])
     ap.add_argument("--port", type=int, default=50001)
     ap.add_argument("--driver", default="127.0.0.1:5500")
     ap.add_argument("--dataset", default="replay-dataset.hdf5")   # main.py:131
@@ -86,9 +88,9 @@ def get_args(argv=None):
 
 def build_worker(args):
     model = None if args.model in ("none", "None") else args.model
-    net = BaristaNet(args.architecture, model, args.driver, logpath=None)
+    net = BaristaNet(args.architecture, model, args.driver, logpath=None, mode=args.mode)
     replay = ReplayDataset(args.dataset, net.state[0].shape, dset_size=args.dset_size,
-                           overwrite=args.overwrite, batch_size=net.batch_size)
+                           overwrite=args.overwrite, batch_size=net.batch_size, mode=args.mode)
     net.add_dataset(replay)
     game = SnakeGame()
     pre = eg.generate_preprocessor(net.state.shape[2:], gray_scale)

@@ -26,12 +26,15 @@ BLOBS = {"Q_out": 4, "P_out": 4, "Q_sa": 1, "P_sa": 1, "target_Q_sa": 1, "loss":
 class DeepQNet:
     """Device-resident deepq network (both towers) + minibatch + replay ring."""
 
-    def __init__(self, batch=32, frame=16, device=0, gamma=GAMMA):
-        self.lib = _lib.load()
+    def __init__(self, batch=32, frame=16, device=0, gamma=GAMMA, mode="gpu"):
+        """mode "gpu": libddq_hip.so on HIP device ``device``; "cpu": the CPU
+        twin libddq_cpu.so (the reference's Caffe CPU mode, no GPU)."""
+        self.mode = mode
+        self.lib = _lib.load(mode=mode)
         self.batch, self.frame, self.device = int(batch), int(frame), int(device)
         desc = _lib.NetDesc(self.batch, self.frame, NFRAME, NUM_ACTIONS, gamma)
         ctx = ctypes.c_void_p()
-        check(self.lib.ddq_create(ctypes.byref(ctx), self.device, ctypes.byref(desc)))
+        check(self.lib.ddq_create(ctypes.byref(ctx), self.device, ctypes.byref(desc)), None, self.lib)
         self.ctx = ctx
         self.num_params = int(self.lib.ddq_num_params(ctx))
         n = _lib._i32()
@@ -49,7 +52,7 @@ class DeepQNet:
 
     # ------------------------------------------------------------------ utils
     def _check(self, rc):
-        return check(rc, self.ctx)
+        return check(rc, self.ctx, self.lib)
 
     def close(self):
         if getattr(self, "ctx", None):

@@ -44,10 +44,10 @@ def get_snapshot_name(iteration):
 class ParamServer:
     def __init__(self, frame=16, batch=32, update="rmsprop", lr=1e-4, rmsprop_decay=0.9,
                  special_update=10, snapshot_freq=500, stats_freq=500, device=0,
-                 on_snapshot=None):
+                 on_snapshot=None, mode="gpu"):
         if update not in ("sgd", "rmsprop", "adagrad"):
             raise ValueError("update must be one of adagrad, rmsprop, sgd")
-        self.net = DeepQNet(batch=batch, frame=frame, device=device)
+        self.net = DeepQNet(batch=batch, frame=frame, device=device, mode=mode)
         self.update = update
         self.learning_rate = float(lr)
         self.rmsprop_decay = float(rmsprop_decay)

@@ -39,7 +39,7 @@ from .net import DeepQNet
 
 class ReplayDataset:
     def __init__(self, filename, state_shape, dset_size=1000, overwrite=False, batch_size=32,
-                 device=0, net=None):
+                 device=0, net=None, mode="gpu"):
         self.filename = filename
         self.state_shape = tuple(int(x) for x in state_shape)
         if len(self.state_shape) != 3 or self.state_shape[0] != 4 or \
@@ -59,7 +59,7 @@ class ReplayDataset:
         self.dset_size = int(dset_size)
         self._net = net if net is not None else DeepQNet(batch=batch_size,
                                                          frame=self.state_shape[1],
-                                                         device=device)
+                                                         device=device, mode=mode)
         self._own_net = net is None
         self._net.replay_create(self.dset_size)
         if loaded is not None:

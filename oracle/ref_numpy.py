@@ -217,10 +217,11 @@ def net_forward(x, p, prefix="Q"):
     B = x.shape[0]
     flat = h.reshape(B, -1)                 # NCHW flatten: c*S4^2 + y*S4 + x
     W4, b4 = p[names[3]]
-    h4 = relu(flat @ W4.reshape(FC4, -1).T + b4.reshape(-1))
+    pre4 = flat @ W4.reshape(FC4, -1).T + b4.reshape(-1)
+    h4 = relu(pre4)
     W5, b5 = p[names[4]]
     out = h4 @ W5.reshape(NUM_ACTIONS, -1).T + b5.reshape(-1)
-    cache.update(flat=flat, h4=h4, out=out)
+    cache.update(flat=flat, pre4=pre4, h4=h4, out=out)
     return cache
 
 
@@ -234,7 +235,7 @@ def route_codes(act, arg):
 
 
 def full_pass(pQ, pP, state, action, reward, next_state, non_terminal, routes=None,
-              return_cache=False):
+              return_cache=False, h4_mask=None):
     """BaristaNet.full_pass (baristanet.py:138-140) = net.forward(); net.backward().
 
     Inputs in the reference's MEMORY_DATA shapes: state/next_state (B,4,S,S),
@@ -267,7 +268,9 @@ def full_pass(pQ, pP, state, action, reward, next_state, non_terminal, routes=No
     h4 = cq["h4"]
     gW5 = dQ.T @ h4
     gb5 = dQ.sum(0)
-    dh4 = (dQ @ W5) * (h4 > 0)                       # IP bottom diff, ReLU mask
+    # IP bottom diff, ReLU mask (h4_mask: an externally decided fc4 ReLU mask,
+    # the parity harness's adoption of the GPU's side of a proven near-tie)
+    dh4 = (dQ @ W5) * ((h4 > 0) if h4_mask is None else h4_mask)
     W4 = pQ[names[3]][0].reshape(FC4, -1)
     flat = cq["flat"]
     gW4 = dh4.T @ flat
@@ -303,7 +306,8 @@ def full_pass(pQ, pP, state, action, reward, next_state, non_terminal, routes=No
     return blobs, grads
 
 
-def magnitudes(pQ, pP, state, action, reward, next_state, non_terminal, routes=None):
+def magnitudes(pQ, pP, state, action, reward, next_state, non_terminal, routes=None,
+               h4_mask=None):
     """Per-element magnitude M of every blob and gradient of ``full_pass``:
     the same computation with every operand replaced by its absolute value
     (|W|, |x|, |b|, |dQ| ...) along the same ReLU / max-pool routing.  M is the
@@ -326,7 +330,7 @@ def magnitudes(pQ, pP, state, action, reward, next_state, non_terminal, routes=N
     cp = net_forward(np.asarray(next_state, np.float64),
                      {k: [np.asarray(w, np.float64) for w in v] for k, v in pP.items()}, "P")
 
-    def fwd_mag(x, pa, cache, prefix, rts):
+    def fwd_mag(x, pa, cache, prefix, rts, m4=None):
         names = layer_names(prefix)
         h = f64(x)
         ins = []
@@ -354,12 +358,14 @@ def magnitudes(pQ, pP, state, action, reward, next_state, non_terminal, routes=N
                 h = np.take_along_axis(win, arg[..., None], -1)[..., 0]
         flat = h.reshape(B, -1)
         W4, b4 = pa[names[3]]
-        mh4 = (flat @ W4.reshape(FC4, -1).T + b4.reshape(-1)) * (cache["h4"] > 0)
+        mh4 = (flat @ W4.reshape(FC4, -1).T + b4.reshape(-1)) * (
+            (cache["h4"] > 0) if m4 is None else m4)
         W5, b5 = pa[names[4]]
         mout = mh4 @ W5.reshape(NUM_ACTIONS, -1).T + b5.reshape(-1)
         return ins, flat, mh4, mout
 
-    insq, mflat, mh4, mQ = fwd_mag(state, pQa, cq, "Q", routes)
+    mask4 = (cq["h4"] > 0) if h4_mask is None else h4_mask
+    insq, mflat, mh4, mQ = fwd_mag(state, pQa, cq, "Q", routes, mask4)
     _, _, _, mP = fwd_mag(next_state, pPa, cp, "P", None)
     Q, P = cq["out"], cp["out"]
     m_qsa = (mQ * act).sum(axis=1)
@@ -378,7 +384,7 @@ def magnitudes(pQ, pP, state, action, reward, next_state, non_terminal, routes=N
     g = collections.OrderedDict()
     gW5 = mdQ.T @ mh4                    # products of magnitudes bound both error terms
     gb5 = mdQ.sum(0)
-    mdh4 = (mdQ @ W5) * (cq["h4"] > 0)
+    mdh4 = (mdQ @ W5) * mask4
     W4 = pQa[names[3]][0].reshape(FC4, -1)
     gW4 = mdh4.T @ mflat
     gb4 = mdh4.sum(0)

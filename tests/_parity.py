@@ -71,13 +71,53 @@ def close(gpu, ref, rtol=RTOL, what="", floor=FLOOR, atol=ATOL, quiet=False, mag
     return max_rel
 
 
-def full_pass_gpu_routing(ref, net, pQ, pP, mb, max_frac=1e-4, tie=2e-5):
+def fc4_near_ties(ref, net, cache, grads, blobs, pQ, mb, g_gpu=None, tie4=1e-6, max_ties=4):
+    """fc4's ReLU (train_val.prototxt:186-191) at a genuine fp32-vs-fp64
+    near-tie: a unit (b, n) whose float64 pre-activation lies within tie4 of
+    its own sum of |terms| of 0 may be live on the GPU and dead in the oracle
+    (or the reverse).  Its side is read off the GPU's fc4 bias gradient
+    (db4[n] = sum_b dh4[b][n]: that unit's dh4 is in it or not -- the two
+    candidates differ by |dQ . W5[:, n]|, far above fp32 rounding) and adopted
+    for that unit only.  Returns (h4 mask or None, adopted count)."""
+    pre4, flat = cache["pre4"], cache["flat"]
+    W4 = np.asarray(pQ["Qfc4"][0], np.float64).reshape(512, -1)
+    b4 = np.asarray(pQ["Qfc4"][1], np.float64).reshape(-1)
+    m4 = np.abs(flat) @ np.abs(W4).T + np.abs(b4)
+    near = np.argwhere((np.abs(pre4) <= tie4 * m4) & (m4 > 0))   # (exact zeros agree)
+    if len(near) == 0:
+        return None, 0
+    assert len(near) <= max_ties, ("too many fc4 near-ties", len(near))
+    if g_gpu is None:
+        g_gpu = net.get_grads_flat()
+    db4_gpu = np.asarray(net.split(g_gpu, "Q")["Qfc4"][1], np.float64).reshape(-1)
+    db4_ref = np.asarray(grads["Qfc4"][1], np.float64).reshape(-1)
+    B = pre4.shape[0]
+    act = np.asarray(mb[1], np.float64).reshape(B, 4)
+    dq = act * ((blobs["Q_sa"] - blobs["target_Q_sa"]) / B)[:, None]
+    W5 = np.asarray(pQ["Q_out"][0], np.float64).reshape(4, 512)
+    full = dq @ W5                                   # dh4 before the ReLU mask
+    mask = pre4 > 0
+    adopted = 0
+    for (b, n) in near:
+        d = full[b, n] * (-1.0 if mask[b, n] else 1.0)   # what flipping does to db4[n]
+        if abs(db4_gpu[n] - (db4_ref[n] + d)) < abs(db4_gpu[n] - db4_ref[n]):
+            mask[b, n] = not mask[b, n]
+            db4_ref = db4_ref.copy()
+            db4_ref[n] += d
+            adopted += 1
+    return (mask if adopted else None), adopted
+
+
+def full_pass_gpu_routing(ref, net, pQ, pP, mb, max_frac=1e-4, tie=2e-5, g_gpu=None,
+                          with_mask=False):
     """The oracle's full pass on minibatch ``mb`` with max-pool routing taken
     from the GPU's last forward (``net.pool_mask``) wherever the two differ --
     and only there, after proving every difference is a genuine fp32-vs-fp64
     near-tie: both candidate values (or the max vs 0 for a ReLU'd window)
     agree to ``tie`` of the layer's activation scale, and at most ``max_frac``
-    of the windows differ.  Returns (blobs, grads, n_ties)."""
+    of the windows differ -- and fc4's ReLU mask likewise at proven near-ties
+    (fc4_near_ties).  Returns (blobs, grads, n_ties) (+ the fc4 mask with
+    with_mask)."""
     blobs, grads, cache = ref.full_pass(pQ, pP, *mb, return_cache=True)
     routes, nties = {}, 0
     for i in (1, 2, 3):
@@ -99,6 +139,12 @@ def full_pass_gpu_routing(ref, net, pQ, pP, mb, max_frac=1e-4, tie=2e-5):
         routes[i] = g_code
     if nties:
         blobs, grads = ref.full_pass(pQ, pP, *mb, routes=routes)
+    h4_mask, n4 = fc4_near_ties(ref, net, cache, grads, blobs, pQ, mb, g_gpu)
+    if n4:
+        blobs, grads = ref.full_pass(pQ, pP, *mb, routes=routes, h4_mask=h4_mask)
+        nties += n4
+    if with_mask:
+        return blobs, grads, nties, h4_mask
     return blobs, grads, nties
 
 
@@ -106,9 +152,10 @@ def check_full_pass(ref, net, pQ, pP, mb, grads_gpu=None, quiet=False, what=""):
     """Blobs and Q gradients of the GPU's last forward/backward on ``mb``
     against the oracle (GPU routing at proven near-ties), each element within
     rtol 1e-4 + COND (2e-7) * (its sum of |terms|).  Returns the near-tie count."""
-    blobs, grads, nties = full_pass_gpu_routing(ref, net, pQ, pP, mb)
+    blobs, grads, nties, h4_mask = full_pass_gpu_routing(ref, net, pQ, pP, mb, g_gpu=grads_gpu,
+                                                         with_mask=True)
     routes = {i: net.pool_mask(i) for i in (1, 2, 3)}
-    mblobs, mgrads = ref.magnitudes(pQ, pP, *mb, routes=routes)
+    mblobs, mgrads = ref.magnitudes(pQ, pP, *mb, routes=routes, h4_mask=h4_mask)
     B = net.batch
     for name, shape in (("Q_out", (B, 4)), ("P_out", (B, 4)), ("Q_sa", (B,)), ("P_sa", (B,)),
                         ("target_Q_sa", (B,))):
