@@ -2006,8 +2006,12 @@ void small_groups(int B, int* G2, int* G3) {
 
 // K4's dynamic LDS (launch_small_bwd)
 static int wgrad16_lds() {
+  // (the staging buffers; the cross-wave sums of a tile's NT accumulators
+  // and, with one group, the tile's sums)
+  constexpr int NT2 = 5, NT3 = 6;
   return std::max({2 * sm16::Wg2::BUF * 2, 2 * sm16::Wg3::BUF * 2,
-                   4 * 16 * 64 * 4 + sm16::Wg3::SLAB * 4}) + 16;
+                   NT2 * 4 * 16 * 64 * 4 + sm16::Wg2::SLAB * 4,
+                   NT3 * 4 * 16 * 64 * 4 + sm16::Wg3::SLAB * 4}) + 16;
 }
 
 hipError_t small_coresident(int B, int* ok, char* why, int nwhy) {

@@ -1263,7 +1263,8 @@ struct Wg16 {
   static constexpr int VIN = NI * 3 * HW * HW * (CIN / 8);
   static constexpr int VD = NI * 3 * NPX * 4;
   static constexpr int PIN = (VIN + 255) / 256, PD = (VD + 255) / 256;
-  static constexpr int kSmem = (2 * BUF * 2 > 4 * 16 * 64 * 4 ? 2 * BUF * 2 : 4 * 16 * 64 * 4) + 16;
+  static constexpr int RED = NT * 4 * 16 * 64 * 4 + SLAB * 4;   // the tile sums (wg_tile)
+  static constexpr int kSmem = (2 * BUF * 2 > RED ? 2 * BUF * 2 : RED) + 16;
 };
 using Wg2 = Wg16<32, 5, 8>;
 using Wg3 = Wg16<64, 3, 4>;
@@ -1554,27 +1555,32 @@ __device__ __forceinline__ void wg_tile(const WgArgs& a, char* smem, int tile, i
     }
   }
   DDQ_STAMP(SB + 2);
-  // ---- the waves' tiles summed in fixed order -> LDS (G == 1) or the slab ----
-  float* red = reinterpret_cast<float*>(smem);        // [4 waves][16][64]
-  float* fin = red + 4 * 16 * 64;                     // G == 1: the tile's sums [SLAB]
+  // ---- the waves' tiles summed in fixed order -> LDS (G == 1) or the slab:
+  // every accumulator of every wave into LDS at once (the staging buffers are
+  // dead), one barrier, then each thread's 4-wave sums of all NT tiles ----
+  float* red = reinterpret_cast<float*>(smem);        // [NT][4 waves][16][64]
+  float* fin = red + NT * 4 * 16 * 64;                // G == 1: the tile's sums [SLAB]
   float* slab = slabs + ((int64_t)tile * G + g) * SLAB;
   const __amdgpu_buffer_rsrc_t srs = wt_rsrc(slab, (uint32_t)(SLAB * 4));
+  __syncthreads();                                    // (bias slice sums read above)
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    __syncthreads();
+  for (int t = 0; t < NT; ++t)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) red[(wid * 16 + r) * 64 + lane] = acc[t][r];
-    __syncthreads();
-    {   // thread = (tile row r, lanes 4q..4q+3)
-      const int r = tid >> 4, l0 = 4 * (tid & 15);
-      const int e = r * 64 + l0;
-      const float4 a0 = *reinterpret_cast<const float4*>(red + e);
-      const float4 a1 = *reinterpret_cast<const float4*>(red + 1024 + e);
-      const float4 a2 = *reinterpret_cast<const float4*>(red + 2048 + e);
-      const float4 a3 = *reinterpret_cast<const float4*>(red + 3072 + e);
+    for (int r = 0; r < 16; ++r) red[((t * 4 + wid) * 16 + r) * 64 + lane] = acc[t][r];
+  __syncthreads();
+  {   // thread = (tile row r, lanes 4q..4q+3)
+    const int r = tid >> 4, l0 = 4 * (tid & 15);
+    const int e = r * 64 + l0;
+    const int co = (r & 3) + 8 * (r >> 2) + 4 * (l0 >> 5);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const float* rt = red + t * 4096 + e;
+      const float4 a0 = *reinterpret_cast<const float4*>(rt);
+      const float4 a1 = *reinterpret_cast<const float4*>(rt + 1024);
+      const float4 a2 = *reinterpret_cast<const float4*>(rt + 2048);
+      const float4 a3 = *reinterpret_cast<const float4*>(rt + 3072);
       const float4 v = make_float4((a0.x + a1.x) + (a2.x + a3.x), (a0.y + a1.y) + (a2.y + a3.y),
                                    (a0.z + a1.z) + (a2.z + a3.z), (a0.w + a1.w) + (a2.w + a3.w));
-      const int co = (r & 3) + 8 * (r >> 2) + 4 * (l0 >> 5);
       const int kk = t / W::NCB, c = t % W::NCB;
       const int o = (co * KX + kk) * W::CIN + 32 * c + (l0 & 31);
       if (G == 1) *reinterpret_cast<float4*>(fin + o) = v;

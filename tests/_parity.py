@@ -71,10 +71,11 @@ def close(gpu, ref, rtol=RTOL, what="", floor=FLOOR, atol=ATOL, quiet=False, mag
     return max_rel
 
 
-def fc4_near_ties(ref, net, cache, grads, blobs, pQ, mb, g_gpu=None, tie4=1e-6, max_ties=4):
+def fc4_near_ties(ref, net, cache, grads, blobs, pQ, mb, g_gpu=None, tie4=COND, max_frac=1e-4):
     """fc4's ReLU (train_val.prototxt:186-191) at a genuine fp32-vs-fp64
     near-tie: a unit (b, n) whose float64 pre-activation lies within tie4 of
-    its own sum of |terms| of 0 may be live on the GPU and dead in the oracle
+    its own sum of |terms| (COND: the fp32 rounding bound of the blobs) of 0
+    may be live on the GPU and dead in the oracle
     (or the reverse).  Its side is read off the GPU's fc4 bias gradient
     (db4[n] = sum_b dh4[b][n]: that unit's dh4 is in it or not -- the two
     candidates differ by |dQ . W5[:, n]|, far above fp32 rounding) and adopted
@@ -86,7 +87,7 @@ def fc4_near_ties(ref, net, cache, grads, blobs, pQ, mb, g_gpu=None, tie4=1e-6, 
     near = np.argwhere((np.abs(pre4) <= tie4 * m4) & (m4 > 0))   # (exact zeros agree)
     if len(near) == 0:
         return None, 0
-    assert len(near) <= max_ties, ("too many fc4 near-ties", len(near))
+    assert len(near) <= max(4, max_frac * pre4.size), ("too many fc4 near-ties", len(near))
     if g_gpu is None:
         g_gpu = net.get_grads_flat()
     db4_gpu = np.asarray(net.split(g_gpu, "Q")["Qfc4"][1], np.float64).reshape(-1)
