@@ -206,14 +206,17 @@ void tower_fwd(ddq_ctx* c, int z, const float* frames, int B) {
 }
 
 // ---- backward (Q tower) ----
-// gW[co][ci][ky][kx] = sum_{b,y,x} d[b][co][y][x] in[b][ci][y+ky-p][x+kx-p]; gb[co] = sum d
+// gW[co][ci][ky][kx] = sum_{b,y,x} d[b][co][y][x] in[b][ci][y+ky-p][x+kx-p]; gb[co] = sum d.
+// Per (co, ci) the products accumulate elementwise into one double row per
+// tap ([tap][x]: independent lanes, so the inner loop vectorises), summed
+// over x at the end.
 void conv_wgrad(const float* in, const float* d, int B, int H, const Conv& cv, float* gW,
                 float* gb) {
   const int k = cv.k, p = cv.pad, HW = H * H;
 #pragma omp parallel for collapse(2) schedule(dynamic)
   for (int co = 0; co < cv.cout; ++co)
     for (int ci = 0; ci < cv.cin; ++ci) {
-      std::vector<double> acc((size_t)k * k, 0.0);
+      std::vector<double> acc((size_t)k * k * H, 0.0);
       for (int b = 0; b < B; ++b) {
         const float* src = in + ((size_t)b * cv.cin + ci) * HW;
         const float* dd = d + ((size_t)b * cv.cout + co) * HW;
@@ -221,17 +224,20 @@ void conv_wgrad(const float* in, const float* d, int B, int H, const Conv& cv, f
           for (int kx = 0; kx < k; ++kx) {
             const int y0 = std::max(0, p - ky), y1 = std::min(H, H + p - ky);
             const int x0 = std::max(0, p - kx), x1 = std::min(H, H + p - kx);
-            double a = 0.0;
+            double* a = acc.data() + (size_t)(ky * k + kx) * H;
             for (int y = y0; y < y1; ++y) {
               const float* row = src + (y + ky - p) * H + (kx - p);
               const float* dr = dd + y * H;
-              for (int x = x0; x < x1; ++x) a += (double)dr[x] * row[x];
+              for (int x = x0; x < x1; ++x) a[x] += (double)dr[x] * row[x];
             }
-            acc[ky * k + kx] += a;
           }
       }
       float* g = gW + ((size_t)co * cv.cin + ci) * k * k;
-      for (int i = 0; i < k * k; ++i) g[i] = (float)acc[i];
+      for (int t = 0; t < k * k; ++t) {
+        double v = 0.0;
+        for (int x = 0; x < H; ++x) v += acc[(size_t)t * H + x];
+        g[t] = (float)v;
+      }
     }
 #pragma omp parallel for schedule(static)
   for (int co = 0; co < cv.cout; ++co) {
