@@ -40,8 +40,10 @@ constexpr int CH_WS = 0;
 constexpr int CH_XS = CH_WS + 2 * kFcN * kXP;
 constexpr int CH_RED = CH_XS + 2 * kBC * kXP;
 constexpr int CH_H = CH_RED + 3 * 2 * 4 * 64;   // (k parts - 1 + tower slot) x half
-constexpr int CH_DH = CH_H + kMaxB * kFcN;
-constexpr int CH_QP = CH_DH + kMaxB * kFcN;
+constexpr int kHS = 18;                           // H / DH row stride: conflict-free operand
+                                                  // reads (rows 18 floats apart, 64 banks)
+constexpr int CH_DH = CH_H + kMaxB * kHS;
+constexpr int CH_QP = CH_DH + kMaxB * kHS;
 constexpr int CH_DQ = CH_QP + 2 * kMaxB * 4;
 constexpr int CH_TMP = CH_DQ + kMaxB * 4;          // squared errors [kMaxB]
 constexpr int CH_W5 = CH_TMP + kMaxB;             // Q's Q_out columns of the units [4][16]
@@ -252,7 +254,7 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
           wt_store4(rq, (uint32_t)((((jb * 2 + wz) * B + b) * 4) * 4), make_float4(q[0], q[1], q[2], q[3]));
         if (wz == 0)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) H[b * kFcN + 4 * kq + i] = hv[i];
+          for (int i = 0; i < 4; ++i) H[b * kHS + 4 * kq + i] = hv[i];
       }
     }
   }
@@ -315,11 +317,11 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
   const bool ap = ap0 && !pois && mword == 0;
   // dh4 of the workgroup's units: (dQ W5) masked by h4 > 0 (ReLU backward)
   for (int e = lo * kFcN + tid; e < hi * kFcN; e += 512) {
-    const int b = e >> 4, n = e & 15;
+    const int b = e >> 4, n = e & 15, eh = b * kHS + n;
     const float* w5 = csm + CH_W5 + n;
     const float* dq = DQ + b * 4;
     const float v = dq[0] * w5[0] + dq[1] * w5[16] + dq[2] * w5[32] + dq[3] * w5[48];
-    DH[e] = H[e] > 0.f ? v : 0.f;
+    DH[eh] = H[eh] > 0.f ? v : 0.f;
   }
   __syncthreads();
   DDQ_STAMP(45);
@@ -338,9 +340,9 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
       } else {
         const int r = q >> 4, n = q & 15;            // r 0: db4, 1..4: dW5[r - 1]
         if (r == 0) {
-          for (int b = lo + r4; b < hi; b += 4) v += DH[b * kFcN + n];
+          for (int b = lo + r4; b < hi; b += 4) v += DH[b * kHS + n];
         } else {
-          for (int b = lo + r4; b < hi; b += 4) v += DQ[b * 4 + r - 1] * H[b * kFcN + n];
+          for (int b = lo + r4; b < hi; b += 4) v += DQ[b * 4 + r - 1] * H[b * kHS + n];
         }
       }
     }
@@ -396,7 +398,7 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int b = 4 * q + kq;
-        av8[q] = b < nb ? DH[(bb0 + b) * kFcN + lr] : 0.f;
+        av8[q] = b < nb ? DH[(bb0 + b) * kHS + lr] : 0.f;
 #pragma unroll
         for (int u = 0; u < 2; ++u) bv8[q][u] = XS[b * kXP + 16 * (2 * wid + u) + lr];
       }
@@ -417,7 +419,7 @@ __global__ __launch_bounds__(512) void fc4_chain16_kernel(const ChainArgs c) {
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const int n = 4 * s + kq;
-        dav[u][s] = b < hi ? DH[b * kFcN + n] : 0.f;
+        dav[u][s] = b < hi ? DH[b * kHS + n] : 0.f;
         dbv[u][s] = WS[n * kXP + 16 * kb + lr];
       }
     }
