@@ -1774,10 +1774,6 @@ __global__ __launch_bounds__(256) void wgrad16_kernel(const WgArgs a) {
     return;
   }
   bid -= n2;
-#ifdef DDQ_T_DELAY
-  // (experiment: the streaming blocks start after the tiles' first loads)
-  for (int i = 0; i < DDQ_T_DELAY; ++i) __builtin_amdgcn_s_sleep(63);
-#endif
   if (bid >= kW1Blocks) {   // the fc4 weights' (and unit sums') update, then the next
     const int x = bid - kW1Blocks;   // step's gather (B = 256: 512 short blocks, last)
     if (x < a.nw4) {
