@@ -274,9 +274,11 @@ int ddq_create(ddq_ctx** out, int device, const ddq_net_desc* desc) {
       TRY(dalloc(c, &nb.h4[z], (size_t)B * 512));
       TRY(dalloc(c, &nb.theta[z], (size_t)P + kShardPad));
       TRY(dalloc(c, &nb.wks[z], (size_t)3 * nb.L.wks_total));   // zero: conv1's kx 7 stays 0
-      TRY(dalloc(c, &nb.pool1s[z], (size_t)3 * B * S2 * S2 * 32));
-      TRY(dalloc(c, &nb.pool2s[z], (size_t)3 * B * S3 * S3 * 64));
+      TRY(dalloc(c, &nb.pool1f[z], (size_t)B * S2 * S2 * 32));
+      TRY(dalloc(c, &nb.pool2f[z], (size_t)B * S3 * S3 * 64));
     }
+    TRY(dalloc(c, &nb.pool1s[0], (size_t)3 * B * S2 * S2 * 32));   // Q tower only
+    TRY(dalloc(c, &nb.pool2s[0], (size_t)3 * B * S3 * S3 * 64));
     TRY(dalloc(c, &nb.mask1, (size_t)B * S2 * S2 * 32));
     TRY(dalloc(c, &nb.mask2, (size_t)B * S3 * S3 * 64));
     TRY(dalloc(c, &nb.mask3, (size_t)B * S4 * S4 * 64));

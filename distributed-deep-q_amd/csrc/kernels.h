@@ -54,10 +54,14 @@ struct NetBuffers {
   float *state, *next_state, *action, *reward, *nonterm;
   int32_t* idx;
   // activations per tower z (0 = Q on state, 1 = P on next_state): pool1 /
-  // pool2 only split (split.h: the next conv and the Q weight gradients read
-  // them split), pool3 fp32 in Caffe order (fc4's input)
+  // pool2 in one buffer each, sized for their split form (3 bf16 planes,
+  // NHWC) -- the S = 16 small-map step keeps the Q tower's split there (its K4
+  // reads them split); the general kernels keep fp32 NHWC in the same bytes
+  // (pool1f / pool2f: the next conv and the Q weight gradients split them
+  // while staging); pool3 fp32 in Caffe order (fc4's input)
   float *pool3[2], *h4[2];
-  __bf16 *pool1s[2], *pool2s[2];    // split pool1 / pool2 (3 planes, NHWC)
+  __bf16 *pool1s[2], *pool2s[2];    // split pool1 / pool2 (3 planes, NHWC): small-map step
+  float *pool1f[2], *pool2f[2];     // the same bytes, fp32 NHWC: general kernels
   uint8_t *mask1, *mask2, *mask3;   // Q tower only
   float* fc4_part;                  // [splits][2][B][512]
   int fc4_splits;

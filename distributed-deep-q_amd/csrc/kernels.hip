@@ -1426,7 +1426,9 @@ __global__ __launch_bounds__(256, 4) void wgrad_reduce_kernel(
     return;
   }
   bid -= fat.nfa;
-  const WredDims& d = bid >= d1.blk0 ? d1 : (bid >= d2.blk0 ? d2 : d0);
+  // (by value: a reference to a runtime-chosen kernel argument put the
+  // three in scratch memory)
+  const WredDims d = bid >= d1.blk0 ? d1 : (bid >= d2.blk0 ? d2 : d0);
   if (d.G == 1)
     wred_block<1>(part, grad, d, bid - d.blk0, red, rest, fat, faa);
   else if (d.G == 2)
@@ -1871,17 +1873,17 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
   if (!tower && (!nb.fwd_only || nb.fwd_only == 1)) {
     // conv1 (train_val.prototxt:39-78): bf16 matrix cores, fp32-exact
     // (split.h): frames are exact in bf16, so 3 MFMAs per 32x32x16 block; the
-    // pooled output goes out split (conv2's input) and, for the Q tower, fp32
-    // (conv2's weight gradient)
+    // pooled output goes out fp32 NHWC (conv2 splits it while staging and
+    // writes the Q tower's split for conv2's weight gradient)
     Conv1Args c1{};
     c1.B = B; c1.H = S; c1.W = S;
     for (int z = 0; z < 2; ++z) {
       c1.in[z] = in[z];
       c1.wk[z] = nb.wks[z] + L.wks_off[0];
       c1.bias[z] = nb.theta[z] + L.b[0];
-      c1.out_split[z] = nb.pool1s[z];
+      c1.out[z] = nb.pool1f[z];
     }
-    c1.out[0] = c1.out[1] = nullptr;   // conv2 and conv2's weight gradient read it split
+    c1.out_split[0] = c1.out_split[1] = nullptr;
     c1.out_elems = (int64_t)B * (S / 2) * (S / 2) * 32;
     c1.mask[0] = nb.mask1; c1.mask[1] = nullptr;
     M("conv1_fwd");
@@ -1894,14 +1896,14 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     SplitArgs a2{};
     a2.B = B; a2.H = H; a2.W = H; a2.pad = 2;
     for (int z = 0; z < 2; ++z) {
-      a2.in[z] = nb.pool1s[z];
+      a2.in32[z] = nb.pool1f[z];
       a2.wk[z] = nb.wks[z] + L.wks_off[1];
       a2.bias[z] = nb.theta[z] + L.b[1];
-      a2.out_split[z] = nb.pool2s[z];
+      a2.out[z] = nb.pool2f[z];   // fp32 NHWC (conv3 splits it while staging)
     }
-    a2.in_elems = (int64_t)B * H * H * 32;
     a2.wk_elems = L.wks_total;
-    a2.out[0] = a2.out[1] = nullptr;   // conv3 and conv3's weight gradient read it split
+    // the Q tower's staged input, split, for conv2's weight gradient
+    a2.xsplit = nb.pool1s[0]; a2.x_elems = (int64_t)B * H * H * 32;
     a2.out_elems = (int64_t)B * (H / 2) * (H / 2) * 64;
     a2.mask[0] = nb.mask2; a2.mask[1] = nullptr;
     M("conv2_fwd");
@@ -1915,12 +1917,12 @@ hipError_t launch_forward(const NetBuffers& nb, int nz, hipStream_t s,
     SplitArgs a3{};
     a3.B = B; a3.H = H; a3.W = H; a3.pad = 1;
     for (int z = 0; z < 2; ++z) {
-      a3.in[z] = nb.pool2s[z];
+      a3.in32[z] = nb.pool2f[z];
       a3.wk[z] = nb.wks[z] + L.wks_off[2];
       a3.bias[z] = nb.theta[z] + L.b[2];
       a3.out[z] = nb.pool3[z];
     }
-    a3.in_elems = (int64_t)B * H * H * 64;
+    a3.xsplit = nb.pool2s[0]; a3.x_elems = (int64_t)B * H * H * 64;   // (conv3's weight gradient)
     a3.wk_elems = L.wks_total;
     a3.nchw = 1;
     a3.mask[0] = nb.mask3; a3.mask[1] = nullptr;
@@ -2290,7 +2292,10 @@ hipError_t launch_act(const NetBuffers& nb, const float* in, int n, float* pool3
   a.next_state = const_cast<float*>(in);
   a.pool3[0] = pool3; a.h4[0] = h4;
   a.pool3[1] = pool3; a.h4[1] = h4;
-  a.pool1s[0] = a.pool1s[1] = pool1s; a.pool2s[0] = a.pool2s[1] = pool2s;
+  // (no weight gradient: no split side outputs; the scratch holds fp32)
+  a.pool1s[0] = a.pool1s[1] = nullptr; a.pool2s[0] = a.pool2s[1] = nullptr;
+  a.pool1f[0] = a.pool1f[1] = reinterpret_cast<float*>(pool1s);
+  a.pool2f[0] = a.pool2f[1] = reinterpret_cast<float*>(pool2s);
   a.mask1 = a.mask2 = a.mask3 = nullptr;
   a.fc4_part = part;
   a.q_out = qout; a.p_out = qout;

@@ -18,10 +18,11 @@
 // same per-element bound as the f32 MFMA path (tests/_parity.py).
 //
 // Storage: a "split tensor" of E elements is 3 bf16 planes of E (plane p at
-// +p*E), each in the layout of the fp32 tensor it stands for.  Producers
-// split once in their epilogue (activations: the pool epilogue; gradients:
-// the dgrad epilogue; weights: the apply / relayout) so the MFMA loops only
-// load: no conversion in any K loop.
+// +p*E), each in the layout of the fp32 tensor it stands for.  Gradients are
+// split once by their producer (the dgrad epilogue), weights by the apply /
+// relayout; activations travel as fp32 (4 bytes a value instead of 6 through
+// HBM) and are split while a consumer stages them into LDS.  Either way the
+// MFMA loops only load: no conversion in any K loop.
 //
 // Direct convolution (fwd and dgrad), one workgroup = one image b x a TY x TX
 // tile of output pixels x all N output channels, as in direct.h: the halo
@@ -88,6 +89,21 @@ __device__ __forceinline__ void route_keep(uint32_t mw, uint32_t q4, uint32_t& k
   const uint32_t kb = (nz ^ 0x01010101u) * 0xFFu;                 // 0xFF iff routed to q
   k01 = __builtin_amdgcn_perm(kb, kb, 0x01010000u);
   k23 = __builtin_amdgcn_perm(kb, kb, 0x03030202u);
+}
+
+// The split planes of 8 consecutive fp32 values (a: values 0..3, b: 4..7) as
+// three 16-byte vectors of bf16 pairs (v[p] = plane p; pair e = values 2e, 2e+1)
+__device__ __forceinline__ void split_pack8(const float4& a, const float4& b, u32x4 (&v)[3]) {
+  const float x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    __bf16 h0, m0, l0, h1, m1, l1;
+    split3(x[2 * e], h0, m0, l0);
+    split3(x[2 * e + 1], h1, m1, l1);
+    v[0][e] = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+    v[1][e] = (uint32_t)__builtin_bit_cast(uint16_t, m0) | ((uint32_t)__builtin_bit_cast(uint16_t, m1) << 16);
+    v[2][e] = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+  }
 }
 
 // Store the split of v at element e of a split tensor of E elements.
@@ -230,8 +246,10 @@ struct SplitArgs {
   int B, H, W;               // conv grid (stride 1, same padding)
   int tiles_x;
   int pad;
-  const __bf16* in[2];       // split NHWC (B,H,W,CPT); dgrad pooled: (B,H/2,W/2,CPT)
+  const __bf16* in[2];       // dgrad: split pooled NHWC (B,H/2,W/2,CPT)
   int64_t in_elems;          // E of the input split tensor
+  const float* in32[2];      // fwd: the input activations, fp32 NHWC (B,H,W,CPT), split
+                             // while staged
   const __bf16* wk[2];       // split weights [n][tap][CPT] (dgrad: transposed + flipped)
   int64_t wk_elems;          // E of the weight split tensor (plane stride)
   const float* bias[2];      // fwd
@@ -246,9 +264,9 @@ struct SplitArgs {
   float* pd;                 // dgrad: fp32 gradient of the previous pool output (nullable)
   __bf16* pd_split;          // dgrad: split gradient of the previous pool output (nullable)
   int64_t pd_elems;
-  __bf16* xsplit;            // dgrad, one channel chunk: the staged source expanded and
-  int64_t x_elems;           // split, NHWC (B,H,W,CPT), written once (nullable) -- the
-                             // layer's weight gradient then copies rows (wgrads DSRC 2)
+  __bf16* xsplit;            // one channel chunk: the staged source split (dgrad: expanded),
+  int64_t x_elems;           // NHWC (B,H,W,CPT), written once (nullable; fwd: tower 0 only)
+                             // -- the layer's weight gradient reads it (wgrads)
   // conv2's data gradient only (N = 32): conv1's weight gradient fused in
   // (w1_tile_wgrad) -- w1_part non-null turns it on
   const uint8_t* w1_route;   // pool1's routing bytes, NHWC (B,H,W,32): the dgrad's grid
@@ -420,13 +438,13 @@ __device__ __forceinline__ void split_epilogue_fwd_lds(const SplitArgs& a,
         const int pyy = y0 / 2 + win / (TX / 2), pxx = x0 / 2 + win % (TX / 2);
         if (pyy < Hp && pxx < Wp) outz[(((size_t)b * N + n) * Hp + pyy) * Wp + pxx] = fv[win * N + n];
       }
-    } else {
+    } else {   // NHWC (the next layer's input: conv1 / conv2), write-through as above
+      const __amdgpu_buffer_rsrc_t ro = wt_rsrc(outz, (uint32_t)(a.out_elems * 4));
       for (int f = tid; f < NWIN * (N / 4); f += NT) {
         const int win = f / (N / 4), c = f % (N / 4);
         int off;
         if (pix(win, off))
-          *reinterpret_cast<float4*>(outz + (size_t)off * N + 4 * c) =
-              *reinterpret_cast<const float4*>(fv + win * N + 4 * c);
+          wt_store4(ro, (uint32_t)((off * N + 4 * c) * 4), *reinterpret_cast<const float4*>(fv + win * N + 4 * c));
       }
     }
   }
@@ -762,6 +780,8 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
   constexpr int NV = C::PH * C::PW * (CP / 8);             // 16-byte vectors per plane
   constexpr int NIT = (3 * NV + C::kThreads - 1) / C::kThreads;
   constexpr int BAT = NIT < 8 ? NIT : 8;
+  constexpr int NIT1 = (NV + C::kThreads - 1) / C::kThreads;   // fp32 items (one per vector)
+  constexpr int BAT1 = NIT1 < 4 ? NIT1 : 4;
   auto patch_load = [&](int ch, int i0, u32x4 (&v)[BAT], int (&dst)[BAT]) {
 #pragma unroll
     for (int u = 0; u < BAT; ++u) {
@@ -782,24 +802,20 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
       // bounds-checked buffer loads: outside the image (or past the
       // items) the offset is out of range and the vector reads 0 -- no
       // branch, select or 64-bit address per vector
-      if (DGRAD) {   // pooled source: expand through the routing bytes
-        const uint32_t o = (uint32_t)(((b * (a.H >> 1) + (gy >> 1)) * (a.W >> 1) + (gx >> 1)) * CPT +
-                                      ch * CP + 8 * c8);
-        const u32x4 uw = __builtin_bit_cast(
-            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rin, (int)(in_img ? (p * (uint32_t)a.in_elems + o) * 2 : kOOB), 0, 0));
-        const u32x2 m = __builtin_bit_cast(
-            u32x2, __builtin_amdgcn_raw_buffer_load_b64(rroute, (int)(in_img ? o : kOOB), 0, 0));
-        const uint32_t q4 = ((((gy & 1) << 1) | (gx & 1))) * 0x01010101u;
-        uint32_t k[4];   // bf16 pair e = channels 2e, 2e+1 (zeros route nothing)
-        route_keep(m[0], q4, k[0], k[1]);
-        route_keep(m[1], q4, k[2], k[3]);
+      // (the data gradient's pooled split source, expanded through the
+      // routing bytes; the forward stages fp32: stage_patch_x32)
+      const uint32_t o = (uint32_t)(((b * (a.H >> 1) + (gy >> 1)) * (a.W >> 1) + (gx >> 1)) * CPT +
+                                    ch * CP + 8 * c8);
+      const u32x4 uw = __builtin_bit_cast(
+          u32x4, __builtin_amdgcn_raw_buffer_load_b128(rin, (int)(in_img ? (p * (uint32_t)a.in_elems + o) * 2 : kOOB), 0, 0));
+      const u32x2 m = __builtin_bit_cast(
+          u32x2, __builtin_amdgcn_raw_buffer_load_b64(rroute, (int)(in_img ? o : kOOB), 0, 0));
+      const uint32_t q4 = ((((gy & 1) << 1) | (gx & 1))) * 0x01010101u;
+      uint32_t k[4];   // bf16 pair e = channels 2e, 2e+1 (zeros route nothing)
+      route_keep(m[0], q4, k[0], k[1]);
+      route_keep(m[1], q4, k[2], k[3]);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[u][e] = uw[e] & k[e];
-      } else {
-        const uint32_t o = (uint32_t)(((b * a.H + gy) * a.W + gx) * CPT + ch * CP + 8 * c8);
-        v[u] = __builtin_bit_cast(
-            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rin, (int)(in_img ? (p * (uint32_t)a.in_elems + o) * 2 : kOOB), 0, 0));
-      }
+      for (int e = 0; e < 4; ++e) v[u][e] = uw[e] & k[e];
     }
   };
   auto patch_store = [&](__bf16* buf, const u32x4 (&v)[BAT], const int (&dst)[BAT]) {
@@ -807,7 +823,7 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
     for (int u = 0; u < BAT; ++u)
       if (dst[u] >= 0) *reinterpret_cast<u32x4*>(buf + dst[u]) = v[u];
   };
-  auto stage_patch_split = [&](int ch) {
+  auto stage_patch_split = [&](int ch) {   // (DGRAD)
 #pragma unroll
     for (int i0 = 0; i0 < NIT; i0 += BAT) {
       u32x4 v[BAT];
@@ -878,8 +894,48 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
       }
     }
   };
+  // forward: the fp32 activations, an (pixel, 8-channel) item = two 16-byte
+  // loads, split (split_pack8) and stored as three plane vectors -- 4 bytes
+  // a value through HBM instead of the 6 of a split source, and the producer
+  // writes 4 instead of 6 (conv1 / conv2 forward epilogues)
+  const __amdgpu_buffer_rsrc_t rin32 = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(z ? a.in32[1] : a.in32[0]), (short)0, (int)(DGRAD ? 0u : src_elems * 4), 0x00020000);
+  auto stage_patch_x32 = [&](int ch) {
+#pragma unroll
+    for (int i0 = 0; i0 < NIT1; i0 += BAT1) {
+      float4 f[BAT1][2];
+      int dst[BAT1];
+#pragma unroll
+      for (int u = 0; u < BAT1; ++u) {
+        const int f0 = tid + (i0 + u) * C::kThreads;
+        const bool live = i0 + u < NIT1 && f0 < NV;
+        const int r = live ? f0 : 0;
+        const int pix0 = r / (CP / 8), c8 = r % (CP / 8);
+        constexpr int NPX = C::PH * C::PW;
+        const int pix = pix0 < (NPX & ~7) ? pair_rows<CP, C::CS>(pix0) : pix0;   // (patch_load)
+        const int py = pix / C::PW, px = pix % C::PW;
+        const int gy = y0 - a.pad + py, gx = x0 - a.pad + px;
+        const bool in_img = live && (unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W;
+        dst[u] = live ? py * C::RS + px * C::CS + 8 * c8 : -1;
+        const uint32_t o = (uint32_t)(((b * a.H + gy) * a.W + gx) * CPT + ch * CP + 8 * c8) * 4;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh)
+          f[u][hh] = __builtin_bit_cast(
+              float4, __builtin_amdgcn_raw_buffer_load_b128(rin32, (int)(in_img ? o + 16 * hh : kOOB), 0, 0));
+      }
+#pragma unroll
+      for (int u = 0; u < BAT1; ++u) {
+        if (dst[u] < 0) continue;
+        u32x4 v[3];
+        split_pack8(f[u][0], f[u][1], v);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) *reinterpret_cast<u32x4*>(patch + p * C::kPlane + dst[u]) = v[p];
+      }
+    }
+  };
   auto stage_patch = [&](int ch) {
-    if (DGRAD && a.in_f32) stage_patch_f32(ch);
+    if constexpr (!DGRAD) stage_patch_x32(ch);
+    else if (a.in_f32) stage_patch_f32(ch);
     else stage_patch_split(ch);
   };
 
@@ -897,8 +953,12 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
   ws0.store(wbuf, tid);
   if (NSTEP > 1) wload(ws1, 1);
   __syncthreads();
-  if (DGRAD && NCH == 1 && a.xsplit) {   // the tile's own pixels of the staged source
+  // the tile's own pixels of the staged (split) source, for the layer's weight
+  // gradient: the data gradient's expanded dconv3, the forward's Q-tower input
+  // (its split is made here anyway; the stores drain under the taps' MFMAs)
+  if ((DGRAD || z == 0) && NCH == 1 && a.xsplit) {
     constexpr int NV = TY * TX * (CPT / 8);
+    const __amdgpu_buffer_rsrc_t rx = wt_rsrc(a.xsplit, (uint32_t)(3 * a.x_elems * 2));
 #pragma unroll
     for (int i = 0; i < (3 * NV + C::kThreads - 1) / C::kThreads; ++i) {
       const int f = tid + i * C::kThreads;
@@ -908,10 +968,11 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
         const int ty = pix / TX, tx = pix % TX;
         const int gy = y0 + ty, gx = x0 + tx;
         if (gy < a.H && gx < a.W)
-          *reinterpret_cast<u32x4*>(a.xsplit + p * a.x_elems +
-                                    (((size_t)b * a.H + gy) * a.W + gx) * CPT + 8 * c8) =
+          __builtin_amdgcn_raw_buffer_store_b128(
               *reinterpret_cast<const u32x4*>(patch + p * C::kPlane + (ty + a.pad) * C::RS +
-                                              (tx + a.pad) * C::CS + 8 * c8);
+                                              (tx + a.pad) * C::CS + 8 * c8),
+              rx, (int)((p * (uint32_t)a.x_elems + ((b * a.H + gy) * a.W + gx) * CPT + 8 * c8) * 2),
+              0, 16);
       }
     }
   }
