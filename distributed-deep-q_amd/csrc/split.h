@@ -1060,23 +1060,60 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
         for (int r = 0; r < 4; ++r) { acc4[i][j][r] = 0.f; cor4[i][j][r] = 0.f; }
   }
 
+  // The A operands (patch) of a tap's first k-step do not depend on the
+  // weight ring, so they are read for tap s + 1 right after tap s's MFMAs
+  // issue, before the ring's barrier; after the barrier a wave reads only its
+  // B operands (the first MFMA waits for one read instead of seven of twelve,
+  // and the 16 waves' post-barrier LDS burst halves).  Not across a chunk
+  // edge, where the patch is restaged after the barrier.  Forward kernels
+  // only: conv2 forward 25.1 -> 24.5 / 24.8 -> 24.3 us in two same-box A/Bs,
+  // the step unchanged (conv3's data gradient, whose ISA is identical in
+  // both builds, read 0.5 us slower in-step); with it the data gradients went
+  // 24.7 -> 24.4 (conv2) and 8.2 -> 9.0 us (conv3).
+  constexpr bool kPre = !DGRAD;
+  bf16x8 an[3][NA];
+  auto aload = [&](int s) {
+    const int t = s % T, ky = t / KS, kx = t % KS;
+    const __bf16* pa = patch + ky * C::RS + kx * C::CS;
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int i = 0; i < NA; ++i)
+        an[p][i] = *reinterpret_cast<const bf16x8*>(pa + p * C::kPlane + abase[i]);
+  };
+  auto prefetched = [&](int s) { return kPre && (NCH == 1 || s % T != 0); };   // (s > 0)
   // one step: the MFMAs of tap t of the resident chunk on ring slot `slot`
   auto tap_step = [&](int s, int slot) {
     const int t = s % T;
     const __bf16* wb = wbuf + slot * 3 * C::kWSlot;
     const int ky = t / KS, kx = t % KS;
     const __bf16* pa = patch + ky * C::RS + kx * C::CS;
+    const bool pre = kPre && (s == 0 || prefetched(s));
 #pragma unroll
     for (int g = 0; g < C::KSW; ++g) {
       bf16x8 av[3][NA], bv[3][NB];
+      if constexpr (kPre) {
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
+        for (int j = 0; j < NB; ++j)   // in the MFMAs' order of use
 #pragma unroll
-        for (int i = 0; i < NA; ++i)
-          av[p][i] = *reinterpret_cast<const bf16x8*>(pa + p * C::kPlane + abase[i] + KW * g);
+          for (int p = 0; p < 3; ++p)
+            bv[p][j] = *reinterpret_cast<const bf16x8*>(wb + p * C::kWSlot + bbase[j] + KW * g);
 #pragma unroll
-        for (int j = 0; j < NB; ++j)
-          bv[p][j] = *reinterpret_cast<const bf16x8*>(wb + p * C::kWSlot + bbase[j] + KW * g);
+        for (int p = 0; p < 3; ++p)
+#pragma unroll
+          for (int i = 0; i < NA; ++i)
+            av[p][i] = g == 0 && pre ? an[p][i]
+                                     : *reinterpret_cast<const bf16x8*>(pa + p * C::kPlane + abase[i] + KW * g);
+      } else {
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+#pragma unroll
+          for (int i = 0; i < NA; ++i)
+            av[p][i] = *reinterpret_cast<const bf16x8*>(pa + p * C::kPlane + abase[i] + KW * g);
+#pragma unroll
+          for (int j = 0; j < NB; ++j)
+            bv[p][j] = *reinterpret_cast<const bf16x8*>(wb + p * C::kWSlot + bbase[j] + KW * g);
+        }
       }
       if constexpr (MF) {
 #pragma unroll
@@ -1104,6 +1141,11 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
           }
       }
     }
+    // the next tap's A operands, issued behind this tap's MFMAs
+    if constexpr (kPre) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + 1 < NSTEP && prefetched(s + 1)) aload(s + 1);
+    }
   };
   // end of step s: store step s+1's weights, restage the patch at a chunk
   // boundary (the barrier before fences every wave's reads of the old chunk)
@@ -1120,6 +1162,7 @@ __device__ __forceinline__ void split_conv_body(const SplitArgs& a, char* smem, 
     w.store(wbuf + ((s + 1) & 1) * 3 * C::kWSlot, tid);
     __syncthreads();
   };
+  if (kPre) aload(0);
   for (int s = 0; s < NSTEP; s += 2) {
     if (s + 2 < NSTEP) {
       wload(ws0, s + 2);
