@@ -587,11 +587,20 @@ def exchange_paths(net, rule, steps=240, warmup=24, profile=5):
                     net.step(cfg)
         run(warmup)
         net.synchronize()
-        t0 = time.perf_counter()
-        run(steps)
-        net.synchronize()
-        dt = (time.perf_counter() - t0) / steps
-        e = {"updates_per_s": round(1 / dt, 2), "ms_per_step": round(dt * 1e3, 4), "mode": mode}
+        # timed in 6 chunks (a drain between chunks): the total is the value,
+        # the chunk median separates a host hiccup from the path's own cost
+        # (the host-driven ticket leg varied 0.62 -- 0.79 across boxes)
+        nch = 6   # (40-step chunks: whole 8-step pipelined and 10-round async graphs)
+        per = [steps // nch + (1 if i < steps % nch else 0) for i in range(nch)]
+        ct = []
+        for k in per:
+            t0 = time.perf_counter()
+            run(k)
+            net.synchronize()
+            ct.append(time.perf_counter() - t0)
+        dt = sum(ct) / steps
+        e = {"updates_per_s": round(1 / dt, 2), "ms_per_step": round(dt * 1e3, 4), "mode": mode,
+             "chunk_median_updates_per_s": round(float(np.median([k / t for k, t in zip(per, ct)])), 2)}
         if ex != "async":
             prof = {}
             for _ in range(profile):
@@ -606,6 +615,7 @@ def exchange_paths(net, rule, steps=240, warmup=24, profile=5):
     ref = 0.5 * (ref_before + ref_after)
     for e in out.values():
         e["vs_exchange_free"] = round(e["updates_per_s"] / ref, 4)
+        e["chunk_median_vs_exchange_free"] = round(e["chunk_median_updates_per_s"] / ref, 4)
     return {"note": "world-1 RCCL communicator: the N>1 per-GPU step (kernels, RCCL calls, "
                     "comm-stream overlap, graphs) without wire time; vs_exchange_free = "
                     "this path's updates/s over an exchange-free pipelined leg of the same "
