@@ -549,10 +549,18 @@ def exchange_paths(net, rule, steps=240, warmup=24, profile=5):
         base.step_prepare(c0, "pipelined")
         base.step_pipelined(c0, warmup)
         base.synchronize()
-        t0 = time.perf_counter()
-        base.step_pipelined(c0, steps)
-        base.synchronize()
-        return steps / (time.perf_counter() - t0)
+        t = 0.0
+        for k in chunks:   # the same chunks (and drains) as the paths
+            t0 = time.perf_counter()
+            base.step_pipelined(c0, k)
+            base.synchronize()
+            t += time.perf_counter() - t0
+        return steps / t
+    # timed in 6 chunks (a drain between chunks): the total is the value, the
+    # chunk median separates a host hiccup from the path's own cost (the
+    # host-driven ticket leg varied 0.62 -- 0.79 across boxes)
+    nch = 6   # (40-step chunks: whole 8-step pipelined and 10-round async graphs)
+    chunks = [steps // nch + (1 if i < steps % nch else 0) for i in range(nch)]
     ref_before = free_leg()
     for label, ex, ov, mode in EXCHANGE_PATHS:
         if ex == "async":     # a fresh worker: once begun, a ctx runs async steps only
@@ -587,11 +595,7 @@ def exchange_paths(net, rule, steps=240, warmup=24, profile=5):
                     net.step(cfg)
         run(warmup)
         net.synchronize()
-        # timed in 6 chunks (a drain between chunks): the total is the value,
-        # the chunk median separates a host hiccup from the path's own cost
-        # (the host-driven ticket leg varied 0.62 -- 0.79 across boxes)
-        nch = 6   # (40-step chunks: whole 8-step pipelined and 10-round async graphs)
-        per = [steps // nch + (1 if i < steps % nch else 0) for i in range(nch)]
+        per = chunks
         ct = []
         for k in per:
             t0 = time.perf_counter()
@@ -619,7 +623,7 @@ def exchange_paths(net, rule, steps=240, warmup=24, profile=5):
     return {"note": "world-1 RCCL communicator: the N>1 per-GPU step (kernels, RCCL calls, "
                     "comm-stream overlap, graphs) without wire time; vs_exchange_free = "
                     "this path's updates/s over an exchange-free pipelined leg of the same "
-                    "length (%d steps after %d warmup) timed before and after the paths"
+                    "length (%d steps after %d warmup, in the same 6 chunks) timed before and after the paths"
                     % (steps, warmup),
             "exchange_free": {"updates_per_s_before": round(ref_before, 2),
                               "updates_per_s_after": round(ref_after, 2)},
